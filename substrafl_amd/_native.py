@@ -1,0 +1,101 @@
+"""ctypes binding of ``libfedagg.so`` (the C ABI declared in ``include/fedagg.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``hipcc --offload-arch=gfx950``).
+There is deliberately no fallback: if the shared object is missing or does not load, every
+aggregation call raises :class:`NativeLibraryError` -- the engine never silently computes on
+the CPU or through another backend.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("FEDAGG_LIB", str(_HERE / "libfedagg.so")))
+
+c_u64 = ctypes.c_uint64
+c_int = ctypes.c_int
+c_void = ctypes.c_void_p
+c_dbl = ctypes.c_double
+c_size = ctypes.c_size_t
+P = ctypes.POINTER
+
+# Every symbol include/fedagg.h declares, with its ctypes signature.
+SIGNATURES = {
+    "fedagg_abi_version": (c_int, []),
+    "fedagg_last_error": (ctypes.c_char_p, []),
+    "fedagg_set_launch": (c_int, [c_int, c_int]),
+    "fedagg_fedavg_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void]),
+    "fedagg_fedavg_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void]),
+    "fedagg_fedavg_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_void, c_void]),
+    "fedagg_fedavg_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_void, c_void]),
+    "fedagg_pairwise_ws_bytes": (c_size, [c_int, c_int, c_int]),
+    "fedagg_fedavg_pairwise_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_pairwise_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_pairwise_f64": (c_int, [P(c_void), P(c_dbl), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_pairwise_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_scaffold_f32": (c_int, [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, c_dbl, c_void, c_void, c_void]),
+    "fedagg_scaffold_f64": (c_int, [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, c_dbl, c_void, c_void, c_void]),
+    "fedagg_scaffold_pairwise_f32": (
+        c_int,
+        [P(c_void), P(c_void), c_void, P(c_dbl), c_int, P(c_u64), c_int, c_dbl, c_void, c_void, c_void, c_void],
+    ),
+    "fedagg_scaffold_pairwise_f64": (
+        c_int,
+        [P(c_void), P(c_void), c_void, P(c_dbl), c_int, P(c_u64), c_int, c_dbl, c_void, c_void, c_void, c_void],
+    ),
+    "fedagg_equal_count_f32": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
+    "fedagg_equal_count_f64": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
+    "fedagg_read_probe_f32": (c_int, [c_void, c_u64, c_void, c_int, c_void]),
+}
+
+FEDAGG_KCHUNK = 128
+FEDAGG_KCHUNK_SCAFFOLD = 64
+FEDAGG_MAX_PAIRWISE = 64
+
+
+class NativeLibraryError(RuntimeError):
+    """libfedagg.so is missing, failed to load, or a call returned an error code."""
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise loudly if it is not there."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). The aggregation engine has no CPU fallback."
+        )
+    try:
+        lib = ctypes.CDLL(str(LIB_PATH))
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fedagg_abi_version() != 1:
+        raise NativeLibraryError("libfedagg ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().fedagg_last_error().decode(errors="replace")
+        raise NativeLibraryError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (c_void * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = int(p)
+    return arr

@@ -1,0 +1,84 @@
+"""FedAvg with the aggregation on MI355X.
+
+Drop-in for ``substrafl.strategies.FedAvg`` (substrafl/strategies/fed_avg.py:23-274) on the
+aggregation hot path: same class name, constructor, ``name``, ``@remote`` method
+``avg_shared_states(shared_states) -> FedAvgAveragedState``, same exceptions, and results
+bit-identical to the reference's NumPy arithmetic (fed_avg.py:217-222): the weighted sum of the
+client buckets runs in libfedagg's HIP kernels (substrafl_amd/csrc/fedagg.hip).
+"""
+
+from typing import List, Optional
+
+import numpy as np
+
+from ..engine import AggregationEngine, default_engine
+from ..exceptions import EmptySharedStatesError
+from ..remote import remote
+from ..schemas import FedAvgAveragedState, FedAvgSharedState, StrategyName
+from .strategy import Strategy
+
+
+def check_same_shapes(per_client_layers: List[List[np.ndarray]]) -> None:
+    """``np.sum(list, axis=0)`` raises ValueError when the stacked arrays are inhomogeneous
+    (fed_avg.py:222, scaffold.py:263/293)."""
+    ref = per_client_layers[0]
+    for other in per_client_layers[1:]:
+        for a, b in zip(ref, other):
+            if np.shape(a) != np.shape(b):
+                raise ValueError(
+                    "setting an array element with a sequence. The requested array has an inhomogeneous shape "
+                    f"({np.shape(a)} vs {np.shape(b)})"
+                )
+
+
+class FedAvg(Strategy):
+    """Federated averaging: ``Δw = Σ_k (n_k / n) Δw_k`` (fed_avg.py:23-52)."""
+
+    def __init__(self, algo, metric_functions=None, device: Optional[int] = None):
+        if device is None:
+            super().__init__(algo=algo, metric_functions=metric_functions)
+        else:
+            super().__init__(algo=algo, metric_functions=metric_functions, device=device)
+        self._device = device
+        self._local_states = None
+        self._shared_states = None
+
+    @property
+    def name(self) -> StrategyName:
+        return StrategyName.FEDERATED_AVERAGING
+
+    def _engine(self) -> AggregationEngine:
+        return default_engine() if self._device is None else AggregationEngine(self._device)
+
+    @remote
+    def avg_shared_states(self, shared_states: List[FedAvgSharedState]) -> FedAvgAveragedState:
+        """Weighted average of the clients' ``parameters_update`` by ``n_samples`` (fed_avg.py:176-224).
+
+        Raises:
+            EmptySharedStatesError: ``shared_states`` is empty (fed_avg.py:207-211).
+            AssertionError: clients do not have the same number of layers (fed_avg.py:213-215).
+            ZeroDivisionError: ``sum(n_samples) == 0`` (fed_avg.py:221).
+            ValueError: a layer's shape differs between clients (``np.sum``, fed_avg.py:222).
+            pydantic.ValidationError: a 0-d layer (its average is a scalar, schemas.py:29).
+        """
+        if len(shared_states) == 0:
+            raise EmptySharedStatesError(
+                "Your shared_states is empty. Please ensure that "
+                "the train method of your algorithm returns a FedAvgSharedState object."
+            )
+        parameters_update_len = len(shared_states[0].parameters_update)
+        assert all(
+            [len(shared_state.parameters_update) == parameters_update_len for shared_state in shared_states]
+        ), "Not the same number of layers for every input parameters."
+
+        n_samples = [state.n_samples for state in shared_states]
+        n_all_samples = sum(n_samples)
+        if parameters_update_len == 0:
+            return FedAvgAveragedState(avg_parameters_update=[])
+        if n_all_samples == 0:
+            raise ZeroDivisionError("division by zero")
+        updates = [list(state.parameters_update) for state in shared_states]
+        check_same_shapes(updates)
+
+        averaged_states = self._engine().fedavg(updates, n_samples)
+        return FedAvgAveragedState(avg_parameters_update=averaged_states)

@@ -1,0 +1,81 @@
+"""Scaffold with the two-bucket aggregation on MI355X.
+
+Drop-in for ``substrafl.strategies.Scaffold`` (substrafl/strategies/scaffold.py:22-387) on the
+aggregation hot path.  NumPy 2 (NEP 50) makes the reference compute everything in fp64 -- the
+client weights are a float64 array (scaffold.py:319-320) -- and return fp64 arrays; the HIP
+kernel does the same, adds the server control variate ``c`` last (scaffold.py:262-263) and
+applies ``aggregation_lr`` after the sum (scaffold.py:293).  The check that every client sent
+the same ``c`` (scaffold.py:193-196) runs on the GPU too.
+"""
+
+from typing import List, Optional
+
+from ..engine import AggregationEngine, default_engine
+from ..remote import remote
+from ..schemas import ScaffoldAveragedStates, ScaffoldSharedState, StrategyName
+from .fed_avg import check_same_shapes
+from .strategy import Strategy
+
+
+class Scaffold(Strategy):
+    def __init__(self, algo, aggregation_lr: float = 1, metric_functions=None, device: Optional[int] = None):
+        if device is None:
+            super().__init__(algo=algo, aggregation_lr=aggregation_lr, metric_functions=metric_functions)
+        else:
+            super().__init__(algo=algo, aggregation_lr=aggregation_lr, metric_functions=metric_functions,
+                             device=device)
+        if aggregation_lr < 0:
+            raise ValueError("aggregation_lr must be >=0")
+        self._aggregation_lr = aggregation_lr
+        self._device = device
+        self._local_states = None
+        self._shared_states = None
+
+    @property
+    def name(self) -> StrategyName:
+        return StrategyName.SCAFFOLD
+
+    def _engine(self) -> AggregationEngine:
+        return default_engine() if self._device is None else AggregationEngine(self._device)
+
+    def _check_shared_states(self, shared_states: List[ScaffoldSharedState]) -> None:
+        """Host-decidable half of scaffold.py:168-202 (types, list lengths, shapes of ``c``);
+        the element-wise ``c`` equality runs on the GPU (``equal_count`` kernel)."""
+        assert shared_states, "shared_states should contain at least one element"
+        assert isinstance(shared_states, (list, tuple)), "shared_states should be a list"
+        first = shared_states[0]
+        for shared_state in shared_states:
+            assert isinstance(shared_state, ScaffoldSharedState) or type(shared_state).__name__ == (
+                "ScaffoldSharedState"
+            ), "shared_state should be an instance of ScaffoldSharedState"
+            assert len(shared_state.control_variate_update) == len(
+                first.control_variate_update
+            ), "the length of control_variate_update should be the same for each shared_state"
+            assert len(shared_state.parameters_update) == len(
+                first.parameters_update
+            ), "the length of parameters_update should be the same for each shared_state"
+            assert len(shared_state.server_control_variate) == len(
+                first.server_control_variate
+            ), "the length of server_control_variate should be the same for each shared_state"
+            for c, ci in zip(first.server_control_variate, shared_state.server_control_variate):
+                assert c.shape == ci.shape, "all server_control_variate in the shared_states are not equal"
+        assert (
+            len(first.control_variate_update) == len(first.server_control_variate) == len(first.parameters_update)
+        ), "the length of server_control_variate, parameters_update and server_control_variate should be the same"
+
+    @remote
+    def avg_shared_states(self, shared_states: List[ScaffoldSharedState]) -> ScaffoldAveragedStates:
+        """Scaffold server step (scaffold.py:297-337): averaged weight update times
+        ``aggregation_lr`` and updated server control variate, both fp64."""
+        self._check_shared_states(shared_states=shared_states)
+        cvs = [list(s.control_variate_update) for s in shared_states]
+        pus = [list(s.parameters_update) for s in shared_states]
+        c0 = list(shared_states[0].server_control_variate)
+        check_same_shapes([*cvs, c0])  # np.sum([w*cv_k ..., c]) (scaffold.py:263)
+        check_same_shapes(pus)  # np.sum([w*Δ_k ...]) (scaffold.py:293)
+        mismatches, new_c, avg = self._engine().scaffold(
+            pus, cvs, [list(s.server_control_variate) for s in shared_states],
+            [s.n_samples for s in shared_states], self._aggregation_lr,
+        )
+        assert mismatches == 0, "all server_control_variate in the shared_states are not equal"
+        return ScaffoldAveragedStates(server_control_variate=new_c, avg_parameters_update=avg)

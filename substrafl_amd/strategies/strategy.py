@@ -1,0 +1,32 @@
+"""Strategy base: constructor contract of substrafl/strategies/strategy.py:30-73.
+
+Every constructor argument is recorded in ``self.args`` / ``self.kwargs``
+(compute_plan_builder.py:15-29) so ``RemoteStruct`` can re-create the strategy with
+``cls(*args, **kwargs)`` in the task process, and ``name`` must be in ``algo.strategies``.
+Graph building (``build_compute_plan``, ``perform_round``) is Substra control plane and out of
+scope for this engine.
+"""
+
+from abc import abstractmethod
+
+from ..exceptions import IncompatibleAlgoStrategyError
+from ..schemas import StrategyName
+
+
+class Strategy:
+    def __init__(self, algo, metric_functions=None, *args, **kwargs):
+        self.args = args
+        self.kwargs = dict(kwargs, algo=algo, metric_functions=metric_functions)
+        self.algo = algo
+        self.metric_functions = metric_functions
+        if self.name not in algo.strategies:
+            raise IncompatibleAlgoStrategyError(
+                f"The algo {algo.__class__.__name__} is not compatible with the strategy "
+                f"{self.__class__.__name__}, named {self.name}. Check the algo strategies property: "
+                "algo.strategies to see the list of compatible strategies."
+            )
+
+    @property
+    @abstractmethod
+    def name(self) -> StrategyName:
+        raise NotImplementedError

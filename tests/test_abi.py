@@ -1,0 +1,52 @@
+"""The C-ABI library loads and exports every symbol include/fedagg.h declares (CPU only: no
+kernel is launched; argument validation returns before any HIP call)."""
+
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+from substrafl_amd import _native
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "fedagg.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fedagg_[a-z0-9_]+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    assert "fedagg_fedavg_f32" in names and "fedagg_scaffold_f32" in names
+    assert len(names) >= 18
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(str(_native.LIB_PATH))
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    # and the ctypes binding covers exactly the declared set
+    assert sorted(_native.SIGNATURES) == declared_functions()
+
+
+def test_abi_version_and_invalid_arguments():
+    lib = _native.load()
+    assert lib.fedagg_abi_version() == 1
+    w = (ctypes.c_float * 1)(1.0)
+    ptrs = _native.ptr_array([0])
+    assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, None) == -1  # K == 0
+    assert b"K must be > 0" in lib.fedagg_last_error()
+    assert lib.fedagg_fedavg_f32(ptrs, w, 1, 16, None, None) == -1  # NULL out
+    assert lib.fedagg_pairwise_ws_bytes(8, 3, 4) == 2 * 64 * 9 * 8
+    with pytest.raises(_native.NativeLibraryError):
+        _native.check(-1, "x")
+
+
+def test_missing_library_is_loud(monkeypatch, tmp_path):
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", tmp_path / "nope.so")
+    with pytest.raises(_native.NativeLibraryError, match="no CPU fallback"):
+        _native.load()

@@ -1,0 +1,366 @@
+"""Parity of the HIP path (through libfedagg.so's C ABI) with the oracle and the reference's
+golden vectors.  Bar: bit-exact (the reference arithmetic is deterministic IEEE fp32/fp64)."""
+
+import ctypes
+import pickle
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pydantic
+import pytest
+
+from oracle import fedavg_reference_structure, numpy_pairwise_sum, scaffold_reference_structure
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _bits(a):
+    a = np.asarray(a)
+    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize])
+
+
+def _assert_same(got, ref):
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        assert isinstance(g, np.ndarray)
+        assert g.dtype == r.dtype and g.shape == r.shape, (g.dtype, r.dtype, g.shape, r.shape)
+        assert np.array_equal(_bits(g), _bits(r))
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from substrafl_amd import _native
+
+    _native.load()
+    return torch
+
+
+# ------------------------------------------------------------------------------------------
+# golden vectors (captured from the reference itself)
+# ------------------------------------------------------------------------------------------
+def test_golden_fedavg(golden, torch_gpu, dummy_algo_class):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    arrays, meta = golden
+    strategy = FedAvg(algo=dummy_algo_class())
+    n = 0
+    for case in [c for c in meta["cases"] if c["strategy"] == "fedavg"]:
+        key, K, L = case["key"], case["K"], case["layers"]
+        ns = [int(v) for v in arrays[f"{key}/n_samples"]]
+        states = [FedAvgSharedState(n_samples=ns[k], parameters_update=[arrays[f"{key}/x{li}"][k] for li in range(L)])
+                  for k in range(K)]
+        got = strategy.avg_shared_states(shared_states=states, _skip=True).avg_parameters_update
+        _assert_same(got, [arrays[f"{key}/out{li}"] for li in range(L)])
+        n += 1
+    assert n >= 40
+
+
+def test_golden_scaffold(golden, torch_gpu, dummy_algo_class):
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    arrays, meta = golden
+    for case in [c for c in meta["cases"] if c["strategy"] == "scaffold"]:
+        key, K, L = case["key"], case["K"], case["layers"]
+        lr = int(case["lr"]) if case["lr_is_int"] else float(case["lr"])
+        ns = [int(v) for v in arrays[f"{key}/n_samples"]]
+        c = [arrays[f"{key}/c{li}"] for li in range(L)]
+        states = [
+            ScaffoldSharedState(
+                parameters_update=[arrays[f"{key}/pu{li}"][k] for li in range(L)],
+                control_variate_update=[arrays[f"{key}/cv{li}"][k] for li in range(L)],
+                n_samples=ns[k],
+                server_control_variate=c,
+            )
+            for k in range(K)
+        ]
+        res = Scaffold(algo=dummy_algo_class(), aggregation_lr=lr).avg_shared_states(shared_states=states, _skip=True)
+        _assert_same(res.avg_parameters_update, [arrays[f"{key}/avg{li}"] for li in range(L)])
+        _assert_same(res.server_control_variate, [arrays[f"{key}/newc{li}"] for li in range(L)])
+
+
+@pytest.mark.parametrize("n_samples, factor", [([1, 0, 0], 1.0), ([1, 1, 1], 1.0), ([1, 0, 1], 1.5)])
+def test_reference_unit_fedavg(torch_gpu, dummy_algo_class, n_samples, factor, golden):
+    """tests/strategies/test_fed_avg.py:17-38 (float64 inputs, exact equality)."""
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    states = [
+        FedAvgSharedState(parameters_update=[np.ones((5, 10))], n_samples=n_samples[0]),
+        FedAvgSharedState(parameters_update=[np.zeros((5, 10))], n_samples=n_samples[1]),
+        FedAvgSharedState(parameters_update=[2 * np.ones((5, 10))], n_samples=n_samples[2]),
+    ]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    assert (factor * np.ones((5, 10)) == got).all() and got[0].dtype == np.float64
+
+
+def test_reference_unit_int64_layers(torch_gpu, dummy_algo_class, golden):
+    """tests/strategies/test_fed_avg.py:41-54: int64 layers promote to float64."""
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    arrays, _ = golden
+    states = [
+        FedAvgSharedState(parameters_update=[np.asarray([[0, 1], [2, 4]]), np.asarray([[6, 8], [10, 12]])], n_samples=1),
+        FedAvgSharedState(parameters_update=[np.asarray([[16, 20], [18, 20]]), np.asarray([[22, 24], [26, 28]])],
+                          n_samples=3),
+    ]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, [arrays["g5/unit_fedavg_int64_0"], arrays["g5/unit_fedavg_int64_1"]])
+
+
+@pytest.mark.parametrize(
+    "aggregation_lr, expected",
+    [(0, [np.zeros(5), np.zeros(5)]), (1, [0.75 * np.ones(5), 1.75 * np.ones(5)]), (2, [1.5 * np.ones(5), 3.5 * np.ones(5)])],
+)
+def test_reference_unit_scaffold_lr(torch_gpu, dummy_algo_class, aggregation_lr, expected):
+    """tests/strategies/test_scaffold.py:149-176."""
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    states = [
+        ScaffoldSharedState(parameters_update=[0 * np.ones(5), np.ones(5)], control_variate_update=[np.ones(5), np.ones(5)],
+                            n_samples=1, server_control_variate=[np.ones(5), np.ones(5)]),
+        ScaffoldSharedState(parameters_update=[np.ones(5), 2 * np.ones(5)], control_variate_update=[np.ones(5), np.ones(5)],
+                            n_samples=3, server_control_variate=[np.ones(5), np.ones(5)]),
+    ]
+    res = Scaffold(algo=dummy_algo_class(), aggregation_lr=aggregation_lr).avg_shared_states(shared_states=states,
+                                                                                           _skip=True)
+    for g, e in zip(res.avg_parameters_update, expected):
+        assert np.allclose(g, e)
+    for g in res.server_control_variate:
+        assert np.allclose(g, 2 * np.ones(5))
+
+
+# ------------------------------------------------------------------------------------------
+# randomized parity against the oracle: client-count edges, chunking, dtypes
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("K", [1, 2, 7, 8, 9, 127, 128, 129, 300])
+def test_fedavg_random_vs_oracle(torch_gpu, dummy_algo_class, K):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    rng = np.random.default_rng(K)
+    shapes = [(33, 17), (1,), (5,), (1, 1), (2, 1, 3), (1031,)]
+    pus = [[(rng.standard_normal(s) * 10.0 ** rng.integers(-3, 3)).astype(np.float32) for s in shapes] for _ in range(K)]
+    if K % 2:
+        pus = [[(a + np.float32(1e4 * (-1) ** k)).astype(np.float32) for a in p] for k, p in enumerate(pus)]
+    ns = [int(v) for v in rng.integers(0, 5000, K)]
+    ns[0] += 1
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float16, np.int32])
+def test_fedavg_other_dtypes(torch_gpu, dummy_algo_class, dtype):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    rng = np.random.default_rng(3)
+    shapes = [(40, 3), (1,), (17,)]
+    K = 11
+    pus = [[(rng.standard_normal(s) * 20).astype(dtype) for s in shapes] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+
+
+def test_fedavg_mixed_dtypes_in_one_layer(torch_gpu, dummy_algo_class):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    rng = np.random.default_rng(4)
+    K = 5
+    pus = [[rng.standard_normal((9, 7)).astype(np.float32 if k % 2 else np.float64),
+            rng.standard_normal(4).astype(np.float32)] for k in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+
+
+def test_fedavg_0d_layer_fails_validation_like_reference(torch_gpu, dummy_algo_class):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    states = [FedAvgSharedState(parameters_update=[np.ones((), np.float32)], n_samples=1)] * 2
+    with pytest.raises(pydantic.ValidationError):
+        FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True)
+
+
+@pytest.mark.parametrize("K, lr", [(1, 1), (3, 0.7), (64, 2), (65, 0), (130, 1.3)])
+def test_scaffold_random_vs_oracle(torch_gpu, dummy_algo_class, K, lr):
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    rng = np.random.default_rng(100 + K)
+    shapes = [(13, 7), (1,), (1, 1), (130,)]
+    mk = lambda: [(rng.standard_normal(s) * 10.0 ** rng.integers(-3, 3)).astype(np.float32) for s in shapes]  # noqa
+    pus, cvs, c = [mk() for _ in range(K)], [mk() for _ in range(K)], mk()
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    states = [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                  server_control_variate=c) for k in range(K)]
+    res = Scaffold(algo=dummy_algo_class(), aggregation_lr=lr).avg_shared_states(shared_states=states, _skip=True)
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)
+
+
+def test_scaffold_fp64_inputs_and_c_check(torch_gpu, dummy_algo_class):
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    rng = np.random.default_rng(9)
+    K = 4
+    shapes = [(6, 2), (1,)]
+    pus = [[rng.standard_normal(s) for s in shapes] for _ in range(K)]
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [np.array([[np.nan, 0.0]] * 6), np.array([-0.0])]
+    ns = [3, 1, 4, 1]
+    states = [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                  server_control_variate=[a.copy() for a in c]) for k in range(K)]
+    states[2].server_control_variate[1] = np.array([0.0])  # +0 == -0 and NaN == NaN for assert_array_equal
+    res = Scaffold(algo=dummy_algo_class(), aggregation_lr=1).avg_shared_states(shared_states=states, _skip=True)
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 1)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)
+    states[3].server_control_variate[0] = np.ones((6, 2))
+    with pytest.raises(AssertionError):
+        Scaffold(algo=dummy_algo_class()).avg_shared_states(shared_states=states, _skip=True)
+
+
+# ------------------------------------------------------------------------------------------
+# device-resident plans through the C ABI (bf16, unaligned rows, full size)
+# ------------------------------------------------------------------------------------------
+def test_bf16_plan_equals_reference_on_upcast(torch_gpu):
+    torch = torch_gpu
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 37, 10_007
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn((K, M + 9), generator=g, device="cuda").to(torch.bfloat16)
+    ns = list(range(1, K + 1))
+    out = torch.empty(M + 9, dtype=torch.float32, device="cuda")
+    FedAvgPlan("bf16", x, fedavg_weights(ns, "bf16"), M, out, [5, M - 1]).launch()
+    torch.cuda.synchronize()
+    up = x.float().cpu().numpy()[:, :M]
+    ref = fedavg_reference_structure([[up[k].copy()] for k in range(K)], ns)[0]
+    got = out.cpu().numpy()[:M]
+    mask = np.ones(M, bool)
+    mask[[5, M - 1]] = False
+    assert np.array_equal(_bits(got[mask]), _bits(ref[mask]))
+    w = fedavg_weights(ns, "f32")
+    for p in (5, M - 1):
+        prods = (up[:, p] * w).astype(np.float32)
+        assert _bits(np.float32(0.0) + numpy_pairwise_sum(prods)) == _bits(got[p])
+
+
+def test_unaligned_rows_take_scalar_path(torch_gpu):
+    torch = torch_gpu
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 5, 4099
+    base = torch.randn(K * (M + 1) + 1, device="cuda")
+    rows = [base.data_ptr() + 4 * (1 + k * (M + 1)) for k in range(K)]  # 4-B aligned only
+    out = torch.empty(M, device="cuda")
+    ns = [5, 4, 3, 2, 1]
+    FedAvgPlan("f32", rows, fedavg_weights(ns, "f32"), M, out).launch()
+    torch.cuda.synchronize()
+    h = base.cpu().numpy()
+    pus = [[h[1 + k * (M + 1): 1 + k * (M + 1) + M].copy()] for k in range(K)]
+    assert np.array_equal(_bits(out.cpu().numpy()), _bits(fedavg_reference_structure(pus, ns)[0]))
+
+
+@pytest.mark.parametrize("K, M", [(8, 25_000_000), (64, 4_000_000), (200, 1_000_000)])
+def test_full_size_vs_torch_sequential(torch_gpu, K, M):
+    """At BASELINE sizes: bit-exact against a torch fp32 eager sequential reference on the device
+    (every torch op is one separately rounded IEEE op: same order as the reference)."""
+    torch = torch_gpu
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+
+    shapes = synthetic_state_dict_shapes(M)
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn((K, lay.ld), generator=g, device="cuda")
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    w = fedavg_weights(ns, "f32")
+    out = torch.empty(lay.ld, device="cuda")
+    FedAvgPlan("f32", x, w, M, out, lay.pairwise_idx).launch()
+    acc = torch.zeros(M, device="cuda")
+    for k in range(K):
+        acc = acc + x[k, :M] * torch.tensor(w[k], device="cuda")
+    torch.cuda.synchronize()
+    mask = torch.ones(M, dtype=torch.bool, device="cuda")
+    mask[torch.from_numpy(lay.pairwise_idx.astype(np.int64)).cuda()] = False
+    assert torch.equal(out[:M][mask].view(torch.int32), acc[mask].view(torch.int32))
+    for p in lay.pairwise_idx.astype(np.int64):
+        prods = (x[:, p].cpu().numpy() * w).astype(np.float32)
+        assert _bits(np.float32(0.0) + numpy_pairwise_sum(prods)) == _bits(out[p].cpu().numpy())
+
+
+def test_equal_count_kernel(torch_gpu):
+    torch = torch_gpu
+    from substrafl_amd.engine import equal_count
+
+    K, M = 9, 100_003
+    c = torch.randn(M, device="cuda")
+    copies = c.repeat(K, 1)
+    copies[3, 17] = 1e9
+    copies[7, M - 1] = float("nan")
+    copies[:, 5] = float("nan")  # NaN == NaN
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    equal_count("f32", copies, M, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 2
+
+
+# ------------------------------------------------------------------------------------------
+# subprocess-mode emulation: the aggregate task in its own process (generic_function contract)
+# ------------------------------------------------------------------------------------------
+def test_generic_function_in_child_process(torch_gpu, tmp_path, dummy_algo_class):
+    from substrafl_amd.remote import PickleSerializer
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    rng = np.random.default_rng(21)
+    shapes = [(128, 64), (64,), (1,)]
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(3)]
+    ns = [100, 250, 7]
+    paths = []
+    for k in range(3):
+        p = tmp_path / f"shared_{k}"
+        PickleSerializer.save(FedAvgSharedState(n_samples=ns[k], parameters_update=pus[k]), p)
+        paths.append(str(p))
+    import cloudpickle
+
+    cloudpickle.register_pickle_by_value(sys.modules[__name__])  # the child cannot import this test module
+    FedAvg(algo=_PicklableAlgo()).avg_shared_states(shared_states=paths).remote_struct.save(tmp_path)
+    out = tmp_path / "out_shared"
+    script = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from substrafl_amd.remote import RemoteStruct\n"
+        "rs = RemoteStruct.load(__import__('pathlib').Path(%r))\n"
+        "rs.get_remote_instance().generic_function({'shared': %r}, {'shared': %r}, {})\n"
+    ) % (str(ROOT), str(tmp_path), paths, str(out))
+    subprocess.run([sys.executable, "-c", script], check=True, timeout=300)
+    with open(out, "rb") as f:  # our own output file
+        res = pickle.load(f)
+    _assert_same(res.avg_parameters_update, fedavg_reference_structure(pus, ns))
+
+
+class _PicklableAlgo:
+    def __init__(self, *args, **kwargs):
+        self.args, self.kwargs = args, kwargs
+
+    strategies = ["Federated Averaging", "Scaffold"]

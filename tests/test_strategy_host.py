@@ -1,0 +1,114 @@
+"""Host-side behaviour of the drop-in strategies: error conventions (reference
+tests/strategies/test_fed_avg.py:57-65, test_scaffold.py:56-146), the @remote contract
+(tests/remote/test_decorator.py) and the absence of any CPU fallback.  CPU only."""
+
+import cloudpickle
+import numpy as np
+import pydantic
+import pytest
+import torch
+
+from substrafl_amd import _native
+from substrafl_amd.exceptions import EmptySharedStatesError, IncompatibleAlgoStrategyError
+from substrafl_amd.remote import RemoteOperation, RemoteStruct
+from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState, StrategyName
+from substrafl_amd.strategies import FedAvg, Scaffold
+
+no_gpu = pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+
+
+def test_fedavg_empty(dummy_algo_class):
+    with pytest.raises(EmptySharedStatesError):
+        FedAvg(algo=dummy_algo_class()).avg_shared_states([], _skip=True)
+
+
+def test_fedavg_different_length(dummy_algo_class):
+    shared_states = [
+        FedAvgSharedState(parameters_update=[np.ones((5, 10)), np.ones((5, 10))], n_samples=1),
+        FedAvgSharedState(parameters_update=[np.zeros((5, 10))], n_samples=1),
+    ]
+    with pytest.raises(AssertionError):
+        FedAvg(algo=dummy_algo_class()).avg_shared_states(shared_states, _skip=True)
+
+
+def test_fedavg_zero_samples_and_shape_mismatch(dummy_algo_class):
+    s = FedAvg(algo=dummy_algo_class())
+    with pytest.raises(ZeroDivisionError):
+        s.avg_shared_states([FedAvgSharedState(parameters_update=[np.ones(3, np.float32)], n_samples=0)] * 2,
+                            _skip=True)
+    with pytest.raises(ValueError):
+        s.avg_shared_states([FedAvgSharedState(parameters_update=[np.ones(3, np.float32)], n_samples=1),
+                             FedAvgSharedState(parameters_update=[np.ones(4, np.float32)], n_samples=1)], _skip=True)
+
+
+def test_fedavg_no_layers_returns_empty(dummy_algo_class):
+    out = FedAvg(algo=dummy_algo_class()).avg_shared_states(
+        [FedAvgSharedState(parameters_update=[], n_samples=0)] * 2, _skip=True)
+    assert out.avg_parameters_update == []
+
+
+def test_float_n_samples_rejected():
+    with pytest.raises(pydantic.ValidationError):
+        FedAvgSharedState(parameters_update=[np.ones(3)], n_samples=1.5)
+
+
+def test_name_and_compat(dummy_algo_class):
+    assert FedAvg(algo=dummy_algo_class()).name == StrategyName.FEDERATED_AVERAGING
+    assert Scaffold(algo=dummy_algo_class()).name == StrategyName.SCAFFOLD
+
+    class OnlyFedAvg(dummy_algo_class):
+        @property
+        def strategies(self):
+            return [StrategyName.FEDERATED_AVERAGING]
+
+    with pytest.raises(IncompatibleAlgoStrategyError):
+        Scaffold(algo=OnlyFedAvg())
+
+
+@pytest.mark.parametrize("shared_states", [[], ScaffoldSharedState(
+    parameters_update=[np.array([0, 1, 1])], control_variate_update=[np.array([0, 1, 1])], n_samples=1,
+    server_control_variate=[np.array([0, 1, 1])])])
+def test_scaffold_type_error(dummy_algo_class, shared_states):
+    with pytest.raises(AssertionError):
+        Scaffold(algo=dummy_algo_class()).avg_shared_states(shared_states, _skip=True)
+
+
+def test_scaffold_negative_lr(dummy_algo_class):
+    with pytest.raises(ValueError):
+        Scaffold(algo=dummy_algo_class(), aggregation_lr=-1)
+
+
+@pytest.mark.parametrize(
+    "parameters_update, control_variate_update, server_control_variate",
+    [
+        ([np.zeros(5), np.zeros(5)], [np.zeros(5)], [np.zeros(5)]),
+        ([np.zeros(5)], [np.zeros(5), np.zeros(5)], [np.zeros(5)]),
+        ([np.zeros(5)], [np.zeros(5)], [np.zeros(5), np.zeros(5)]),
+    ],
+)
+def test_scaffold_len_states_same(dummy_algo_class, parameters_update, control_variate_update,
+                                  server_control_variate):
+    s = [ScaffoldSharedState(parameters_update=parameters_update, control_variate_update=control_variate_update,
+                             n_samples=1, server_control_variate=server_control_variate)]
+    with pytest.raises(AssertionError):
+        Scaffold(algo=dummy_algo_class(), aggregation_lr=0).avg_shared_states(shared_states=s, _skip=True)
+
+
+def test_remote_operation_and_struct_roundtrip(dummy_algo_class, tmp_path):
+    strategy = Scaffold(algo=dummy_algo_class(), aggregation_lr=2)
+    op = strategy.avg_shared_states(shared_states=["dummy"])
+    assert isinstance(op, RemoteOperation) and op.shared_states == ["dummy"]
+    op.remote_struct.save(tmp_path)
+    rs = RemoteStruct.load(tmp_path)
+    inst = rs.get_instance()
+    assert isinstance(inst, Scaffold) and inst._aggregation_lr == 2
+    assert rs.summary() == {"type": "Scaffold", "method_name": "avg_shared_states"}
+    # strategies stay picklable after use (no engine state captured)
+    cloudpickle.loads(cloudpickle.dumps(FedAvg(algo=dummy_algo_class())))
+
+
+@no_gpu
+def test_no_cpu_fallback(dummy_algo_class):
+    s = [FedAvgSharedState(parameters_update=[np.ones(3, np.float32)], n_samples=1)] * 2
+    with pytest.raises(_native.NativeLibraryError, match="no CPU fallback"):
+        FedAvg(algo=dummy_algo_class()).avg_shared_states(s, _skip=True)
