@@ -85,8 +85,10 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     lib = _native.load()
-    if args.grid_cap or args.nontemporal >= 0:
-        lib.fedagg_set_launch(args.grid_cap, args.nontemporal)
+    if args.grid_cap:
+        _native.tune(grid_cap=args.grid_cap)
+    if args.nontemporal >= 0:
+        _native.tune(nt_load=args.nontemporal)
 
     wl = WORKLOADS[args.workload]
     K, M, kind = wl["K"], wl["M"], wl["kind"]
@@ -130,9 +132,8 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         starts[s].record(stream)
-        plan.launch_main(stream)
+        plan.launch(stream)
         ends[s].record(stream)
-        plan.launch_pairwise(stream)
     torch.cuda.synchronize(device)
     barrier()
     elapsed = time.perf_counter() - t0

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# One GPU-box session: parity tests, smoke, tuning sweep, bench.
 # Every GPU step has its own time limit; a crash/abort/timeout stops the script
 # (test FAILURES, exit 1, do not: the later steps are still informative).
 set -u
@@ -7,7 +7,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-TAG=${TAG:-r01}
 step() {  # step <name> <timeout_s> <cmd...>
   local name=$1 t=$2; shift 2
   echo "=== $name ($(date +%T))"
@@ -17,10 +16,9 @@ step() {  # step <name> <timeout_s> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench_c2 600 python bench.py --steps 50 --warmup 10
-if [ "${PROFILE:-1}" = "1" ]; then
-  step rocprof_c2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${TAG}_c2 -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline
-fi
+[ "${TESTS:-1}" = "1" ] && step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+[ "${TESTS:-1}" = "1" ] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[ "${TUNE:-0}" = "1" ] && step tune_c2 600 python tools/tune_fedavg.py --K 8 --M 25000000
+[ "${TUNE:-0}" = "1" ] && step tune_c3 600 python tools/tune_fedavg.py --K 64 --M 125000000 --rounds 3 --iters 5
+for wl in ${BENCH:-c2}; do step bench_$wl 600 python bench.py --workload $wl --steps 50 --warmup 10; done
 echo "=== done"

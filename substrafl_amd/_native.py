@@ -27,33 +27,29 @@ P = ctypes.POINTER
 SIGNATURES = {
     "fedagg_abi_version": (c_int, []),
     "fedagg_last_error": (ctypes.c_char_p, []),
-    "fedagg_set_launch": (c_int, [c_int, c_int]),
-    "fedagg_fedavg_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void]),
-    "fedagg_fedavg_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void]),
-    "fedagg_fedavg_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_void, c_void]),
-    "fedagg_fedavg_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_void, c_void]),
+    "fedagg_tune": (c_int, [ctypes.c_char_p, ctypes.c_longlong]),
     "fedagg_pairwise_ws_bytes": (c_size, [c_int, c_int, c_int]),
-    "fedagg_fedavg_pairwise_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
-    "fedagg_fedavg_pairwise_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
-    "fedagg_fedavg_pairwise_f64": (c_int, [P(c_void), P(c_dbl), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
-    "fedagg_fedavg_pairwise_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, P(c_u64), c_int, c_void, c_void, c_void]),
-    "fedagg_scaffold_f32": (c_int, [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, c_dbl, c_void, c_void, c_void]),
-    "fedagg_scaffold_f64": (c_int, [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, c_dbl, c_void, c_void, c_void]),
-    "fedagg_scaffold_pairwise_f32": (
+    "fedagg_fedavg_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_scaffold_f32": (
         c_int,
-        [P(c_void), P(c_void), c_void, P(c_dbl), c_int, P(c_u64), c_int, c_dbl, c_void, c_void, c_void, c_void],
+        [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, P(c_u64), c_int, c_void, c_dbl, c_void, c_void, c_void],
     ),
-    "fedagg_scaffold_pairwise_f64": (
+    "fedagg_scaffold_f64": (
         c_int,
-        [P(c_void), P(c_void), c_void, P(c_dbl), c_int, P(c_u64), c_int, c_dbl, c_void, c_void, c_void, c_void],
+        [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, P(c_u64), c_int, c_void, c_dbl, c_void, c_void, c_void],
     ),
     "fedagg_equal_count_f32": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_equal_count_f64": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_read_probe_f32": (c_int, [c_void, c_u64, c_void, c_int, c_void]),
 }
 
+ABI_VERSION = 2
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
+FEDAGG_FUSED_PAIRWISE = 16
 FEDAGG_MAX_PAIRWISE = 64
 
 
@@ -82,7 +78,7 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fedagg_abi_version() != 1:
+    if lib.fedagg_abi_version() != ABI_VERSION:
         raise NativeLibraryError("libfedagg ABI version mismatch")
     _lib = lib
     return lib
@@ -99,3 +95,11 @@ def ptr_array(ptrs) -> ctypes.Array:
     for i, p in enumerate(ptrs):
         arr[i] = int(p)
     return arr
+
+
+def tune(**knobs) -> None:
+    """Set launch knobs of the library (``fedagg_tune``): grid_cap, nt_load, nt_store, vpt,
+    fuse_pairwise."""
+    lib = load()
+    for k, v in knobs.items():
+        check(lib.fedagg_tune(k.encode(), int(v)), f"fedagg_tune({k})")

@@ -7,14 +7,18 @@
 //     8 fp16 elements) and walks the K clients IN LIST ORDER, which is the order the
 //     reference's np.sum(list, axis=0) adds them (fed_avg.py:221-222);
 //   * the client loop is unrolled by FA_UNROLL with all loads issued before the dependent
-//     add chain, so every lane keeps FA_UNROLL x 16 B in flight (the HBM latency cover);
+//     add chain, so every lane keeps FA_UNROLL x 16 B (x VPT vectors) in flight;
 //   * client pointers and weights live in the kernel-argument segment (scalar loads,
 //     no device-side table, graph-capturable); clients beyond FEDAGG_KCHUNK continue
 //     from the partial sum already in `out`, which is exact because the accumulator
 //     type is the stored type;
-//   * grid-stride over the bucket with a launch of a few thousand 256-thread
-//     workgroups (>> 256 CUs; blocks are dealt round-robin over the 8 XCDs and have no
-//     reuse to localise, so no XCD remap is needed here).
+//   * numel == 1 tensors (NumPy pairwise order) are patched inside the
+//     same launch by the thread that owns their vector, computing the pairwise tree from the
+//     client pointers directly (single-chunk launches, <= FEDAGG_FUSED_PAIRWISE indices);
+//     larger cases fall back to the separate gather + tree kernels;
+//   * grid-stride over the bucket with a launch of a few thousand 256-thread workgroups
+//     (>> 256 CUs; blocks are dealt round-robin over the 8 XCDs and have no reuse to
+//     localise, so no XCD remap is needed here).
 // Bit parity with NumPy requires every product and sum to be rounded separately: the
 // file is compiled with -ffp-contract=off AND every kernel body carries
 // `#pragma clang fp contract(off)` (hipcc otherwise emits v_fmac_f32 for acc + x*w).
@@ -34,8 +38,8 @@ namespace {
 
 thread_local char g_err[512] = "";
 
-int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
-  snprintf(g_err, sizeof(g_err), fmt, a, b);
+int fail(int code, const char* fmt, long long b = 0) {
+  snprintf(g_err, sizeof(g_err), fmt, b);
   return code;
 }
 
@@ -48,21 +52,25 @@ int check_launch(const char* what) {
   return FEDAGG_OK;
 }
 
-// Launch shape (tunable through fedagg_set_launch; defaults measured on MI355X).
-int g_grid_cap = 4096;   // workgroups per launch before grid-striding
-int g_nontemporal = 1;   // client streams are read once: non-temporal loads
+// Launch shape (fedagg_tune); defaults are the values measured best on MI355X.
+int g_grid_cap = 4096;  // workgroups per launch before grid-striding
+int g_nt_load = 1;      // client streams are read once: non-temporal loads
+int g_nt_store = 0;     // non-temporal output stores
+int g_vpt = 1;          // 16-byte vectors per thread per grid-stride step
+int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------
-// element types: storage type TIn, product/accumulate type TP, output storage TOut
+// element types: storage type In, product/accumulate type P, output storage Out,
+// pairwise-sum accumulation type W (NumPy's HALF_pairwise_sum sums in fp32)
 // ------------------------------------------------------------------------------------
 struct F32 {
   using In = float;
   using P = float;
   using Out = float;
+  using W = float;
   static constexpr int L = 4;  // elements per 16-byte vector
   __device__ static P cvt(In v) { return v; }
   __device__ static void unpack(u32x4 r, P* o) {
@@ -76,6 +84,7 @@ struct BF16 {
   using In = uint16_t;
   using P = float;
   using Out = float;
+  using W = float;
   static constexpr int L = 8;
   __device__ static P cvt(In v) { return __uint_as_float(((uint32_t)v) << 16); }  // exact upcast
   __device__ static void unpack(u32x4 r, P* o) {
@@ -92,6 +101,7 @@ struct F64 {
   using In = double;
   using P = double;
   using Out = double;
+  using W = double;
   static constexpr int L = 2;
   __device__ static P cvt(In v) { return v; }
   __device__ static void unpack(u32x4 r, P* o) {
@@ -105,6 +115,7 @@ struct F16 {
   using In = uint16_t;  // fp16 bit pattern
   using P = _Float16;
   using Out = uint16_t;
+  using W = float;
   static constexpr int L = 8;
   __device__ static P bits(uint16_t b) {
     P h;
@@ -133,6 +144,12 @@ struct FaArgs {
   typename E::P w[KC];
 };
 
+// numel == 1 element indices patched inside the bucket launch
+struct PwArgs {
+  uint64_t idx[FEDAGG_FUSED_PAIRWISE];
+  int n;
+};
+
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const void* p) {
   if constexpr (NT)
@@ -141,8 +158,16 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
     return *reinterpret_cast<const u32x4*>(p);
 }
 
-// out[v*L .. v*L+L) for one 16-byte vector of Out elements of width L.
-template <typename E>
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else
+    *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// out[v*L .. v*L+L) for one 16-byte input vector (L Out elements: 16 or 32 bytes).
+template <typename E, bool NTS>
 __device__ __forceinline__ void store_vec(typename E::Out* out, uint64_t v, const typename E::P* acc) {
   typename E::Out o[E::L];
 #pragma unroll
@@ -150,9 +175,8 @@ __device__ __forceinline__ void store_vec(typename E::Out* out, uint64_t v, cons
   constexpr int bytes = E::L * sizeof(typename E::Out);
   static_assert(bytes % 16 == 0, "output vector must be whole 16-byte stores");
   const u32x4* src = reinterpret_cast<const u32x4*>(o);
-  u32x4* dst = reinterpret_cast<u32x4*>(out + v * E::L);
 #pragma unroll
-  for (int s = 0; s < bytes / 16; ++s) dst[s] = src[s];
+  for (int s = 0; s < bytes / 16; ++s) st16<NTS>(reinterpret_cast<u32x4*>(out + v * E::L) + s, src[s]);
 }
 
 template <typename E>
@@ -168,55 +192,187 @@ __device__ __forceinline__ void load_vec(const typename E::Out* out, uint64_t v,
 }
 
 // ------------------------------------------------------------------------------------
+// NumPy pairwise summation (loops_utils.h.src pairwise_sum, PW_BLOCKSIZE 128), on a
+// generator get(i) of the n terms.  n <= 128: one leaf.
+// ------------------------------------------------------------------------------------
+template <typename T, typename G>
+__device__ __forceinline__ T pw_leaf(const G& get, int64_t lo, int64_t n) {
+#pragma clang fp contract(off)
+  if (n < 8) {
+    T res = T(-0.0);
+    for (int64_t i = 0; i < n; ++i) res = res + get(lo + i);
+    return res;
+  }
+  T r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = get(lo + j);
+  int64_t i = 8;
+  for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + get(lo + i + j);
+  }
+  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res = res + get(lo + i);
+  return res;
+}
+
+// Iterative form of the recursive split (n > 128: split at n/2 rounded down to a multiple of 8).
+template <typename T, typename G>
+__device__ T pw_sum(const G& get, int64_t n) {
+#pragma clang fp contract(off)
+  if (n <= 128) return pw_leaf<T>(get, 0, n);
+  int64_t lo[64], nn[64];
+  T left[64];
+  int stage[64];
+  int sp = 0;
+  lo[0] = 0;
+  nn[0] = n;
+  stage[0] = 0;
+  T ret = T(0);
+  for (;;) {
+    while (nn[sp] > 128) {  // descend into left halves
+      int64_t n2 = nn[sp] / 2;
+      n2 -= n2 % 8;
+      stage[sp] = 1;
+      lo[sp + 1] = lo[sp];
+      nn[sp + 1] = n2;
+      stage[sp + 1] = 0;
+      ++sp;
+    }
+    ret = pw_leaf<T>(get, lo[sp], nn[sp]);
+    bool done = true;
+    while (sp > 0) {  // ascend: left done -> start right; right done -> combine
+      --sp;
+      if (stage[sp] == 1) {
+        left[sp] = ret;
+        stage[sp] = 2;
+        int64_t n2 = nn[sp] / 2;
+        n2 -= n2 % 8;
+        lo[sp + 1] = lo[sp] + n2;
+        nn[sp + 1] = nn[sp] - n2;
+        stage[sp + 1] = 0;
+        ++sp;
+        done = false;
+        break;
+      }
+      ret = left[sp] + ret;
+    }
+    if (done) return ret;
+  }
+}
+
+// Fused numel==1 patch: +0.0 + pairwise over the K products of element e.
+template <typename E, int KC>
+__device__ __forceinline__ typename E::P fedavg_pairwise_elem(const FaArgs<E, KC>& a, int K, uint64_t e) {
+#pragma clang fp contract(off)
+  using W = typename E::W;
+  auto get = [&](int64_t k) -> W { return (W)(E::cvt(a.x[k][e]) * a.w[k]); };
+  const W s = W(0.0f) + pw_leaf<W>(get, 0, K);
+  return (typename E::P)s;
+}
+
+// ------------------------------------------------------------------------------------
 // FedAvg bucket kernel (fed_avg.py:217-222)
 // ------------------------------------------------------------------------------------
-template <typename E, int KC, bool NT>
+template <typename E, int KC, bool NT, int N>
+__device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int K, const int first,
+                                               const uint64_t* v, typename E::P (*acc)[E::L],
+                                               const typename E::Out* out) {
+#pragma clang fp contract(off)
+  using P = typename E::P;
+  constexpr int L = E::L;
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    if (first) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) acc[n][j] = P(0.0f);  // NumPy seeds add.reduce with +0.0
+    } else {
+      load_vec<E>(out, v[n], acc[n]);
+    }
+  }
+  int k = 0;
+  for (; k + FA_UNROLL <= K; k += FA_UNROLL) {
+    u32x4 raw[N][FA_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FA_UNROLL; ++u)
+#pragma unroll
+      for (int n = 0; n < N; ++n) raw[n][u] = ld16<NT>(a.x[k + u] + v[n] * L);
+#pragma unroll
+    for (int u = 0; u < FA_UNROLL; ++u) {
+      const P w = a.w[k + u];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        P xs[L];
+        E::unpack(raw[n][u], xs);
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const P p = xs[j] * w;        // fl(x_k * w_k)
+          acc[n][j] = acc[n][j] + p;    // fl(acc + p), client order
+        }
+      }
+    }
+  }
+  for (; k < K; ++k) {
+    const P w = a.w[k];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      P xs[L];
+      E::unpack(ld16<NT>(a.x[k] + v[n] * L), xs);
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const P p = xs[j] * w;
+        acc[n][j] = acc[n][j] + p;
+      }
+    }
+  }
+}
+
+template <typename E, int KC>
+__device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwArgs& pw, const int K, uint64_t v,
+                                               typename E::P* acc) {
+  constexpr int L = E::L;
+  for (int p = 0; p < pw.n; ++p) {
+    const uint64_t e = pw.idx[p];
+    if (e / L == v) {
+      const typename E::P val = fedavg_pairwise_elem<E, KC>(a, K, e);
+      const int j = (int)(e % L);
+#pragma unroll
+      for (int jj = 0; jj < L; ++jj)
+        if (jj == j) acc[jj] = val;
+    }
+  }
+}
+
+template <typename E, int KC, bool NT, bool NTS, int VPT>
 __global__ void __launch_bounds__(FA_BLOCK)
-    fedavg_kernel(const FaArgs<E, KC> a, const int K, const int first, const uint64_t nvec, const uint64_t M,
-                  typename E::Out* __restrict__ out) {
+    fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
+                  const uint64_t M, typename E::Out* __restrict__ out) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
   const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
 
-  for (uint64_t v = gid; v < nvec; v += stride) {
-    P acc[L];
-    if (first) {
+  uint64_t v0 = gid;
+  if constexpr (VPT > 1) {
+    for (; v0 + (VPT - 1) * stride < nvec; v0 += VPT * stride) {
+      uint64_t v[VPT];
 #pragma unroll
-      for (int j = 0; j < L; ++j) acc[j] = P(0.0f);  // NumPy seeds add.reduce with +0.0
-    } else {
-      load_vec<E>(out, v, acc);
-    }
-    int k = 0;
-    for (; k + FA_UNROLL <= K; k += FA_UNROLL) {
-      u32x4 raw[FA_UNROLL];
+      for (int n = 0; n < VPT; ++n) v[n] = v0 + n * stride;
+      P acc[VPT][L];
+      fedavg_vectors<E, KC, NT, VPT>(a, K, first, v, acc, out);
 #pragma unroll
-      for (int u = 0; u < FA_UNROLL; ++u) raw[u] = ld16<NT>(a.x[k + u] + v * L);
-#pragma unroll
-      for (int u = 0; u < FA_UNROLL; ++u) {
-        P xs[L];
-        E::unpack(raw[u], xs);
-        const P w = a.w[k + u];
-#pragma unroll
-        for (int j = 0; j < L; ++j) {
-          const P p = xs[j] * w;  // fl(x_k * w_k)
-          acc[j] = acc[j] + p;    // fl(acc + p), client order
-        }
+      for (int n = 0; n < VPT; ++n) {
+        if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
+        store_vec<E, NTS>(out, v[n], acc[n]);
       }
     }
-    for (; k < K; ++k) {
-      const u32x4 raw = ld16<NT>(a.x[k] + v * L);
-      P xs[L];
-      E::unpack(raw, xs);
-      const P w = a.w[k];
-#pragma unroll
-      for (int j = 0; j < L; ++j) {
-        const P p = xs[j] * w;
-        acc[j] = acc[j] + p;
-      }
-    }
-    store_vec<E>(out, v, acc);
+  }
+  for (; v0 < nvec; v0 += stride) {
+    P acc[1][L];
+    fedavg_vectors<E, KC, NT, 1>(a, K, first, &v0, acc, out);
+    if (pw.n) patch_pairwise<E, KC>(a, pw, K, v0, acc[0]);
+    store_vec<E, NTS>(out, v0, acc[0]);
   }
 
   // Scalar remainder (M % L elements, or everything when a pointer is not 16-B aligned).
@@ -226,6 +382,8 @@ __global__ void __launch_bounds__(FA_BLOCK)
       const P p = E::cvt(a.x[k][i]) * a.w[k];
       acc = acc + p;
     }
+    for (int p = 0; p < pw.n; ++p)
+      if (pw.idx[p] == i) acc = fedavg_pairwise_elem<E, KC>(a, K, i);
     out[i] = E::out(acc);
   }
 }
@@ -251,9 +409,21 @@ __device__ __forceinline__ void unpack_d(u32x4 r, double* o) {
   }
 }
 
+// Fused numel==1 patch for Scaffold: delta = lr*(0 + pw_K(w*d)), c' = 0 + pw_{K+1}(w*cv, c)
+template <typename TIn, int KC>
+__device__ __forceinline__ void scaffold_pairwise_elem(const ScArgs<TIn, KC>& a, int K, const TIn* c, double lr,
+                                                    uint64_t e, double* dval, double* cval) {
+#pragma clang fp contract(off)
+  auto gd = [&](int64_t k) -> double { return a.w[k] * (double)a.d[k][e]; };
+  auto gc = [&](int64_t k) -> double { return k < K ? a.w[k] * (double)a.cv[k][e] : (double)c[e]; };
+  const double sd = 0.0 + pw_leaf<double>(gd, 0, K);
+  *dval = lr * sd;
+  *cval = 0.0 + pw_leaf<double>(gc, 0, K + 1);
+}
+
 template <typename TIn, int KC, bool NT>
 __global__ void __launch_bounds__(FA_BLOCK)
-    scaffold_kernel(const ScArgs<TIn, KC> a, const int K, const int first, const int last,
+    scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
                     double* __restrict__ dout, double* __restrict__ cout) {
 #pragma clang fp contract(off)
@@ -319,6 +489,20 @@ __global__ void __launch_bounds__(FA_BLOCK)
         ad[j] = lr * ad[j];      // aggregation_lr * sum (scaffold.py:293)
       }
     }
+    for (int p = 0; p < pw.n; ++p) {
+      const uint64_t e = pw.idx[p];
+      if (e / L == v) {
+        double dv, cvv;
+        scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, e, &dv, &cvv);
+        const int j = (int)(e % L);
+#pragma unroll
+        for (int jj = 0; jj < L; ++jj)
+          if (jj == j) {
+            ad[jj] = dv;
+            ac[jj] = cvv;
+          }
+      }
+    }
     f64x2* dd = reinterpret_cast<f64x2*>(dout + v * L);
     f64x2* cc = reinterpret_cast<f64x2*>(cout + v * L);
 #pragma unroll
@@ -342,30 +526,31 @@ __global__ void __launch_bounds__(FA_BLOCK)
       ac = ac + (double)c[i];
       ad = lr * ad;
     }
+    for (int p = 0; p < pw.n; ++p)
+      if (pw.idx[p] == i) scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, i, &ad, &ac);
     dout[i] = ad;
     cout[i] = ac;
   }
 }
 
 // ------------------------------------------------------------------------------------
-// NumPy pairwise summation for numel == 1 tensors
+// Separate numel==1 path (K > one chunk, or more indices than fit the kernel arguments)
 // ------------------------------------------------------------------------------------
 struct IdxArgs {
   uint64_t idx[FEDAGG_MAX_PAIRWISE];
 };
 
-// Stage 1: ws[p * stride + kbase + k] = fl(x_k[idx_p] * w_k), written in the
-// accumulation type of the pairwise sum (fp32 for fp16 inputs: HALF_pairwise_sum).
-template <typename E, int KC, typename TW>
+// Stage 1: ws[p * stride + kbase + k] = fl(x_k[idx_p] * w_k), in the pairwise-sum type W.
+template <typename E, int KC>
 __global__ void __launch_bounds__(FA_BLOCK)
     pairwise_gather_kernel(const FaArgs<E, KC> a, const int Kc, const int kbase, const IdxArgs ix, const int P,
-                           const int64_t stride, TW* __restrict__ ws) {
+                           const int64_t stride, typename E::W* __restrict__ ws) {
 #pragma clang fp contract(off)
   const int t = blockIdx.x * FA_BLOCK + threadIdx.x;
   if (t >= P * Kc) return;
   const int p = t / Kc, k = t % Kc;
   const typename E::P prod = E::cvt(a.x[k][ix.idx[p]]) * a.w[k];
-  ws[p * stride + kbase + k] = (TW)prod;
+  ws[p * stride + kbase + k] = (typename E::W)prod;
 }
 
 template <typename TIn, int KC>
@@ -381,102 +566,36 @@ __global__ void __launch_bounds__(FA_BLOCK)
   ws_c[p * (K + 1) + kbase + k] = a.w[k] * (double)a.cv[k][i];
 }
 
-template <typename T>
-__device__ T pw_leaf(const T* a, int64_t n) {
+// Stage 2: out[idx_p] = (+0.0 + pairwise(ws[p]))
+template <typename E>
+__global__ void pairwise_tree_kernel(const typename E::W* __restrict__ ws, const int64_t n, const IdxArgs ix,
+                                     const int P, typename E::Out* __restrict__ out) {
 #pragma clang fp contract(off)
-  if (n < 8) {
-    T res = T(-0.0);
-    for (int64_t i = 0; i < n; ++i) res = res + a[i];
-    return res;
-  }
-  T r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = a[j];
-  int64_t i = 8;
-  for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
-  }
-  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res = res + a[i];
-  return res;
-}
-
-// Iterative form of NumPy's recursive pairwise_sum (blocks of <= 128, split at n/2
-// rounded down to a multiple of 8).
-template <typename T>
-__device__ T pw_sum(const T* a, int64_t n) {
-#pragma clang fp contract(off)
-  int64_t lo[64], nn[64];
-  T left[64];
-  int stage[64];
-  int sp = 0;
-  lo[0] = 0;
-  nn[0] = n;
-  stage[0] = 0;
-  T ret = T(0);
-  for (;;) {
-    // descend
-    while (nn[sp] > 128) {
-      int64_t n2 = nn[sp] / 2;
-      n2 -= n2 % 8;
-      stage[sp] = 1;
-      lo[sp + 1] = lo[sp];
-      nn[sp + 1] = n2;
-      stage[sp + 1] = 0;
-      ++sp;
-    }
-    ret = pw_leaf(a + lo[sp], nn[sp]);
-    // ascend
-    bool done = true;
-    while (sp > 0) {
-      --sp;
-      if (stage[sp] == 1) {
-        left[sp] = ret;
-        stage[sp] = 2;
-        int64_t n2 = nn[sp] / 2;
-        n2 -= n2 % 8;
-        lo[sp + 1] = lo[sp] + n2;
-        nn[sp + 1] = nn[sp] - n2;
-        stage[sp + 1] = 0;
-        ++sp;
-        done = false;
-        break;
-      }
-      ret = left[sp] + ret;
-    }
-    if (done) return ret;
-  }
-}
-
-// Stage 2: out[idx_p] = (+0.0 + pairwise(ws[p])) (times lr for Scaffold's delta).
-template <typename TW, typename E>
-__global__ void pairwise_tree_kernel(const TW* __restrict__ ws, const int64_t n, const IdxArgs ix, const int P,
-                                     typename E::Out* __restrict__ out) {
-#pragma clang fp contract(off)
+  using W = typename E::W;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  const TW s = TW(0.0f) + pw_sum(ws + p * n, n);
+  const W* row = ws + p * n;
+  auto get = [&](int64_t i) -> W { return row[i]; };
+  const W s = W(0.0f) + pw_sum<W>(get, n);
   out[ix.idx[p]] = E::out((typename E::P)s);
 }
 
-__global__ void scaffold_tree_kernel(const double* __restrict__ ws_d, const double* __restrict__ ws_c,
+template <typename TIn>
+__global__ void scaffold_tree_kernel(const double* __restrict__ ws_d, double* __restrict__ ws_c, const TIn* c,
                                      const int64_t K, const IdxArgs ix, const int P, const double lr,
                                      double* __restrict__ dout, double* __restrict__ cout) {
 #pragma clang fp contract(off)
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  const double sd = 0.0 + pw_sum(ws_d + p * K, K);
-  const double sc = 0.0 + pw_sum(ws_c + p * (K + 1), K + 1);
+  const double* rd = ws_d + p * K;
+  double* rc = ws_c + p * (K + 1);
+  rc[K] = (double)c[ix.idx[p]];  // server c is the last term (scaffold.py:262)
+  auto gd = [&](int64_t i) -> double { return rd[i]; };
+  auto gc = [&](int64_t i) -> double { return rc[i]; };
+  const double sd = 0.0 + pw_sum<double>(gd, K);
+  const double sc = 0.0 + pw_sum<double>(gc, K + 1);
   dout[ix.idx[p]] = lr * sd;
   cout[ix.idx[p]] = sc;
-}
-
-__global__ void scaffold_c_tail_kernel(const float* c32, const double* c64, const IdxArgs ix, const int P,
-                                       const int64_t K, double* __restrict__ ws_c) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  ws_c[p * (K + 1) + K] = c32 ? (double)c32[ix.idx[p]] : c64[ix.idx[p]];
 }
 
 // ------------------------------------------------------------------------------------
@@ -500,26 +619,25 @@ __global__ void __launch_bounds__(FA_BLOCK)
       bad += !((v == r) || (v != v && r != r));
     }
   }
-  // wave reduction, then one atomic per wave
   for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(cnt, bad);
 }
 
 // ------------------------------------------------------------------------------------
-// read-stream probe
+// read-stream probe (same 16-B non-temporal load path as the bucket kernels)
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(FA_BLOCK) read_probe_kernel(const float* __restrict__ x, uint64_t nvec,
                                                               float* __restrict__ sink) {
   const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   for (uint64_t v = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x; v < nvec; v += stride) {
     u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(x) + v);
-    s.x += __uint_as_float(r.x);
-    s.y += __uint_as_float(r.y);
-    s.z += __uint_as_float(r.z);
-    s.w += __uint_as_float(r.w);
+    s0 += __uint_as_float(r.x);
+    s1 += __uint_as_float(r.y);
+    s2 += __uint_as_float(r.z);
+    s3 += __uint_as_float(r.w);
   }
-  float t = s.x + s.y + s.z + s.w;
+  float t = s0 + s1 + s2 + s3;
   for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
   if (threadIdx.x == 0) sink[blockIdx.x] = t;
 }
@@ -532,51 +650,41 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline unsigned grid_for(uint64_t work) {
   uint64_t g = (work + FA_BLOCK - 1) / FA_BLOCK;
   if (g < 1) g = 1;
-  if (g > (uint64_t)g_grid_cap) g = (uint64_t)g_grid_cap;
+  if (g_grid_cap > 0 && g > (uint64_t)g_grid_cap) g = (uint64_t)g_grid_cap;
   return (unsigned)g;
 }
 
-template <typename E>
-int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K, uint64_t M,
-                  typename E::Out* out, hipStream_t s) {
-  if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg: K must be > 0 (got %s%lld)", "", K);
-  if (!x || !w || !out) return fail(FEDAGG_EINVAL, "fedavg: NULL argument%s%lld", "", 0);
-  if (M == 0) return FEDAGG_OK;
-  bool vec = aligned16(out);
-  for (int k = 0; k < K && vec; ++k) {
-    if (!x[k]) return fail(FEDAGG_EINVAL, "fedavg: client pointer %s%lld is NULL", "", k);
-    vec = aligned16(x[k]);
-  }
-  const uint64_t nvec = vec ? M / E::L : 0;
-  const unsigned grid = grid_for(nvec ? nvec : M);
-  for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
-    const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
-    FaArgs<E, FEDAGG_KCHUNK> a;
-    memset(&a, 0, sizeof(a));
-    for (int k = 0; k < kc; ++k) {
-      if (!x[k0 + k]) return fail(FEDAGG_EINVAL, "fedavg: client pointer %s%lld is NULL", "", k0 + k);
-      a.x[k] = x[k0 + k];
-      a.w[k] = w[k0 + k];
-    }
-    if (g_nontemporal)
-      hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, true>), dim3(grid), dim3(FA_BLOCK), 0, s, a, kc,
-                         k0 == 0 ? 1 : 0, nvec, M, out);
-    else
-      hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, false>), dim3(grid), dim3(FA_BLOCK), 0, s, a, kc,
-                         k0 == 0 ? 1 : 0, nvec, M, out);
-    int rc = check_launch("fedavg_kernel");
-    if (rc) return rc;
-  }
-  return FEDAGG_OK;
+template <typename E, bool NT, bool NTS, int VPT>
+void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
+                           int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
+  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT>), dim3(grid), dim3(FA_BLOCK), 0, s, a, pw, kc,
+                     first, nvec, M, out);
 }
 
-template <typename E, typename TW>
+template <typename E>
+void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
+                   int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
+  const int sel = (g_nt_load ? 1 : 0) | (g_nt_store ? 2 : 0) | (g_vpt >= 2 ? 4 : 0);
+  switch (sel) {
+    case 0: launch_fedavg_variant<E, false, false, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    case 1: launch_fedavg_variant<E, true, false, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    case 2: launch_fedavg_variant<E, false, true, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    case 3: launch_fedavg_variant<E, true, true, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    case 4: launch_fedavg_variant<E, false, false, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    case 5: launch_fedavg_variant<E, true, false, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    case 6: launch_fedavg_variant<E, false, true, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
+    default: launch_fedavg_variant<E, true, true, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
+  }
+}
+
+template <typename E>
 int fedavg_pairwise_launch(const typename E::In* const* x, const typename E::P* w, int K, const uint64_t* idx, int P,
                            void* ws, typename E::Out* out, hipStream_t s) {
   if (P == 0) return FEDAGG_OK;
   if (K <= 0 || P < 0 || !x || !w || !idx || !ws || !out)
-    return fail(FEDAGG_EINVAL, "fedavg_pairwise: invalid argument%s%lld", "", 0);
-  TW* wsT = static_cast<TW*>(ws);
+    return fail(FEDAGG_EINVAL, "fedavg_pairwise: invalid argument (K=%lld)", K);
+  using W = typename E::W;
+  W* wsT = static_cast<W*>(ws);
   for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
     const int pc = (P - p0) < FEDAGG_MAX_PAIRWISE ? (P - p0) : FEDAGG_MAX_PAIRWISE;
     IdxArgs ix;
@@ -591,53 +699,55 @@ int fedavg_pairwise_launch(const typename E::In* const* x, const typename E::P* 
         a.w[k] = w[k0 + k];
       }
       const unsigned g = (unsigned)((pc * kc + FA_BLOCK - 1) / FA_BLOCK);
-      hipLaunchKernelGGL((pairwise_gather_kernel<E, FEDAGG_KCHUNK, TW>), dim3(g), dim3(FA_BLOCK), 0, s, a, kc, k0,
-                         ix, pc, (int64_t)K, wsT);
+      hipLaunchKernelGGL((pairwise_gather_kernel<E, FEDAGG_KCHUNK>), dim3(g), dim3(FA_BLOCK), 0, s, a, kc, k0, ix,
+                         pc, (int64_t)K, wsT);
       int rc = check_launch("pairwise_gather_kernel");
       if (rc) return rc;
     }
-    hipLaunchKernelGGL((pairwise_tree_kernel<TW, E>), dim3(1), dim3(64), 0, s, wsT, (int64_t)K, ix, pc, out);
+    hipLaunchKernelGGL((pairwise_tree_kernel<E>), dim3(1), dim3(64), 0, s, (const W*)wsT, (int64_t)K, ix, pc, out);
     int rc = check_launch("pairwise_tree_kernel");
     if (rc) return rc;
   }
   return FEDAGG_OK;
 }
 
-template <typename TIn>
-int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, const double* w, int K, uint64_t M,
-                    double lr, double* dout, double* cout, hipStream_t s) {
-  if (K <= 0) return fail(FEDAGG_EINVAL, "scaffold: K must be > 0 (got %s%lld)", "", K);
-  if (!d || !cv || !c || !w || !dout || !cout) return fail(FEDAGG_EINVAL, "scaffold: NULL argument%s%lld", "", 0);
+template <typename E>
+int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K, uint64_t M, const uint64_t* idx,
+                  int P, void* ws, typename E::Out* out, hipStream_t s) {
+  if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg: K must be > 0 (got %lld)", K);
+  if (!x || !w || !out) return fail(FEDAGG_EINVAL, "fedavg: NULL argument");
+  if (P < 0 || (P > 0 && !idx)) return fail(FEDAGG_EINVAL, "fedavg: bad pairwise index list (P=%lld)", P);
+  for (int p = 0; p < P; ++p)
+    if (idx[p] >= M) return fail(FEDAGG_EINVAL, "fedavg: pairwise index %lld out of range", (long long)idx[p]);
   if (M == 0) return FEDAGG_OK;
-  bool vec = aligned16(c) && aligned16(dout) && aligned16(cout);
-  for (int k = 0; k < K && vec; ++k) {
-    if (!d[k] || !cv[k]) return fail(FEDAGG_EINVAL, "scaffold: client pointer %s%lld is NULL", "", k);
-    vec = aligned16(d[k]) && aligned16(cv[k]);
+  bool vec = aligned16(out);
+  for (int k = 0; k < K; ++k) {
+    if (!x[k]) return fail(FEDAGG_EINVAL, "fedavg: client pointer %lld is NULL", k);
+    vec = vec && aligned16(x[k]);
   }
-  constexpr int L = 16 / sizeof(TIn);
-  const uint64_t nvec = vec ? M / L : 0;
+  const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK;
+  if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg: workspace needed for %lld pairwise segments", P);
+  const uint64_t nvec = vec ? M / E::L : 0;
   const unsigned grid = grid_for(nvec ? nvec : M);
-  for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
-    const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
-    ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a;
+  for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
+    const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
+    FaArgs<E, FEDAGG_KCHUNK> a;
     memset(&a, 0, sizeof(a));
     for (int k = 0; k < kc; ++k) {
-      if (!d[k0 + k] || !cv[k0 + k])
-        return fail(FEDAGG_EINVAL, "scaffold: client pointer %s%lld is NULL", "", k0 + k);
-      a.d[k] = d[k0 + k];
-      a.cv[k] = cv[k0 + k];
+      a.x[k] = x[k0 + k];
       a.w[k] = w[k0 + k];
     }
-    const int first = k0 == 0, last = (k0 + kc) == K;
-    if (g_nontemporal)
-      hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true>), dim3(grid), dim3(FA_BLOCK), 0, s, a,
-                         kc, first, last, c, lr, nvec, M, dout, cout);
-    else
-      hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, false>), dim3(grid), dim3(FA_BLOCK), 0, s,
-                         a, kc, first, last, c, lr, nvec, M, dout, cout);
-    int rc = check_launch("scaffold_kernel");
+    PwArgs pw;
+    memset(&pw, 0, sizeof(pw));
+    if (fuse) {
+      pw.n = P;
+      for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
+    }
+    launch_fedavg<E>(grid, s, a, pw, kc, k0 == 0 ? 1 : 0, nvec, M, out);
+    int rc = check_launch("fedavg_kernel");
     if (rc) return rc;
   }
+  if (P > 0 && !fuse) return fedavg_pairwise_launch<E>(x, w, K, idx, P, ws, out, s);
   return FEDAGG_OK;
 }
 
@@ -647,7 +757,7 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
                              hipStream_t s) {
   if (P == 0) return FEDAGG_OK;
   if (K <= 0 || P < 0 || !d || !cv || !c || !w || !idx || !ws || !dout || !cout)
-    return fail(FEDAGG_EINVAL, "scaffold_pairwise: invalid argument%s%lld", "", 0);
+    return fail(FEDAGG_EINVAL, "scaffold_pairwise: invalid argument (K=%lld)", K);
   double* ws_d = static_cast<double*>(ws);
   double* ws_c = ws_d + (size_t)FEDAGG_MAX_PAIRWISE * K;
   for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
@@ -670,20 +780,65 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
       int rc = check_launch("scaffold_gather_kernel");
       if (rc) return rc;
     }
-    const float* c32 = sizeof(TIn) == 4 ? reinterpret_cast<const float*>(c) : nullptr;
-    const double* c64 = sizeof(TIn) == 8 ? reinterpret_cast<const double*>(c) : nullptr;
-    hipLaunchKernelGGL(scaffold_c_tail_kernel, dim3(1), dim3(64), 0, s, c32, c64, ix, pc, (int64_t)K, ws_c);
-    hipLaunchKernelGGL(scaffold_tree_kernel, dim3(1), dim3(64), 0, s, ws_d, ws_c, (int64_t)K, ix, pc, lr, dout,
-                       cout);
+    hipLaunchKernelGGL((scaffold_tree_kernel<TIn>), dim3(1), dim3(64), 0, s, (const double*)ws_d, ws_c, c,
+                       (int64_t)K, ix, pc, lr, dout, cout);
     int rc = check_launch("scaffold_tree_kernel");
     if (rc) return rc;
   }
   return FEDAGG_OK;
 }
 
+template <typename TIn>
+int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, const double* w, int K, uint64_t M,
+                    const uint64_t* idx, int P, void* ws, double lr, double* dout, double* cout, hipStream_t s) {
+  if (K <= 0) return fail(FEDAGG_EINVAL, "scaffold: K must be > 0 (got %lld)", K);
+  if (!d || !cv || !c || !w || !dout || !cout) return fail(FEDAGG_EINVAL, "scaffold: NULL argument");
+  if (P < 0 || (P > 0 && !idx)) return fail(FEDAGG_EINVAL, "scaffold: bad pairwise index list (P=%lld)", P);
+  for (int p = 0; p < P; ++p)
+    if (idx[p] >= M) return fail(FEDAGG_EINVAL, "scaffold: pairwise index %lld out of range", (long long)idx[p]);
+  if (M == 0) return FEDAGG_OK;
+  bool vec = aligned16(c) && aligned16(dout) && aligned16(cout);
+  for (int k = 0; k < K; ++k) {
+    if (!d[k] || !cv[k]) return fail(FEDAGG_EINVAL, "scaffold: client pointer %lld is NULL", k);
+    vec = vec && aligned16(d[k]) && aligned16(cv[k]);
+  }
+  const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK_SCAFFOLD;
+  if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "scaffold: workspace needed for %lld pairwise segments", P);
+  constexpr int L = 16 / sizeof(TIn);
+  const uint64_t nvec = vec ? M / L : 0;
+  const unsigned grid = grid_for(nvec ? nvec : M);
+  for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
+    const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
+    ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a;
+    memset(&a, 0, sizeof(a));
+    for (int k = 0; k < kc; ++k) {
+      a.d[k] = d[k0 + k];
+      a.cv[k] = cv[k0 + k];
+      a.w[k] = w[k0 + k];
+    }
+    PwArgs pw;
+    memset(&pw, 0, sizeof(pw));
+    if (fuse) {
+      pw.n = P;
+      for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
+    }
+    const int first = k0 == 0, last = (k0 + kc) == K;
+    if (g_nt_load)
+      hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true>), dim3(grid), dim3(FA_BLOCK), 0, s, a,
+                         pw, kc, first, last, c, lr, nvec, M, dout, cout);
+    else
+      hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, false>), dim3(grid), dim3(FA_BLOCK), 0, s,
+                         a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+    int rc = check_launch("scaffold_kernel");
+    if (rc) return rc;
+  }
+  if (P > 0 && !fuse) return scaffold_pairwise_launch<TIn>(d, cv, c, w, K, idx, P, lr, ws, dout, cout, s);
+  return FEDAGG_OK;
+}
+
 template <typename T>
 int equal_launch(const T* const* x, int K, uint64_t M, unsigned long long* cnt, hipStream_t s) {
-  if (K <= 0 || !x || !cnt) return fail(FEDAGG_EINVAL, "equal_count: invalid argument%s%lld", "", 0);
+  if (K <= 0 || !x || !cnt) return fail(FEDAGG_EINVAL, "equal_count: invalid argument (K=%lld)", K);
   if (M == 0 || K == 1) return FEDAGG_OK;
   const unsigned grid = grid_for(M);
   for (int k0 = 1; k0 < K; k0 += FEDAGG_KCHUNK) {
@@ -699,6 +854,11 @@ int equal_launch(const T* const* x, int K, uint64_t M, unsigned long long* cnt, 
   return FEDAGG_OK;
 }
 
+template <typename T>
+const T* cptr(const void* p) {
+  return static_cast<const T*>(p);
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -709,87 +869,56 @@ extern "C" {
 int fedagg_abi_version(void) { return FEDAGG_ABI_VERSION; }
 const char* fedagg_last_error(void) { return g_err; }
 
-int fedagg_set_launch(int grid_cap, int nontemporal) {
-  if (grid_cap > 0) g_grid_cap = grid_cap;
-  if (nontemporal >= 0) g_nontemporal = nontemporal ? 1 : 0;
+int fedagg_tune(const char* key, long long value) {
+  if (!key) return fail(FEDAGG_EINVAL, "fedagg_tune: NULL key");
+  if (!strcmp(key, "grid_cap")) g_grid_cap = (int)value;
+  else if (!strcmp(key, "nt_load")) g_nt_load = value ? 1 : 0;
+  else if (!strcmp(key, "nt_store")) g_nt_store = value ? 1 : 0;
+  else if (!strcmp(key, "vpt")) g_vpt = value >= 2 ? 2 : 1;
+  else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
+  else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
-}
-
-int fedagg_fedavg_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, float* d_out,
-                      void* stream) {
-  return fedavg_launch<F32>(d_clients, h_w, K, M, d_out, (hipStream_t)stream);
-}
-int fedagg_fedavg_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, float* d_out,
-                       void* stream) {
-  return fedavg_launch<BF16>(d_clients, h_w, K, M, d_out, (hipStream_t)stream);
-}
-int fedagg_fedavg_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, double* d_out,
-                      void* stream) {
-  return fedavg_launch<F64>(d_clients, h_w, K, M, d_out, (hipStream_t)stream);
-}
-int fedagg_fedavg_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, uint64_t M, uint16_t* d_out,
-                      void* stream) {
-  if (!h_w) return fail(FEDAGG_EINVAL, "fedavg_f16: NULL weights%s%lld", "", 0);
-  _Float16 w[FEDAGG_KCHUNK];
-  // weights travel as fp16 bit patterns; reinterpret in chunks
-  if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg_f16: K must be > 0 (got %s%lld)", "", K);
-  // fedavg_launch reads w[k] for k < K; build a contiguous _Float16 copy
-  _Float16* wf = K <= FEDAGG_KCHUNK ? w : new _Float16[K];
-  memcpy(wf, h_w, sizeof(uint16_t) * (size_t)K);
-  int rc = fedavg_launch<F16>(d_clients, wf, K, M, d_out, (hipStream_t)stream);
-  if (wf != w) delete[] wf;
-  return rc;
 }
 
 size_t fedagg_pairwise_ws_bytes(int K, int P, int elem_bytes) {
   (void)P;
+  (void)elem_bytes;
   if (K <= 0) return 0;
-  // per launch chunk: up to FEDAGG_MAX_PAIRWISE segments x (K + 1) terms, two buckets
-  return (size_t)2 * FEDAGG_MAX_PAIRWISE * (size_t)(K + 1) * (size_t)(elem_bytes < 8 ? 8 : elem_bytes);
+  // per launch chunk: up to FEDAGG_MAX_PAIRWISE segments x (K + 1) terms, two buckets, 8-B terms
+  return (size_t)2 * FEDAGG_MAX_PAIRWISE * (size_t)(K + 1) * 8;
 }
 
-int fedagg_fedavg_pairwise_f32(const float* const* d_clients, const float* h_w, int K, const uint64_t* h_idx, int P,
-                               void* d_ws, float* d_out, void* stream) {
-  return fedavg_pairwise_launch<F32, float>(d_clients, h_w, K, h_idx, P, d_ws, d_out, (hipStream_t)stream);
+int fedagg_fedavg_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, const uint64_t* h_idx,
+                      int P, void* d_ws, float* d_out, void* stream) {
+  return fedavg_launch<F32>(d_clients, h_w, K, M, h_idx, P, d_ws, d_out, (hipStream_t)stream);
 }
-int fedagg_fedavg_pairwise_bf16(const uint16_t* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,
-                                int P, void* d_ws, float* d_out, void* stream) {
-  return fedavg_pairwise_launch<BF16, float>(d_clients, h_w, K, h_idx, P, d_ws, d_out, (hipStream_t)stream);
+int fedagg_fedavg_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, const uint64_t* h_idx,
+                       int P, void* d_ws, float* d_out, void* stream) {
+  return fedavg_launch<BF16>(d_clients, h_w, K, M, h_idx, P, d_ws, d_out, (hipStream_t)stream);
 }
-int fedagg_fedavg_pairwise_f64(const double* const* d_clients, const double* h_w, int K, const uint64_t* h_idx, int P,
-                               void* d_ws, double* d_out, void* stream) {
-  return fedavg_pairwise_launch<F64, double>(d_clients, h_w, K, h_idx, P, d_ws, d_out, (hipStream_t)stream);
+int fedagg_fedavg_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, const uint64_t* h_idx,
+                      int P, void* d_ws, double* d_out, void* stream) {
+  return fedavg_launch<F64>(d_clients, h_w, K, M, h_idx, P, d_ws, d_out, (hipStream_t)stream);
 }
-int fedagg_fedavg_pairwise_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, const uint64_t* h_idx,
-                               int P, void* d_ws, uint16_t* d_out, void* stream) {
-  if (K <= 0 || !h_w) return fail(FEDAGG_EINVAL, "fedavg_pairwise_f16: invalid argument%s%lld", "", 0);
-  _Float16* wf = new _Float16[K];
-  memcpy(wf, h_w, sizeof(uint16_t) * (size_t)K);
-  int rc = fedavg_pairwise_launch<F16, float>(d_clients, wf, K, h_idx, P, d_ws, d_out, (hipStream_t)stream);
-  delete[] wf;
-  return rc;
+int fedagg_fedavg_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, uint64_t M,
+                      const uint64_t* h_idx, int P, void* d_ws, uint16_t* d_out, void* stream) {
+  if (!h_w || K <= 0) return fail(FEDAGG_EINVAL, "fedavg_f16: invalid weights (K=%lld)", K);
+  // weights travel as fp16 bit patterns: same bytes as _Float16
+  return fedavg_launch<F16>(d_clients, reinterpret_cast<const _Float16*>(h_w), K, M, h_idx, P, d_ws, d_out,
+                            (hipStream_t)stream);
 }
 
 int fedagg_scaffold_f32(const float* const* d_delta, const float* const* d_cv, const float* d_c, const double* h_w,
-                        int K, uint64_t M, double lr, double* d_delta_out, double* d_c_out, void* stream) {
-  return scaffold_launch<float>(d_delta, d_cv, d_c, h_w, K, M, lr, d_delta_out, d_c_out, (hipStream_t)stream);
+                        int K, uint64_t M, const uint64_t* h_idx, int P, void* d_ws, double lr, double* d_delta_out,
+                        double* d_c_out, void* stream) {
+  return scaffold_launch<float>(d_delta, d_cv, d_c, h_w, K, M, h_idx, P, d_ws, lr, d_delta_out, d_c_out,
+                                (hipStream_t)stream);
 }
 int fedagg_scaffold_f64(const double* const* d_delta, const double* const* d_cv, const double* d_c,
-                        const double* h_w, int K, uint64_t M, double lr, double* d_delta_out, double* d_c_out,
-                        void* stream) {
-  return scaffold_launch<double>(d_delta, d_cv, d_c, h_w, K, M, lr, d_delta_out, d_c_out, (hipStream_t)stream);
-}
-int fedagg_scaffold_pairwise_f32(const float* const* d_delta, const float* const* d_cv, const float* d_c,
-                                 const double* h_w, int K, const uint64_t* h_idx, int P, double lr, void* d_ws,
-                                 double* d_delta_out, double* d_c_out, void* stream) {
-  return scaffold_pairwise_launch<float>(d_delta, d_cv, d_c, h_w, K, h_idx, P, lr, d_ws, d_delta_out, d_c_out,
-                                         (hipStream_t)stream);
-}
-int fedagg_scaffold_pairwise_f64(const double* const* d_delta, const double* const* d_cv, const double* d_c,
-                                 const double* h_w, int K, const uint64_t* h_idx, int P, double lr, void* d_ws,
-                                 double* d_delta_out, double* d_c_out, void* stream) {
-  return scaffold_pairwise_launch<double>(d_delta, d_cv, d_c, h_w, K, h_idx, P, lr, d_ws, d_delta_out, d_c_out,
-                                          (hipStream_t)stream);
+                        const double* h_w, int K, uint64_t M, const uint64_t* h_idx, int P, void* d_ws, double lr,
+                        double* d_delta_out, double* d_c_out, void* stream) {
+  return scaffold_launch<double>(d_delta, d_cv, d_c, h_w, K, M, h_idx, P, d_ws, lr, d_delta_out, d_c_out,
+                                 (hipStream_t)stream);
 }
 
 int fedagg_equal_count_f32(const float* const* d_copies, int K, uint64_t M, unsigned long long* d_mismatches,
@@ -802,8 +931,7 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
 }
 
 int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid, void* stream) {
-  if (!d_x || !d_sink || grid <= 0 || !aligned16(d_x))
-    return fail(FEDAGG_EINVAL, "read_probe: invalid argument%s%lld", "", 0);
+  if (!d_x || !d_sink || grid <= 0 || !aligned16(d_x)) return fail(FEDAGG_EINVAL, "read_probe: invalid argument");
   hipLaunchKernelGGL(read_probe_kernel, dim3(grid), dim3(FA_BLOCK), 0, (hipStream_t)stream, d_x, M / 4, d_sink);
   return check_launch("read_probe_kernel");
 }

@@ -130,27 +130,20 @@ class FedAvgPlan:
         self.P = int(idx.size)
         self._idx = (ctypes.c_uint64 * max(1, self.P))(*[int(v) for v in idx])
         self._ws = 0
-        if self.P:
-            if ws is None:
+        if self.P > _native.FEDAGG_FUSED_PAIRWISE or (self.P and self.K > _native.FEDAGG_KCHUNK):
+            if ws is None:  # the numel==1 patch cannot be fused into the bucket launch
                 torch = _torch()
                 nbytes = self.lib.fedagg_pairwise_ws_bytes(self.K, self.P, 8)
                 ws = torch.empty(nbytes, dtype=torch.uint8, device=out.device)
                 self._keep = (clients, out, ws)
             self._ws = int(ws.data_ptr())
         self._main = getattr(self.lib, f"fedagg_fedavg_{kind}")
-        self._pw = getattr(self.lib, f"fedagg_fedavg_pairwise_{kind}")
-
-    def launch_main(self, stream=None) -> None:
-        _native.check(self._main(self._ptrs, self._w, self.K, self.M, self._out, _stream_handle(stream)), "fedavg")
-
-    def launch_pairwise(self, stream=None) -> None:
-        if self.P:
-            rc = self._pw(self._ptrs, self._w, self.K, self._idx, self.P, self._ws, self._out, _stream_handle(stream))
-            _native.check(rc, "fedavg_pairwise")
 
     def launch(self, stream=None) -> None:
-        self.launch_main(stream)
-        self.launch_pairwise(stream)
+        """Enqueue the bucket reduction (numel==1 patch fused when possible) on ``stream``."""
+        rc = self._main(self._ptrs, self._w, self.K, self.M, self._idx, self.P, self._ws, self._out,
+                        _stream_handle(stream))
+        _native.check(rc, "fedavg")
 
     def bytes_alg(self) -> int:
         s_in = {"f32": 4, "bf16": 2, "f64": 8, "f16": 2}[self.kind]
@@ -184,7 +177,7 @@ class ScaffoldPlan:
         self.P = int(idx.size)
         self._idx = (ctypes.c_uint64 * max(1, self.P))(*[int(v) for v in idx])
         self._ws = 0
-        if self.P:
+        if self.P > _native.FEDAGG_FUSED_PAIRWISE or (self.P and self.K > _native.FEDAGG_KCHUNK_SCAFFOLD):
             if ws is None:
                 torch = _torch()
                 ws = torch.empty(self.lib.fedagg_pairwise_ws_bytes(self.K, self.P, 8), dtype=torch.uint8,
@@ -192,22 +185,11 @@ class ScaffoldPlan:
                 self._keep.append(ws)
             self._ws = int(ws.data_ptr())
         self._main = getattr(self.lib, f"fedagg_scaffold_{kind}")
-        self._pw = getattr(self.lib, f"fedagg_scaffold_pairwise_{kind}")
-
-    def launch_main(self, stream=None) -> None:
-        rc = self._main(self._dp, self._cp, self._c, self._w, self.K, self.M, self.lr, self._dout, self._cout,
-                        _stream_handle(stream))
-        _native.check(rc, "scaffold")
-
-    def launch_pairwise(self, stream=None) -> None:
-        if self.P:
-            rc = self._pw(self._dp, self._cp, self._c, self._w, self.K, self._idx, self.P, self.lr, self._ws,
-                          self._dout, self._cout, _stream_handle(stream))
-            _native.check(rc, "scaffold_pairwise")
 
     def launch(self, stream=None) -> None:
-        self.launch_main(stream)
-        self.launch_pairwise(stream)
+        rc = self._main(self._dp, self._cp, self._c, self._w, self.K, self.M, self._idx, self.P, self._ws, self.lr,
+                        self._dout, self._cout, _stream_handle(stream))
+        _native.check(rc, "scaffold")
 
     def bytes_alg(self) -> int:
         s_in = 4 if self.kind == "f32" else 8

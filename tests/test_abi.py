@@ -21,7 +21,7 @@ def declared_functions():
 def test_header_declares_the_abi():
     names = declared_functions()
     assert "fedagg_fedavg_f32" in names and "fedagg_scaffold_f32" in names
-    assert len(names) >= 18
+    assert len(names) >= 12
 
 
 def test_library_exports_every_declared_symbol():
@@ -34,13 +34,18 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_invalid_arguments():
     lib = _native.load()
-    assert lib.fedagg_abi_version() == 1
+    assert lib.fedagg_abi_version() == 2
     w = (ctypes.c_float * 1)(1.0)
     ptrs = _native.ptr_array([0])
-    assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, None) == -1  # K == 0
+    assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, 0, None, None, None) == -1  # K == 0
     assert b"K must be > 0" in lib.fedagg_last_error()
-    assert lib.fedagg_fedavg_f32(ptrs, w, 1, 16, None, None) == -1  # NULL out
+    assert lib.fedagg_fedavg_f32(ptrs, w, 1, 16, None, 0, None, None, None) == -1  # NULL out
+    idx = (ctypes.c_uint64 * 1)(16)
+    assert lib.fedagg_fedavg_f32(ptrs, w, 1, 16, idx, 1, None, 64, None) == -1  # index out of range
+    assert b"out of range" in lib.fedagg_last_error()
     assert lib.fedagg_pairwise_ws_bytes(8, 3, 4) == 2 * 64 * 9 * 8
+    assert lib.fedagg_tune(b"no_such_knob", 1) == -1
+    assert lib.fedagg_tune(b"grid_cap", 4096) == 0
     with pytest.raises(_native.NativeLibraryError):
         _native.check(-1, "x")
 

@@ -364,3 +364,52 @@ class _PicklableAlgo:
         self.args, self.kwargs = args, kwargs
 
     strategies = ["Federated Averaging", "Scaffold"]
+
+
+@pytest.mark.parametrize("fuse", [1, 0])
+def test_many_numel1_layers_fused_and_separate(torch_gpu, dummy_algo_class, fuse):
+    """P > FEDAGG_FUSED_PAIRWISE numel==1 tensors, and the fused path switched off."""
+    from substrafl_amd import _native
+    from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState
+    from substrafl_amd.strategies import FedAvg, Scaffold
+
+    rng = np.random.default_rng(31)
+    shapes = [(1,)] * 9 + [(3, 4)] + [(1, 1)] * 12 + [(5,)]
+    K = 12
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    _native.tune(fuse_pairwise=fuse)
+    try:
+        got = FedAvg(algo=dummy_algo_class()).avg_shared_states(
+            [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)], _skip=True)
+        _assert_same(got.avg_parameters_update, fedavg_reference_structure(pus, ns))
+        res = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.3).avg_shared_states(
+            [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                 server_control_variate=c) for k in range(K)], _skip=True)
+        rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.3)
+        _assert_same(res.server_control_variate, rc)
+        _assert_same(res.avg_parameters_update, ra)
+    finally:
+        _native.tune(fuse_pairwise=1)
+
+
+@pytest.mark.parametrize("knobs", [dict(vpt=2), dict(nt_load=0), dict(nt_store=1), dict(grid_cap=7)])
+def test_launch_variants_bit_identical(torch_gpu, knobs):
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 9, 1_000_003
+    x = torch.randn((K, M + 5), device="cuda")
+    ns = list(range(3, 3 + K))
+    outs = []
+    for kn in (dict(vpt=1, nt_load=1, nt_store=0, grid_cap=4096), knobs):
+        _native.tune(**kn)
+        out = torch.empty(M + 5, device="cuda")
+        FedAvgPlan("f32", x, fedavg_weights(ns, "f32"), M, out, [0, 17, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append(out[:M].clone())
+    _native.tune(vpt=1, nt_load=1, nt_store=0, grid_cap=4096)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Launch-shape sweep of the FedAvg bucket kernel on one MI355X (interleaved rounds in ONE
+process, cdna_hip_programming.md §5.4 rule 24).  Prints one JSON line per variant with the
+median / min kernel time and GB/s of algorithmic bytes."""
+
+import argparse
+import itertools
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=8)
+    ap.add_argument("--M", type=int, default=25_000_000)
+    ap.add_argument("--kind", default="f32")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+
+    import torch
+
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+
+    shapes = synthetic_state_dict_shapes(args.M)
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    dt = torch.bfloat16 if args.kind == "bf16" else torch.float32
+    x = torch.randn((args.K, lay.ld), device="cuda").to(dt)
+    out = torch.empty(lay.ld, device="cuda")
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
+    plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
+    nbytes = plan.bytes_alg()
+
+    variants = [dict(grid_cap=g, vpt=v, nt_load=nl, nt_store=ns_)
+                for g, v, nl, ns_ in itertools.product([1024, 2048, 4096, 8192, 16384, 0], [1, 2], [1, 0], [0, 1])]
+    times = {i: [] for i in range(len(variants))}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for r in range(args.rounds):
+        for i, kn in enumerate(variants):
+            _native.tune(**kn)
+            for _ in range(3):
+                plan.launch()
+            ev[0].record()
+            for _ in range(args.iters):
+                plan.launch()
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[i].append(ev[0].elapsed_time(ev[1]) / args.iters)
+    res = []
+    for i, kn in enumerate(variants):
+        t = np.array(times[i])
+        res.append(dict(kn, kind=args.kind, K=args.K, M=args.M, median_us=round(float(np.median(t)) * 1e3, 2),
+                        min_us=round(float(t.min()) * 1e3, 2), GBps=round(nbytes / (np.median(t) / 1e3) / 1e9, 1)))
+    for r in sorted(res, key=lambda d: d["median_us"]):
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
