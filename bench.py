@@ -171,16 +171,17 @@ def main():
     # ---- read-stream ceiling on the same box (same 16-B nt load path) ----
     probe_n = min(clients.numel() if wl["strategy"] == "fedavg" else delta.numel(), 2_000_000_000)
     src = clients if wl["strategy"] == "fedavg" else delta
-    sink = torch.empty(4096, dtype=torch.float32, device=device)
     nbytes_probe = probe_n * src.element_size()
     floats = nbytes_probe // 4 // 4 * 4
+    pgrid = int(min(floats // 4 // 256, 1 << 20))  # one 16-B vector per thread, like the bucket kernel
+    sink = torch.empty(pgrid, dtype=torch.float32, device=device)
     for _ in range(3):
-        _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), 4096,
+        _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
                                                 stream.cuda_stream), "probe")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(10):
-        lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), 4096, stream.cuda_stream)
+        lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid, stream.cuda_stream)
     e1.record(stream)
     torch.cuda.synchronize(device)
     read_ceiling = floats * 4 / (e0.elapsed_time(e1) / 10 / 1e3) / 1e9

@@ -28,6 +28,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 
 #include "fedagg.h"
 
@@ -53,11 +54,15 @@ int check_launch(const char* what) {
 }
 
 // Launch shape (fedagg_tune); defaults are the values measured best on MI355X.
-int g_grid_cap = 4096;  // workgroups per launch before grid-striding
+int g_grid_cap = 0;     // workgroups per launch before grid-striding (0: one vector per thread)
 int g_nt_load = 1;      // client streams are read once: non-temporal loads
-int g_nt_store = 0;     // non-temporal output stores
-int g_vpt = 1;          // 16-byte vectors per thread per grid-stride step
+int g_nt_store = -1;    // non-temporal output stores (-1: auto, on from NT_STORE_MIN_K clients)
+int g_vpt = 1;          // 16-byte vectors per thread per step
+int g_unroll = 8;       // clients per load group (fp32 experiments: 4 / 8 / 16)
+int g_pipe = 0;         // software-pipelined client groups (fp32 experiment)
+int g_tile = 0;         // contiguous per-workgroup tiles when vpt > 1 (fp32 experiment)
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
+constexpr int NT_STORE_MIN_K = 16;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -274,7 +279,41 @@ __device__ __forceinline__ typename E::P fedavg_pairwise_elem(const FaArgs<E, KC
 // ------------------------------------------------------------------------------------
 // FedAvg bucket kernel (fed_avg.py:217-222)
 // ------------------------------------------------------------------------------------
-template <typename E, int KC, bool NT, int N>
+// One group of U clients for N vectors: products and in-order adds.
+template <typename E, int N, int U>
+__device__ __forceinline__ void fedavg_accumulate(const u32x4 (&raw)[N][U], const typename E::P* w,
+                                                  typename E::P (*acc)[E::L]) {
+#pragma clang fp contract(off)
+  using P = typename E::P;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const P wu = w[u];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      P xs[E::L];
+      E::unpack(raw[n][u], xs);
+#pragma unroll
+      for (int j = 0; j < E::L; ++j) {
+        const P p = xs[j] * wu;       // fl(x_k * w_k)
+        acc[n][j] = acc[n][j] + p;    // fl(acc + p), client order
+      }
+    }
+  }
+}
+
+template <typename E, int KC, bool NT, int N, int U>
+__device__ __forceinline__ void fedavg_load_group(const FaArgs<E, KC>& a, int k, const uint64_t* v,
+                                                  u32x4 (&raw)[N][U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int n = 0; n < N; ++n) raw[n][u] = ld16<NT>(a.x[k + u] + v[n] * E::L);
+}
+
+// acc[n][:] = sum over the K clients (in order) for the N 16-byte vectors v[n].
+// PIPE: the loads of client group g+1 are issued before the adds of group g (two register
+// buffers), so a wave keeps 2*U*N loads in flight across the add chain.
+template <typename E, int KC, bool NT, int N, int U, bool PIPE>
 __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int K, const int first,
                                                const uint64_t* v, typename E::P (*acc)[E::L],
                                                const typename E::Out* out) {
@@ -291,25 +330,28 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
     }
   }
   int k = 0;
-  for (; k + FA_UNROLL <= K; k += FA_UNROLL) {
-    u32x4 raw[N][FA_UNROLL];
-#pragma unroll
-    for (int u = 0; u < FA_UNROLL; ++u)
-#pragma unroll
-      for (int n = 0; n < N; ++n) raw[n][u] = ld16<NT>(a.x[k + u] + v[n] * L);
-#pragma unroll
-    for (int u = 0; u < FA_UNROLL; ++u) {
-      const P w = a.w[k + u];
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        P xs[L];
-        E::unpack(raw[n][u], xs);
-#pragma unroll
-        for (int j = 0; j < L; ++j) {
-          const P p = xs[j] * w;        // fl(x_k * w_k)
-          acc[n][j] = acc[n][j] + p;    // fl(acc + p), client order
-        }
+  if constexpr (PIPE) {
+    if (K >= U) {
+      u32x4 ra[N][U], rb[N][U];
+      fedavg_load_group<E, KC, NT, N, U>(a, 0, v, ra);
+      for (;;) {
+        const bool mb = k + 2 * U <= K;
+        if (mb) fedavg_load_group<E, KC, NT, N, U>(a, k + U, v, rb);
+        fedavg_accumulate<E, N, U>(ra, a.w + k, acc);
+        k += U;
+        if (!mb) break;
+        const bool ma = k + 2 * U <= K;
+        if (ma) fedavg_load_group<E, KC, NT, N, U>(a, k + U, v, ra);
+        fedavg_accumulate<E, N, U>(rb, a.w + k, acc);
+        k += U;
+        if (!ma) break;
       }
+    }
+  } else {
+    for (; k + U <= K; k += U) {
+      u32x4 raw[N][U];
+      fedavg_load_group<E, KC, NT, N, U>(a, k, v, raw);
+      fedavg_accumulate<E, N, U>(raw, a.w + k, acc);
     }
   }
   for (; k < K; ++k) {
@@ -343,7 +385,11 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
   }
 }
 
-template <typename E, int KC, bool NT, bool NTS, int VPT>
+// Variant knobs (fedagg_tune): NT/NTS non-temporal loads/stores; VPT vectors per thread per
+// step; U clients per load group; PIPE software-pipelined client groups; TILE: a workgroup owns
+// VPT*256 CONTIGUOUS vectors per step (a wave reads VPT KiB contiguous per client) instead of
+// VPT grid-strided vectors.
+template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
 __global__ void __launch_bounds__(FA_BLOCK)
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
                   const uint64_t M, typename E::Out* __restrict__ out) {
@@ -353,26 +399,51 @@ __global__ void __launch_bounds__(FA_BLOCK)
   const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
 
-  uint64_t v0 = gid;
-  if constexpr (VPT > 1) {
-    for (; v0 + (VPT - 1) * stride < nvec; v0 += VPT * stride) {
-      uint64_t v[VPT];
+  if constexpr (TILE) {
+    const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+    for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+      if (base + (VPT - 1) * FA_BLOCK < nvec) {
+        uint64_t v[VPT];
 #pragma unroll
-      for (int n = 0; n < VPT; ++n) v[n] = v0 + n * stride;
-      P acc[VPT][L];
-      fedavg_vectors<E, KC, NT, VPT>(a, K, first, v, acc, out);
+        for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+        P acc[VPT][L];
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, acc, out);
 #pragma unroll
-      for (int n = 0; n < VPT; ++n) {
-        if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
-        store_vec<E, NTS>(out, v[n], acc[n]);
+        for (int n = 0; n < VPT; ++n) {
+          if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
+          store_vec<E, NTS>(out, v[n], acc[n]);
+        }
+      } else {
+        for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK) {
+          P acc[1][L];
+          fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
+          if (pw.n) patch_pairwise<E, KC>(a, pw, K, v0, acc[0]);
+          store_vec<E, NTS>(out, v0, acc[0]);
+        }
       }
     }
-  }
-  for (; v0 < nvec; v0 += stride) {
-    P acc[1][L];
-    fedavg_vectors<E, KC, NT, 1>(a, K, first, &v0, acc, out);
-    if (pw.n) patch_pairwise<E, KC>(a, pw, K, v0, acc[0]);
-    store_vec<E, NTS>(out, v0, acc[0]);
+  } else {
+    uint64_t v0 = gid;
+    if constexpr (VPT > 1) {
+      for (; v0 + (VPT - 1) * stride < nvec; v0 += VPT * stride) {
+        uint64_t v[VPT];
+#pragma unroll
+        for (int n = 0; n < VPT; ++n) v[n] = v0 + n * stride;
+        P acc[VPT][L];
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, acc, out);
+#pragma unroll
+        for (int n = 0; n < VPT; ++n) {
+          if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
+          store_vec<E, NTS>(out, v[n], acc[n]);
+        }
+      }
+    }
+    for (; v0 < nvec; v0 += stride) {
+      P acc[1][L];
+      fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
+      if (pw.n) patch_pairwise<E, KC>(a, pw, K, v0, acc[0]);
+      store_vec<E, NTS>(out, v0, acc[0]);
+    }
   }
 
   // Scalar remainder (M % L elements, or everything when a pointer is not 16-B aligned).
@@ -654,27 +725,51 @@ inline unsigned grid_for(uint64_t work) {
   return (unsigned)g;
 }
 
-template <typename E, bool NT, bool NTS, int VPT>
+template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
-  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT>), dim3(grid), dim3(FA_BLOCK), 0, s, a, pw, kc,
-                     first, nvec, M, out);
+  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE>), dim3(grid), dim3(FA_BLOCK), 0,
+                     s, a, pw, kc, first, nvec, M, out);
 }
 
+// Production variants: every element type gets NT x NTS at the default shape.  The shape
+// experiments (vpt / unroll / pipe / tile) are instantiated for fp32 only.
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
-                   int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
-  const int sel = (g_nt_load ? 1 : 0) | (g_nt_store ? 2 : 0) | (g_vpt >= 2 ? 4 : 0);
-  switch (sel) {
-    case 0: launch_fedavg_variant<E, false, false, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    case 1: launch_fedavg_variant<E, true, false, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    case 2: launch_fedavg_variant<E, false, true, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    case 3: launch_fedavg_variant<E, true, true, 1>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    case 4: launch_fedavg_variant<E, false, false, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    case 5: launch_fedavg_variant<E, true, false, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    case 6: launch_fedavg_variant<E, false, true, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
-    default: launch_fedavg_variant<E, true, true, 2>(grid, s, a, pw, kc, first, nvec, M, out); break;
+                   int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts) {
+#define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
+  const bool ntl = g_nt_load != 0;
+  if constexpr (std::is_same<E, F32>::value) {
+    if (g_vpt == 2 && g_tile) {
+      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 2, 8, false, true>(FA_ARGS);
+      if (ntl && nts) return launch_fedavg_variant<E, true, true, 2, 8, false, true>(FA_ARGS);
+    }
+    if (g_vpt == 4 && g_tile) {
+      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 4, 8, false, true>(FA_ARGS);
+      if (ntl && nts) return launch_fedavg_variant<E, true, true, 4, 8, false, true>(FA_ARGS);
+    }
+    if (g_vpt == 2 && !g_tile) {
+      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 2, 8, false, false>(FA_ARGS);
+      if (ntl && nts) return launch_fedavg_variant<E, true, true, 2, 8, false, false>(FA_ARGS);
+    }
+    if (g_pipe) {
+      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, 8, true, false>(FA_ARGS);
+      if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, 8, true, false>(FA_ARGS);
+    }
+    if (g_unroll == 16) {
+      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, 16, false, false>(FA_ARGS);
+      if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, 16, false, false>(FA_ARGS);
+    }
+    if (g_unroll == 4) {
+      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, 4, false, false>(FA_ARGS);
+      if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, 4, false, false>(FA_ARGS);
+    }
   }
+  if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, FA_UNROLL, false, false>(FA_ARGS);
+  if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, FA_UNROLL, false, false>(FA_ARGS);
+  if (!ntl && !nts) return launch_fedavg_variant<E, false, false, 1, FA_UNROLL, false, false>(FA_ARGS);
+  return launch_fedavg_variant<E, false, true, 1, FA_UNROLL, false, false>(FA_ARGS);
+#undef FA_ARGS
 }
 
 template <typename E>
@@ -743,7 +838,8 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
       pw.n = P;
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
-    launch_fedavg<E>(grid, s, a, pw, kc, k0 == 0 ? 1 : 0, nvec, M, out);
+    const bool nts = g_nt_store < 0 ? K >= NT_STORE_MIN_K : g_nt_store != 0;
+    launch_fedavg<E>(grid, s, a, pw, kc, k0 == 0 ? 1 : 0, nvec, M, out, nts);
     int rc = check_launch("fedavg_kernel");
     if (rc) return rc;
   }
@@ -873,8 +969,11 @@ int fedagg_tune(const char* key, long long value) {
   if (!key) return fail(FEDAGG_EINVAL, "fedagg_tune: NULL key");
   if (!strcmp(key, "grid_cap")) g_grid_cap = (int)value;
   else if (!strcmp(key, "nt_load")) g_nt_load = value ? 1 : 0;
-  else if (!strcmp(key, "nt_store")) g_nt_store = value ? 1 : 0;
-  else if (!strcmp(key, "vpt")) g_vpt = value >= 2 ? 2 : 1;
+  else if (!strcmp(key, "nt_store")) g_nt_store = value < 0 ? -1 : (value ? 1 : 0);
+  else if (!strcmp(key, "vpt")) g_vpt = value >= 4 ? 4 : (value >= 2 ? 2 : 1);
+  else if (!strcmp(key, "unroll")) g_unroll = value >= 16 ? 16 : (value <= 4 ? 4 : 8);
+  else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
+  else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;

@@ -395,21 +395,24 @@ def test_many_numel1_layers_fused_and_separate(torch_gpu, dummy_algo_class, fuse
         _native.tune(fuse_pairwise=1)
 
 
-@pytest.mark.parametrize("knobs", [dict(vpt=2), dict(nt_load=0), dict(nt_store=1), dict(grid_cap=7)])
+@pytest.mark.parametrize("knobs", [dict(vpt=2), dict(nt_load=0), dict(nt_store=1), dict(grid_cap=7),
+                                   dict(unroll=4), dict(unroll=16), dict(pipe=1), dict(vpt=2, tile=1),
+                                   dict(vpt=4, tile=1, grid_cap=5)])
 def test_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
     from substrafl_amd.engine import FedAvgPlan, fedavg_weights
 
-    K, M = 9, 1_000_003
+    K, M = 19, 1_000_003
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    for kn in (dict(vpt=1, nt_load=1, nt_store=0, grid_cap=4096), knobs):
+    default = dict(vpt=1, nt_load=1, nt_store=-1, grid_cap=0, unroll=8, pipe=0, tile=0)
+    for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
         FedAvgPlan("f32", x, fedavg_weights(ns, "f32"), M, out, [0, 17, M - 1]).launch()
         torch.cuda.synchronize()
         outs.append(out[:M].clone())
-    _native.tune(vpt=1, nt_load=1, nt_store=0, grid_cap=4096)
+    _native.tune(**default)
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))

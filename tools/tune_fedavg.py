@@ -4,7 +4,6 @@ process, cdna_hip_programming.md §5.4 rule 24).  Prints one JSON line per varia
 median / min kernel time and GB/s of algorithmic bytes."""
 
 import argparse
-import itertools
 import json
 import sys
 from pathlib import Path
@@ -38,8 +37,10 @@ def main():
     plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
 
-    variants = [dict(grid_cap=g, vpt=v, nt_load=nl, nt_store=ns_)
-                for g, v, nl, ns_ in itertools.product([1024, 2048, 4096, 8192, 16384, 0], [1, 2], [1, 0], [0, 1])]
+    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0)
+    shapes = [dict(), dict(unroll=4), dict(unroll=16), dict(pipe=1), dict(vpt=2), dict(vpt=2, tile=1),
+              dict(vpt=4, tile=1), dict(grid_cap=16384), dict(grid_cap=8192, vpt=2, tile=1)]
+    variants = [dict(base, **sh, nt_store=nts) for sh in shapes for nts in (0, 1)]
     times = {i: [] for i in range(len(variants))}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for r in range(args.rounds):
@@ -53,6 +54,21 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[i].append(ev[0].elapsed_time(ev[1]) / args.iters)
+    # read-stream probe ceiling at several grid sizes (same process, same buffer)
+    sink = torch.empty(1 << 20, device="cuda")
+    nfl = x.numel() * x.element_size() // 4 // 4 * 4
+    for g in (4096, 16384, 65536, int(min(nfl // 4 // 256, 1 << 20))):
+        tt = []
+        for _ in range(args.rounds):
+            ev[0].record()
+            for _ in range(args.iters):
+                _native.check(_native.load().fedagg_read_probe_f32(x.data_ptr(), nfl, sink.data_ptr(), g,
+                                                                   torch.cuda.current_stream().cuda_stream), "probe")
+            ev[1].record()
+            torch.cuda.synchronize()
+            tt.append(ev[0].elapsed_time(ev[1]) / args.iters)
+        print(json.dumps(dict(probe_grid=g, bytes=nfl * 4, median_us=round(float(np.median(tt)) * 1e3, 2),
+                              GBps=round(nfl * 4 / (np.median(tt) / 1e3) / 1e9, 1))))
     res = []
     for i, kn in enumerate(variants):
         t = np.array(times[i])
