@@ -54,13 +54,13 @@ int check_launch(const char* what) {
 }
 
 // Launch shape (fedagg_tune); defaults are the values measured best on MI355X.
-int g_grid_cap = 0;     // workgroups per launch before grid-striding (0: one vector per thread)
+int g_grid_cap = 0;     // workgroups per launch before grid-striding (0: one step per workgroup)
 int g_nt_load = 1;      // client streams are read once: non-temporal loads
-int g_nt_store = -1;    // non-temporal output stores (-1: auto, on from NT_STORE_MIN_K clients)
-int g_vpt = 1;          // 16-byte vectors per thread per step
-int g_unroll = 8;       // clients per load group (fp32 experiments: 4 / 8 / 16)
-int g_pipe = 0;         // software-pipelined client groups (fp32 experiment)
-int g_tile = 0;         // contiguous per-workgroup tiles when vpt > 1 (fp32 experiment)
+int g_nt_store = 1;     // non-temporal output stores (-1: auto, on from NT_STORE_MIN_K clients)
+int g_vpt = 4;          // 16-byte vectors per thread per step
+int g_unroll = 8;       // clients per load group
+int g_pipe = 0;         // software-pipelined client groups
+int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -732,44 +732,41 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
                      s, a, pw, kc, first, nvec, M, out);
 }
 
-// Production variants: every element type gets NT x NTS at the default shape.  The shape
-// experiments (vpt / unroll / pipe / tile) are instantiated for fp32 only.
+// Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
+// type: contiguous tiles of VPT*256 vectors per workgroup step with U-client load groups, the
+// grid-strided single-vector shape, and the pipelined variant; each with plain or
+// non-temporal output stores.  Client loads are non-temporal unless nt_load = 0 (one shape).
+template <typename E, bool NTS>
+void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
+                         int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
+#define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
+  if (!g_nt_load) return launch_fedavg_variant<E, false, NTS, 1, 8, false, false>(FA_ARGS);
+  if (g_tile) {
+    if (g_vpt >= 8) {
+      if (g_unroll <= 4) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true>(FA_ARGS);
+      return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
+    }
+    if (g_vpt >= 4) {
+      if (g_unroll <= 4) return launch_fedavg_variant<E, true, NTS, 4, 4, false, true>(FA_ARGS);
+      return launch_fedavg_variant<E, true, NTS, 4, 8, false, true>(FA_ARGS);
+    }
+    if (g_vpt >= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, true>(FA_ARGS);
+  }
+  if (g_pipe) return launch_fedavg_variant<E, true, NTS, 1, 8, true, false>(FA_ARGS);
+  if (g_vpt >= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, false>(FA_ARGS);
+  if (g_unroll >= 16) return launch_fedavg_variant<E, true, NTS, 1, 16, false, false>(FA_ARGS);
+  if (g_unroll <= 4) return launch_fedavg_variant<E, true, NTS, 1, 4, false, false>(FA_ARGS);
+  return launch_fedavg_variant<E, true, NTS, 1, 8, false, false>(FA_ARGS);
+#undef FA_ARGS
+}
+
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
                    int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts) {
-#define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
-  const bool ntl = g_nt_load != 0;
-  if constexpr (std::is_same<E, F32>::value) {
-    if (g_vpt == 2 && g_tile) {
-      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 2, 8, false, true>(FA_ARGS);
-      if (ntl && nts) return launch_fedavg_variant<E, true, true, 2, 8, false, true>(FA_ARGS);
-    }
-    if (g_vpt == 4 && g_tile) {
-      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 4, 8, false, true>(FA_ARGS);
-      if (ntl && nts) return launch_fedavg_variant<E, true, true, 4, 8, false, true>(FA_ARGS);
-    }
-    if (g_vpt == 2 && !g_tile) {
-      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 2, 8, false, false>(FA_ARGS);
-      if (ntl && nts) return launch_fedavg_variant<E, true, true, 2, 8, false, false>(FA_ARGS);
-    }
-    if (g_pipe) {
-      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, 8, true, false>(FA_ARGS);
-      if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, 8, true, false>(FA_ARGS);
-    }
-    if (g_unroll == 16) {
-      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, 16, false, false>(FA_ARGS);
-      if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, 16, false, false>(FA_ARGS);
-    }
-    if (g_unroll == 4) {
-      if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, 4, false, false>(FA_ARGS);
-      if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, 4, false, false>(FA_ARGS);
-    }
-  }
-  if (ntl && !nts) return launch_fedavg_variant<E, true, false, 1, FA_UNROLL, false, false>(FA_ARGS);
-  if (ntl && nts) return launch_fedavg_variant<E, true, true, 1, FA_UNROLL, false, false>(FA_ARGS);
-  if (!ntl && !nts) return launch_fedavg_variant<E, false, false, 1, FA_UNROLL, false, false>(FA_ARGS);
-  return launch_fedavg_variant<E, false, true, 1, FA_UNROLL, false, false>(FA_ARGS);
-#undef FA_ARGS
+  if (nts)
+    launch_fedavg_shape<E, true>(grid, s, a, pw, kc, first, nvec, M, out);
+  else
+    launch_fedavg_shape<E, false>(grid, s, a, pw, kc, first, nvec, M, out);
 }
 
 template <typename E>
@@ -823,7 +820,8 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
   const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK;
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg: workspace needed for %lld pairwise segments", P);
   const uint64_t nvec = vec ? M / E::L : 0;
-  const unsigned grid = grid_for(nvec ? nvec : M);
+  const uint64_t per_thread = (g_tile && g_nt_load) ? (uint64_t)g_vpt : 1;
+  const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
     const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
     FaArgs<E, FEDAGG_KCHUNK> a;
@@ -970,7 +968,7 @@ int fedagg_tune(const char* key, long long value) {
   if (!strcmp(key, "grid_cap")) g_grid_cap = (int)value;
   else if (!strcmp(key, "nt_load")) g_nt_load = value ? 1 : 0;
   else if (!strcmp(key, "nt_store")) g_nt_store = value < 0 ? -1 : (value ? 1 : 0);
-  else if (!strcmp(key, "vpt")) g_vpt = value >= 4 ? 4 : (value >= 2 ? 2 : 1);
+  else if (!strcmp(key, "vpt")) g_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "unroll")) g_unroll = value >= 16 ? 16 : (value <= 4 ? 4 : 8);
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;

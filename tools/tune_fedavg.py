@@ -31,15 +31,18 @@ def main():
     shapes = synthetic_state_dict_shapes(args.M)
     lay = BucketLayout(range(len(shapes)), shapes, np.float32)
     dt = torch.bfloat16 if args.kind == "bf16" else torch.float32
-    x = torch.randn((args.K, lay.ld), device="cuda").to(dt)
+    x = torch.empty((args.K, lay.ld), device="cuda", dtype=dt)
+    for k in range(args.K):  # row by row: a full fp32 temporary of C5 would not fit
+        x[k].copy_(torch.randn(lay.ld, device="cuda"))
     out = torch.empty(lay.ld, device="cuda")
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
     plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
 
     base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0)
-    shapes = [dict(), dict(unroll=4), dict(unroll=16), dict(pipe=1), dict(vpt=2), dict(vpt=2, tile=1),
-              dict(vpt=4, tile=1), dict(grid_cap=16384), dict(grid_cap=8192, vpt=2, tile=1)]
+    shapes = [dict(), dict(unroll=16), dict(vpt=2, tile=1), dict(vpt=4, tile=1), dict(vpt=4, tile=1, unroll=4),
+              dict(vpt=8, tile=1, unroll=4), dict(vpt=8, tile=1, unroll=2), dict(vpt=4, tile=1, grid_cap=8192),
+              dict(vpt=4, tile=1, grid_cap=2048)]
     variants = [dict(base, **sh, nt_store=nts) for sh in shapes for nts in (0, 1)]
     times = {i: [] for i in range(len(variants))}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
