@@ -125,19 +125,21 @@ def main():
     torch.cuda.synchronize(device)
 
     # ---- timed region: exactly `steps` steps, barrier + sync on both sides ----
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # HIP events on the launch stream bracket the region: kern_ms = region / steps is the
+    # average launch duration of the bucket kernel (back-to-back launches, so it includes the
+    # ~1-2 us inter-kernel boundary: an upper bound; rocprofv3 gives the exact duration).
+    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        starts[s].record(stream)
+    ev_start.record(stream)
+    for _ in range(args.steps):
         plan.launch(stream)
-        ends[s].record(stream)
+    ev_end.record(stream)
     torch.cuda.synchronize(device)
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]))
+    kern_ms = ev_start.elapsed_time(ev_end) / args.steps
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)

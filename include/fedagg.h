@@ -48,7 +48,10 @@ const char* fedagg_last_error(void);
 /* Process-wide launch knobs (defaults are the values measured best on MI355X):
  *   "grid_cap"      workgroups per launch before the kernels grid-stride (<= 0: no cap)
  *   "nt_load"       non-temporal client loads (0/1)      "nt_store"  non-temporal output stores
- *   "vpt"           16-B vectors per thread per step (1/2)
+ *   "vpt"           16-B vectors per thread per step (0 = auto by K, 1/2/4/8)
+ *   "unroll"        clients per load group (2/4/8/16, with an explicit vpt)
+ *   "tile"          a workgroup step covers vpt*256 contiguous vectors (0/1)
+ *   "pipe"          software-pipelined client groups (0/1, vpt 1 only)
  *   "fuse_pairwise" patch numel==1 tensors inside the bucket launch (0/1)
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);

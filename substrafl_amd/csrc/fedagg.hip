@@ -57,8 +57,8 @@ int check_launch(const char* what) {
 int g_grid_cap = 0;     // workgroups per launch before grid-striding (0: one step per workgroup)
 int g_nt_load = 1;      // client streams are read once: non-temporal loads
 int g_nt_store = 1;     // non-temporal output stores (-1: auto, on from NT_STORE_MIN_K clients)
-int g_vpt = 4;          // 16-byte vectors per thread per step
-int g_unroll = 8;       // clients per load group
+int g_vpt = 0;          // 16-byte vectors per thread per step (0: auto, see shape_for)
+int g_unroll = 8;       // clients per load group (ignored when vpt is auto)
 int g_pipe = 0;         // software-pipelined client groups
 int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
@@ -736,37 +736,48 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
 // type: contiguous tiles of VPT*256 vectors per workgroup step with U-client load groups, the
 // grid-strided single-vector shape, and the pipelined variant; each with plain or
 // non-temporal output stores.  Client loads are non-temporal unless nt_load = 0 (one shape).
+// Measured on MI355X (tools/tune_fedavg.py, profiles/r01_tune_*.log): 4 KiB per wave per client
+// (vpt 4, 8-client groups) is best at 8 clients; 8 KiB per wave with 4-client groups from 16
+// clients up (64 x 125M fp32: 6.44 TB/s; 128 x 350M bf16: 6.34 TB/s).
+struct Shape {
+  int vpt, unroll;
+};
+inline Shape shape_for(int K) {
+  if (g_vpt > 0) return {g_vpt, g_unroll};
+  return K >= 16 ? Shape{8, 4} : Shape{4, 8};
+}
+
 template <typename E, bool NTS>
 void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
-                         int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
+                         int first, uint64_t nvec, uint64_t M, typename E::Out* out, Shape sh) {
 #define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
   if (!g_nt_load) return launch_fedavg_variant<E, false, NTS, 1, 8, false, false>(FA_ARGS);
   if (g_tile) {
-    if (g_vpt >= 8) {
-      if (g_unroll <= 4) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true>(FA_ARGS);
+    if (sh.vpt >= 8) {
+      if (sh.unroll <= 2) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
     }
-    if (g_vpt >= 4) {
-      if (g_unroll <= 4) return launch_fedavg_variant<E, true, NTS, 4, 4, false, true>(FA_ARGS);
+    if (sh.vpt >= 4) {
+      if (sh.unroll <= 4) return launch_fedavg_variant<E, true, NTS, 4, 4, false, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 4, 8, false, true>(FA_ARGS);
     }
-    if (g_vpt >= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, true>(FA_ARGS);
+    if (sh.vpt >= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, true>(FA_ARGS);
   }
   if (g_pipe) return launch_fedavg_variant<E, true, NTS, 1, 8, true, false>(FA_ARGS);
-  if (g_vpt >= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, false>(FA_ARGS);
-  if (g_unroll >= 16) return launch_fedavg_variant<E, true, NTS, 1, 16, false, false>(FA_ARGS);
-  if (g_unroll <= 4) return launch_fedavg_variant<E, true, NTS, 1, 4, false, false>(FA_ARGS);
+  if (sh.vpt >= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, false>(FA_ARGS);
+  if (sh.unroll >= 16) return launch_fedavg_variant<E, true, NTS, 1, 16, false, false>(FA_ARGS);
+  if (sh.unroll <= 4) return launch_fedavg_variant<E, true, NTS, 1, 4, false, false>(FA_ARGS);
   return launch_fedavg_variant<E, true, NTS, 1, 8, false, false>(FA_ARGS);
 #undef FA_ARGS
 }
 
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
-                   int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts) {
+                   int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts, Shape sh) {
   if (nts)
-    launch_fedavg_shape<E, true>(grid, s, a, pw, kc, first, nvec, M, out);
+    launch_fedavg_shape<E, true>(grid, s, a, pw, kc, first, nvec, M, out, sh);
   else
-    launch_fedavg_shape<E, false>(grid, s, a, pw, kc, first, nvec, M, out);
+    launch_fedavg_shape<E, false>(grid, s, a, pw, kc, first, nvec, M, out, sh);
 }
 
 template <typename E>
@@ -820,7 +831,8 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
   const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK;
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg: workspace needed for %lld pairwise segments", P);
   const uint64_t nvec = vec ? M / E::L : 0;
-  const uint64_t per_thread = (g_tile && g_nt_load) ? (uint64_t)g_vpt : 1;
+  const Shape sh = shape_for(K);
+  const uint64_t per_thread = (g_tile && g_nt_load) ? (uint64_t)sh.vpt : 1;
   const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
     const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
@@ -837,7 +849,7 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const bool nts = g_nt_store < 0 ? K >= NT_STORE_MIN_K : g_nt_store != 0;
-    launch_fedavg<E>(grid, s, a, pw, kc, k0 == 0 ? 1 : 0, nvec, M, out, nts);
+    launch_fedavg<E>(grid, s, a, pw, kc, k0 == 0 ? 1 : 0, nvec, M, out, nts, sh);
     int rc = check_launch("fedavg_kernel");
     if (rc) return rc;
   }
@@ -968,8 +980,8 @@ int fedagg_tune(const char* key, long long value) {
   if (!strcmp(key, "grid_cap")) g_grid_cap = (int)value;
   else if (!strcmp(key, "nt_load")) g_nt_load = value ? 1 : 0;
   else if (!strcmp(key, "nt_store")) g_nt_store = value < 0 ? -1 : (value ? 1 : 0);
-  else if (!strcmp(key, "vpt")) g_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
-  else if (!strcmp(key, "unroll")) g_unroll = value >= 16 ? 16 : (value <= 4 ? 4 : 8);
+  else if (!strcmp(key, "vpt")) g_vpt = value <= 0 ? 0 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
+  else if (!strcmp(key, "unroll")) g_unroll = value >= 16 ? 16 : (value <= 2 ? 2 : (value <= 4 ? 4 : 8));
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;

@@ -397,7 +397,8 @@ def test_many_numel1_layers_fused_and_separate(torch_gpu, dummy_algo_class, fuse
 
 @pytest.mark.parametrize("knobs", [dict(vpt=2), dict(nt_load=0), dict(nt_store=1), dict(grid_cap=7),
                                    dict(unroll=4), dict(unroll=16), dict(pipe=1), dict(vpt=2, tile=1),
-                                   dict(vpt=4, tile=1, grid_cap=5)])
+                                   dict(vpt=4, tile=1, grid_cap=5), dict(vpt=8, unroll=2, tile=1),
+                                   dict(vpt=8, unroll=4, tile=1, grid_cap=3), dict(vpt=1, tile=0)])
 def test_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -407,7 +408,7 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    default = dict(vpt=1, nt_load=1, nt_store=-1, grid_cap=0, unroll=8, pipe=0, tile=0)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
