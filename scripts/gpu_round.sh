@@ -20,6 +20,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 [ "${TESTS:-1}" = "1" ] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [ "${TUNE:-0}" = "1" ] && step tune_c2 600 python tools/tune_fedavg.py --K 8 --M 25000000
 [ "${TUNE:-0}" = "1" ] && step tune_c3 600 python tools/tune_fedavg.py --K 64 --M 125000000 --rounds 3 --iters 5
+[ "${TUNESC:-0}" = "1" ] && step tune_c4 600 python tools/tune_scaffold.py --K 16 --M 25000000
 [ "${TUNE5:-0}" = "1" ] && step tune_c5 900 python tools/tune_fedavg.py --K 128 --M 350000000 --kind bf16 --rounds 2 --iters 3
 for wl in ${BENCH:-c2}; do step bench_$wl 600 python bench.py --workload $wl --steps 50 --warmup 10; done
 echo "=== done"

@@ -62,6 +62,8 @@ int g_unroll = 8;       // clients per load group (ignored when vpt is auto)
 int g_pipe = 0;         // software-pipelined client groups
 int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
+int g_sc_vpt = 2;       // Scaffold: 16-byte vectors per thread per step (1/2)
+int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4)
 constexpr int NT_STORE_MIN_K = 16;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -492,96 +494,123 @@ __device__ __forceinline__ void scaffold_pairwise_elem(const ScArgs<TIn, KC>& a,
   *cval = 0.0 + pw_leaf<double>(gc, 0, K + 1);
 }
 
-template <typename TIn, int KC, bool NT>
-__global__ void __launch_bounds__(FA_BLOCK)
-    scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
-                    const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
-                    double* __restrict__ dout, double* __restrict__ cout) {
+// N 16-byte vectors of both buckets: in-order fp64 sums over the K clients, then (last chunk)
+// + c and * lr, the fused numel==1 patch, and the fp64 stores.
+template <typename TIn, int KC, bool NT, bool NTS, int N, int SU>
+__device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
+                                                 const int first, const int last, const TIn* __restrict__ c,
+                                                 const double lr, const uint64_t* v, double* __restrict__ dout,
+                                                 double* __restrict__ cout) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
-  constexpr int SU = FA_UNROLL / 2;  // two streams per client
-  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
-  const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
-
-  for (uint64_t v = gid; v < nvec; v += stride) {
-    double ad[L], ac[L];
-    if (first) {
+  double ad[N][L], ac[N][L];
 #pragma unroll
-      for (int j = 0; j < L; ++j) ad[j] = ac[j] = 0.0;
-    } else {
+  for (int n = 0; n < N; ++n) {
 #pragma unroll
-      for (int j = 0; j < L; ++j) {
-        ad[j] = dout[v * L + j];
-        ac[j] = cout[v * L + j];
-      }
+    for (int j = 0; j < L; ++j) {
+      ad[n][j] = first ? 0.0 : dout[v[n] * L + j];
+      ac[n][j] = first ? 0.0 : cout[v[n] * L + j];
     }
-    int k = 0;
-    for (; k + SU <= K; k += SU) {
-      u32x4 rd[SU], rc[SU];
+  }
+  int k = 0;
+  for (; k + SU <= K; k += SU) {
+    u32x4 rd[N][SU], rc[N][SU];
 #pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        rd[u] = ld16<NT>(a.d[k + u] + v * L);
-        rc[u] = ld16<NT>(a.cv[k + u] + v * L);
+    for (int u = 0; u < SU; ++u)
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        rd[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
+        rc[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
       }
 #pragma unroll
-      for (int u = 0; u < SU; ++u) {
+    for (int u = 0; u < SU; ++u) {
+      const double w = a.w[k + u];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
         double xd[L], xc[L];
-        unpack_d<TIn>(rd[u], xd);
-        unpack_d<TIn>(rc[u], xc);
-        const double w = a.w[k + u];
+        unpack_d<TIn>(rd[n][u], xd);
+        unpack_d<TIn>(rc[n][u], xc);
 #pragma unroll
         for (int j = 0; j < L; ++j) {
           const double pd = w * xd[j];
           const double pc = w * xc[j];
-          ad[j] = ad[j] + pd;
-          ac[j] = ac[j] + pc;
+          ad[n][j] = ad[n][j] + pd;
+          ac[n][j] = ac[n][j] + pc;
         }
       }
     }
-    for (; k < K; ++k) {
+  }
+  for (; k < K; ++k) {
+    const double w = a.w[k];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
       double xd[L], xc[L];
-      unpack_d<TIn>(ld16<NT>(a.d[k] + v * L), xd);
-      unpack_d<TIn>(ld16<NT>(a.cv[k] + v * L), xc);
-      const double w = a.w[k];
+      unpack_d<TIn>(ld16<NT>(a.d[k] + v[n] * L), xd);
+      unpack_d<TIn>(ld16<NT>(a.cv[k] + v[n] * L), xc);
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const double pd = w * xd[j];
         const double pc = w * xc[j];
-        ad[j] = ad[j] + pd;
-        ac[j] = ac[j] + pc;
+        ad[n][j] = ad[n][j] + pd;
+        ac[n][j] = ac[n][j] + pc;
       }
     }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
     if (last) {
       double xcc[L];
-      unpack_d<TIn>(ld16<NT>(c + v * L), xcc);
+      unpack_d<TIn>(ld16<NT>(c + v[n] * L), xcc);
 #pragma unroll
       for (int j = 0; j < L; ++j) {
-        ac[j] = ac[j] + xcc[j];  // server c appended LAST (scaffold.py:262-263)
-        ad[j] = lr * ad[j];      // aggregation_lr * sum (scaffold.py:293)
+        ac[n][j] = ac[n][j] + xcc[j];  // server c appended LAST (scaffold.py:262-263)
+        ad[n][j] = lr * ad[n][j];      // aggregation_lr * sum (scaffold.py:293)
       }
     }
     for (int p = 0; p < pw.n; ++p) {
       const uint64_t e = pw.idx[p];
-      if (e / L == v) {
+      if (e / L == v[n]) {
         double dv, cvv;
         scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, e, &dv, &cvv);
         const int j = (int)(e % L);
 #pragma unroll
         for (int jj = 0; jj < L; ++jj)
           if (jj == j) {
-            ad[jj] = dv;
-            ac[jj] = cvv;
+            ad[n][jj] = dv;
+            ac[n][jj] = cvv;
           }
       }
     }
-    f64x2* dd = reinterpret_cast<f64x2*>(dout + v * L);
-    f64x2* cc = reinterpret_cast<f64x2*>(cout + v * L);
 #pragma unroll
-    for (int s = 0; s < L / 2; ++s) {
-      f64x2 t0 = {ad[2 * s], ad[2 * s + 1]};
-      f64x2 t1 = {ac[2 * s], ac[2 * s + 1]};
-      dd[s] = t0;
-      cc[s] = t1;
+    for (int s2 = 0; s2 < L / 2; ++s2) {
+      f64x2 t0 = {ad[n][2 * s2], ad[n][2 * s2 + 1]};
+      f64x2 t1 = {ac[n][2 * s2], ac[n][2 * s2 + 1]};
+      st16<NTS>(reinterpret_cast<f64x2*>(dout + v[n] * L) + s2, __builtin_bit_cast(u32x4, t0));
+      st16<NTS>(reinterpret_cast<f64x2*>(cout + v[n] * L) + s2, __builtin_bit_cast(u32x4, t1));
+    }
+  }
+}
+
+// Same tiling as fedavg_kernel: a workgroup step covers VPT*256 contiguous vectors.
+template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU>
+__global__ void __launch_bounds__(FA_BLOCK)
+    scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
+                    const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
+                    double* __restrict__ dout, double* __restrict__ cout) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
+  const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
+  const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+  for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+    if (base + (VPT - 1) * FA_BLOCK < nvec) {
+      uint64_t v[VPT];
+#pragma unroll
+      for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+      scaffold_vectors<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout);
+    } else {
+      for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
+        scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout);
     }
   }
   for (uint64_t i = nvec * L + gid; i < M; i += stride) {
@@ -894,6 +923,36 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
   return FEDAGG_OK;
 }
 
+template <typename TIn, bool NT, bool NTS, int VPT, int SU>
+void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
+                             const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
+                             uint64_t M, double* dout, double* cout) {
+  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU>), dim3(grid), dim3(FA_BLOCK), 0,
+                     s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+}
+
+// Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
+
+template <typename TIn>
+void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
+                     int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
+                     double* cout) {
+#define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
+  const bool nts = g_nt_store != 0;
+  if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
+  if (g_sc_vpt >= 2) {
+    if (g_sc_unroll <= 2) {
+      if (nts) return launch_scaffold_variant<TIn, true, true, 2, 2>(SC_ARGS);
+      return launch_scaffold_variant<TIn, true, false, 2, 2>(SC_ARGS);
+    }
+    if (nts) return launch_scaffold_variant<TIn, true, true, 2, 4>(SC_ARGS);
+    return launch_scaffold_variant<TIn, true, false, 2, 4>(SC_ARGS);
+  }
+  if (nts) return launch_scaffold_variant<TIn, true, true, 1, 4>(SC_ARGS);
+  return launch_scaffold_variant<TIn, true, false, 1, 4>(SC_ARGS);
+#undef SC_ARGS
+}
+
 template <typename TIn>
 int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, const double* w, int K, uint64_t M,
                     const uint64_t* idx, int P, void* ws, double lr, double* dout, double* cout, hipStream_t s) {
@@ -912,7 +971,8 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "scaffold: workspace needed for %lld pairwise segments", P);
   constexpr int L = 16 / sizeof(TIn);
   const uint64_t nvec = vec ? M / L : 0;
-  const unsigned grid = grid_for(nvec ? nvec : M);
+  const uint64_t per_thread = g_nt_load ? (uint64_t)g_sc_vpt : 1;
+  const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
     const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
     ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a;
@@ -929,12 +989,7 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0, last = (k0 + kc) == K;
-    if (g_nt_load)
-      hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true>), dim3(grid), dim3(FA_BLOCK), 0, s, a,
-                         pw, kc, first, last, c, lr, nvec, M, dout, cout);
-    else
-      hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, false>), dim3(grid), dim3(FA_BLOCK), 0, s,
-                         a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+    launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
     int rc = check_launch("scaffold_kernel");
     if (rc) return rc;
   }
@@ -985,6 +1040,8 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
+  else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 2 ? 2 : 1;
+  else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 2 ? 2 : 4;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

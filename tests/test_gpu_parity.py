@@ -417,3 +417,44 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
         outs.append(out[:M].clone())
     _native.tune(**default)
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
+@pytest.mark.parametrize("knobs", [dict(sc_vpt=1), dict(sc_vpt=2, sc_unroll=2), dict(nt_store=0), dict(nt_load=0),
+                                   dict(grid_cap=3)])
+def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import ScaffoldPlan, scaffold_weights
+
+    K, M = 11, 300_007
+    d = torch.randn((K, M + 1), device="cuda")
+    cv = torch.randn((K, M + 1), device="cuda")
+    c = torch.randn(M + 1, device="cuda")
+    w = scaffold_weights(list(range(5, 5 + K)))
+    default = dict(sc_vpt=2, sc_unroll=4, nt_store=1, nt_load=1, grid_cap=0)
+    outs = []
+    for kn in (default, knobs):
+        _native.tune(**kn)
+        do = torch.empty(M + 1, dtype=torch.float64, device="cuda")
+        co = torch.empty(M + 1, dtype=torch.float64, device="cuda")
+        ScaffoldPlan("f32", [d[k].data_ptr() for k in range(K)], [cv[k].data_ptr() for k in range(K)], c, w, M, 0.9,
+                     do, co, [3, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append((do[:M].clone(), co[:M].clone()))
+    _native.tune(**default)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+    # and against the oracle on a sample of elements (fp64 sequential order)
+    idx = np.array([0, 1, 2, 3, 4, 1000, M // 2, M - 2, M - 1])
+    hd, hc, hcc = d.cpu().numpy(), cv.cpu().numpy(), c.cpu().numpy()
+    for i in idx:
+        pu = [[hd[k, i:i + 1].copy()] for k in range(K)]
+        cu = [[hc[k, i:i + 1].copy()] for k in range(K)]
+        if i in (3, M - 1):
+            rc, ra = scaffold_reference_structure(pu, cu, [hcc[i:i + 1].copy()], list(range(5, 5 + K)), 0.9)
+        else:  # numel >= 2 order: use a 2-element layer holding the element twice
+            pu2 = [[np.repeat(p[0], 2)] for p in pu]
+            cu2 = [[np.repeat(p[0], 2)] for p in cu]
+            rc, ra = scaffold_reference_structure(pu2, cu2, [np.repeat(hcc[i:i + 1], 2)], list(range(5, 5 + K)), 0.9)
+        assert _bits(ra[0].reshape(-1)[0]) == _bits(outs[0][0][i].cpu().numpy())
+        assert _bits(rc[0].reshape(-1)[0]) == _bits(outs[0][1][i].cpu().numpy())

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Launch-shape sweep of the Scaffold two-bucket kernel (interleaved rounds, one process)."""
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=16)
+    ap.add_argument("--M", type=int, default=25_000_000)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from substrafl_amd import _native
+    from substrafl_amd.engine import ScaffoldPlan, scaffold_weights
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+
+    shapes = synthetic_state_dict_shapes(args.M)
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    d = torch.randn((args.K, lay.ld), device="cuda")
+    cv = torch.randn((args.K, lay.ld), device="cuda")
+    c = torch.randn(lay.ld, device="cuda")
+    dout = torch.empty(lay.ld, dtype=torch.float64, device="cuda")
+    cout = torch.empty(lay.ld, dtype=torch.float64, device="cuda")
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
+    plan = ScaffoldPlan("f32", d, cv, c, scaffold_weights(ns), args.M, 1.0, dout, cout, lay.pairwise_idx)
+    nbytes = plan.bytes_alg()
+    variants = [dict(sc_vpt=v, sc_unroll=u, nt_store=n, grid_cap=g)
+                for v, u in ((1, 4), (2, 2), (2, 4)) for n in (0, 1) for g in (0, 8192)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = {i: [] for i in range(len(variants))}
+    for _ in range(args.rounds):
+        for i, kn in enumerate(variants):
+            _native.tune(**kn)
+            plan.launch()
+            ev[0].record()
+            for _ in range(args.iters):
+                plan.launch()
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[i].append(ev[0].elapsed_time(ev[1]) / args.iters)
+    res = []
+    for i, kn in enumerate(variants):
+        t = np.array(times[i])
+        res.append(dict(kn, K=args.K, M=args.M, median_us=round(float(np.median(t)) * 1e3, 2),
+                        GBps=round(nbytes / (np.median(t) / 1e3) / 1e9, 1)))
+    for r in sorted(res, key=lambda d: d["median_us"]):
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
