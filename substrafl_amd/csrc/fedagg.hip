@@ -186,6 +186,45 @@ __device__ __forceinline__ void store_vec(typename E::Out* out, uint64_t v, cons
   for (int s = 0; s < bytes / 16; ++s) st16<NTS>(reinterpret_cast<u32x4*>(out + v * E::L) + s, src[s]);
 }
 
+// A wave's 64 lanes each own 32 contiguous output bytes (bf16->fp32 FedAvg, fp32->fp64
+// Scaffold) of one 2 KiB run.  Stored directly, every store instruction would write 16 B per
+// lane at a 32-B stride (half of each 64-B line per instruction: PMC WRITE_SIZE showed 1.36x
+// the written bytes).  Transposing through 2 KiB of LDS turns them into two fully coalesced
+// 1 KiB store instructions.  Requires all 64 lanes active (callers check wave-uniformly).
+template <bool NTS>
+__device__ __forceinline__ void store32_coalesced(void* wave_dst, u32x4 lo, u32x4 hi, u32x4* lds_wave) {
+  const int lane = threadIdx.x & 63;
+  lds_wave[2 * lane] = lo;
+  lds_wave[2 * lane + 1] = hi;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const u32x4 a = lds_wave[lane];
+  const u32x4 b = lds_wave[64 + lane];
+  st16<NTS>(reinterpret_cast<u32x4*>(wave_dst) + lane, a);
+  st16<NTS>(reinterpret_cast<u32x4*>(wave_dst) + 64 + lane, b);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // WAR before the buffer is reused
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <typename E, bool NTS>
+__device__ __forceinline__ void store_vec_wave(typename E::Out* out, uint64_t v, const typename E::P* acc,
+                                               bool wave_full, u32x4* lds_wave) {
+  constexpr int bytes = E::L * sizeof(typename E::Out);
+  if constexpr (bytes == 32) {
+    if (wave_full) {
+      typename E::Out o[E::L];
+#pragma unroll
+      for (int j = 0; j < E::L; ++j) o[j] = E::out(acc[j]);
+      const u32x4* src = reinterpret_cast<const u32x4*>(o);
+      const uint64_t v0 = v - (threadIdx.x & 63);
+      store32_coalesced<NTS>(out + v0 * E::L, src[0], src[1], lds_wave);
+      return;
+    }
+  }
+  store_vec<E, NTS>(out, v, acc);
+}
+
 template <typename E>
 __device__ __forceinline__ void load_vec(const typename E::Out* out, uint64_t v, typename E::P* acc) {
   typename E::Out o[E::L];
@@ -402,8 +441,13 @@ __global__ void __launch_bounds__(FA_BLOCK)
   const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
 
   if constexpr (TILE) {
+    constexpr bool WIDE = E::L * sizeof(typename E::Out) == 32;
+    __shared__ u32x4 stage[WIDE ? FA_BLOCK / 64 : 1][128];
+    u32x4* lds_wave = stage[WIDE ? threadIdx.x / 64 : 0];
     const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
     for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+      // wave-uniform: every lane of this wave has all VPT vectors in range
+      const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
       if (base + (VPT - 1) * FA_BLOCK < nvec) {
         uint64_t v[VPT];
 #pragma unroll
@@ -413,7 +457,7 @@ __global__ void __launch_bounds__(FA_BLOCK)
 #pragma unroll
         for (int n = 0; n < VPT; ++n) {
           if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
-          store_vec<E, NTS>(out, v[n], acc[n]);
+          store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
         }
       } else {
         for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK) {
@@ -500,7 +544,7 @@ template <typename TIn, int KC, bool NT, bool NTS, int N, int SU>
 __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                  const int first, const int last, const TIn* __restrict__ c,
                                                  const double lr, const uint64_t* v, double* __restrict__ dout,
-                                                 double* __restrict__ cout) {
+                                                 double* __restrict__ cout, bool wave_full, u32x4* lds_wave) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
   double ad[N][L], ac[N][L];
@@ -581,6 +625,16 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
           }
       }
     }
+    if constexpr (L == 4) {
+      if (wave_full) {  // fp32 in -> 32 B of fp64 out per lane: coalesce through LDS
+        const uint64_t v0 = v[n] - (threadIdx.x & 63);
+        const f64x2 d0 = {ad[n][0], ad[n][1]}, d1 = {ad[n][2], ad[n][3]};
+        const f64x2 c0 = {ac[n][0], ac[n][1]}, c1 = {ac[n][2], ac[n][3]};
+        store32_coalesced<NTS>(dout + v0 * L, __builtin_bit_cast(u32x4, d0), __builtin_bit_cast(u32x4, d1), lds_wave);
+        store32_coalesced<NTS>(cout + v0 * L, __builtin_bit_cast(u32x4, c0), __builtin_bit_cast(u32x4, c1), lds_wave);
+        continue;
+      }
+    }
 #pragma unroll
     for (int s2 = 0; s2 < L / 2; ++s2) {
       f64x2 t0 = {ad[n][2 * s2], ad[n][2 * s2 + 1]};
@@ -601,16 +655,20 @@ __global__ void __launch_bounds__(FA_BLOCK)
   constexpr int L = 16 / sizeof(TIn);
   const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
+  __shared__ u32x4 stage[FA_BLOCK / 64][128];
+  u32x4* lds_wave = stage[threadIdx.x / 64];
   const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
   for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+    const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
     if (base + (VPT - 1) * FA_BLOCK < nvec) {
       uint64_t v[VPT];
 #pragma unroll
       for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
-      scaffold_vectors<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout);
+      scaffold_vectors<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
+                                                   lds_wave);
     } else {
       for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
-        scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout);
+        scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout, false, lds_wave);
     }
   }
   for (uint64_t i = nvec * L + gid; i < M; i += stride) {

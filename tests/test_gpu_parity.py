@@ -281,8 +281,9 @@ def test_unaligned_rows_take_scalar_path(torch_gpu):
     assert np.array_equal(_bits(out.cpu().numpy()), _bits(fedavg_reference_structure(pus, ns)[0]))
 
 
-@pytest.mark.parametrize("K, M", [(8, 25_000_000), (64, 4_000_000), (200, 1_000_000)])
-def test_full_size_vs_torch_sequential(torch_gpu, K, M):
+@pytest.mark.parametrize("K, M, kind", [(8, 25_000_000, "f32"), (64, 4_000_000, "f32"), (200, 1_000_000, "f32"),
+                                        (8, 9_000_011, "bf16"), (128, 2_000_000, "bf16")])
+def test_full_size_vs_torch_sequential(torch_gpu, K, M, kind):
     """At BASELINE sizes: bit-exact against a torch fp32 eager sequential reference on the device
     (every torch op is one separately rounded IEEE op: same order as the reference)."""
     torch = torch_gpu
@@ -293,10 +294,13 @@ def test_full_size_vs_torch_sequential(torch_gpu, K, M):
     lay = BucketLayout(range(len(shapes)), shapes, np.float32)
     g = torch.Generator(device="cuda").manual_seed(7)
     x = torch.randn((K, lay.ld), generator=g, device="cuda")
+    if kind == "bf16":
+        x = x.to(torch.bfloat16)
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
     w = fedavg_weights(ns, "f32")
     out = torch.empty(lay.ld, device="cuda")
-    FedAvgPlan("f32", x, w, M, out, lay.pairwise_idx).launch()
+    FedAvgPlan(kind, x, w, M, out, lay.pairwise_idx).launch()
+    x = x.float()
     acc = torch.zeros(M, device="cuda")
     for k in range(K):
         acc = acc + x[k, :M] * torch.tensor(w[k], device="cuda")
@@ -307,6 +311,34 @@ def test_full_size_vs_torch_sequential(torch_gpu, K, M):
     for p in lay.pairwise_idx.astype(np.int64):
         prods = (x[:, p].cpu().numpy() * w).astype(np.float32)
         assert _bits(np.float32(0.0) + numpy_pairwise_sum(prods)) == _bits(out[p].cpu().numpy())
+
+
+@pytest.mark.parametrize("K, M", [(16, 5_000_011), (3, 2_000_000)])
+def test_scaffold_full_size_vs_torch_fp64(torch_gpu, K, M):
+    """Scaffold at size: bit-exact against torch fp64 eager ops (w*x, +, c last, lr*) on the device."""
+    torch = torch_gpu
+    from substrafl_amd.engine import ScaffoldPlan, scaffold_weights
+
+    ld = (M + 63) // 64 * 64
+    d = torch.randn((K, ld), device="cuda")
+    cv = torch.randn((K, ld), device="cuda")
+    c = torch.randn(ld, device="cuda")
+    ns = [int(v) for v in np.random.default_rng(3).integers(100, 10000, K)]
+    w = scaffold_weights(ns)
+    do = torch.empty(ld, dtype=torch.float64, device="cuda")
+    co = torch.empty(ld, dtype=torch.float64, device="cuda")
+    ScaffoldPlan("f32", d, cv, c, w, M, 0.7, do, co).launch()
+    ad = torch.zeros(M, dtype=torch.float64, device="cuda")
+    ac = torch.zeros(M, dtype=torch.float64, device="cuda")
+    for k in range(K):
+        wk = torch.tensor(w[k], dtype=torch.float64, device="cuda")
+        ad = ad + wk * d[k, :M].double()
+        ac = ac + wk * cv[k, :M].double()
+    ac = ac + c[:M].double()
+    ad = torch.tensor(0.7, dtype=torch.float64, device="cuda") * ad
+    torch.cuda.synchronize()
+    assert torch.equal(do[:M].view(torch.int64), ad.view(torch.int64))
+    assert torch.equal(co[:M].view(torch.int64), ac.view(torch.int64))
 
 
 def test_equal_count_kernel(torch_gpu):
