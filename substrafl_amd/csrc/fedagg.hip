@@ -62,7 +62,7 @@ int g_unroll = 8;       // clients per load group (ignored when vpt is auto)
 int g_pipe = 0;         // software-pipelined client groups
 int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
-int g_sc_vpt = 2;       // Scaffold: 16-byte vectors per thread per step (1/2)
+int g_sc_vpt = 2;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -410,18 +410,26 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
   }
 }
 
-template <typename E, int KC>
-__device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwArgs& pw, const int K, uint64_t v,
-                                               typename E::P* acc) {
+// numel==1 patch for the N vectors v[] of this thread: one call site of the pairwise tree
+// (the owner vector is found first) keeps the unrolled kernel body small.
+template <typename E, int KC, int N>
+__device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwArgs& pw, const int K,
+                                               const uint64_t* v, typename E::P (*acc)[E::L]) {
   constexpr int L = E::L;
   for (int p = 0; p < pw.n; ++p) {
     const uint64_t e = pw.idx[p];
-    if (e / L == v) {
+    int owner = -1;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if (e / L == v[n]) owner = n;
+    if (owner >= 0) {
       const typename E::P val = fedavg_pairwise_elem<E, KC>(a, K, e);
       const int j = (int)(e % L);
 #pragma unroll
-      for (int jj = 0; jj < L; ++jj)
-        if (jj == j) acc[jj] = val;
+      for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int jj = 0; jj < L; ++jj)
+          if (n == owner && jj == j) acc[n][jj] = val;
     }
   }
 }
@@ -454,16 +462,14 @@ __global__ void __launch_bounds__(FA_BLOCK)
         for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
         P acc[VPT][L];
         fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, acc, out);
+        if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
 #pragma unroll
-        for (int n = 0; n < VPT; ++n) {
-          if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
-          store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
-        }
+        for (int n = 0; n < VPT; ++n) store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
       } else {
         for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK) {
           P acc[1][L];
           fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
-          if (pw.n) patch_pairwise<E, KC>(a, pw, K, v0, acc[0]);
+          if (pw.n) patch_pairwise<E, KC, 1>(a, pw, K, &v0, acc);
           store_vec<E, NTS>(out, v0, acc[0]);
         }
       }
@@ -477,17 +483,15 @@ __global__ void __launch_bounds__(FA_BLOCK)
         for (int n = 0; n < VPT; ++n) v[n] = v0 + n * stride;
         P acc[VPT][L];
         fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, acc, out);
+        if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
 #pragma unroll
-        for (int n = 0; n < VPT; ++n) {
-          if (pw.n) patch_pairwise<E, KC>(a, pw, K, v[n], acc[n]);
-          store_vec<E, NTS>(out, v[n], acc[n]);
-        }
+        for (int n = 0; n < VPT; ++n) store_vec<E, NTS>(out, v[n], acc[n]);
       }
     }
     for (; v0 < nvec; v0 += stride) {
       P acc[1][L];
       fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
-      if (pw.n) patch_pairwise<E, KC>(a, pw, K, v0, acc[0]);
+      if (pw.n) patch_pairwise<E, KC, 1>(a, pw, K, &v0, acc);
       store_vec<E, NTS>(out, v0, acc[0]);
     }
   }
@@ -611,20 +615,29 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
         ad[n][j] = lr * ad[n][j];      // aggregation_lr * sum (scaffold.py:293)
       }
     }
-    for (int p = 0; p < pw.n; ++p) {
-      const uint64_t e = pw.idx[p];
-      if (e / L == v[n]) {
-        double dv, cvv;
-        scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, e, &dv, &cvv);
-        const int j = (int)(e % L);
+  }
+  for (int p = 0; p < pw.n; ++p) {  // numel==1 patch (fused launches are single-chunk: first & last)
+    const uint64_t e = pw.idx[p];
+    int owner = -1;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if (e / L == v[n]) owner = n;
+    if (owner >= 0) {
+      double dv, cvv;
+      scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, e, &dv, &cvv);
+      const int j = (int)(e % L);
+#pragma unroll
+      for (int n = 0; n < N; ++n)
 #pragma unroll
         for (int jj = 0; jj < L; ++jj)
-          if (jj == j) {
+          if (n == owner && jj == j) {
             ad[n][jj] = dv;
             ac[n][jj] = cvv;
           }
-      }
     }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
     if constexpr (L == 4) {
       if (wave_full) {  // fp32 in -> 32 B of fp64 out per lane: coalesce through LDS
         const uint64_t v0 = v[n] - (threadIdx.x & 63);
@@ -998,6 +1011,18 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
 #define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
   const bool nts = g_nt_store != 0;
   if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
+  if (g_sc_vpt >= 8) {
+    if (nts) return launch_scaffold_variant<TIn, true, true, 8, 1>(SC_ARGS);
+    return launch_scaffold_variant<TIn, true, false, 8, 1>(SC_ARGS);
+  }
+  if (g_sc_vpt >= 4) {
+    if (g_sc_unroll <= 2) {
+      if (nts) return launch_scaffold_variant<TIn, true, true, 4, 2>(SC_ARGS);
+      return launch_scaffold_variant<TIn, true, false, 4, 2>(SC_ARGS);
+    }
+    if (nts) return launch_scaffold_variant<TIn, true, true, 4, 4>(SC_ARGS);
+    return launch_scaffold_variant<TIn, true, false, 4, 4>(SC_ARGS);
+  }
   if (g_sc_vpt >= 2) {
     if (g_sc_unroll <= 2) {
       if (nts) return launch_scaffold_variant<TIn, true, true, 2, 2>(SC_ARGS);
@@ -1098,7 +1123,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
-  else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 2 ? 2 : 1;
+  else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 2 ? 2 : 4;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;

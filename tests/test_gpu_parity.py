@@ -452,7 +452,8 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
 
 
 @pytest.mark.parametrize("knobs", [dict(sc_vpt=1), dict(sc_vpt=2, sc_unroll=2), dict(nt_store=0), dict(nt_load=0),
-                                   dict(grid_cap=3)])
+                                   dict(grid_cap=3), dict(sc_vpt=4, sc_unroll=2), dict(sc_vpt=4, sc_unroll=4),
+                                   dict(sc_vpt=8), dict(sc_vpt=8, grid_cap=2)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native

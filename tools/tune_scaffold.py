@@ -35,7 +35,7 @@ def main():
     plan = ScaffoldPlan("f32", d, cv, c, scaffold_weights(ns), args.M, 1.0, dout, cout, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
     variants = [dict(sc_vpt=v, sc_unroll=u, nt_store=n, grid_cap=g)
-                for v, u in ((1, 4), (2, 2), (2, 4)) for n in (0, 1) for g in (0, 8192)]
+                for v, u in ((1, 4), (2, 2), (2, 4), (4, 2), (4, 4), (8, 1)) for n in (1,) for g in (0,)]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {i: [] for i in range(len(variants))}
     for _ in range(args.rounds):
