@@ -62,7 +62,7 @@ int g_unroll = 8;       // clients per load group (ignored when vpt is auto)
 int g_pipe = 0;         // software-pipelined client groups
 int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
-int g_sc_vpt = 2;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8)
+int g_sc_vpt = 4;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8); 4 measured best
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -836,15 +836,17 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
 // type: contiguous tiles of VPT*256 vectors per workgroup step with U-client load groups, the
 // grid-strided single-vector shape, and the pipelined variant; each with plain or
 // non-temporal output stores.  Client loads are non-temporal unless nt_load = 0 (one shape).
-// Measured on MI355X (tools/tune_fedavg.py, profiles/r01_tune_*.log): 4 KiB per wave per client
-// (vpt 4, 8-client groups) is best at 8 clients; 8 KiB per wave with 4-client groups from 16
-// clients up (64 x 125M fp32: 6.44 TB/s; 128 x 350M bf16: 6.34 TB/s).
+// Measured on MI355X (tools/tune_fedavg.py, profiles/r01_tune_*.log): 8 KiB per wave per client
+// (vpt 8) with 4-client load groups is the best or within noise of it at every size measured
+// (8 x 25M fp32: 6.54 TB/s; 64 x 125M fp32: 6.43 TB/s; 128 x 350M bf16: 6.34 TB/s before the
+// coalesced fp32 stores).  4 KiB x 8 clients ties at 8 clients (box-to-box spread ~3 %).
 struct Shape {
   int vpt, unroll;
 };
 inline Shape shape_for(int K) {
+  (void)K;
   if (g_vpt > 0) return {g_vpt, g_unroll};
-  return K >= 16 ? Shape{8, 4} : Shape{4, 8};
+  return Shape{8, 4};
 }
 
 template <typename E, bool NTS>
