@@ -257,20 +257,31 @@ class AggregationEngine:
 
     # ----------------------------------------------------------------------------------
     def _stage(self, rows: List[List[np.ndarray]], layout: BucketLayout, K: int):
-        """Pack K clients' layers into a pinned [K, ld] buffer and enqueue its H2D copy."""
+        """Pack K clients' layers into a pinned [K, ld] staging buffer and copy it to HBM.
+
+        Rows are packed by a thread pool; each row's H2D copy is enqueued as soon as that row is
+        packed, so the PCIe transfer of client k overlaps the packing of the clients after it."""
         torch = self._setup() if not hasattr(self, "device") else _torch()
         tdt = torch_dtype(layout.dtype)
         t0 = time.perf_counter()
         host = torch.empty((K, layout.ld), dtype=tdt, pin_memory=True)
+        t1 = time.perf_counter()
+        dev = torch.empty((K, layout.ld), dtype=tdt, device=self.device)
         hv = host.numpy()
         if K > 1:
             with self._pool(K) as ex:
-                list(ex.map(lambda k: layout.pack_row(rows[k], hv[k]), range(K)))
+                futs = [ex.submit(layout.pack_row, rows[k], hv[k]) for k in range(K)]
+                for k, f in enumerate(futs):
+                    f.result()
+                    dev[k].copy_(host[k], non_blocking=True)
         else:
             layout.pack_row(rows[0], hv[0])
-        self.last_timing["pack_s"] = self.last_timing.get("pack_s", 0.0) + time.perf_counter() - t0
-        dev = torch.empty((K, layout.ld), dtype=tdt, device=self.device)
-        dev.copy_(host, non_blocking=True)
+            dev.copy_(host, non_blocking=True)
+        t2 = time.perf_counter()
+        tm = self.last_timing
+        tm["pin_alloc_s"] = tm.get("pin_alloc_s", 0.0) + t1 - t0
+        tm["pack_enqueue_s"] = tm.get("pack_enqueue_s", 0.0) + t2 - t1
+        tm["h2d_bytes"] = tm.get("h2d_bytes", 0) + K * layout.ld * host.element_size()
         return dev, host
 
     def _fetch(self, dev_out, layout: BucketLayout) -> np.ndarray:
@@ -321,23 +332,30 @@ class AggregationEngine:
                         if np.dtype(d) == R:
                             w[k] = fedavg_weights(n_samples, kind)[k]
                 out = torch.empty(layout.ld, dtype=torch_dtype(kind), device=self.device)
-                ev0 = torch.cuda.Event(enable_timing=True)
-                ev1 = torch.cuda.Event(enable_timing=True)
-                ev0.record(stream)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                ev[0].record(stream)  # after the H2D copies
                 plan = FedAvgPlan(kind, dev, w, layout.M, out, layout.pairwise_idx)
                 plan.launch(stream)
-                ev1.record(stream)
+                ev[1].record(stream)
                 host_out = self._fetch(out, layout)
-                pending.append((layout, host_out, ev0, ev1, host_in, dev, plan))
+                ev[2].record(stream)
+                pending.append((layout, host_out, ev, host_in, dev, plan))
+            t_wait = time.perf_counter()
             stream.synchronize()
-            kernel_ms = 0.0
-            for layout, host_out, ev0, ev1, _hin, _dev, _plan in pending:
-                kernel_ms += ev0.elapsed_time(ev1)
+            t_sync = time.perf_counter()
+            kernel_ms = d2h_ms = 0.0
+            for layout, host_out, ev, _hin, _dev, _plan in pending:
+                kernel_ms += ev[0].elapsed_time(ev[1])
+                d2h_ms += ev[1].elapsed_time(ev[2])
                 flat = np.array(host_out.numpy()[: layout.M], copy=True)
                 for li, arr in layout.unpack(flat):
                     results[li] = arr
-        self.last_timing["kernel_s"] = kernel_ms / 1e3
-        self.last_timing["total_s"] = time.perf_counter() - t_start
+        tm = self.last_timing
+        tm["kernel_s"] = kernel_ms / 1e3
+        tm["d2h_s"] = d2h_ms / 1e3
+        tm["sync_wait_s"] = t_sync - t_wait
+        tm["unpack_s"] = time.perf_counter() - t_sync
+        tm["total_s"] = time.perf_counter() - t_start
         return results  # type: ignore[return-value]
 
     def _stage_mixed(self, parameters_updates, layout: BucketLayout, K: int, pds, n_samples):

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""End-to-end (PCIe-inclusive) timing of the drop-in path vs the reference CPU path.
+
+What a Substra aggregate task does: unpickle K shared-state files, run
+avg_shared_states, pickle the result.  Timed here per phase:
+  unpickle (PickleSerializer.load of K files), the engine's pack + H2D + kernel + D2H + unpack,
+  pickle of the output, and the oracle's reference-call-structure FedAvg on the same inputs.
+Prints one JSON line per configuration (cold = first call in the process, warm = repeated)."""
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=8)
+    ap.add_argument("--M", type=int, default=25_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=0)
+    args = ap.parse_args()
+
+    from oracle import fedavg_reference_structure
+    from substrafl_amd.engine import AggregationEngine
+    from substrafl_amd.layout import synthetic_state_dict_shapes
+    from substrafl_amd.remote import PickleSerializer
+    from substrafl_amd.schemas import FedAvgAveragedState, FedAvgSharedState
+
+    shapes = synthetic_state_dict_shapes(args.M)
+    rng = np.random.default_rng(0)
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
+    tmp = Path(tempfile.mkdtemp(prefix="e2e_", dir=os.environ.get("TMPDIR", "/tmp")))
+    paths = []
+    for k in range(args.K):
+        st = FedAvgSharedState(n_samples=ns[k], parameters_update=[rng.standard_normal(s, dtype=np.float32)
+                                                                   for s in shapes])
+        p = tmp / f"shared_{k}"
+        PickleSerializer.save(st, p)
+        paths.append(p)
+        del st
+    eng = AggregationEngine(device=0, pack_threads=args.threads or None)
+    bytes_alg = args.K * args.M * 4 + args.M * 4
+    for rep in range(args.reps):
+        t0 = time.perf_counter()
+        states = [PickleSerializer.load(p) for p in paths]
+        t1 = time.perf_counter()
+        updates = [list(s.parameters_update) for s in states]
+        out = eng.fedavg(updates, [s.n_samples for s in states])
+        t2 = time.perf_counter()
+        res = FedAvgAveragedState(avg_parameters_update=out)
+        PickleSerializer.save(res, tmp / "out")
+        t3 = time.perf_counter()
+        ref = fedavg_reference_structure(updates, [s.n_samples for s in states])
+        t4 = time.perf_counter()
+        exact = all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(out, ref))
+        line = dict(K=args.K, M=args.M, rep=rep, cold=rep == 0, unpickle_s=round(t1 - t0, 4),
+                    engine_s=round(t2 - t1, 4), pickle_out_s=round(t3 - t2, 4), reference_cpu_s=round(t4 - t3, 4),
+                    engine_breakdown={k: (round(v, 5) if isinstance(v, float) else v) for k, v in eng.last_timing.items()},
+                    engine_GBps_alg=round(bytes_alg / (t2 - t1) / 1e9, 2),
+                    reference_GBps_alg=round(bytes_alg / (t4 - t3) / 1e9, 2),
+                    task_total_s=round(t3 - t0, 4), bit_exact=bool(exact),
+                    pack_threads=args.threads or min(8, os.cpu_count() or 1))
+        print(json.dumps(line), flush=True)
+        del states, updates, out, ref
+    for p in paths:
+        p.unlink()
+
+
+if __name__ == "__main__":
+    main()
