@@ -347,7 +347,9 @@ class AggregationEngine:
             for layout, host_out, ev, _hin, _dev, _plan in pending:
                 kernel_ms += ev[0].elapsed_time(ev[1])
                 d2h_ms += ev[1].elapsed_time(ev[2])
-                flat = np.array(host_out.numpy()[: layout.M], copy=True)
+                # zero-copy: the per-layer views keep the pinned output block alive (its ndarray
+                # base is the tensor), so it is recycled only once the caller drops the result
+                flat = host_out.numpy()[: layout.M]
                 for li, arr in layout.unpack(flat):
                     results[li] = arr
         tm = self.last_timing

@@ -24,6 +24,8 @@ from pathlib import Path
 
 import numpy as np
 
+sys.dont_write_bytecode = True  # never write into /root/reference
+
 REF = Path("/root/reference")
 OUT = Path(__file__).resolve().parent
 
