@@ -123,11 +123,56 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
                            void* stream);
 
 /* ---------------------------------------------------------------------------
+ * dtype plumbing (device side, NumPy semantics).  Kinds: */
+enum {
+  FEDAGG_F16 = 0, FEDAGG_F32 = 1, FEDAGG_F64 = 2,
+  FEDAGG_I8 = 3, FEDAGG_I16 = 4, FEDAGG_I32 = 5, FEDAGG_I64 = 6,
+  FEDAGG_U8 = 7, FEDAGG_U16 = 8, FEDAGG_U32 = 9, FEDAGG_U64 = 10, FEDAGG_BOOL = 11,
+};
+/* out[i] = (out_kind) in[i]: integer/bool -> float as NumPy's astype (round to nearest),
+ * float widening exact.  Used for integer layers (x_int * python_float is a float64 loop). */
+int fedagg_cast(const void* d_in, int in_kind, void* d_out, int out_kind, uint64_t n, void* stream);
+/* out[i] = (out_kind) fl_in(in[i] * fl_in(w)): one client's product in its own float type,
+ * then widened -- a layer whose clients carry different dtypes (fed_avg.py:221-222 stacks the
+ * per-client products, then promotes). */
+int fedagg_scale_cast(const void* d_in, int in_kind, double w, void* d_out, int out_kind, uint64_t n, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Measurement helper: streams M floats (16-B non-temporal loads, the load path of the
  * bucket kernels) and writes one float per workgroup to d_sink.  Gives the read-stream
  * ceiling the roofline fraction is also quoted against.
  * -------------------------------------------------------------------------*/
 int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Host runtime ("session"): one GPU, one HIP stream, grow-only HBM buffers, a pinned
+ * staging ring and a worker pool.  It replaces the plumbing around the reference's hot path
+ * (shared states arrive as host pickles, substratools_methods.py:54-66, and the result is
+ * pickled back, :82-86) without PyTorch on the task's critical path.
+ * -------------------------------------------------------------------------*/
+#define FEDAGG_SESSION_BUFFERS 16
+typedef struct fedagg_session fedagg_session;
+/* NULL on failure (no device, ...): see fedagg_last_error(). */
+fedagg_session* fedagg_session_create(int device);
+void fedagg_session_destroy(fedagg_session* s);
+/* the session's hipStream_t, to pass as `stream` to the kernel entry points */
+void* fedagg_session_stream(fedagg_session* s);
+/* knobs: "threads" (pack workers), "chunk_bytes" (pinned slot size), "slots" (ring length) */
+int fedagg_session_set(fedagg_session* s, const char* key, long long value);
+/* grow-only device buffer number `slot` (0..FEDAGG_SESSION_BUFFERS-1) of at least `bytes` */
+int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr);
+/* Pack K host rows into HBM: row k = concatenation of the nseg host segments
+ * h_seg[k*nseg + i] (seg_bytes[i] bytes each), written at d_dst + k*ld_bytes.  Host memory
+ * may be pageable; the copies are pipelined through the pinned ring and enqueued on the
+ * session stream (the host segments may be released once the call returns). */
+int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
+                         const void* const* h_seg, const uint64_t* seg_bytes);
+/* Copy `bytes` from HBM into (pageable) host memory; returns when the data is in h_dst. */
+int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes);
+int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes);
+int fedagg_session_sync(fedagg_session* s);
+/* wall time of the last stage / fetch call, seconds */
+int fedagg_session_timing(fedagg_session* s, double* stage_s, double* fetch_s);
 
 #ifdef __cplusplus
 }

@@ -1,10 +1,12 @@
 #!/usr/bin/env bash
-# End-to-end (host pickles -> GPU -> host) timing of the drop-in path.
+# End-to-end (host pickles -> GPU -> host) timing of the drop-in path + cold-start probe.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python tools/e2e_bench.py --K 8 --M 25000000 --reps 3 > gpurun_out/e2e_c2.log 2>&1 || exit $?
-timeout -k 10 900 python tools/e2e_bench.py --K 8 --M 25000000 --reps 2 --threads 16 > gpurun_out/e2e_c2_t16.log 2>&1 || exit $?
-timeout -k 10 900 python tools/e2e_bench.py --K 64 --M 4000000 --reps 2 --threads 16 > gpurun_out/e2e_k64.log 2>&1 || exit $?
+run() { local name=$1; shift; timeout -k 10 600 "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -n 4 gpurun_out/$name.log; [ $rc -eq 0 ] || exit $rc; }
+run cold_native python tools/coldstart_probe.py --mode native
+run cold_torch python tools/coldstart_probe.py --mode torch
+run e2e_c2 python tools/e2e_bench.py --K 8 --M 25000000 --reps 3
+run e2e_k64 python tools/e2e_bench.py --K 64 --M 4000000 --reps 2
 echo done

@@ -44,6 +44,18 @@ SIGNATURES = {
     "fedagg_equal_count_f32": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_equal_count_f64": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_read_probe_f32": (c_int, [c_void, c_u64, c_void, c_int, c_void]),
+    "fedagg_cast": (c_int, [c_void, c_int, c_void, c_int, c_u64, c_void]),
+    "fedagg_scale_cast": (c_int, [c_void, c_int, c_dbl, c_void, c_int, c_u64, c_void]),
+    "fedagg_session_create": (c_void, [c_int]),
+    "fedagg_session_destroy": (None, [c_void]),
+    "fedagg_session_stream": (c_void, [c_void]),
+    "fedagg_session_set": (c_int, [c_void, ctypes.c_char_p, ctypes.c_longlong]),
+    "fedagg_session_buffer": (c_int, [c_void, c_int, c_u64, P(c_void)]),
+    "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
+    "fedagg_session_fetch": (c_int, [c_void, c_void, c_void, c_u64]),
+    "fedagg_session_memset": (c_int, [c_void, c_void, c_int, c_u64]),
+    "fedagg_session_sync": (c_int, [c_void]),
+    "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
 ABI_VERSION = 2

@@ -795,6 +795,80 @@ __global__ void __launch_bounds__(FA_BLOCK)
 }
 
 // ------------------------------------------------------------------------------------
+// dtype plumbing on the device (exact widening casts; per-client pre-scaling for layers whose
+// clients do not share one dtype) -- NumPy semantics: int/bool -> float64 is the C cast
+// (round to nearest), float widening is exact, x * w is computed in x's own float type.
+// ------------------------------------------------------------------------------------
+template <typename TI>
+__device__ __forceinline__ double ld_as_double(const void* p, uint64_t i) {
+  return (double)static_cast<const TI*>(p)[i];
+}
+
+__device__ double load_kind(const void* p, int kind, uint64_t i) {
+  switch (kind) {
+    case FEDAGG_F16: return (double)static_cast<const _Float16*>(p)[i];
+    case FEDAGG_F32: return (double)static_cast<const float*>(p)[i];
+    case FEDAGG_F64: return static_cast<const double*>(p)[i];
+    case FEDAGG_I8: return ld_as_double<int8_t>(p, i);
+    case FEDAGG_I16: return ld_as_double<int16_t>(p, i);
+    case FEDAGG_I32: return ld_as_double<int32_t>(p, i);
+    case FEDAGG_I64: return ld_as_double<int64_t>(p, i);
+    case FEDAGG_U8: return ld_as_double<uint8_t>(p, i);
+    case FEDAGG_U16: return ld_as_double<uint16_t>(p, i);
+    case FEDAGG_U32: return ld_as_double<uint32_t>(p, i);
+    case FEDAGG_U64: return ld_as_double<uint64_t>(p, i);
+    case FEDAGG_BOOL: return static_cast<const uint8_t*>(p)[i] ? 1.0 : 0.0;
+    default: return 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(FA_BLOCK)
+    cast_kernel(const void* __restrict__ in, int in_kind, void* __restrict__ out, int out_kind, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x; i < n; i += stride) {
+    if (in_kind == FEDAGG_I64 || in_kind == FEDAGG_U64) {
+      // 64-bit integers: convert straight to the output type (one rounding, like NumPy)
+      if (out_kind == FEDAGG_F64)
+        static_cast<double*>(out)[i] = in_kind == FEDAGG_I64 ? (double)static_cast<const int64_t*>(in)[i]
+                                                            : (double)static_cast<const uint64_t*>(in)[i];
+      else
+        static_cast<float*>(out)[i] = in_kind == FEDAGG_I64 ? (float)static_cast<const int64_t*>(in)[i]
+                                                           : (float)static_cast<const uint64_t*>(in)[i];
+      continue;
+    }
+    const double v = load_kind(in, in_kind, i);  // exact for every other supported input
+    if (out_kind == FEDAGG_F64)
+      static_cast<double*>(out)[i] = v;
+    else if (out_kind == FEDAGG_F32)
+      static_cast<float*>(out)[i] = (float)v;
+    else
+      static_cast<_Float16*>(out)[i] = (_Float16)v;
+  }
+}
+
+__global__ void __launch_bounds__(FA_BLOCK)
+    scale_cast_kernel(const void* __restrict__ in, int in_kind, double w, void* __restrict__ out, int out_kind,
+                      uint64_t n) {
+#pragma clang fp contract(off)
+  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x; i < n; i += stride) {
+    double p;
+    if (in_kind == FEDAGG_F16)
+      p = (double)(static_cast<const _Float16*>(in)[i] * (_Float16)w);
+    else if (in_kind == FEDAGG_F32)
+      p = (double)(static_cast<const float*>(in)[i] * (float)w);
+    else
+      p = static_cast<const double*>(in)[i] * w;
+    if (out_kind == FEDAGG_F64)
+      static_cast<double*>(out)[i] = p;
+    else if (out_kind == FEDAGG_F32)
+      static_cast<float*>(out)[i] = (float)p;
+    else
+      static_cast<_Float16*>(out)[i] = (_Float16)p;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // read-stream probe (same 16-B non-temporal load path as the bucket kernels)
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(FA_BLOCK) read_probe_kernel(const float* __restrict__ x, uint64_t nvec,
@@ -1107,6 +1181,10 @@ const T* cptr(const void* p) {
 
 }  // namespace
 
+namespace fedagg_internal {
+void set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
+}  // namespace fedagg_internal
+
 // ======================================================================================
 // C ABI
 // ======================================================================================
@@ -1179,6 +1257,26 @@ int fedagg_equal_count_f32(const float* const* d_copies, int K, uint64_t M, unsi
 int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, unsigned long long* d_mismatches,
                            void* stream) {
   return equal_launch<double>(d_copies, K, M, d_mismatches, (hipStream_t)stream);
+}
+
+static bool is_float_kind(int k) { return k == FEDAGG_F16 || k == FEDAGG_F32 || k == FEDAGG_F64; }
+
+int fedagg_cast(const void* d_in, int in_kind, void* d_out, int out_kind, uint64_t n, void* stream) {
+  if (!d_in || !d_out || in_kind < 0 || in_kind > FEDAGG_BOOL || !is_float_kind(out_kind))
+    return fail(FEDAGG_EINVAL, "fedagg_cast: unsupported kinds (out %lld)", out_kind);
+  if (n == 0) return FEDAGG_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(FA_BLOCK), 0, (hipStream_t)stream, d_in, in_kind, d_out,
+                     out_kind, n);
+  return check_launch("cast_kernel");
+}
+
+int fedagg_scale_cast(const void* d_in, int in_kind, double w, void* d_out, int out_kind, uint64_t n, void* stream) {
+  if (!d_in || !d_out || !is_float_kind(in_kind) || !is_float_kind(out_kind))
+    return fail(FEDAGG_EINVAL, "fedagg_scale_cast: float kinds only (in %lld)", in_kind);
+  if (n == 0) return FEDAGG_OK;
+  hipLaunchKernelGGL(scale_cast_kernel, dim3(grid_for(n)), dim3(FA_BLOCK), 0, (hipStream_t)stream, d_in, in_kind, w,
+                     d_out, out_kind, n);
+  return check_launch("scale_cast_kernel");
 }
 
 int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid, void* stream) {

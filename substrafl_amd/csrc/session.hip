@@ -1,0 +1,383 @@
+// session.hip -- native host runtime of the aggregation engine: one GPU, one HIP stream,
+// grow-only HBM buffers, a pinned staging ring and a worker pool that packs the clients'
+// host arrays into the ring while earlier chunks are already on the PCIe link.
+//
+// Why native: an aggregate task is one short-lived process (remote/register/register.py:96-121)
+// that receives K host pickles.  Doing the pack + H2D + D2H plumbing here (instead of through
+// PyTorch) keeps torch's CUDA context creation off the task's critical path and overlaps the
+// host memcpy with the DMA, which a Python loop cannot do without holding the GIL per chunk.
+//
+// Data path of fedagg_session_stage (one call per bucket):
+//   client k's row = its layer arrays back to back (segments); the row is cut into chunks of
+//   `chunk_bytes`; chunk u is packed by a worker into pinned slot u % R, then the main thread
+//   enqueues hipMemcpyAsync(slot -> HBM row k) on the session stream and records the slot's
+//   event; a slot is reused only after its event completed.  W workers, R >= W slots.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "fedagg.h"
+
+// defined in fedagg.hip
+extern "C" const char* fedagg_last_error(void);
+namespace fedagg_internal {
+void set_error(const char* msg);
+}
+
+namespace {
+
+int hip_fail(const char* what, hipError_t e) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+  fedagg_internal::set_error(buf);
+  return FEDAGG_EHIP;
+}
+
+#define HIP_TRY(call)                                     \
+  do {                                                    \
+    hipError_t e_ = (call);                               \
+    if (e_ != hipSuccess) return hip_fail(#call, e_);     \
+  } while (0)
+
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+  int size() const { return (int)th_.size(); }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [this] { return stop_ || !q_.empty(); });
+        if (stop_ && q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::deque<std::function<void()>> q_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+// completion flag for one packed chunk
+struct Done {
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;
+  void set() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      done = true;
+    }
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [this] { return done; });
+  }
+};
+
+}  // namespace
+
+struct fedagg_session {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int threads = 8;
+  uint64_t chunk_bytes = 16ull << 20;
+  int slots = 12;
+  std::vector<void*> ring;
+  std::vector<hipEvent_t> ring_ev;
+  std::vector<bool> ring_used;
+  void* dbuf[FEDAGG_SESSION_BUFFERS] = {};
+  uint64_t dbytes[FEDAGG_SESSION_BUFFERS] = {};
+  Pool* pool = nullptr;
+  double last_stage_s = 0, last_fetch_s = 0;
+
+  int ensure_ring() {
+    if ((int)ring.size() == slots) return FEDAGG_OK;
+    release_ring();
+    ring.assign(slots, nullptr);
+    ring_ev.assign(slots, nullptr);
+    ring_used.assign(slots, false);
+    for (int i = 0; i < slots; ++i) {
+      HIP_TRY(hipHostMalloc(&ring[i], chunk_bytes, hipHostMallocDefault));
+      HIP_TRY(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming));
+    }
+    return FEDAGG_OK;
+  }
+  void release_ring() {
+    for (size_t i = 0; i < ring.size(); ++i) {
+      if (ring_ev[i]) {
+        (void)hipEventSynchronize(ring_ev[i]);
+        (void)hipEventDestroy(ring_ev[i]);
+      }
+      if (ring[i]) (void)hipHostFree(ring[i]);
+    }
+    ring.clear();
+    ring_ev.clear();
+    ring_used.clear();
+  }
+  Pool& workers() {
+    if (!pool || pool->size() != threads) {
+      delete pool;
+      pool = new Pool(threads);
+    }
+    return *pool;
+  }
+};
+
+namespace {
+
+// Copy bytes [a, b) of the concatenation of segments (ptr[i], len[i]) into dst.
+void gather_range(const void* const* ptr, const uint64_t* len, int nseg, uint64_t a, uint64_t b, char* dst) {
+  uint64_t off = 0;
+  for (int i = 0; i < nseg && off < b; ++i) {
+    const uint64_t s0 = off, s1 = off + len[i];
+    off = s1;
+    const uint64_t lo = std::max(a, s0), hi = std::min(b, s1);
+    if (lo >= hi) continue;
+    memcpy(dst + (lo - a), static_cast<const char*>(ptr[i]) + (lo - s0), hi - lo);
+  }
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+extern "C" {
+
+fedagg_session* fedagg_session_create(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    hip_fail("fedagg_session_create: no HIP device", e == hipSuccess ? hipErrorNoDevice : e);
+    return nullptr;
+  }
+  if (device < 0 || device >= n) {
+    fedagg_internal::set_error("fedagg_session_create: device index out of range");
+    return nullptr;
+  }
+  if ((e = hipSetDevice(device)) != hipSuccess) {
+    hip_fail("hipSetDevice", e);
+    return nullptr;
+  }
+  auto* s = new fedagg_session();
+  s->device = device;
+  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) {
+    hip_fail("hipStreamCreate", e);
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void fedagg_session_destroy(fedagg_session* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  (void)hipStreamSynchronize(s->stream);
+  s->release_ring();
+  for (int i = 0; i < FEDAGG_SESSION_BUFFERS; ++i)
+    if (s->dbuf[i]) (void)hipFree(s->dbuf[i]);
+  (void)hipStreamDestroy(s->stream);
+  delete s->pool;
+  delete s;
+}
+
+void* fedagg_session_stream(fedagg_session* s) { return s ? (void*)s->stream : nullptr; }
+
+int fedagg_session_set(fedagg_session* s, const char* key, long long value) {
+  if (!s || !key) return FEDAGG_EINVAL;
+  if (!strcmp(key, "threads") && value >= 1 && value <= 256) {
+    s->threads = (int)value;
+    if (s->slots < s->threads + 2) {
+      s->release_ring();
+      s->slots = s->threads + 2;
+    }
+  } else if (!strcmp(key, "chunk_bytes") && value >= (1 << 16)) {
+    s->release_ring();
+    s->chunk_bytes = (uint64_t)value;
+  } else if (!strcmp(key, "slots") && value >= 2 && value <= 1024) {
+    s->release_ring();
+    s->slots = (int)std::max<long long>(value, s->threads + 1);
+  } else {
+    fedagg_internal::set_error("fedagg_session_set: unknown key or bad value");
+    return FEDAGG_EINVAL;
+  }
+  return FEDAGG_OK;
+}
+
+int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr) {
+  if (!s || slot < 0 || slot >= FEDAGG_SESSION_BUFFERS || !d_ptr) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(s->device));
+  if (s->dbytes[slot] < bytes) {
+    if (s->dbuf[slot]) {
+      HIP_TRY(hipStreamSynchronize(s->stream));
+      HIP_TRY(hipFree(s->dbuf[slot]));
+      s->dbuf[slot] = nullptr;
+      s->dbytes[slot] = 0;
+    }
+    HIP_TRY(hipMalloc(&s->dbuf[slot], bytes));
+    s->dbytes[slot] = bytes;
+  }
+  *d_ptr = s->dbuf[slot];
+  return FEDAGG_OK;
+}
+
+int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
+                         const void* const* h_seg, const uint64_t* seg_bytes) {
+  if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes))) return FEDAGG_EINVAL;
+  const double t0 = now_s();
+  HIP_TRY(hipSetDevice(s->device));
+  int rc = s->ensure_ring();
+  if (rc) return rc;
+  uint64_t row = 0;
+  for (int i = 0; i < nseg; ++i) row += seg_bytes[i];
+  if (row > ld_bytes) {
+    fedagg_internal::set_error("fedagg_session_stage: segments exceed the row stride");
+    return FEDAGG_EINVAL;
+  }
+  for (int k = 0; k < K; ++k)
+    for (int i = 0; i < nseg; ++i)
+      if (!h_seg[(size_t)k * nseg + i] && seg_bytes[i]) {
+        fedagg_internal::set_error("fedagg_session_stage: NULL host segment");
+        return FEDAGG_EINVAL;
+      }
+  const uint64_t cb = s->chunk_bytes;
+  const uint64_t per_row = row ? (row + cb - 1) / cb : 0;
+  const uint64_t units = per_row * (uint64_t)K;
+  const int R = (int)s->ring.size();
+  Pool& pool = s->workers();
+  std::vector<Done> done(units ? std::min<uint64_t>(units, (uint64_t)R) : 1);
+  // In-order window: unit u lives in slot u % R.  R-1 packs run ahead of the copy being
+  // enqueued; a slot is refilled only after the copy that read it completed, while the next
+  // copy is already in flight, so the link never waits on the main thread.
+  uint64_t next_submit = 0;
+  auto submit = [&](uint64_t u) {
+    const int slot = (int)(u % R);
+    if (s->ring_used[slot]) (void)hipEventSynchronize(s->ring_ev[slot]);  // H2D of unit u-R done
+    s->ring_used[slot] = false;
+    Done& d = done[slot];
+    d.done = false;
+    const int k = (int)(u / per_row);
+    const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
+    const void* const* segs = h_seg + (size_t)k * nseg;
+    char* dst = static_cast<char*>(s->ring[slot]);
+    pool.submit([=, &d] {
+      gather_range(segs, seg_bytes, nseg, a, b, dst);
+      d.set();
+    });
+  };
+  for (; next_submit < units && next_submit + 1 < (uint64_t)R; ++next_submit) submit(next_submit);
+  for (uint64_t u = 0; u < units; ++u) {
+    const int slot = (int)(u % R);
+    done[slot].wait();
+    const int k = (int)(u / per_row);
+    const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
+    char* dst = static_cast<char*>(d_dst) + (uint64_t)k * ld_bytes + a;
+    HIP_TRY(hipMemcpyAsync(dst, s->ring[slot], b - a, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipEventRecord(s->ring_ev[slot], s->stream));
+    s->ring_used[slot] = true;
+    if (next_submit < units) submit(next_submit++);
+  }
+  s->last_stage_s = now_s() - t0;
+  return FEDAGG_OK;
+}
+
+int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes) {
+  if (!s || !d_src || (!h_dst && bytes)) return FEDAGG_EINVAL;
+  const double t0 = now_s();
+  HIP_TRY(hipSetDevice(s->device));
+  int rc = s->ensure_ring();
+  if (rc) return rc;
+  const uint64_t cb = s->chunk_bytes;
+  const uint64_t units = (bytes + cb - 1) / cb;
+  const int R = (int)s->ring.size();
+  Pool& pool = s->workers();
+  std::vector<Done> done(R);
+  std::vector<bool> pending(R, false);
+  // D2H chunk u into slot u % R; a worker copies it out once its event completes
+  for (uint64_t u = 0; u < units; ++u) {
+    const int slot = (int)(u % R);
+    if (pending[slot]) done[slot].wait();
+    const uint64_t a = u * cb, b = std::min(bytes, a + cb);
+    HIP_TRY(hipMemcpyAsync(s->ring[slot], static_cast<const char*>(d_src) + a, b - a, hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipEventRecord(s->ring_ev[slot], s->stream));
+    s->ring_used[slot] = true;
+    done[slot].done = false;
+    pending[slot] = true;
+    hipEvent_t ev = s->ring_ev[slot];
+    char* src = static_cast<char*>(s->ring[slot]);
+    char* dst = static_cast<char*>(h_dst) + a;
+    Done* d = &done[slot];
+    pool.submit([=] {
+      (void)hipEventSynchronize(ev);
+      memcpy(dst, src, b - a);
+      d->set();
+    });
+  }
+  for (int i = 0; i < R; ++i)
+    if (pending[i]) done[i].wait();
+  s->last_fetch_s = now_s() - t0;
+  return FEDAGG_OK;
+}
+
+int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes) {
+  if (!s || !d) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipMemsetAsync(d, value, bytes, s->stream));
+  return FEDAGG_OK;
+}
+
+int fedagg_session_sync(fedagg_session* s) {
+  if (!s) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  return FEDAGG_OK;
+}
+
+int fedagg_session_timing(fedagg_session* s, double* stage_s, double* fetch_s) {
+  if (!s) return FEDAGG_EINVAL;
+  if (stage_s) *stage_s = s->last_stage_s;
+  if (fetch_s) *fetch_s = s->last_fetch_s;
+  return FEDAGG_OK;
+}
+
+}  // extern "C"

@@ -25,7 +25,6 @@ from __future__ import annotations
 import ctypes
 import os
 import time
-from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -88,6 +87,8 @@ def scaffold_weights(n_samples: Sequence[int]) -> np.ndarray:
 
 
 def _stream_handle(stream) -> int:
+    if isinstance(stream, int):
+        return stream
     torch = _torch()
     if stream is None:
         stream = torch.cuda.current_stream()
@@ -118,7 +119,7 @@ class FedAvgPlan:
         self.M = int(M)
         self._keep = (clients, out, ws)
         self._ptrs = _native.ptr_array(ptrs)
-        self._out = int(out.data_ptr())
+        self._out = _ptr(out)
         if kind in ("f32", "bf16"):
             self._w = (ctypes.c_float * self.K)(*[float(v) for v in np.asarray(weights, np.float32)])
         elif kind == "f64":
@@ -136,7 +137,7 @@ class FedAvgPlan:
                 nbytes = self.lib.fedagg_pairwise_ws_bytes(self.K, self.P, 8)
                 ws = torch.empty(nbytes, dtype=torch.uint8, device=out.device)
                 self._keep = (clients, out, ws)
-            self._ws = int(ws.data_ptr())
+            self._ws = _ptr(ws)
         self._main = getattr(self.lib, f"fedagg_fedavg_{kind}")
 
     def launch(self, stream=None) -> None:
@@ -169,10 +170,10 @@ class ScaffoldPlan:
         self._keep = [delta, cv, c, delta_out, c_out, ws]
         self._dp = _native.ptr_array(dp)
         self._cp = _native.ptr_array(cp)
-        self._c = int(c.data_ptr())
+        self._c = _ptr(c)
         self._w = (ctypes.c_double * self.K)(*[float(v) for v in np.asarray(weights, np.float64)])
-        self._dout = int(delta_out.data_ptr())
-        self._cout = int(c_out.data_ptr())
+        self._dout = _ptr(delta_out)
+        self._cout = _ptr(c_out)
         idx = np.asarray(pairwise_idx if pairwise_idx is not None else [], dtype=np.uint64)
         self.P = int(idx.size)
         self._idx = (ctypes.c_uint64 * max(1, self.P))(*[int(v) for v in idx])
@@ -183,7 +184,7 @@ class ScaffoldPlan:
                 ws = torch.empty(self.lib.fedagg_pairwise_ws_bytes(self.K, self.P, 8), dtype=torch.uint8,
                                  device=delta_out.device)
                 self._keep.append(ws)
-            self._ws = int(ws.data_ptr())
+            self._ws = _ptr(ws)
         self._main = getattr(self.lib, f"fedagg_scaffold_{kind}")
 
     def launch(self, stream=None) -> None:
@@ -201,11 +202,17 @@ def equal_count(kind: str, copies, M: int, counter, stream=None) -> None:
     lib = _native.load()
     ptrs = _row_pointers(copies)
     fn = getattr(lib, f"fedagg_equal_count_{kind}")
-    _native.check(fn(_native.ptr_array(ptrs), len(ptrs), int(M), int(counter.data_ptr()), _stream_handle(stream)),
+    _native.check(fn(_native.ptr_array(ptrs), len(ptrs), int(M), _ptr(counter), _stream_handle(stream)),
                   "equal_count")
 
 
+def _ptr(x) -> int:
+    return int(x) if isinstance(x, int) else int(x.data_ptr())
+
+
 def _row_pointers(clients) -> List[int]:
+    if isinstance(clients, (list, tuple)) and all(isinstance(c, int) for c in clients):
+        return [int(c) for c in clients]
     torch = _torch()
     if isinstance(clients, torch.Tensor):
         if clients.dim() != 2:
@@ -230,156 +237,111 @@ def _row_pointers(clients) -> List[int]:
 # host entry (drop-in path)
 # ======================================================================================
 class AggregationEngine:
-    """Per-process engine bound to one GPU (``device`` or ``LOCAL_RANK`` or 0), created lazily."""
+    """Drop-in host path bound to one GPU (``device``, else ``LOCAL_RANK``, else 0).
+
+    Runs on the native session (:mod:`substrafl_amd.runtime`): pinned-ring pack + H2D, the HIP
+    kernels on the session stream, D2H into owned NumPy arrays.  No PyTorch on this path."""
+
+    # HBM buffer slots of the session
+    _B_BUCKET, _B_OUT, _B_WS, _B_TMP, _B_CV, _B_C, _B_COUT, _B_CNT = range(8)
 
     def __init__(self, device: Optional[int] = None, pack_threads: Optional[int] = None):
         self._device_index = device
         self._pack_threads = pack_threads
         self.last_timing: Dict[str, float] = {}
 
-    # ----------------------------------------------------------------------------------
-    def _setup(self):
-        torch = _torch()
-        _native.load()
-        if not torch.cuda.is_available():
-            raise _native.NativeLibraryError(
-                "no ROCm GPU visible to this process: the aggregation engine runs on MI355X only (no CPU fallback)"
-            )
+    def session(self):
+        from . import runtime
+
         idx = self._device_index
         if idx is None:
-            idx = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-        self.device = torch.device("cuda", idx)
-        return torch
-
-    def _pool(self, n):
-        t = self._pack_threads or min(8, os.cpu_count() or 1)
-        return ThreadPoolExecutor(max_workers=max(1, min(t, n)))
+            idx = int(os.environ.get("LOCAL_RANK", "0"))
+        s = runtime.session(idx)
+        if self._pack_threads:
+            s.set("threads", self._pack_threads)
+        return s
 
     # ----------------------------------------------------------------------------------
-    def _stage(self, rows: List[List[np.ndarray]], layout: BucketLayout, K: int):
-        """Pack K clients' layers into a pinned [K, ld] staging buffer and copy it to HBM.
-
-        Rows are packed by a thread pool; each row's H2D copy is enqueued as soon as that row is
-        packed, so the PCIe transfer of client k overlaps the packing of the clients after it."""
-        torch = self._setup() if not hasattr(self, "device") else _torch()
-        tdt = torch_dtype(layout.dtype)
-        t0 = time.perf_counter()
-        host = torch.empty((K, layout.ld), dtype=tdt, pin_memory=True)
-        t1 = time.perf_counter()
-        dev = torch.empty((K, layout.ld), dtype=tdt, device=self.device)
-        hv = host.numpy()
-        if K > 1:
-            with self._pool(K) as ex:
-                futs = [ex.submit(layout.pack_row, rows[k], hv[k]) for k in range(K)]
-                for k, f in enumerate(futs):
-                    f.result()
-                    dev[k].copy_(host[k], non_blocking=True)
-        else:
-            layout.pack_row(rows[0], hv[0])
-            dev.copy_(host, non_blocking=True)
-        t2 = time.perf_counter()
-        tm = self.last_timing
-        tm["pin_alloc_s"] = tm.get("pin_alloc_s", 0.0) + t1 - t0
-        tm["pack_enqueue_s"] = tm.get("pack_enqueue_s", 0.0) + t2 - t1
-        tm["h2d_bytes"] = tm.get("h2d_bytes", 0) + K * layout.ld * host.element_size()
-        return dev, host
-
-    def _fetch(self, dev_out, layout: BucketLayout) -> np.ndarray:
-        torch = _torch()
-        host = torch.empty(dev_out.shape, dtype=dev_out.dtype, pin_memory=True)
-        host.copy_(dev_out, non_blocking=True)
-        return host
+    def _stage_rows(self, s, rows: List[List[np.ndarray]], layout: BucketLayout, d_bucket: int,
+                    prescale: Optional[Dict[int, float]] = None) -> None:
+        """Stage K clients' arrays (in ``layout`` segment order) as ``[K, ld]`` rows of
+        ``layout.dtype`` at ``d_bucket``.  Arrays of another dtype are staged raw and converted on
+        the device (exact casts); clients listed in ``prescale`` are multiplied by their weight in
+        their own float type first (mixed-dtype layers)."""
+        isz = layout.dtype.itemsize
+        ld_bytes = layout.ld * isz
+        prescale = prescale or {}
+        direct = not prescale and all(a.dtype == layout.dtype for row in rows for a in row)
+        if direct:
+            s.stage(d_bucket, ld_bytes, rows)
+            return
+        for k, row in enumerate(rows):
+            for seg, a in zip(layout.segments, row):
+                dst = d_bucket + k * ld_bytes + seg.offset * isz
+                if k not in prescale and a.dtype == layout.dtype:
+                    s.stage(dst, a.nbytes, [[a]])
+                    continue
+                tmp = s.buffer(self._B_TMP, a.nbytes)
+                s.stage(tmp, a.nbytes, [[a]])
+                if k in prescale:
+                    s.scale_cast(tmp, a.dtype, prescale[k], dst, layout.dtype, a.size)
+                else:
+                    s.cast(tmp, a.dtype, dst, layout.dtype, a.size)
+                s.sync()  # tmp is reused by the next segment's stage
 
     # ----------------------------------------------------------------------------------
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int]) -> List[np.ndarray]:
         """GPU equivalent of fed_avg.py:217-222 for validated inputs (same layer count and shapes
         across clients, ``sum(n_samples) != 0``).  Returns one array per layer (0-d layers as
         NumPy scalars, like ``np.sum``)."""
-        torch = self._setup()
-        self.last_timing = {}
         t_start = time.perf_counter()
+        s = self.session()
+        self.last_timing = tm = {}
         K = len(parameters_updates)
         L = len(parameters_updates[0])
         if L == 0:
             return []
-        # group layers by (result dtype, per-client product dtypes); NumPy promotion per layer
+        # group layers by (result dtype, per-client product dtypes): NumPy promotion per layer
         groups: Dict[Tuple, List[int]] = {}
         for li in range(L):
             pds = tuple(np.result_type(pu[li].dtype, 1.0) for pu in parameters_updates)
             for d in pds:
-                if d.kind != "f" or d not in (np.float16, np.float32, np.float64):
+                if d not in (np.float16, np.float32, np.float64):
                     raise NotImplementedError(f"FedAvg engine: unsupported layer dtype {d}")
             R = np.result_type(*pds)
             key = (R.str, None if all(d == R for d in pds) else tuple(d.str for d in pds))
             groups.setdefault(key, []).append(li)
 
-        stream = torch.cuda.current_stream(self.device)
         results: List[Optional[np.ndarray]] = [None] * L
-        pending = []
-        with torch.cuda.device(self.device):
-            for (rstr, mixed), layer_ids in groups.items():
-                R = np.dtype(rstr)
-                kind = kind_of(R)
-                shapes = [parameters_updates[0][li].shape for li in layer_ids]
-                layout = BucketLayout(layer_ids, shapes, R)
-                w = fedavg_weights(n_samples, kind)
-                if mixed is None:
-                    dev, host_in = self._stage(parameters_updates, layout, K)
-                else:
-                    dev, host_in = self._stage_mixed(parameters_updates, layout, K, mixed, n_samples)
-                    w = np.ones(K, dtype=w.dtype)
-                    for k, d in enumerate(mixed):
-                        if np.dtype(d) == R:
-                            w[k] = fedavg_weights(n_samples, kind)[k]
-                out = torch.empty(layout.ld, dtype=torch_dtype(kind), device=self.device)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-                ev[0].record(stream)  # after the H2D copies
-                plan = FedAvgPlan(kind, dev, w, layout.M, out, layout.pairwise_idx)
-                plan.launch(stream)
-                ev[1].record(stream)
-                host_out = self._fetch(out, layout)
-                ev[2].record(stream)
-                pending.append((layout, host_out, ev, host_in, dev, plan))
-            t_wait = time.perf_counter()
-            stream.synchronize()
-            t_sync = time.perf_counter()
-            kernel_ms = d2h_ms = 0.0
-            for layout, host_out, ev, _hin, _dev, _plan in pending:
-                kernel_ms += ev[0].elapsed_time(ev[1])
-                d2h_ms += ev[1].elapsed_time(ev[2])
-                # zero-copy: the per-layer views keep the pinned output block alive (its ndarray
-                # base is the tensor), so it is recycled only once the caller drops the result
-                flat = host_out.numpy()[: layout.M]
-                for li, arr in layout.unpack(flat):
-                    results[li] = arr
-        tm = self.last_timing
-        tm["kernel_s"] = kernel_ms / 1e3
-        tm["d2h_s"] = d2h_ms / 1e3
-        tm["sync_wait_s"] = t_sync - t_wait
-        tm["unpack_s"] = time.perf_counter() - t_sync
+        for (rstr, mixed), layer_ids in groups.items():
+            R = np.dtype(rstr)
+            kind = kind_of(R)
+            layout = BucketLayout(layer_ids, [parameters_updates[0][li].shape for li in layer_ids], R)
+            rows = [[pu[li] for li in layer_ids] for pu in parameters_updates]
+            w = fedavg_weights(n_samples, kind)
+            prescale = None
+            if mixed is not None:
+                w64 = [int(n) / sum(int(m) for m in n_samples) for n in n_samples]
+                prescale = {k: w64[k] for k, d in enumerate(mixed) if np.dtype(d) != R}
+                for k in prescale:
+                    w[k] = 1  # x * 1 is exact: the client's product was formed in its own dtype
+            d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * R.itemsize)
+            t0 = time.perf_counter()
+            self._stage_rows(s, rows, layout, d_bucket, prescale)
+            tm["stage_s"] = tm.get("stage_s", 0.0) + time.perf_counter() - t0
+            d_out = s.buffer(self._B_OUT, layout.ld * R.itemsize)
+            ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, layout.pairwise_idx.size, 8))
+            ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
+            t1 = time.perf_counter()
+            FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
+            out = np.empty(layout.M, dtype=R)
+            s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
+            tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
+            for li, arr in layout.unpack(out):
+                results[li] = arr
+        tm.update({f"native_{k}": v for k, v in s.timing().items()})
         tm["total_s"] = time.perf_counter() - t_start
         return results  # type: ignore[return-value]
-
-    def _stage_mixed(self, parameters_updates, layout: BucketLayout, K: int, pds, n_samples):
-        """Mixed-dtype layer group (e.g. fp32 and fp64 clients): NumPy computes each client's
-        product in its own dtype and then upcasts it when stacking (fed_avg.py:221-222).  Clients
-        whose product dtype differs from the result dtype are pre-multiplied on the device in their
-        own dtype (one IEEE multiply), cast exactly to the result dtype, and enter the bucket
-        kernel with weight 1 (x * 1 is exact)."""
-        torch = _torch()
-        dev, host = self._stage(parameters_updates, layout, K)  # rows for same-dtype clients
-        R = layout.dtype
-        for k, d in enumerate(pds):
-            d = np.dtype(d)
-            if d == R:
-                continue
-            sub = BucketLayout([s.layer for s in layout.segments], [s.shape for s in layout.segments], d)
-            h = np.empty(sub.ld, dtype=d)
-            sub.pack_row(parameters_updates[k], h)
-            t = torch.from_numpy(h[: sub.M]).to(self.device)
-            wk = torch.tensor(fedavg_weights(n_samples, kind_of(d))[k], dtype=t.dtype, device=self.device)
-            dev[k, : layout.M].copy_(torch.mul(t, wk).to(torch_dtype(R)))
-        return dev, host
 
     # ----------------------------------------------------------------------------------
     def scaffold(
@@ -393,72 +355,69 @@ class AggregationEngine:
         """GPU equivalent of scaffold.py:193-196 (c equality check, returned as the mismatch
         count) and scaffold.py:297-337 (fp64 reductions).  Returns
         ``(mismatches, new_server_control_variate, avg_parameters_update)``."""
-        torch = self._setup()
-        self.last_timing = {}
         t_start = time.perf_counter()
+        s = self.session()
+        self.last_timing = tm = {}
         K = len(parameters_updates)
         L = len(parameters_updates[0])
         if L == 0:
             return 0, [], []
-        all_f32 = all(
-            a.dtype == np.float32
-            for lst in (parameters_updates, control_variate_updates, server_control_variates)
-            for client in lst
-            for a in client
-        )
-        for lst in (parameters_updates, control_variate_updates, server_control_variates):
+        lists = (parameters_updates, control_variate_updates, server_control_variates)
+        for lst in lists:
             for client in lst:
                 for a in client:
-                    if a.dtype.kind not in "biuf":
+                    if a.dtype.kind not in "biuf" or a.dtype == np.longdouble:
                         raise NotImplementedError(f"Scaffold engine: unsupported dtype {a.dtype}")
+        all_f32 = all(a.dtype == np.float32 for lst in lists for client in lst for a in client)
         kind = "f32" if all_f32 else "f64"
-        sdt = np.float32 if all_f32 else np.float64
+        sdt = np.dtype(np.float32 if all_f32 else np.float64)
         lid = list(range(L))
         lay_d = BucketLayout(lid, [a.shape for a in parameters_updates[0]], sdt)
         lay_c = BucketLayout(lid, [a.shape for a in control_variate_updates[0]], sdt)
         lay_s = BucketLayout(lid, [a.shape for a in server_control_variates[0]], sdt)
         w = scaffold_weights(n_samples)
         lr = float(aggregation_lr)
-        stream = torch.cuda.current_stream(self.device)
-        with torch.cuda.device(self.device):
-            d_dev, h1 = self._stage(parameters_updates, lay_d, K)
-            c_dev, h2 = self._stage(control_variate_updates, lay_c, K)
-            s_dev, h3 = self._stage(server_control_variates, lay_s, K)
-            counter = torch.zeros(1, dtype=torch.int64, device=self.device)
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev0.record(stream)
-            equal_count(kind, s_dev, lay_s.M, counter, stream)
-            same = [s.shape for s in lay_d.segments] == [s.shape for s in lay_c.segments]
-            dout = torch.empty(lay_d.ld, dtype=torch.float64, device=self.device)
-            cout = torch.empty(lay_c.ld, dtype=torch.float64, device=self.device)
-            c_row = s_dev[0]
-            if same:
-                ScaffoldPlan(kind, d_dev, c_dev, c_row, w, lay_d.M, lr, dout, cout, lay_d.pairwise_idx).launch(stream)
-            else:
-                # delta and control-variate layers have different shapes: run the two
-                # reductions as two passes of the fused kernel (the unused half is scratch)
-                scratch_c = torch.empty(lay_d.ld, dtype=torch.float64, device=self.device)
-                zeros = torch.zeros(lay_d.ld, dtype=d_dev.dtype, device=self.device)
-                ScaffoldPlan(kind, d_dev, d_dev, zeros, w, lay_d.M, lr, dout, scratch_c,
-                             lay_d.pairwise_idx).launch(stream)
-                scratch_d = torch.empty(lay_c.ld, dtype=torch.float64, device=self.device)
-                ScaffoldPlan(kind, c_dev, c_dev, c_row, w, lay_c.M, lr, scratch_d, cout,
-                             lay_c.pairwise_idx).launch(stream)
-            ev1.record(stream)
-            hd = self._fetch(dout, lay_d)
-            hc = self._fetch(cout, lay_c)
-            hcnt = torch.empty(1, dtype=torch.int64, pin_memory=True)
-            hcnt.copy_(counter, non_blocking=True)
-            stream.synchronize()
-            mismatches = int(hcnt.item())
-            flat_d = np.array(hd.numpy()[: lay_d.M], copy=True)
-            flat_c = np.array(hc.numpy()[: lay_c.M], copy=True)
-        avg = [a for _, a in lay_d.unpack(flat_d)]
-        new_c = [a for _, a in lay_c.unpack(flat_c)]
-        self.last_timing["kernel_s"] = ev0.elapsed_time(ev1) / 1e3
-        self.last_timing["total_s"] = time.perf_counter() - t_start
-        return mismatches, new_c, avg
+        isz = sdt.itemsize
+        t0 = time.perf_counter()
+        d_d = s.buffer(self._B_BUCKET, K * lay_d.ld * isz)
+        d_cv = s.buffer(self._B_CV, K * lay_c.ld * isz)
+        d_cc = s.buffer(self._B_C, K * lay_s.ld * isz)
+        self._stage_rows(s, [list(r) for r in parameters_updates], lay_d, d_d)
+        self._stage_rows(s, [list(r) for r in control_variate_updates], lay_c, d_cv)
+        self._stage_rows(s, [list(r) for r in server_control_variates], lay_s, d_cc)
+        tm["stage_s"] = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        cnt = s.buffer(self._B_CNT, 8)
+        s.memset(cnt, 0, 8)
+        equal_count(kind, [d_cc + k * lay_s.ld * isz for k in range(K)], lay_s.M, cnt, s.stream)
+        dout = s.buffer(self._B_OUT, lay_d.ld * 8)
+        cout = s.buffer(self._B_COUT, lay_c.ld * 8)
+        ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, max(1, lay_d.pairwise_idx.size), 8))
+        rows_d = [d_d + k * lay_d.ld * isz for k in range(K)]
+        rows_c = [d_cv + k * lay_c.ld * isz for k in range(K)]
+        if [g.shape for g in lay_d.segments] == [g.shape for g in lay_c.segments]:
+            ScaffoldPlan(kind, rows_d, rows_c, d_cc, w, lay_d.M, lr, dout, cout, lay_d.pairwise_idx, ws).launch(s.stream)
+        else:
+            # delta and control-variate layers have different shapes: two passes of the fused
+            # kernel, each one's other half written to scratch
+            scratch = s.buffer(self._B_TMP, max(lay_d.ld, lay_c.ld) * 8 + 16)
+            zeros = s.buffer(self._B_CNT + 1, lay_d.ld * isz)
+            s.memset(zeros, 0, lay_d.ld * isz)
+            ScaffoldPlan(kind, rows_d, rows_d, zeros, w, lay_d.M, lr, dout, scratch, lay_d.pairwise_idx,
+                         ws).launch(s.stream)
+            ScaffoldPlan(kind, rows_c, rows_c, d_cc, w, lay_c.M, lr, scratch, cout, lay_c.pairwise_idx,
+                         ws).launch(s.stream)
+        out_d = np.empty(lay_d.M, np.float64)
+        out_c = np.empty(lay_c.M, np.float64)
+        mism = np.zeros(1, np.int64)
+        s.fetch(cnt, mism)
+        s.fetch(dout, out_d)
+        s.fetch(cout, out_c)
+        tm["kernel_fetch_s"] = time.perf_counter() - t1
+        avg = [a for _, a in lay_d.unpack(out_d)]
+        new_c = [a for _, a in lay_c.unpack(out_c)]
+        tm["total_s"] = time.perf_counter() - t_start
+        return int(mism[0]), new_c, avg
 
 
 _default_engine: Optional[AggregationEngine] = None

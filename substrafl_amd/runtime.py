@@ -1,0 +1,143 @@
+"""Python handle on the native host runtime (``fedagg_session_*`` in include/fedagg.h).
+
+A :class:`Session` owns one GPU, one HIP stream, grow-only HBM buffers and the pinned staging
+ring of ``libfedagg.so``; the drop-in aggregation path (:mod:`substrafl_amd.engine`) runs
+entirely through it, so an aggregate task process never creates a PyTorch CUDA context.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _native
+
+KIND_CODE = {
+    np.dtype(np.float16): 0,
+    np.dtype(np.float32): 1,
+    np.dtype(np.float64): 2,
+    np.dtype(np.int8): 3,
+    np.dtype(np.int16): 4,
+    np.dtype(np.int32): 5,
+    np.dtype(np.int64): 6,
+    np.dtype(np.uint8): 7,
+    np.dtype(np.uint16): 8,
+    np.dtype(np.uint32): 9,
+    np.dtype(np.uint64): 10,
+    np.dtype(np.bool_): 11,
+}
+
+
+def kind_code(dtype) -> int:
+    d = np.dtype(dtype)
+    if d not in KIND_CODE:
+        raise NotImplementedError(f"no device conversion for dtype {d}")
+    return KIND_CODE[d]
+
+
+class Session:
+    """One GPU's native runtime context (create lazily; never pickled)."""
+
+    def __init__(self, device: int = 0, threads: Optional[int] = None):
+        self.lib = _native.load()
+        h = self.lib.fedagg_session_create(int(device))
+        if not h:
+            raise _native.NativeLibraryError(
+                "cannot open a HIP session on device %d: %s (the aggregation engine runs on MI355X only, "
+                "no CPU fallback)" % (device, self.lib.fedagg_last_error().decode(errors="replace"))
+            )
+        self._h = ctypes.c_void_p(h)
+        self.device = int(device)
+        self.stream = int(self.lib.fedagg_session_stream(self._h) or 0)
+        nthreads = threads or int(os.environ.get("FEDAGG_PACK_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        self.set("threads", nthreads)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.fedagg_session_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __reduce__(self):
+        raise TypeError("a Session holds a GPU context and cannot be pickled")
+
+    # ----------------------------------------------------------------------------------
+    def set(self, key: str, value: int) -> None:
+        _native.check(self.lib.fedagg_session_set(self._h, key.encode(), int(value)), f"session_set({key})")
+
+    def buffer(self, slot: int, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        _native.check(self.lib.fedagg_session_buffer(self._h, int(slot), max(16, int(nbytes)), ctypes.byref(p)),
+                      "session_buffer")
+        return int(p.value)
+
+    def stage(self, d_dst: int, ld_bytes: int, rows: Sequence[Sequence[np.ndarray]]) -> None:
+        """rows[k] = client k's host arrays, in bucket order, each C-contiguous; row k lands at
+        ``d_dst + k * ld_bytes``."""
+        K = len(rows)
+        nseg = len(rows[0]) if K else 0
+        keep: List[np.ndarray] = []
+        ptrs = (ctypes.c_void_p * max(1, K * nseg))()
+        sizes = (ctypes.c_uint64 * max(1, nseg))()
+        for k, row in enumerate(rows):
+            if len(row) != nseg:
+                raise ValueError("every client row needs the same segments")
+            for i, a in enumerate(row):
+                a = np.ascontiguousarray(a)
+                keep.append(a)
+                ptrs[k * nseg + i] = a.ctypes.data if a.nbytes else None
+                if k == 0:
+                    sizes[i] = a.nbytes
+                elif a.nbytes != sizes[i]:
+                    raise ValueError("segment sizes differ between clients")
+        _native.check(self.lib.fedagg_session_stage(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K, nseg, ptrs,
+                                                    sizes), "session_stage")
+
+    def fetch(self, d_src: int, out: np.ndarray) -> np.ndarray:
+        """Copy ``out.nbytes`` from HBM into ``out`` (synchronous)."""
+        if not out.flags.c_contiguous:
+            raise ValueError("fetch destination must be C-contiguous")
+        _native.check(self.lib.fedagg_session_fetch(self._h, ctypes.c_void_p(d_src),
+                                                    ctypes.c_void_p(out.ctypes.data), out.nbytes), "session_fetch")
+        return out
+
+    def memset(self, d: int, value: int, nbytes: int) -> None:
+        _native.check(self.lib.fedagg_session_memset(self._h, ctypes.c_void_p(d), int(value), int(nbytes)),
+                      "session_memset")
+
+    def sync(self) -> None:
+        _native.check(self.lib.fedagg_session_sync(self._h), "session_sync")
+
+    def timing(self) -> Dict[str, float]:
+        a, b = ctypes.c_double(), ctypes.c_double()
+        self.lib.fedagg_session_timing(self._h, ctypes.byref(a), ctypes.byref(b))
+        return {"stage_s": a.value, "fetch_s": b.value}
+
+    # ----------------------------------------------------------------------------------
+    def cast(self, d_in: int, in_dtype, d_out: int, out_dtype, n: int) -> None:
+        _native.check(self.lib.fedagg_cast(ctypes.c_void_p(d_in), kind_code(in_dtype), ctypes.c_void_p(d_out),
+                                           kind_code(out_dtype), int(n), ctypes.c_void_p(self.stream)), "cast")
+
+    def scale_cast(self, d_in: int, in_dtype, w: float, d_out: int, out_dtype, n: int) -> None:
+        _native.check(self.lib.fedagg_scale_cast(ctypes.c_void_p(d_in), kind_code(in_dtype), float(w),
+                                                 ctypes.c_void_p(d_out), kind_code(out_dtype), int(n),
+                                                 ctypes.c_void_p(self.stream)), "scale_cast")
+
+
+_sessions: Dict[int, Session] = {}
+
+
+def session(device: int = 0) -> Session:
+    """The process-wide session of ``device`` (created on first use)."""
+    s = _sessions.get(device)
+    if s is None:
+        s = _sessions[device] = Session(device)
+    return s
