@@ -81,7 +81,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
+        # Parameter-range sharding has no data-path collective: the process group only carries
+        # the barrier and the max-over-ranks timing, on the host (gloo).
+        dist.init_process_group("gloo")
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)  # lets a 1-GPU box rehearse N > 1 (ranks then share the GPU)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     lib = _native.load()
@@ -142,7 +146,7 @@ def main():
     kern_ms = ev_start.elapsed_time(ev_end) / args.steps
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
