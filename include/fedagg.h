@@ -123,6 +123,28 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
                            void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Client-side flat-bucket ops (the producer / consumer of the buckets, SURVEY.md §8(a)
+ * a5-a7).  A model's L parameter tensors (device pointers d_layers[l], numel[l] fp32 elements
+ * each, in weight_manager.model_parameters order, weight_manager.py:53-76) map onto one flat
+ * bucket (layers back to back).  One launch per 32 layers instead of one torch op per layer.
+ *   gather:    flat = concat(layers)                       get_parameters  (weight_manager.py:79-100)
+ *   scatter:   layers = split(flat)                        set_parameters  (:215-238)
+ *   wsum:      flat = sum() of layers_j * coeffs[j]         weighted_sum_parameters (:182-212),
+ *              Python sum() order from int 0: acc = fl(0 + fl(x_0*fl32(c_0))), acc = fl(acc + fl(x_j*fl32(c_j)));
+ *              d_layers is list-major [nlists][L], nlists <= FEDAGG_FLAT_MAX_LISTS
+ *              (subtract_parameters :140-158 = coeffs {1,-1}; add_parameters :161-179 = {1,1};
+ *              Scaffold's control-variate update torch_scaffold_algo.py:451-458 = {-1, -1/(lr*n)})
+ *   increment: layers += fl32(multiplier) * flat           increment_parameters (:103-137)
+ * -------------------------------------------------------------------------*/
+#define FEDAGG_FLAT_MAX_LISTS 4
+int fedagg_flat_gather_f32(const float* const* d_layers, const uint64_t* numel, int L, float* d_flat, void* stream);
+int fedagg_flat_scatter_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat, void* stream);
+int fedagg_flat_wsum_f32(const float* const* d_layers, int nlists, const double* coeffs, const uint64_t* numel, int L,
+                         float* d_flat, void* stream);
+int fedagg_flat_increment_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat,
+                              double multiplier, void* stream);
+
+/* ---------------------------------------------------------------------------
  * dtype plumbing (device side, NumPy semantics).  Kinds: */
 enum {
   FEDAGG_F16 = 0, FEDAGG_F32 = 1, FEDAGG_F64 = 2,

@@ -45,6 +45,10 @@ SIGNATURES = {
     "fedagg_equal_count_f64": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_read_probe_f32": (c_int, [c_void, c_u64, c_void, c_int, c_void]),
     "fedagg_cast": (c_int, [c_void, c_int, c_void, c_int, c_u64, c_void]),
+    "fedagg_flat_gather_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_void]),
+    "fedagg_flat_scatter_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_void]),
+    "fedagg_flat_wsum_f32": (c_int, [P(c_void), c_int, P(c_dbl), P(c_u64), c_int, c_void, c_void]),
+    "fedagg_flat_increment_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_dbl, c_void]),
     "fedagg_scale_cast": (c_int, [c_void, c_int, c_dbl, c_void, c_int, c_u64, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),

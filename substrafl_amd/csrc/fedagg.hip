@@ -869,6 +869,98 @@ __global__ void __launch_bounds__(FA_BLOCK)
 }
 
 // ------------------------------------------------------------------------------------
+// Client-side flat-bucket ops: the producer / consumer of the
+// buckets, i.e. weight_manager's per-layer torch loops (weight_manager.py:103-238) done as one
+// launch over up to SEG_GROUP layers.  Workgroup b serves layer l with
+// block_start[l] <= b < block_start[l+1], elements [(b - block_start[l]) * SEG_CHUNK, ...).
+// Semantics follow the reference's torch ops bit for bit:
+//   weighted_sum_parameters (:182-212): Python sum() from int 0 over param * coeff, i.e.
+//     acc = fl(0 + fl(x_0 * fl32(c_0))); acc = fl(acc + fl(x_i * fl32(c_i)))  (-0 becomes +0)
+//   increment_parameters (:103-137):  w = fl(w + fl(fl32(mult) * u))
+//   get_parameters / set_parameters: plain copies.
+// ------------------------------------------------------------------------------------
+#define SEG_GROUP 32
+#define SEG_CHUNK 8192  // elements per workgroup
+
+struct SegArgs {
+  const void* p[FEDAGG_FLAT_MAX_LISTS][SEG_GROUP];  // list-major layer pointers
+  uint64_t n[SEG_GROUP];
+  uint64_t flat_off[SEG_GROUP];
+  uint32_t block_start[SEG_GROUP + 1];
+  float coeff[FEDAGG_FLAT_MAX_LISTS];
+  int nl, nlists;
+};
+
+__device__ __forceinline__ int seg_of_block(const SegArgs& a, uint32_t b) {
+  int l = 0;
+  while (l + 1 < a.nl && a.block_start[l + 1] <= b) ++l;  // scalar, <= SEG_GROUP steps
+  return l;
+}
+
+// op 0: gather (flat = p0), 1: scatter (p0 = flat), 2: wsum (flat = sum_i p_i * c_i),
+// 3: increment (p0 = p0 + c0 * flat)
+template <int OP>
+__global__ void __launch_bounds__(FA_BLOCK) flat_seg_kernel(const SegArgs a, float* __restrict__ flat) {
+#pragma clang fp contract(off)
+  const int l = seg_of_block(a, blockIdx.x);
+  const uint64_t base = (uint64_t)(blockIdx.x - a.block_start[l]) * SEG_CHUNK;
+  const uint64_t n = a.n[l];
+  float* f = flat + a.flat_off[l];
+  for (uint64_t i = base + threadIdx.x; i < base + SEG_CHUNK && i < n; i += FA_BLOCK) {
+    if constexpr (OP == 0) {
+      f[i] = static_cast<const float*>(a.p[0][l])[i];
+    } else if constexpr (OP == 1) {
+      const_cast<float*>(static_cast<const float*>(a.p[0][l]))[i] = f[i];
+    } else if constexpr (OP == 2) {
+      float acc = 0.0f + static_cast<const float*>(a.p[0][l])[i] * a.coeff[0];
+      for (int j = 1; j < a.nlists; ++j) {
+        const float t = static_cast<const float*>(a.p[j][l])[i] * a.coeff[j];
+        acc = acc + t;
+      }
+      f[i] = acc;
+    } else {
+      float* w = const_cast<float*>(static_cast<const float*>(a.p[0][l]));
+      const float t = a.coeff[0] * f[i];
+      w[i] = w[i] + t;
+    }
+  }
+}
+
+template <int OP>
+int flat_seg_launch(const void* const* ptrs, int nlists, const double* coeffs, const uint64_t* numel, int L,
+                    float* flat, hipStream_t s) {
+  if (L < 0 || nlists < 1 || nlists > FEDAGG_FLAT_MAX_LISTS || (L > 0 && (!ptrs || !numel || !flat)))
+    return fail(FEDAGG_EINVAL, "flat op: invalid argument (L=%lld)", L);
+  uint64_t off = 0;
+  for (int l0 = 0; l0 < L; l0 += SEG_GROUP) {
+    const int nl = (L - l0) < SEG_GROUP ? (L - l0) : SEG_GROUP;
+    SegArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nl = nl;
+    a.nlists = nlists;
+    for (int j = 0; j < nlists; ++j) a.coeff[j] = coeffs ? (float)coeffs[j] : 1.0f;  // fl32(python float)
+    uint64_t blocks = 0;
+    for (int l = 0; l < nl; ++l) {
+      for (int j = 0; j < nlists; ++j) {
+        a.p[j][l] = ptrs[(size_t)j * L + l0 + l];
+        if (!a.p[j][l] && numel[l0 + l]) return fail(FEDAGG_EINVAL, "flat op: NULL layer pointer %lld", l0 + l);
+      }
+      a.n[l] = numel[l0 + l];
+      a.flat_off[l] = off;
+      a.block_start[l] = (uint32_t)blocks;
+      off += numel[l0 + l];
+      blocks += (numel[l0 + l] + SEG_CHUNK - 1) / SEG_CHUNK;
+    }
+    a.block_start[nl] = (uint32_t)blocks;
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL((flat_seg_kernel<OP>), dim3((unsigned)blocks), dim3(FA_BLOCK), 0, s, a, flat);
+    int rc = check_launch("flat_seg_kernel");
+    if (rc) return rc;
+  }
+  return FEDAGG_OK;
+}
+
+// ------------------------------------------------------------------------------------
 // read-stream probe (same 16-B non-temporal load path as the bucket kernels)
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(FA_BLOCK) read_probe_kernel(const float* __restrict__ x, uint64_t nvec,
@@ -1257,6 +1349,26 @@ int fedagg_equal_count_f32(const float* const* d_copies, int K, uint64_t M, unsi
 int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, unsigned long long* d_mismatches,
                            void* stream) {
   return equal_launch<double>(d_copies, K, M, d_mismatches, (hipStream_t)stream);
+}
+
+int fedagg_flat_gather_f32(const float* const* d_layers, const uint64_t* numel, int L, float* d_flat,
+                           void* stream) {
+  return flat_seg_launch<0>(reinterpret_cast<const void* const*>(d_layers), 1, nullptr, numel, L, d_flat,
+                            (hipStream_t)stream);
+}
+int fedagg_flat_scatter_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat, void* stream) {
+  return flat_seg_launch<1>(reinterpret_cast<const void* const*>(d_layers), 1, nullptr, numel, L,
+                            const_cast<float*>(d_flat), (hipStream_t)stream);
+}
+int fedagg_flat_wsum_f32(const float* const* d_layers, int nlists, const double* coeffs, const uint64_t* numel, int L,
+                         float* d_flat, void* stream) {
+  return flat_seg_launch<2>(reinterpret_cast<const void* const*>(d_layers), nlists, coeffs, numel, L, d_flat,
+                            (hipStream_t)stream);
+}
+int fedagg_flat_increment_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat,
+                              double multiplier, void* stream) {
+  return flat_seg_launch<3>(reinterpret_cast<const void* const*>(d_layers), 1, &multiplier, numel, L,
+                            const_cast<float*>(d_flat), (hipStream_t)stream);
 }
 
 static bool is_float_kind(int k) { return k == FEDAGG_F16 || k == FEDAGG_F32 || k == FEDAGG_F64; }
