@@ -44,3 +44,12 @@ class ScaffoldSharedState(_Model):  # schemas.py:57-74
 class ScaffoldAveragedStates(_Model):  # schemas.py:77-87
     server_control_variate: List[np.ndarray]
     avg_parameters_update: List[np.ndarray]
+
+
+class FedPCAAveragedState(_Model):  # schemas.py:41-45
+    avg_parameters_update: List[np.ndarray]
+
+
+class FedPCASharedState(_Model):  # schemas.py:48-54
+    n_samples: int
+    parameters_update: List[np.ndarray]

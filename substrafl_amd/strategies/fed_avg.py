@@ -47,9 +47,6 @@ class FedAvg(Strategy):
     def name(self) -> StrategyName:
         return StrategyName.FEDERATED_AVERAGING
 
-    def _engine(self) -> AggregationEngine:
-        return default_engine() if self._device is None else AggregationEngine(self._device)
-
     @remote
     def avg_shared_states(self, shared_states: List[FedAvgSharedState]) -> FedAvgAveragedState:
         """Weighted average of the clients' ``parameters_update`` by ``n_samples`` (fed_avg.py:176-224).
@@ -61,24 +58,30 @@ class FedAvg(Strategy):
             ValueError: a layer's shape differs between clients (``np.sum``, fed_avg.py:222).
             pydantic.ValidationError: a 0-d layer (its average is a scalar, schemas.py:29).
         """
-        if len(shared_states) == 0:
-            raise EmptySharedStatesError(
-                "Your shared_states is empty. Please ensure that "
-                "the train method of your algorithm returns a FedAvgSharedState object."
-            )
-        parameters_update_len = len(shared_states[0].parameters_update)
-        assert all(
-            [len(shared_state.parameters_update) == parameters_update_len for shared_state in shared_states]
-        ), "Not the same number of layers for every input parameters."
-
-        n_samples = [state.n_samples for state in shared_states]
-        n_all_samples = sum(n_samples)
-        if parameters_update_len == 0:
-            return FedAvgAveragedState(avg_parameters_update=[])
-        if n_all_samples == 0:
-            raise ZeroDivisionError("division by zero")
-        updates = [list(state.parameters_update) for state in shared_states]
-        check_same_shapes(updates)
-
-        averaged_states = self._engine().fedavg(updates, n_samples)
+        averaged_states = weighted_average(shared_states, "FedAvgSharedState", self._device)
         return FedAvgAveragedState(avg_parameters_update=averaged_states)
+
+
+def weighted_average(shared_states, state_name: str, device: Optional[int] = None) -> List[np.ndarray]:
+    """fed_avg.py:207-222 (also fed_pca.py:244-257): validation on the host, the weighted sum
+    of every layer on the GPU."""
+    if len(shared_states) == 0:
+        raise EmptySharedStatesError(
+            "Your shared_states is empty. Please ensure that "
+            f"the train method of your algorithm returns a {state_name} object."
+        )
+    parameters_update_len = len(shared_states[0].parameters_update)
+    assert all(
+        [len(shared_state.parameters_update) == parameters_update_len for shared_state in shared_states]
+    ), "Not the same number of layers for every input parameters."
+
+    n_samples = [state.n_samples for state in shared_states]
+    n_all_samples = sum(n_samples)
+    if parameters_update_len == 0:
+        return []
+    if n_all_samples == 0:
+        raise ZeroDivisionError("division by zero")
+    updates = [list(state.parameters_update) for state in shared_states]
+    check_same_shapes(updates)
+    engine = default_engine() if device is None else AggregationEngine(device)
+    return engine.fedavg(updates, n_samples)

@@ -67,8 +67,8 @@ def _import_reference():
     sys.path.insert(0, str(REF))
     from substrafl.algorithms.algo import Algo
     from substrafl.remote.decorators import remote_data
-    from substrafl.strategies import FedAvg, Scaffold
-    from substrafl.strategies.schemas import FedAvgSharedState, ScaffoldSharedState, StrategyName
+    from substrafl.strategies import FedAvg, FedPCA, Scaffold
+    from substrafl.strategies.schemas import FedAvgSharedState, FedPCASharedState, ScaffoldSharedState, StrategyName
 
     class DummyAlgo(Algo):  # tests/conftest.py:395-421 (compatible with every strategy)
         @property
@@ -92,6 +92,7 @@ def _import_reference():
         def save_local_state(self, path):
             pass
 
+    globals()["_FEDPCA"] = (FedPCA, FedPCASharedState)
     return FedAvg, Scaffold, FedAvgSharedState, ScaffoldSharedState, DummyAlgo
 
 
@@ -184,6 +185,25 @@ def main():
         meta["cases"].append(
             {"key": key, "strategy": "scaffold", "K": K, "lr": lr, "lr_is_int": isinstance(lr, int), "layers": len(shapes)}
         )
+
+    # ---------------- G9: FedPCA (fed_pca.py:210-299): plain average + QR variant ----------------
+    FedPCA, FedPCASharedState = globals()["_FEDPCA"]
+    pca = FedPCA(algo=DummyAlgo())
+    for ci, K in enumerate((2, 5)):
+        rng = np.random.default_rng(99 + K)
+        shapes = [(4, 30), (3, 17)]  # (n_components, n_features): QR of the transpose
+        ns = [int(v) for v in np.random.default_rng(5 + K).integers(1, 5000, K)]
+        pcs = [[rng.standard_normal(sh).astype(np.float32) for sh in shapes] for _ in range(K)]
+        states = [FedPCASharedState(n_samples=ns[k], parameters_update=pcs[k]) for k in range(K)]
+        avg = pca.avg_shared_states(shared_states=states, _skip=True).avg_parameters_update
+        qr = pca.avg_shared_states_with_qr(shared_states=states, _skip=True).avg_parameters_update
+        key = f"fedpca_{ci:03d}"
+        arrays[f"{key}/n_samples"] = np.array(ns, dtype=np.int64)
+        for li in range(len(shapes)):
+            arrays[f"{key}/x{li}"] = np.stack([c[li] for c in pcs])
+            arrays[f"{key}/avg{li}"] = avg[li]
+            arrays[f"{key}/qr{li}"] = qr[li]
+        meta["cases"].append({"key": key, "strategy": "fedpca", "K": K, "layers": len(shapes)})
 
     # ---------------- G5: reference unit-test inputs verbatim ----------------
     # tests/strategies/test_fed_avg.py:17-38 (float64 ones/zeros) and :41-54 (int64 layers)

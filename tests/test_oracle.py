@@ -128,3 +128,14 @@ def test_signed_zero_seed():
         out = fedavg_reference_structure(pus, [0, 0, 4])[0]
         assert not np.signbit(out).any()
         assert np.array_equal(_bits(out), _bits(fedavg_explicit(pus, [0, 0, 4])[0]))
+
+
+def test_golden_fedpca_is_fedavg_arithmetic(golden):
+    """FedPCA's plain average is FedAvg's arithmetic, bit for bit."""
+    arrays, meta = golden
+    for case in [c for c in meta["cases"] if c["strategy"] == "fedpca"]:
+        key, K, L = case["key"], case["K"], case["layers"]
+        ns = [int(v) for v in arrays[f"{key}/n_samples"]]
+        pus = [[arrays[f"{key}/x{li}"][k] for li in range(L)] for k in range(K)]
+        for g, r in zip(fedavg_reference_structure(pus, ns), [arrays[f"{key}/avg{li}"] for li in range(L)]):
+            assert np.array_equal(_bits(g), _bits(r))

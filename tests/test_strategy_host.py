@@ -53,6 +53,9 @@ def test_float_n_samples_rejected():
 
 
 def test_name_and_compat(dummy_algo_class):
+    from substrafl_amd.strategies import FedPCA
+
+    assert FedPCA(algo=dummy_algo_class()).name == StrategyName.FEDERATED_PCA
     assert FedAvg(algo=dummy_algo_class()).name == StrategyName.FEDERATED_AVERAGING
     assert Scaffold(algo=dummy_algo_class()).name == StrategyName.SCAFFOLD
 
