@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from ..wire import bucket_views, flat_of
 
 _BN = (
     torch.nn.BatchNorm1d,
@@ -165,7 +166,9 @@ def _device_flat(updates, device) -> Optional[torch.Tensor]:
         flat = flat_bucket(updates)
         return flat if flat is not None else _gather_flat(updates)
     if all(isinstance(u, np.ndarray) and u.dtype == np.float32 for u in updates):
-        host = _host_flat(updates)
+        host = flat_of(updates)
+        if host is None:
+            host = _host_flat(updates)
         if host is None:
             host = np.concatenate([np.ascontiguousarray(u).reshape(-1) for u in updates])
         return torch.from_numpy(host).to(device)  # ONE H2D copy instead of one per layer
@@ -246,15 +249,11 @@ def zeros_like_parameters(model: torch.nn.Module, with_batch_norm_parameters: bo
 
 def export_numpy(tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
     """``[p.cpu().detach().numpy() for p in ...]`` (torch_fed_avg_algo.py:227-230) with ONE D2H copy
-    when the tensors are views of one flat bucket; the arrays returned are then views of one host
-    array -- the contiguous per-client row the aggregator stages as a single segment."""
+    when the tensors are views of one flat bucket; the arrays returned are then
+    :class:`wire.BucketArray` layers of one host buffer -- they pickle as that one buffer, and the
+    aggregator stages the client as a single segment."""
     flat = flat_bucket(list(tensors))
     if flat is None or not flat.is_cuda:
         return [t.cpu().detach().numpy() for t in tensors]
     host = flat.detach().cpu().numpy()
-    out, off = [], 0
-    for t in tensors:
-        n = t.numel()
-        out.append(host[off : off + n].reshape(tuple(t.shape)))
-        off += n
-    return out
+    return bucket_views(host, [tuple(t.shape) for t in tensors])

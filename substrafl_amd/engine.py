@@ -31,6 +31,7 @@ import numpy as np
 
 from . import _native
 from .layout import BucketLayout
+from .wire import flat_of
 
 KINDS = ("f32", "bf16", "f64", "f16")
 
@@ -273,6 +274,9 @@ class AggregationEngine:
         prescale = prescale or {}
         direct = not prescale and all(a.dtype == layout.dtype for row in rows for a in row)
         if direct:
+            flats = [flat_of(row) for row in rows]
+            if all(f is not None and f.size == layout.M for f in flats):
+                rows = [[f] for f in flats]  # flat wire format: one segment per client
             s.stage(d_bucket, ld_bytes, rows)
             return
         for k, row in enumerate(rows):

@@ -21,6 +21,8 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
+from .wire import bucket_views
+
 ROW_ALIGN_BYTES = 256
 
 
@@ -60,15 +62,13 @@ class BucketLayout:
             np.copyto(dst[s.offset : s.offset + s.numel], src.reshape(-1), casting="unsafe")
 
     def unpack(self, flat: np.ndarray) -> List[Tuple[int, np.ndarray]]:
-        """Views of ``flat`` shaped like each layer; 0-d layers come back as NumPy scalars, which
-        is what ``np.sum`` of 0-d arrays returns in the reference."""
+        """Views of ``flat`` shaped like each layer -- :class:`wire.BucketArray` layers of one
+        bucket, so a result pickles as one flat buffer; 0-d layers come back as NumPy scalars,
+        which is what ``np.sum`` of 0-d arrays returns in the reference."""
+        views = bucket_views(flat[: self.M], [s.shape for s in self.segments])
         out = []
-        for s in self.segments:
-            v = flat[s.offset : s.offset + s.numel]
-            if len(s.shape) == 0:
-                out.append((s.layer, v[0]))
-            else:
-                out.append((s.layer, v.reshape(s.shape)))
+        for s, v in zip(self.segments, views):
+            out.append((s.layer, flat[s.offset] if len(s.shape) == 0 else v))
         return out
 
     def __repr__(self) -> str:  # pragma: no cover

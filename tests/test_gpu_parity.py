@@ -511,3 +511,35 @@ def test_golden_fedpca(golden, torch_gpu, dummy_algo_class):
                      [arrays[f"{key}/avg{li}"] for li in range(L)])
         _assert_same(s.avg_shared_states_with_qr(states, _skip=True).avg_parameters_update,
                      [arrays[f"{key}/qr{li}"] for li in range(L)])
+
+
+@pytest.mark.parametrize("all_flat", [True, False])
+def test_flat_wire_format_inputs(torch_gpu, dummy_algo_class, all_flat):
+    """Shared states in the flat wire format (substrafl_amd.wire), through the reference's pickle
+    (protocol 4), staged one segment per client; bit-exact, and the result pickles as one buffer."""
+    from substrafl_amd import wire
+    from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState
+    from substrafl_amd.strategies import FedAvg, Scaffold
+
+    rng = np.random.default_rng(5)
+    shapes = [(257, 33), (1,), (33,), (1, 1), (4099,)]
+    K = 9
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    rows = [wire.pack(p) if (all_flat or k % 2) else p for k, p in enumerate(pus)]
+    states = [pickle.loads(pickle.dumps(FedAvgSharedState(n_samples=n, parameters_update=r), protocol=4))
+              for n, r in zip(ns, rows)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True)
+    _assert_same(got.avg_parameters_update, fedavg_reference_structure(pus, ns))
+    assert wire.flat_of(got.avg_parameters_update) is not None
+    back = pickle.loads(pickle.dumps(got))
+    _assert_same(back.avg_parameters_update, got.avg_parameters_update)
+
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    sstates = [ScaffoldSharedState(parameters_update=wire.pack(pus[k]), control_variate_update=wire.pack(cvs[k]),
+                                   n_samples=ns[k], server_control_variate=wire.pack(c)) for k in range(K)]
+    res = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.3).avg_shared_states(sstates, _skip=True)
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.3)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--M", type=int, default=25_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--wire", choices=["layers", "flat"], default="layers",
+                    help="layers: one array per layer (reference); flat: substrafl_amd.wire buckets")
     args = ap.parse_args()
 
     from oracle import fedavg_reference_structure
@@ -33,6 +35,7 @@ def main():
     from substrafl_amd.layout import synthetic_state_dict_shapes
     from substrafl_amd.remote import PickleSerializer
     from substrafl_amd.schemas import FedAvgAveragedState, FedAvgSharedState
+    from substrafl_amd.wire import pack
 
     shapes = synthetic_state_dict_shapes(args.M)
     rng = np.random.default_rng(0)
@@ -40,8 +43,8 @@ def main():
     tmp = Path(tempfile.mkdtemp(prefix="e2e_", dir=os.environ.get("TMPDIR", "/tmp")))
     paths = []
     for k in range(args.K):
-        st = FedAvgSharedState(n_samples=ns[k], parameters_update=[rng.standard_normal(s, dtype=np.float32)
-                                                                   for s in shapes])
+        layers = [rng.standard_normal(s, dtype=np.float32) for s in shapes]
+        st = FedAvgSharedState(n_samples=ns[k], parameters_update=pack(layers) if args.wire == "flat" else layers)
         p = tmp / f"shared_{k}"
         PickleSerializer.save(st, p)
         paths.append(p)
@@ -61,7 +64,7 @@ def main():
         ref = fedavg_reference_structure(updates, [s.n_samples for s in states])
         t4 = time.perf_counter()
         exact = all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(out, ref))
-        line = dict(K=args.K, M=args.M, rep=rep, cold=rep == 0, unpickle_s=round(t1 - t0, 4),
+        line = dict(K=args.K, M=args.M, wire=args.wire, rep=rep, cold=rep == 0, unpickle_s=round(t1 - t0, 4),
                     engine_s=round(t2 - t1, 4), pickle_out_s=round(t3 - t2, 4), reference_cpu_s=round(t4 - t3, 4),
                     engine_breakdown={k: (round(v, 5) if isinstance(v, float) else v) for k, v in eng.last_timing.items()},
                     engine_GBps_alg=round(bytes_alg / (t2 - t1) / 1e9, 2),
