@@ -173,6 +173,26 @@ def main():
             pw_ok &= np.float32(0.0) + numpy_pairwise_sum(prods) == np.float32(out[p].item())
         parity = {"sampled": int(idx.size), "mismatches": int(np.sum(acc.view(np.uint32) != got.view(np.uint32))),
                   "pairwise_ok": bool(pw_ok)}
+    else:  # Scaffold (scaffold.py:262-263,293): fp64 products and sums, c added last, lr after the sum
+        g = np.random.default_rng(123)
+        idx = np.setdiff1d(np.unique(g.integers(0, M, 4096)), layout.pairwise_idx.astype(np.int64))
+        tidx = torch.from_numpy(idx).to(device)
+        xd = delta[:, tidx].double().cpu().numpy()
+        xc = cv[:, tidx].double().cpu().numpy()
+        cc = c[tidx].double().cpu().numpy()
+        w64 = scaffold_weights(n_samples)
+        ad = np.zeros(idx.size, np.float64)
+        ac = np.zeros(idx.size, np.float64)
+        for k in range(K):
+            ad = ad + xd[k] * w64[k]
+            ac = ac + xc[k] * w64[k]
+        ad = 1.0 * ad
+        ac = ac + cc
+        gd = dout[tidx].cpu().numpy()
+        gc = cout[tidx].cpu().numpy()
+        parity = {"sampled": int(idx.size),
+                  "mismatches": int(np.sum(ad.view(np.uint64) != gd.view(np.uint64))
+                                    + np.sum(ac.view(np.uint64) != gc.view(np.uint64)))}
 
     # ---- read-stream ceiling on the same box (same 16-B nt load path) ----
     probe_n = min(clients.numel() if wl["strategy"] == "fedavg" else delta.numel(), 2_000_000_000)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 2
+#define FEDAGG_ABI_VERSION 3
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -143,6 +143,21 @@ int fedagg_flat_wsum_f32(const float* const* d_layers, int nlists, const double*
                          float* d_flat, void* stream);
 int fedagg_flat_increment_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat,
                               double multiplier, void* stream);
+/* Kind-generic forms (kinds FEDAGG_F32 / FEDAGG_F64, enum below) for Scaffold's client side,
+ * where the server control variate arrives as fp64 (scaffold.py:262-263 outputs fp64) and torch
+ * promotes (torch_scaffold_algo.py:256-268 increment with fp64 delta_variate, :424-427, :451-462):
+ *   wsum:      kinds[j] per list; d_flat has the promoted kind (fp64 if any list is fp64).
+ *              p_j = fl_j(x * c_j) in list j's kind (c rounded to fp32 for fp32 lists);
+ *              acc = 0 + p_0, then acc = acc + p_j in the promoted kind of (acc, p_j).
+ *   increment: fp32 parameters += multiplier * flat; an fp64 flat runs in fp64:
+ *              w = fl32(fl64(w) + fl64(m * u)).
+ *   gather:    layers of one kind into a flat bucket of that kind. */
+int fedagg_flat_gather(const void* const* d_layers, int kind, const uint64_t* numel, int L, void* d_flat,
+                       void* stream);
+int fedagg_flat_wsum(const void* const* d_layers, const int* kinds, int nlists, const double* coeffs,
+                     const uint64_t* numel, int L, void* d_flat, int flat_kind, void* stream);
+int fedagg_flat_increment(float* const* d_layers, const uint64_t* numel, int L, const void* d_flat, int flat_kind,
+                          double multiplier, void* stream);
 
 /* ---------------------------------------------------------------------------
  * dtype plumbing (device side, NumPy semantics).  Kinds: */

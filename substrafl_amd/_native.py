@@ -49,6 +49,9 @@ SIGNATURES = {
     "fedagg_flat_scatter_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_void]),
     "fedagg_flat_wsum_f32": (c_int, [P(c_void), c_int, P(c_dbl), P(c_u64), c_int, c_void, c_void]),
     "fedagg_flat_increment_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_dbl, c_void]),
+    "fedagg_flat_gather": (c_int, [P(c_void), c_int, P(c_u64), c_int, c_void, c_void]),
+    "fedagg_flat_wsum": (c_int, [P(c_void), P(c_int), c_int, P(c_dbl), P(c_u64), c_int, c_void, c_int, c_void]),
+    "fedagg_flat_increment": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_int, c_dbl, c_void]),
     "fedagg_scale_cast": (c_int, [c_void, c_int, c_dbl, c_void, c_int, c_u64, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
@@ -62,11 +65,15 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
 FEDAGG_MAX_PAIRWISE = 64
+FEDAGG_FLAT_MAX_LISTS = 4
+FEDAGG_F16 = 0  # kinds (include/fedagg.h enum)
+FEDAGG_F32 = 1
+FEDAGG_F64 = 2
 
 
 class NativeLibraryError(RuntimeError):

@@ -65,10 +65,26 @@ def model_parameters(model: torch.nn.Module, with_batch_norm_parameters: bool):
 # ----------------------------------------------------------------------------------------
 # flat-bucket helpers
 # ----------------------------------------------------------------------------------------
+_KIND = {torch.float32: _native.FEDAGG_F32, torch.float64: _native.FEDAGG_F64}
+
+
+def _kind(tensors: Sequence[torch.Tensor], device=None) -> Optional[int]:
+    """The libfedagg kind when ``tensors`` are contiguous ROCm tensors of ONE dtype (fp32 or fp64)
+    on one device (``device`` if given); else None (the op keeps the reference's torch loop)."""
+    if not tensors:
+        return None
+    t0 = tensors[0]
+    dev = t0.device if device is None else torch.device(device)
+    if not (t0.is_cuda and t0.dtype in _KIND):
+        return None
+    for t in tensors:
+        if not (t.is_cuda and t.dtype == t0.dtype and t.is_contiguous() and t.device == dev):
+            return None
+    return _KIND[t0.dtype]
+
+
 def _fast(tensors: Sequence[torch.Tensor]) -> bool:
-    return bool(tensors) and all(
-        t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.device == tensors[0].device for t in tensors
-    )
+    return _kind(tensors) == _native.FEDAGG_F32
 
 
 def _numel_array(tensors):
@@ -99,7 +115,8 @@ def flat_bucket(tensors: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
     start = base.storage_offset()
     off = start
     for t in tensors:
-        if t.untyped_storage().data_ptr() != storage or t.storage_offset() != off or not t.is_contiguous():
+        if (t.untyped_storage().data_ptr() != storage or t.storage_offset() != off or not t.is_contiguous()
+                or t.dtype != base.dtype):
             return None
         off += t.numel()
     total = off - start
@@ -107,11 +124,12 @@ def flat_bucket(tensors: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
 
 
 def _gather_flat(tensors: Sequence[torch.Tensor]) -> torch.Tensor:
-    flat = torch.empty(sum(t.numel() for t in tensors), dtype=torch.float32, device=tensors[0].device)
+    kind = _kind(tensors)
+    flat = torch.empty(sum(t.numel() for t in tensors), dtype=tensors[0].dtype, device=tensors[0].device)
     lib = _native.load()
-    _native.check(lib.fedagg_flat_gather_f32(_native.ptr_array([t.data_ptr() for t in tensors]),
-                                             _numel_array(tensors), len(tensors), flat.data_ptr(),
-                                             _stream(flat.device)), "flat_gather")
+    _native.check(lib.fedagg_flat_gather(_native.ptr_array([t.data_ptr() for t in tensors]), kind,
+                                         _numel_array(tensors), len(tensors), flat.data_ptr(),
+                                         _stream(flat.device)), "flat_gather")
     return flat
 
 
@@ -123,7 +141,7 @@ def get_parameters(model: torch.nn.Module, with_batch_norm_parameters: bool) -> 
     launch into one flat bucket, returned as per-layer views."""
     with torch.no_grad():
         params = list(model_parameters(model, with_batch_norm_parameters=with_batch_norm_parameters)())
-        if _fast(params):
+        if _kind(params) is not None:
             return _views(_gather_flat(params), params)
         return [p.clone() for p in params]
 
@@ -148,10 +166,10 @@ def increment_parameters(
             flat = _device_flat(updates, params[0].device)
             if flat is not None:
                 lib = _native.load()
-                _native.check(lib.fedagg_flat_increment_f32(_native.ptr_array([p.data.data_ptr() for p in params]),
-                                                            _numel_array(params), len(params), flat.data_ptr(),
-                                                            float(updates_multiplier), _stream(flat.device)),
-                              "flat_increment")
+                _native.check(lib.fedagg_flat_increment(_native.ptr_array([p.data.data_ptr() for p in params]),
+                                                        _numel_array(params), len(params), flat.data_ptr(),
+                                                        _KIND[flat.dtype], float(updates_multiplier),
+                                                        _stream(flat.device)), "flat_increment")
                 return
         for w, u in zip(params, updates):
             u = torch.from_numpy(u).to(w.device) if isinstance(u, np.ndarray) else u
@@ -159,13 +177,15 @@ def increment_parameters(
 
 
 def _device_flat(updates, device) -> Optional[torch.Tensor]:
-    """One fp32 device bucket holding ``updates`` back to back (None if they are not fp32)."""
+    """One device bucket (fp32 or fp64) holding ``updates`` back to back, None if they are not all
+    of one of those dtypes."""
     if all(isinstance(u, torch.Tensor) for u in updates):
-        if not _fast(updates):
+        if _kind(updates, device) is None:
             return None
         flat = flat_bucket(updates)
         return flat if flat is not None else _gather_flat(updates)
-    if all(isinstance(u, np.ndarray) and u.dtype == np.float32 for u in updates):
+    if all(isinstance(u, np.ndarray) for u in updates) and updates[0].dtype in (np.float32, np.float64) and all(
+            u.dtype == updates[0].dtype for u in updates):
         host = flat_of(updates)
         if host is None:
             host = _host_flat(updates)
@@ -202,16 +222,18 @@ def weighted_sum_parameters(parameters_list: List[List[torch.Tensor]], coefficie
         assert all(
             parameters_to_sum[0].data.shape == parameter.data.shape for parameter in parameters_to_sum
         ), "The shape of the parameters are unequal."
-    flat_in = [t for lst in parameters_list for t in lst]
-    if 1 <= len(parameters_list) <= 4 and _fast(flat_in):
+    kinds = [_kind(lst, parameters_list[0][0].device if parameters_list[0] else None) for lst in parameters_list]
+    if 1 <= len(parameters_list) <= _native.FEDAGG_FLAT_MAX_LISTS and all(k is not None for k in kinds):
         like = parameters_list[0]
+        out_dtype = torch.float64 if _native.FEDAGG_F64 in kinds else torch.float32
         with torch.no_grad():
-            out = torch.empty(sum(t.numel() for t in like), dtype=torch.float32, device=like[0].device)
+            out = torch.empty(sum(t.numel() for t in like), dtype=out_dtype, device=like[0].device)
             lib = _native.load()
             coeffs = (ctypes.c_double * len(coefficient_list))(*[float(c) for c in coefficient_list])
-            _native.check(lib.fedagg_flat_wsum_f32(_native.ptr_array([t.data_ptr() for t in flat_in]),
-                                                   len(parameters_list), coeffs, _numel_array(like), len(like),
-                                                   out.data_ptr(), _stream(out.device)), "flat_wsum")
+            _native.check(lib.fedagg_flat_wsum(_native.ptr_array([t.data_ptr() for lst in parameters_list for t in lst]),
+                                               (ctypes.c_int * len(kinds))(*kinds), len(parameters_list), coeffs,
+                                               _numel_array(like), len(like), out.data_ptr(), _KIND[out_dtype],
+                                               _stream(out.device)), "flat_wsum")
         return _views(out, like)
     weighted_sum = []
     for parameters_to_sum in zip(*parameters_list):

@@ -887,7 +887,8 @@ struct SegArgs {
   uint64_t n[SEG_GROUP];
   uint64_t flat_off[SEG_GROUP];
   uint32_t block_start[SEG_GROUP + 1];
-  float coeff[FEDAGG_FLAT_MAX_LISTS];
+  double coeff[FEDAGG_FLAT_MAX_LISTS];
+  uint32_t f64;  // bit j: list j is fp64; bit 31: the flat bucket is fp64
   int nl, nlists;
 };
 
@@ -897,40 +898,80 @@ __device__ __forceinline__ int seg_of_block(const SegArgs& a, uint32_t b) {
   return l;
 }
 
-// op 0: gather (flat = p0), 1: scatter (p0 = flat), 2: wsum (flat = sum_i p_i * c_i),
-// 3: increment (p0 = p0 + c0 * flat)
+// torch's ``tensor * python_float``: fp32 tensors compute in fp32 with the scalar rounded to
+// fp32, fp64 tensors in fp64.  Returned in double (exact for the fp32 product).
+__device__ __forceinline__ double seg_product(const void* p, uint64_t i, bool is64, double c) {
+#pragma clang fp contract(off)
+  if (is64) return static_cast<const double*>(p)[i] * c;
+  return (double)(static_cast<const float*>(p)[i] * (float)c);
+}
+
+// op 0: gather (flat = p0), 1: scatter (p0 = flat), 2: wsum (flat = sum() of p_j * c_j),
+// 3: increment (p0 = p0 + c0 * flat).  Layers and flat are fp32 or fp64 per SegArgs::f64;
+// mixed fp32/fp64 operands follow torch's promotion (the op runs in fp64 once either side is).
 template <int OP>
-__global__ void __launch_bounds__(FA_BLOCK) flat_seg_kernel(const SegArgs a, float* __restrict__ flat) {
+__global__ void __launch_bounds__(FA_BLOCK) flat_seg_kernel(const SegArgs a, void* __restrict__ flat) {
 #pragma clang fp contract(off)
   const int l = seg_of_block(a, blockIdx.x);
   const uint64_t base = (uint64_t)(blockIdx.x - a.block_start[l]) * SEG_CHUNK;
   const uint64_t n = a.n[l];
-  float* f = flat + a.flat_off[l];
+  const bool flat64 = (a.f64 >> 31) & 1u;
+  float* f32 = static_cast<float*>(flat) + a.flat_off[l];
+  double* f64 = static_cast<double*>(flat) + a.flat_off[l];
   for (uint64_t i = base + threadIdx.x; i < base + SEG_CHUNK && i < n; i += FA_BLOCK) {
     if constexpr (OP == 0) {
-      f[i] = static_cast<const float*>(a.p[0][l])[i];
+      if (flat64) f64[i] = static_cast<const double*>(a.p[0][l])[i];
+      else f32[i] = static_cast<const float*>(a.p[0][l])[i];
     } else if constexpr (OP == 1) {
-      const_cast<float*>(static_cast<const float*>(a.p[0][l]))[i] = f[i];
+      if (flat64) const_cast<double*>(static_cast<const double*>(a.p[0][l]))[i] = f64[i];
+      else const_cast<float*>(static_cast<const float*>(a.p[0][l]))[i] = f32[i];
     } else if constexpr (OP == 2) {
-      float acc = 0.0f + static_cast<const float*>(a.p[0][l])[i] * a.coeff[0];
+      // Python sum() from int 0: 0 + p_0 (-0 becomes +0), then acc + p_j in the promoted type
+      bool acc64 = a.f64 & 1u;
+      double acc = seg_product(a.p[0][l], i, acc64, a.coeff[0]);
+      acc = acc64 ? 0.0 + acc : (double)(0.0f + (float)acc);
       for (int j = 1; j < a.nlists; ++j) {
-        const float t = static_cast<const float*>(a.p[j][l])[i] * a.coeff[j];
-        acc = acc + t;
+        const bool is64 = (a.f64 >> j) & 1u;
+        const double t = seg_product(a.p[j][l], i, is64, a.coeff[j]);
+        acc64 = acc64 || is64;
+        acc = acc64 ? acc + t : (double)((float)acc + (float)t);
       }
-      f[i] = acc;
+      if (flat64) f64[i] = acc;
+      else f32[i] = (float)acc;
     } else {
+      // w += m * u with w fp32: u fp32 -> fl32(w + fl32(fl32(m) * u)); u fp64 -> fl32(w + fl64(m * u))
       float* w = const_cast<float*>(static_cast<const float*>(a.p[0][l]));
-      const float t = a.coeff[0] * f[i];
-      w[i] = w[i] + t;
+      if (flat64) {
+        const double t = a.coeff[0] * f64[i];
+        w[i] = (float)((double)w[i] + t);
+      } else {
+        const float t = (float)a.coeff[0] * f32[i];
+        w[i] = w[i] + t;
+      }
     }
   }
 }
 
 template <int OP>
-int flat_seg_launch(const void* const* ptrs, int nlists, const double* coeffs, const uint64_t* numel, int L,
-                    float* flat, hipStream_t s) {
+int flat_seg_launch(const void* const* ptrs, const int* kinds, int nlists, const double* coeffs,
+                    const uint64_t* numel, int L, void* flat, int flat_kind, hipStream_t s) {
   if (L < 0 || nlists < 1 || nlists > FEDAGG_FLAT_MAX_LISTS || (L > 0 && (!ptrs || !numel || !flat)))
     return fail(FEDAGG_EINVAL, "flat op: invalid argument (L=%lld)", L);
+  if (flat_kind != FEDAGG_F32 && flat_kind != FEDAGG_F64)
+    return fail(FEDAGG_EINVAL, "flat op: the flat bucket must be fp32 or fp64 (kind %lld)", flat_kind);
+  uint32_t mask = flat_kind == FEDAGG_F64 ? (1u << 31) : 0u;
+  bool any64 = false;
+  for (int j = 0; j < nlists; ++j) {
+    const int k = kinds ? kinds[j] : FEDAGG_F32;
+    if (k != FEDAGG_F32 && k != FEDAGG_F64) return fail(FEDAGG_EINVAL, "flat op: list %lld is not fp32/fp64", j);
+    if (k == FEDAGG_F64) mask |= 1u << j, any64 = true;
+  }
+  // operand kinds each op supports (the Python layer routes everything else to torch)
+  if ((OP == 0 || OP == 1) && any64 != (flat_kind == FEDAGG_F64))
+    return fail(FEDAGG_EINVAL, "flat copy: layer and flat kinds differ");
+  if (OP == 2 && any64 != (flat_kind == FEDAGG_F64))
+    return fail(FEDAGG_EINVAL, "flat wsum: the result kind must be the promoted kind of the lists");
+  if (OP == 3 && any64) return fail(FEDAGG_EINVAL, "flat increment: parameters must be fp32");
   uint64_t off = 0;
   for (int l0 = 0; l0 < L; l0 += SEG_GROUP) {
     const int nl = (L - l0) < SEG_GROUP ? (L - l0) : SEG_GROUP;
@@ -938,7 +979,8 @@ int flat_seg_launch(const void* const* ptrs, int nlists, const double* coeffs, c
     memset(&a, 0, sizeof(a));
     a.nl = nl;
     a.nlists = nlists;
-    for (int j = 0; j < nlists; ++j) a.coeff[j] = coeffs ? (float)coeffs[j] : 1.0f;  // fl32(python float)
+    a.f64 = mask;
+    for (int j = 0; j < nlists; ++j) a.coeff[j] = coeffs ? coeffs[j] : 1.0;
     uint64_t blocks = 0;
     for (int l = 0; l < nl; ++l) {
       for (int j = 0; j < nlists; ++j) {
@@ -1353,22 +1395,35 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
 
 int fedagg_flat_gather_f32(const float* const* d_layers, const uint64_t* numel, int L, float* d_flat,
                            void* stream) {
-  return flat_seg_launch<0>(reinterpret_cast<const void* const*>(d_layers), 1, nullptr, numel, L, d_flat,
-                            (hipStream_t)stream);
+  return flat_seg_launch<0>(reinterpret_cast<const void* const*>(d_layers), nullptr, 1, nullptr, numel, L, d_flat,
+                            FEDAGG_F32, (hipStream_t)stream);
 }
 int fedagg_flat_scatter_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat, void* stream) {
-  return flat_seg_launch<1>(reinterpret_cast<const void* const*>(d_layers), 1, nullptr, numel, L,
-                            const_cast<float*>(d_flat), (hipStream_t)stream);
+  return flat_seg_launch<1>(reinterpret_cast<const void* const*>(d_layers), nullptr, 1, nullptr, numel, L,
+                            const_cast<float*>(d_flat), FEDAGG_F32, (hipStream_t)stream);
 }
 int fedagg_flat_wsum_f32(const float* const* d_layers, int nlists, const double* coeffs, const uint64_t* numel, int L,
                          float* d_flat, void* stream) {
-  return flat_seg_launch<2>(reinterpret_cast<const void* const*>(d_layers), nlists, coeffs, numel, L, d_flat,
-                            (hipStream_t)stream);
+  return flat_seg_launch<2>(reinterpret_cast<const void* const*>(d_layers), nullptr, nlists, coeffs, numel, L, d_flat,
+                            FEDAGG_F32, (hipStream_t)stream);
 }
 int fedagg_flat_increment_f32(float* const* d_layers, const uint64_t* numel, int L, const float* d_flat,
                               double multiplier, void* stream) {
-  return flat_seg_launch<3>(reinterpret_cast<const void* const*>(d_layers), 1, &multiplier, numel, L,
-                            const_cast<float*>(d_flat), (hipStream_t)stream);
+  return flat_seg_launch<3>(reinterpret_cast<const void* const*>(d_layers), nullptr, 1, &multiplier, numel, L,
+                            const_cast<float*>(d_flat), FEDAGG_F32, (hipStream_t)stream);
+}
+int fedagg_flat_gather(const void* const* d_layers, int kind, const uint64_t* numel, int L, void* d_flat,
+                       void* stream) {
+  return flat_seg_launch<0>(d_layers, &kind, 1, nullptr, numel, L, d_flat, kind, (hipStream_t)stream);
+}
+int fedagg_flat_wsum(const void* const* d_layers, const int* kinds, int nlists, const double* coeffs,
+                     const uint64_t* numel, int L, void* d_flat, int flat_kind, void* stream) {
+  return flat_seg_launch<2>(d_layers, kinds, nlists, coeffs, numel, L, d_flat, flat_kind, (hipStream_t)stream);
+}
+int fedagg_flat_increment(float* const* d_layers, const uint64_t* numel, int L, const void* d_flat, int flat_kind,
+                          double multiplier, void* stream) {
+  return flat_seg_launch<3>(reinterpret_cast<const void* const*>(d_layers), nullptr, 1, &multiplier, numel, L,
+                            const_cast<void*>(d_flat), flat_kind, (hipStream_t)stream);
 }
 
 static bool is_float_kind(int k) { return k == FEDAGG_F16 || k == FEDAGG_F32 || k == FEDAGG_F64; }

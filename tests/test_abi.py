@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_invalid_arguments():
     lib = _native.load()
-    assert lib.fedagg_abi_version() == 2
+    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 3
     w = (ctypes.c_float * 1)(1.0)
     ptrs = _native.ptr_array([0])
     assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, 0, None, None, None) == -1  # K == 0
@@ -46,6 +46,16 @@ def test_abi_version_and_invalid_arguments():
     assert lib.fedagg_pairwise_ws_bytes(8, 3, 4) == 2 * 64 * 9 * 8
     assert lib.fedagg_tune(b"no_such_knob", 1) == -1
     assert lib.fedagg_tune(b"grid_cap", 4096) == 0
+    # kind-generic flat ops: operand kinds are checked before any HIP call
+    numel = (ctypes.c_uint64 * 1)(4)
+    kinds = (ctypes.c_int * 2)(_native.FEDAGG_F32, _native.FEDAGG_F64)
+    two = _native.ptr_array([16, 32])
+    c2 = (ctypes.c_double * 2)(1.0, -1.0)
+    assert lib.fedagg_flat_wsum(two, kinds, 2, c2, numel, 1, 64, _native.FEDAGG_F32, None) == -1  # must be f64
+    assert b"promoted kind" in lib.fedagg_last_error()
+    assert lib.fedagg_flat_wsum(two, kinds, 5, c2, numel, 1, 64, _native.FEDAGG_F64, None) == -1  # > 4 lists
+    assert lib.fedagg_flat_increment(two, numel, 1, 64, _native.FEDAGG_F16, 1.0, None) == -1
+    assert lib.fedagg_flat_gather(two, _native.FEDAGG_F64, numel, 1, None, None) == -1
     with pytest.raises(_native.NativeLibraryError):
         _native.check(-1, "x")
 

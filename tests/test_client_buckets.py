@@ -115,3 +115,62 @@ def test_flat_ops_many_layers():
     o = [torch.zeros(5, device="cuda")]
     got = wm.subtract_parameters(z, o)[0]
     assert _same(got, ref_wsum([z, o], [1, -1])[0]) and not torch.signbit(got).any()
+
+
+@pytest.mark.gpu
+def test_scaffold_client_round_mixed_fp64_vs_torch():
+    """A Scaffold client round (torch_scaffold_algo.py:405-481) after the first aggregation: the
+    server control variate arrives as fp64 (scaffold.py outputs fp64), so the client's torch ops
+    promote -- the flat kernels follow that promotion bit for bit."""
+    assert torch.cuda.is_available()
+    lr, num_updates = 0.05, 7
+    m_ref, m = _model("cuda", seed=4), _model("cuda", seed=4)
+    shapes = [p.shape for p in wm.model_parameters(m, True)()]
+    g = torch.Generator(device="cuda").manual_seed(11)
+    server_c = [torch.randn(s, device="cuda", dtype=torch.float64, generator=g) * 1e-2 for s in shapes]
+    client_c = [torch.randn(s, device="cuda", dtype=torch.float32, generator=g) * 1e-2 for s in shapes]
+
+    def params(model):
+        return list(wm.model_parameters(model, True)())
+
+    # reference semantics, spelled with the reference's own torch expressions
+    orig_ref = [p.detach().clone() for p in params(m_ref)]
+    delta_v_ref = ref_wsum([client_c, server_c], [1, -1])
+    # ours
+    orig = wm.get_parameters(m, True)
+    delta_v = wm.subtract_parameters(client_c, server_c)
+    assert all(d.dtype == torch.float64 for d in delta_v)
+    assert all(_same64(a, b) for a, b in zip(delta_v, delta_v_ref))
+    for step in range(num_updates):
+        noise = [torch.randn(s, device="cuda", generator=g) * 1e-3 for s in shapes]
+        with torch.no_grad():
+            for p, p2, n in zip(params(m_ref), params(m), noise):  # the optimizer step
+                p.add_(n)
+                p2.add_(n)
+            for w, u in zip(params(m_ref), delta_v_ref):  # weight_manager.py:137
+                w.data += lr * u.data
+        wm.increment_parameters(m, delta_v, with_batch_norm_parameters=True, updates_multiplier=lr)
+        assert all(_same(a.data, b.data) for a, b in zip(params(m), params(m_ref))), step
+    pu_ref = ref_wsum([[p.detach().clone() for p in params(m_ref)], orig_ref], [1, -1])
+    pu = wm.subtract_parameters(wm.get_parameters(m, True), orig)
+    assert all(_same(a, b) for a, b in zip(pu, pu_ref))
+    rm = -1.0 / (lr * num_updates)
+    cvu_ref = ref_wsum([server_c, pu_ref], [-1.0, rm])
+    cvu = wm.weighted_sum_parameters([server_c, pu], [-1.0, rm])
+    assert all(a.dtype == torch.float64 and _same64(a, b) for a, b in zip(cvu, cvu_ref))
+    new_c_ref = ref_wsum([client_c, cvu_ref], [1, 1])
+    new_c = wm.add_parameters(client_c, cvu)
+    assert all(_same64(a, b) for a, b in zip(new_c, new_c_ref))
+    # fp64 host arrays (the aggregator's Scaffold output) applied to an fp32 model
+    host = wm.export_numpy(new_c)
+    assert all(h.dtype == np.float64 for h in host)
+    wm.increment_parameters(m, host, with_batch_norm_parameters=True)
+    with torch.no_grad():
+        for w, u in zip(params(m_ref), host):
+            w.data += 1.0 * torch.from_numpy(np.asarray(u)).cuda().data
+    assert all(_same(a.data, b.data) for a, b in zip(params(m), params(m_ref)))
+
+
+def _same64(a, b):
+    return a.shape == b.shape and a.dtype == b.dtype and torch.equal(a.contiguous().view(torch.int64),
+                                                                      b.contiguous().view(torch.int64))
