@@ -294,10 +294,12 @@ class AggregationEngine:
                 s.sync()  # tmp is reused by the next segment's stage
 
     # ----------------------------------------------------------------------------------
-    def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int]) -> List[np.ndarray]:
+    def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
+               wire: bool = False) -> List[np.ndarray]:
         """GPU equivalent of fed_avg.py:217-222 for validated inputs (same layer count and shapes
         across clients, ``sum(n_samples) != 0``).  Returns one array per layer (0-d layers as
-        NumPy scalars, like ``np.sum``)."""
+        NumPy scalars, like ``np.sum``): plain views of one owned array, or with ``wire``
+        :class:`wire.BucketArray` layers that pickle as one buffer."""
         t_start = time.perf_counter()
         s = self.session()
         self.last_timing = tm = {}
@@ -341,7 +343,7 @@ class AggregationEngine:
             out = np.empty(layout.M, dtype=R)
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
             tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
-            for li, arr in layout.unpack(out):
+            for li, arr in layout.unpack(out, wire):
                 results[li] = arr
         tm.update({f"native_{k}": v for k, v in s.timing().items()})
         tm["total_s"] = time.perf_counter() - t_start
@@ -355,6 +357,7 @@ class AggregationEngine:
         server_control_variates: List[List[np.ndarray]],
         n_samples: Sequence[int],
         aggregation_lr,
+        wire: bool = False,
     ):
         """GPU equivalent of scaffold.py:193-196 (c equality check, returned as the mismatch
         count) and scaffold.py:297-337 (fp64 reductions).  Returns
@@ -418,8 +421,8 @@ class AggregationEngine:
         s.fetch(dout, out_d)
         s.fetch(cout, out_c)
         tm["kernel_fetch_s"] = time.perf_counter() - t1
-        avg = [a for _, a in lay_d.unpack(out_d)]
-        new_c = [a for _, a in lay_c.unpack(out_c)]
+        avg = [a for _, a in lay_d.unpack(out_d, wire)]
+        new_c = [a for _, a in lay_c.unpack(out_c, wire)]
         tm["total_s"] = time.perf_counter() - t_start
         return int(mism[0]), new_c, avg
 

@@ -61,11 +61,14 @@ class BucketLayout:
             src = np.asarray(layers[s.layer])
             np.copyto(dst[s.offset : s.offset + s.numel], src.reshape(-1), casting="unsafe")
 
-    def unpack(self, flat: np.ndarray) -> List[Tuple[int, np.ndarray]]:
-        """Views of ``flat`` shaped like each layer -- :class:`wire.BucketArray` layers of one
-        bucket, so a result pickles as one flat buffer; 0-d layers come back as NumPy scalars,
-        which is what ``np.sum`` of 0-d arrays returns in the reference."""
-        views = bucket_views(flat[: self.M], [s.shape for s in self.segments])
+    def unpack(self, flat: np.ndarray, wire: bool = False) -> List[Tuple[int, np.ndarray]]:
+        """Views of ``flat`` shaped like each layer; with ``wire`` they are :class:`wire.BucketArray`
+        layers of one bucket, so the result pickles as one flat buffer.  0-d layers come back as
+        NumPy scalars, which is what ``np.sum`` of 0-d arrays returns in the reference."""
+        if wire:
+            views = bucket_views(flat[: self.M], [s.shape for s in self.segments])
+        else:
+            views = [flat[s.offset : s.offset + s.numel].reshape(s.shape) for s in self.segments]
         out = []
         for s, v in zip(self.segments, views):
             out.append((s.layer, flat[s.offset] if len(s.shape) == 0 else v))

@@ -84,4 +84,5 @@ def weighted_average(shared_states, state_name: str, device: Optional[int] = Non
     updates = [list(state.parameters_update) for state in shared_states]
     check_same_shapes(updates)
     engine = default_engine() if device is None else AggregationEngine(device)
-    return engine.fedavg(updates, n_samples)
+    # substrafl_amd's own schemas already need this package to unpickle: return the flat wire format
+    return engine.fedavg(updates, n_samples, wire=True)

@@ -75,7 +75,7 @@ class Scaffold(Strategy):
         check_same_shapes(pus)  # np.sum([w*Δ_k ...]) (scaffold.py:293)
         mismatches, new_c, avg = self._engine().scaffold(
             pus, cvs, [list(s.server_control_variate) for s in shared_states],
-            [s.n_samples for s in shared_states], self._aggregation_lr,
+            [s.n_samples for s in shared_states], self._aggregation_lr, wire=True,
         )
         assert mismatches == 0, "all server_control_variate in the shared_states are not equal"
         return ScaffoldAveragedStates(server_control_variate=new_c, avg_parameters_update=avg)

@@ -84,7 +84,8 @@ def test_flat_of():
 def test_layout_unpack_gives_one_bucket_and_scalars():
     lay = BucketLayout(list(range(len(SHAPES))), SHAPES, np.float32)
     out = np.arange(lay.M, dtype=np.float32)
-    got = lay.unpack(out)
+    got = lay.unpack(out, wire=True)
+    assert wire.flat_of([a for _, a in lay.unpack(out)][:-1]) is None  # default: plain views
     arrs = [a for _, a in got]
     assert not isinstance(arrs[-1], np.ndarray) and isinstance(arrs[-1], np.float32)  # 0-d -> scalar
     assert wire.flat_of(arrs[:-1]) is not None
