@@ -4,9 +4,11 @@ Files written here are read back only by this process family (our own outputs); 
 never the format for untrusted inputs in tests.
 """
 
+import os
 import pickle
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
-from typing import Any
+from typing import Any, List, Sequence
 
 
 class PickleSerializer:
@@ -19,3 +21,17 @@ class PickleSerializer:
     def load(path: Path) -> Any:
         with Path(path).open("rb") as f:
             return pickle.load(f)
+
+    @staticmethod
+    def load_many(paths: Sequence[Path], max_workers: int = 0) -> List[Any]:
+        """``[load(p) for p in paths]`` with the K file reads overlapped on a thread pool (the
+        read syscalls, where page faulting of the fresh buffers happens, release the GIL).
+        Same objects, same order; the first failing path's exception is raised, as in the
+        reference's sequential loop (substratools_methods.py:61-64)."""
+        paths = list(paths)
+        workers = max_workers or min(len(paths), 16, os.cpu_count() or 1)
+        if workers <= 1 or len(paths) <= 1:
+            return [PickleSerializer.load(p) for p in paths]
+        with ThreadPoolExecutor(workers) as ex:
+            futures = [ex.submit(PickleSerializer.load, p) for p in paths]
+            return [f.result() for f in futures]

@@ -51,7 +51,9 @@ class RemoteMethod:
             elif isinstance(shared, (str, Path)):
                 loaded["shared_state"] = self.load_shared(shared)
             elif isinstance(shared, Iterable):
-                loaded["shared_states"] = [self.load_shared(p) for p in shared]
+                loader = getattr(self.shared_state_serializer, "load_many", None)
+                paths = [Path(p) for p in shared]
+                loaded["shared_states"] = loader(paths) if loader else [self.load_shared(p) for p in paths]
         if InputIdentifiers.datasamples in inputs:
             loaded["data_from_opener"] = inputs[InputIdentifiers.datasamples]
         return loaded
