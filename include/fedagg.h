@@ -54,7 +54,8 @@ const char* fedagg_last_error(void);
  *   "pipe"          software-pipelined client groups (0/1, vpt 1 only)
  *   "fuse_pairwise" patch numel==1 tensors inside the bucket launch (0/1)
  *   "sc_vpt"        Scaffold: 16-B vectors per thread per step (1/2/4/8)
- *   "sc_unroll"     Scaffold: clients per load group (2/4)
+ *   "sc_unroll"     Scaffold: clients per load group (2/4/8)
+ *   "sc_split"      Scaffold: 1 = stream all delta vectors, then all control-variate vectors
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);
 

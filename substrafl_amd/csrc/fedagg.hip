@@ -63,7 +63,8 @@ int g_pipe = 0;         // software-pipelined client groups
 int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 4;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8); 4 measured best
-int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4)
+int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8)
+int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
 constexpr int NT_STORE_MIN_K = 16;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -658,8 +659,121 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
   }
 }
 
+// Phase-split variant (fedagg_tune "sc_split"): the same per-element arithmetic, but the
+// thread streams all K delta vectors first (and stores the delta result), then all K control
+// variate vectors: half the concurrent streams and half the live accumulators of the fused
+// walk, so a wave can own twice the contiguous bytes per stream.
+template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, int PH>
+__device__ __forceinline__ void scaffold_phase(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
+                                               const int first, const int last, const TIn* __restrict__ c,
+                                               const double lr, const uint64_t* v, double* __restrict__ out,
+                                               bool wave_full, u32x4* lds_wave) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+  double acc[N][L];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[n][j] = first ? 0.0 : out[v[n] * L + j];
+  int k = 0;
+  for (; k + SU <= K; k += SU) {
+    u32x4 r[N][SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        if constexpr (PH == 0) r[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
+        else r[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+      }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const double w = a.w[k + u];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        double x[L];
+        unpack_d<TIn>(r[n][u], x);
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const double p = w * x[j];
+          acc[n][j] = acc[n][j] + p;
+        }
+      }
+    }
+  }
+  for (; k < K; ++k) {
+    const double w = a.w[k];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      double x[L];
+      if constexpr (PH == 0) unpack_d<TIn>(ld16<NT>(a.d[k] + v[n] * L), x);
+      else unpack_d<TIn>(ld16<NT>(a.cv[k] + v[n] * L), x);
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const double p = w * x[j];
+        acc[n][j] = acc[n][j] + p;
+      }
+    }
+  }
+  if (last) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      if constexpr (PH == 0) {
+#pragma unroll
+        for (int j = 0; j < L; ++j) acc[n][j] = lr * acc[n][j];  // scaffold.py:293
+      } else {
+        double xc[L];
+        unpack_d<TIn>(ld16<NT>(c + v[n] * L), xc);
+#pragma unroll
+        for (int j = 0; j < L; ++j) acc[n][j] = acc[n][j] + xc[j];  // c last (scaffold.py:262-263)
+      }
+    }
+  }
+  for (int p = 0; p < pw.n; ++p) {
+    const uint64_t e = pw.idx[p];
+    int owner = -1;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if (e / L == v[n]) owner = n;
+    if (owner >= 0) {
+      double dv, cvv;
+      scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, e, &dv, &cvv);
+      const int j = (int)(e % L);
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int jj = 0; jj < L; ++jj)
+          if (n == owner && jj == j) acc[n][jj] = PH == 0 ? dv : cvv;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    if constexpr (L == 4) {
+      if (wave_full) {
+        const uint64_t v0 = v[n] - (threadIdx.x & 63);
+        const f64x2 t0 = {acc[n][0], acc[n][1]}, t1 = {acc[n][2], acc[n][3]};
+        store32_coalesced<NTS>(out + v0 * L, __builtin_bit_cast(u32x4, t0), __builtin_bit_cast(u32x4, t1), lds_wave);
+        continue;
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < L / 2; ++s2) {
+      f64x2 t = {acc[n][2 * s2], acc[n][2 * s2 + 1]};
+      st16<NTS>(reinterpret_cast<f64x2*>(out + v[n] * L) + s2, __builtin_bit_cast(u32x4, t));
+    }
+  }
+}
+
+template <typename TIn, int KC, bool NT, bool NTS, int N, int SU>
+__device__ __forceinline__ void scaffold_vectors_split(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
+                                                       const int first, const int last, const TIn* __restrict__ c,
+                                                       const double lr, const uint64_t* v, double* __restrict__ dout,
+                                                       double* __restrict__ cout, bool wave_full, u32x4* lds_wave) {
+  scaffold_phase<TIn, KC, NT, NTS, N, SU, 0>(a, pw, K, first, last, c, lr, v, dout, wave_full, lds_wave);
+  scaffold_phase<TIn, KC, NT, NTS, N, SU, 1>(a, pw, K, first, last, c, lr, v, cout, wave_full, lds_wave);
+}
+
 // Same tiling as fedavg_kernel: a workgroup step covers VPT*256 contiguous vectors.
-template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU>
+template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT>
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
@@ -677,8 +791,12 @@ __global__ void __launch_bounds__(FA_BLOCK)
       uint64_t v[VPT];
 #pragma unroll
       for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
-      scaffold_vectors<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
-                                                   lds_wave);
+      if constexpr (SPLIT)
+        scaffold_vectors_split<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
+                                                           lds_wave);
+      else
+        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
+                                                     lds_wave);
     } else {
       for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
         scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout, false, lds_wave);
@@ -1204,12 +1322,12 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
   return FEDAGG_OK;
 }
 
-template <typename TIn, bool NT, bool NTS, int VPT, int SU>
+template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false>
 void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
                              uint64_t M, double* dout, double* cout) {
-  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU>), dim3(grid), dim3(FA_BLOCK), 0,
-                     s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT>), dim3(grid),
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
 }
 
 // Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
@@ -1221,6 +1339,14 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
 #define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
   const bool nts = g_nt_store != 0;
   if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
+  if (g_sc_split && nts) {  // phase-split walk (nt stores)
+    if (g_sc_vpt >= 8) {
+      if (g_sc_unroll <= 2) return launch_scaffold_variant<TIn, true, true, 8, 2, true>(SC_ARGS);
+      return launch_scaffold_variant<TIn, true, true, 8, 4, true>(SC_ARGS);
+    }
+    if (g_sc_unroll >= 8) return launch_scaffold_variant<TIn, true, true, 4, 8, true>(SC_ARGS);
+    return launch_scaffold_variant<TIn, true, true, 4, 4, true>(SC_ARGS);
+  }
   if (g_sc_vpt >= 8) {
     if (nts) return launch_scaffold_variant<TIn, true, true, 8, 1>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 8, 1>(SC_ARGS);
@@ -1338,7 +1464,8 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
   else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
-  else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 2 ? 2 : 4;
+  else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 2 ? 2 : (value >= 8 ? 8 : 4);
+  else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

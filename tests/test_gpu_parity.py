@@ -453,7 +453,9 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
 
 @pytest.mark.parametrize("knobs", [dict(sc_vpt=1), dict(sc_vpt=2, sc_unroll=2), dict(nt_store=0), dict(nt_load=0),
                                    dict(grid_cap=3), dict(sc_vpt=4, sc_unroll=2), dict(sc_vpt=2, sc_unroll=4),
-                                   dict(sc_vpt=8), dict(sc_vpt=8, grid_cap=2)])
+                                   dict(sc_vpt=8), dict(sc_vpt=8, grid_cap=2), dict(sc_split=1),
+                                   dict(sc_split=1, sc_unroll=8), dict(sc_split=1, sc_vpt=8, sc_unroll=2),
+                                   dict(sc_split=1, sc_vpt=8, grid_cap=2)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -464,7 +466,7 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     cv = torch.randn((K, M + 1), device="cuda")
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
-    default = dict(sc_vpt=4, sc_unroll=4, nt_store=1, nt_load=1, grid_cap=0)
+    default = dict(sc_vpt=4, sc_unroll=4, sc_split=0, nt_store=1, nt_load=1, grid_cap=0)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)
