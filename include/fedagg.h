@@ -199,6 +199,11 @@ void* fedagg_session_stream(fedagg_session* s);
 int fedagg_session_set(fedagg_session* s, const char* key, long long value);
 /* grow-only device buffer number `slot` (0..FEDAGG_SESSION_BUFFERS-1) of at least `bytes` */
 int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr);
+/* Prepare everything the first aggregation would otherwise pay for, so a one-shot task process
+ * can do it while it is still unpickling its inputs (on another thread): the pinned staging ring,
+ * the worker pool, HBM buffers slot i of slot_bytes[i] bytes (0: skip), and the kernels' code
+ * object (one tiny launch).  Returns when done. */
+int fedagg_session_warm(fedagg_session* s, const uint64_t* slot_bytes, int nslots);
 /* Pack K host rows into HBM: row k = concatenation of the nseg host segments
  * h_seg[k*nseg + i] (seg_bytes[i] bytes each), written at d_dst + k*ld_bytes.  Host memory
  * may be pageable; the copies are pipelined through the pinned ring and enqueued on the

@@ -58,6 +58,7 @@ SIGNATURES = {
     "fedagg_session_stream": (c_void, [c_void]),
     "fedagg_session_set": (c_int, [c_void, ctypes.c_char_p, ctypes.c_longlong]),
     "fedagg_session_buffer": (c_int, [c_void, c_int, c_u64, P(c_void)]),
+    "fedagg_session_warm": (c_int, [c_void, P(c_u64), c_int]),
     "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
     "fedagg_session_fetch": (c_int, [c_void, c_void, c_void, c_u64]),
     "fedagg_session_memset": (c_int, [c_void, c_void, c_int, c_u64]),
@@ -71,6 +72,7 @@ FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
 FEDAGG_MAX_PAIRWISE = 64
 FEDAGG_FLAT_MAX_LISTS = 4
+FEDAGG_SESSION_BUFFERS = 16
 FEDAGG_F16 = 0  # kinds (include/fedagg.h enum)
 FEDAGG_F32 = 1
 FEDAGG_F64 = 2

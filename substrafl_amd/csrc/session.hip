@@ -260,6 +260,33 @@ int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_
   return FEDAGG_OK;
 }
 
+int fedagg_session_warm(fedagg_session* s, const uint64_t* slot_bytes, int nslots) {
+  if (!s || nslots < 0 || nslots > FEDAGG_SESSION_BUFFERS || (nslots > 0 && !slot_bytes)) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(s->device));
+  int rc = s->ensure_ring();
+  if (rc) return rc;
+  (void)s->workers();
+  void* probe = nullptr;
+  for (int i = 0; i < nslots; ++i) {
+    if (!slot_bytes[i]) continue;
+    void* d = nullptr;
+    rc = fedagg_session_buffer(s, i, slot_bytes[i], &d);
+    if (rc) return rc;
+    if (!probe && slot_bytes[i] >= 4096) probe = d;
+  }
+  if (!probe) {
+    rc = fedagg_session_buffer(s, FEDAGG_SESSION_BUFFERS - 1, 4096, &probe);
+    if (rc) return rc;
+  }
+  // one tiny launch loads the kernels' code object now rather than at the first aggregation
+  HIP_TRY(hipMemsetAsync(probe, 0, 4096, s->stream));
+  rc = fedagg_read_probe_f32(static_cast<const float*>(probe), 512, static_cast<float*>(probe) + 512, 1,
+                             (void*)s->stream);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  return FEDAGG_OK;
+}
+
 int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
                          const void* const* h_seg, const uint64_t* seg_bytes) {
   if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes))) return FEDAGG_EINVAL;

@@ -251,13 +251,30 @@ class AggregationEngine:
         self._pack_threads = pack_threads
         self.last_timing: Dict[str, float] = {}
 
+    def _index(self) -> int:
+        idx = self._device_index
+        return int(os.environ.get("LOCAL_RANK", "0")) if idx is None else idx
+
+    def prewarm(self, strategy: str, input_bytes: int, n_clients: int) -> None:
+        """Start :func:`runtime.prewarm` sized for ``n_clients`` shared states of
+        ``input_bytes`` in total (file sizes are a close upper bound of the bucket bytes)."""
+        from . import runtime
+
+        if n_clients <= 0 or input_bytes <= 0:
+            return
+        slack = 1 << 20
+        if strategy == "scaffold":  # three buckets (Δ, cv, c copies) in, two fp64 outputs
+            per = input_bytes // 3 + slack
+            out = 2 * (per // n_clients) + slack
+            slots = {self._B_BUCKET: per, self._B_CV: per, self._B_C: per, self._B_OUT: out, self._B_COUT: out}
+        else:
+            slots = {self._B_BUCKET: input_bytes + slack, self._B_OUT: input_bytes // n_clients + slack}
+        runtime.prewarm(self._index(), slots)
+
     def session(self):
         from . import runtime
 
-        idx = self._device_index
-        if idx is None:
-            idx = int(os.environ.get("LOCAL_RANK", "0"))
-        s = runtime.session(idx)
+        s = runtime.session(self._index())
         if self._pack_threads:
             s.set("threads", self._pack_threads)
         return s

@@ -65,6 +65,12 @@ class RemoteMethod:
             self.save_shared(method_output, outputs[OutputIdentifiers.shared])
 
     def generic_function(self, inputs: Dict, outputs: Dict, task_properties: Dict) -> None:
+        shared = inputs.get(InputIdentifiers.shared)
+        warm = getattr(self.instance, "prewarm_aggregation", None)
+        if callable(warm) and isinstance(shared, Iterable) and not isinstance(shared, (str, Path)):
+            shared = [Path(p) for p in shared]
+            inputs = dict(inputs, **{InputIdentifiers.shared: shared})
+            warm(self.method_name, shared)  # GPU start-up overlaps the unpickling below
         method_inputs = self.load_method_inputs(inputs, outputs)
         method_inputs["_skip"] = True
         method_output = getattr(self.instance, self.method_name)(**method_inputs, **self.method_parameters)

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -73,6 +74,13 @@ class Session:
     def set(self, key: str, value: int) -> None:
         _native.check(self.lib.fedagg_session_set(self._h, key.encode(), int(value)), f"session_set({key})")
 
+    def warm(self, slot_bytes: Dict[int, int]) -> None:
+        """Pinned ring, worker pool, HBM buffers ``{slot: bytes}`` and the kernels' code object,
+        ahead of the first aggregation (``fedagg_session_warm``)."""
+        n = _native.FEDAGG_SESSION_BUFFERS
+        arr = (ctypes.c_uint64 * n)(*[int(slot_bytes.get(i, 0)) for i in range(n)])
+        _native.check(self.lib.fedagg_session_warm(self._h, arr, n), "session_warm")
+
     def buffer(self, slot: int, nbytes: int) -> int:
         p = ctypes.c_void_p()
         _native.check(self.lib.fedagg_session_buffer(self._h, int(slot), max(16, int(nbytes)), ctypes.byref(p)),
@@ -133,11 +141,41 @@ class Session:
 
 
 _sessions: Dict[int, Session] = {}
+_lock = threading.Lock()
+_warming: Dict[int, threading.Thread] = {}
+_warm_errors: Dict[int, BaseException] = {}
 
 
 def session(device: int = 0) -> Session:
-    """The process-wide session of ``device`` (created on first use)."""
-    s = _sessions.get(device)
-    if s is None:
-        s = _sessions[device] = Session(device)
-    return s
+    """The process-wide session of ``device`` (created on first use; waits for a
+    :func:`prewarm` of that device still in flight)."""
+    t = _warming.get(device)
+    if t is not None and t is not threading.current_thread():
+        t.join()
+    with _lock:
+        s = _sessions.get(device)
+        if s is None:
+            s = _sessions[device] = Session(device)
+        return s
+
+
+def prewarm(device: int = 0, slot_bytes: Optional[Dict[int, int]] = None) -> threading.Thread:
+    """Open ``device``'s session and warm it (:meth:`Session.warm`) on a background thread, so a
+    one-shot aggregate task pays HIP start-up, pinned-ring and HBM allocation while it is still
+    unpickling its inputs.  Idempotent per device; a failure here is not raised -- the real call
+    opens the session itself and reports the error then."""
+    with _lock:
+        t = _warming.get(device)
+        if t is not None:
+            return t
+
+        def run():
+            try:
+                session(device).warm(slot_bytes or {})
+            except BaseException as e:  # noqa: BLE001 - surfaced by the aggregation call
+                _warm_errors[device] = e
+
+        t = threading.Thread(target=run, name=f"fedagg-prewarm-{device}", daemon=True)
+        _warming[device] = t
+    t.start()
+    return t

@@ -20,6 +20,8 @@ from .strategy import Strategy
 
 
 class FedPCA(Strategy):
+    _aggregation_methods = {"avg_shared_states": "fedavg", "avg_shared_states_with_qr": "fedavg"}
+
     def __init__(self, algo, metric_functions=None, device: Optional[int] = None):
         if device is None:
             super().__init__(algo=algo, metric_functions=metric_functions)

@@ -18,6 +18,8 @@ from .strategy import Strategy
 
 
 class Scaffold(Strategy):
+    _aggregation_methods = {"avg_shared_states": "scaffold"}
+
     def __init__(self, algo, aggregation_lr: float = 1, metric_functions=None, device: Optional[int] = None):
         if device is None:
             super().__init__(algo=algo, aggregation_lr=aggregation_lr, metric_functions=metric_functions)

@@ -7,7 +7,9 @@ Graph building (``build_compute_plan``, ``perform_round``) is Substra control pl
 scope for this engine.
 """
 
+import os
 from abc import abstractmethod
+from typing import Sequence
 
 from ..exceptions import IncompatibleAlgoStrategyError
 from ..schemas import StrategyName
@@ -30,3 +32,24 @@ class Strategy:
     @abstractmethod
     def name(self) -> StrategyName:
         raise NotImplementedError
+
+    # aggregation methods that stream the shared states through the engine, and the bucket set
+    # they use ("fedavg": one bucket; "scaffold": three)
+    _aggregation_methods = {"avg_shared_states": "fedavg"}
+
+    def prewarm_aggregation(self, method_name: str, shared_paths: Sequence) -> None:
+        """Called by the task adapter (remote/substratools_methods.py) before it unpickles the
+        shared states: opens and sizes the GPU session on a background thread, overlapped with
+        the unpickling.  Not part of the reference interface; a no-op for other methods."""
+        kind = self._aggregation_methods.get(method_name)
+        if kind is None:
+            return
+        try:
+            total = sum(os.path.getsize(p) for p in shared_paths)
+        except OSError:
+            return
+        from ..engine import AggregationEngine, default_engine
+
+        dev = getattr(self, "_device", None)
+        engine = default_engine() if dev is None else AggregationEngine(dev)
+        engine.prewarm(kind, total, len(shared_paths))

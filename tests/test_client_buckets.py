@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 import torch
 
+from substrafl_amd import wire
 from substrafl_amd.algorithms import weight_manager as wm
 
 
@@ -91,7 +92,7 @@ def test_flat_ops_bit_exact_vs_torch_semantics():
     for a, b in zip(wm.model_parameters(m2, True)(), wm.model_parameters(m3, True)()):
         assert _same(a.data, b.data)
     host = wm.export_numpy(delta)
-    assert all(isinstance(h, np.ndarray) for h in host) and wm._host_flat(host) is not None
+    assert all(isinstance(h, np.ndarray) for h in host) and wire.flat_of(host) is not None
     wm.increment_parameters(m2, host, with_batch_norm_parameters=True)
     with torch.no_grad():
         for w, u in zip(wm.model_parameters(m3, True)(), host):

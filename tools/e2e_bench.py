@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--wire", choices=["layers", "flat"], default="layers",
                     help="layers: one array per layer (reference); flat: substrafl_amd.wire buckets")
+    ap.add_argument("--prewarm", action="store_true", help="start the engine's prewarm before loading")
     ap.add_argument("--loader", choices=["seq", "threads"], default="seq",
                     help="seq: the reference's loop; threads: PickleSerializer.load_many")
     args = ap.parse_args()
@@ -55,6 +56,8 @@ def main():
     bytes_alg = args.K * args.M * 4 + args.M * 4
     for rep in range(args.reps):
         t0 = time.perf_counter()
+        if args.prewarm:
+            eng.prewarm("fedavg", sum(p.stat().st_size for p in paths), len(paths))
         states = PickleSerializer.load_many(paths) if args.loader == "threads" else [PickleSerializer.load(p) for p in paths]
         t1 = time.perf_counter()
         updates = [list(s.parameters_update) for s in states]
@@ -66,7 +69,7 @@ def main():
         ref = fedavg_reference_structure(updates, [s.n_samples for s in states])
         t4 = time.perf_counter()
         exact = all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(out, ref))
-        line = dict(K=args.K, M=args.M, wire=args.wire, loader=args.loader, rep=rep, cold=rep == 0, unpickle_s=round(t1 - t0, 4),
+        line = dict(K=args.K, M=args.M, wire=args.wire, loader=args.loader, prewarm=args.prewarm, rep=rep, cold=rep == 0, unpickle_s=round(t1 - t0, 4),
                     engine_s=round(t2 - t1, 4), pickle_out_s=round(t3 - t2, 4), reference_cpu_s=round(t4 - t3, 4),
                     engine_breakdown={k: (round(v, 5) if isinstance(v, float) else v) for k, v in eng.last_timing.items()},
                     engine_GBps_alg=round(bytes_alg / (t2 - t1) / 1e9, 2),

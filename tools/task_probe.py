@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Subprocess-mode aggregate task, timed as Substra runs it: a FRESH Python process
+per task that unpickles K shared-state files, aggregates and pickles the result.
+
+  parent: writes K reference-format pickles once, then runs --reps fresh children per mode and
+          prints one JSON line per child (wall time of the whole child, measured by the parent).
+  child --mode engine:    substrafl_amd's RemoteMethod.generic_function (prewarm + threaded load +
+                          GPU engine), exactly the drop-in task path.
+  child --mode engine-noprewarm: same, with the prewarm hook disabled.
+  child --mode numpy:     the reference's own sequence (sequential pickle.load, NumPy FedAvg in the
+                          reference call structure from oracle/, pickle.dump) -- the CPU baseline.
+"""
+
+import argparse
+import json
+import os
+import pickle
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def child(mode: str, d: Path, K: int) -> None:
+    t0 = time.perf_counter()
+    paths = [d / f"shared_{k}" for k in range(K)]
+    out = d / f"out_{mode}"
+    if mode == "numpy":
+        from oracle import fedavg_reference_structure
+        from substrafl_amd.schemas import FedAvgAveragedState
+
+        states = []
+        for p in paths:
+            with open(p, "rb") as f:
+                states.append(pickle.load(f))
+        t1 = time.perf_counter()
+        avg = fedavg_reference_structure([s.parameters_update for s in states], [s.n_samples for s in states])
+        t2 = time.perf_counter()
+        with open(out, "wb") as f:
+            pickle.dump(FedAvgAveragedState(avg_parameters_update=avg), f)
+    else:
+        from substrafl_amd.remote.substratools_methods import RemoteMethod
+        from substrafl_amd.strategies import FedAvg
+
+        class _Algo:
+            strategies = ["Federated Averaging"]
+
+        strategy = FedAvg(algo=_Algo())
+        if mode == "engine-noprewarm":
+            strategy.prewarm_aggregation = None
+        rm = RemoteMethod(strategy, "avg_shared_states", {})
+        t1 = time.perf_counter()
+        rm.generic_function({"shared": [str(p) for p in paths]}, {"shared": str(out)}, {})
+        t2 = time.perf_counter()
+    t3 = time.perf_counter()
+    print(json.dumps({"child": mode, "in_child_total_s": round(t3 - t0, 4), "setup_s": round(t1 - t0, 4),
+                      "task_s": round(t3 - t1, 4)}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=8)
+    ap.add_argument("--M", type=int, default=25_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--child", default=None)
+    ap.add_argument("--dir", default=None)
+    args = ap.parse_args()
+    if args.child:
+        return child(args.child, Path(args.dir), args.K)
+
+    import numpy as np
+
+    from substrafl_amd.layout import synthetic_state_dict_shapes
+    from substrafl_amd.schemas import FedAvgSharedState
+
+    d = Path(tempfile.mkdtemp(prefix="task_", dir=os.environ.get("TMPDIR", "/tmp")))
+    rng = np.random.default_rng(0)
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
+    for k in range(args.K):
+        st = FedAvgSharedState(n_samples=ns[k], parameters_update=[rng.standard_normal(s, dtype=np.float32)
+                                                                   for s in synthetic_state_dict_shapes(args.M)])
+        with open(d / f"shared_{k}", "wb") as f:
+            pickle.dump(st, f)
+    for rep in range(args.reps):
+        for mode in ("numpy", "engine", "engine-noprewarm"):
+            t0 = time.perf_counter()
+            r = subprocess.run([sys.executable, __file__, "--child", mode, "--dir", str(d), "--K", str(args.K)],
+                               capture_output=True, text=True, timeout=600)
+            wall = time.perf_counter() - t0
+            if r.returncode != 0:
+                print(r.stdout, r.stderr, file=sys.stderr)
+                raise SystemExit(r.returncode)
+            line = json.loads(r.stdout.strip().splitlines()[-1])
+            line.update(K=args.K, M=args.M, rep=rep, process_wall_s=round(wall, 4))
+            print(json.dumps(line), flush=True)
+    a = pickle.load(open(d / "out_numpy", "rb")).avg_parameters_update
+    b = pickle.load(open(d / "out_engine", "rb")).avg_parameters_update
+    same = all(np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)) for x, y in zip(a, b))
+    print(json.dumps({"bit_exact_engine_vs_numpy": bool(same)}), flush=True)
+    for p in d.iterdir():
+        p.unlink()
+    d.rmdir()
+
+
+if __name__ == "__main__":
+    main()
