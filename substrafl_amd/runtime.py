@@ -144,6 +144,7 @@ _sessions: Dict[int, Session] = {}
 _lock = threading.Lock()
 _warming: Dict[int, threading.Thread] = {}
 _warm_errors: Dict[int, BaseException] = {}
+warm_times: Dict[int, tuple] = {}  # device -> (perf_counter at start, at end) of the last prewarm
 
 
 def session(device: int = 0) -> Session:
@@ -170,10 +171,14 @@ def prewarm(device: int = 0, slot_bytes: Optional[Dict[int, int]] = None) -> thr
             return t
 
         def run():
+            import time
+
+            t0 = time.perf_counter()
             try:
                 session(device).warm(slot_bytes or {})
             except BaseException as e:  # noqa: BLE001 - surfaced by the aggregation call
                 _warm_errors[device] = e
+            warm_times[device] = (t0, time.perf_counter())
 
         t = threading.Thread(target=run, name=f"fedagg-prewarm-{device}", daemon=True)
         _warming[device] = t

@@ -34,15 +34,20 @@ def child(mode: str, d: Path, K: int) -> None:
         from substrafl_amd.schemas import FedAvgAveragedState
 
         states = []
+        t1 = time.perf_counter()
         for p in paths:
             with open(p, "rb") as f:
                 states.append(pickle.load(f))
-        t1 = time.perf_counter()
+        t1b = time.perf_counter()
         avg = fedavg_reference_structure([s.parameters_update for s in states], [s.n_samples for s in states])
         t2 = time.perf_counter()
         with open(out, "wb") as f:
             pickle.dump(FedAvgAveragedState(avg_parameters_update=avg), f)
+        t3 = time.perf_counter()
     else:
+        # RemoteMethod.generic_function's steps, timed one by one
+        from substrafl_amd import runtime
+        from substrafl_amd.engine import default_engine
         from substrafl_amd.remote.substratools_methods import RemoteMethod
         from substrafl_amd.strategies import FedAvg
 
@@ -50,15 +55,29 @@ def child(mode: str, d: Path, K: int) -> None:
             strategies = ["Federated Averaging"]
 
         strategy = FedAvg(algo=_Algo())
-        if mode == "engine-noprewarm":
-            strategy.prewarm_aggregation = None
         rm = RemoteMethod(strategy, "avg_shared_states", {})
         t1 = time.perf_counter()
-        rm.generic_function({"shared": [str(p) for p in paths]}, {"shared": str(out)}, {})
-        t2 = time.perf_counter()
-    t3 = time.perf_counter()
-    print(json.dumps({"child": mode, "in_child_total_s": round(t3 - t0, 4), "setup_s": round(t1 - t0, 4),
-                      "task_s": round(t3 - t1, 4)}), flush=True)
+        if mode == "engine":
+            strategy.prewarm_aggregation("avg_shared_states", paths)
+        ta = time.perf_counter()
+        inputs = rm.load_method_inputs({"shared": paths}, {})
+        tb = time.perf_counter()
+        res = strategy.avg_shared_states(**inputs, _skip=True)
+        tc = time.perf_counter()
+        rm.save_method_output(res, {"shared": out})
+        t2 = t3 = time.perf_counter()
+        phases = {"load_s": round(tb - ta, 4), "aggregate_s": round(tc - tb, 4), "save_s": round(t2 - tc, 4),
+                  "engine": {k: round(v, 4) for k, v in default_engine().last_timing.items()}}
+        if 0 in runtime.warm_times:
+            w0, w1 = runtime.warm_times[0]
+            phases["prewarm_s"] = round(w1 - w0, 4)
+            phases["prewarm_done_after_load_s"] = round(w1 - tb, 4)
+    line = {"child": mode, "in_child_total_s": round(t3 - t0, 4), "setup_s": round(t1 - t0, 4),
+            "task_s": round(t3 - t1, 4)}
+    if mode == "numpy":
+        phases = {"load_s": round(t1b - t1, 4), "aggregate_s": round(t2 - t1b, 4), "save_s": round(t3 - t2, 4)}
+    line.update(phases)
+    print(json.dumps(line), flush=True)
 
 
 def main():
