@@ -118,7 +118,7 @@ struct fedagg_session {
   int device = 0;
   hipStream_t stream = nullptr;
   int threads = 8;
-  uint64_t chunk_bytes = 16ull << 20;
+  uint64_t chunk_bytes = 4ull << 20;  // 4 MiB: same staging rate as 16 MiB, a third of the cold ring cost
   int slots = 12;
   std::vector<void*> ring;
   std::vector<hipEvent_t> ring_ev;

@@ -51,9 +51,15 @@ class RemoteMethod:
             elif isinstance(shared, (str, Path)):
                 loaded["shared_state"] = self.load_shared(shared)
             elif isinstance(shared, Iterable):
-                loader = getattr(self.shared_state_serializer, "load_many", None)
                 paths = [Path(p) for p in shared]
-                loaded["shared_states"] = loader(paths) if loader else [self.load_shared(p) for p in paths]
+                states = None
+                ingest = getattr(self.instance, "ingest_shared_states", None)
+                if callable(ingest):  # load + stage to the GPU, overlapped (engine.ingest)
+                    states = ingest(self.method_name, paths, self.shared_state_serializer.load)
+                if states is None:
+                    loader = getattr(self.shared_state_serializer, "load_many", None)
+                    states = loader(paths) if loader else [self.load_shared(p) for p in paths]
+                loaded["shared_states"] = states
         if InputIdentifiers.datasamples in inputs:
             loaded["data_from_opener"] = inputs[InputIdentifiers.datasamples]
         return loaded

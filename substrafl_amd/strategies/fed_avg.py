@@ -11,7 +11,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from ..engine import AggregationEngine, default_engine
+from ..engine import engine_for
 from ..exceptions import EmptySharedStatesError
 from ..remote import remote
 from ..schemas import FedAvgAveragedState, FedAvgSharedState, StrategyName
@@ -83,6 +83,6 @@ def weighted_average(shared_states, state_name: str, device: Optional[int] = Non
         raise ZeroDivisionError("division by zero")
     updates = [list(state.parameters_update) for state in shared_states]
     check_same_shapes(updates)
-    engine = default_engine() if device is None else AggregationEngine(device)
+    engine = engine_for(device)
     # substrafl_amd's own schemas already need this package to unpickle: return the flat wire format
     return engine.fedavg(updates, n_samples, wire=True)

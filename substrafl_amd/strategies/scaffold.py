@@ -10,7 +10,7 @@ the same ``c`` (scaffold.py:193-196) runs on the GPU too.
 
 from typing import List, Optional
 
-from ..engine import AggregationEngine, default_engine
+from ..engine import engine_for
 from ..remote import remote
 from ..schemas import ScaffoldAveragedStates, ScaffoldSharedState, StrategyName
 from .fed_avg import check_same_shapes
@@ -37,8 +37,8 @@ class Scaffold(Strategy):
     def name(self) -> StrategyName:
         return StrategyName.SCAFFOLD
 
-    def _engine(self) -> AggregationEngine:
-        return default_engine() if self._device is None else AggregationEngine(self._device)
+    def _engine(self):
+        return engine_for(self._device)
 
     def _check_shared_states(self, shared_states: List[ScaffoldSharedState]) -> None:
         """Host-decidable half of scaffold.py:168-202 (types, list lengths, shapes of ``c``);

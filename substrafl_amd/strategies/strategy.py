@@ -48,8 +48,21 @@ class Strategy:
             total = sum(os.path.getsize(p) for p in shared_paths)
         except OSError:
             return
-        from ..engine import AggregationEngine, default_engine
+        from ..engine import engine_for
 
         dev = getattr(self, "_device", None)
-        engine = default_engine() if dev is None else AggregationEngine(dev)
+        engine = engine_for(dev)
         engine.prewarm(kind, total, len(shared_paths))
+
+    def ingest_shared_states(self, method_name: str, shared_paths: Sequence, load):
+        """Called by the task adapter instead of its own loading loop: loads the shared states on a
+        thread pool and stages each client to the GPU as it arrives (engine.ingest).  Returns
+        the states in path order, or None for methods that do not aggregate on the engine."""
+        kind = self._aggregation_methods.get(method_name)
+        if kind is None:
+            return None
+        from ..engine import engine_for
+
+        dev = getattr(self, "_device", None)
+        engine = engine_for(dev)
+        return engine.ingest(shared_paths, kind, load)

@@ -545,3 +545,52 @@ def test_flat_wire_format_inputs(torch_gpu, dummy_algo_class, all_flat):
     rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.3)
     _assert_same(res.server_control_variate, rc)
     _assert_same(res.avg_parameters_update, ra)
+
+
+def test_ingest_overlapped_staging(torch_gpu, dummy_algo_class, tmp_path):
+    """engine.ingest (threaded unpickling + per-client H2D as each file lands) feeds the next
+    aggregation; results stay bit-exact, and arrays other than the ingested ones are re-staged."""
+    from substrafl_amd.engine import engine_for
+    from substrafl_amd.remote import PickleSerializer
+    from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState
+    from substrafl_amd.strategies import FedAvg, Scaffold
+
+    rng = np.random.default_rng(21)
+    shapes = [(300, 17), (1,), (17,), (4097,)]
+    K = 7
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    paths = []
+    for k in range(K):
+        paths.append(tmp_path / f"f{k}")
+        PickleSerializer.save(FedAvgSharedState(n_samples=ns[k], parameters_update=pus[k]), paths[-1])
+    strategy = FedAvg(algo=dummy_algo_class())
+    eng = engine_for(None)
+    states = strategy.ingest_shared_states("avg_shared_states", paths, PickleSerializer.load)
+    assert eng.last_ingest["prestaged_clients"] == K
+    got = strategy.avg_shared_states(states, _skip=True).avg_parameters_update
+    assert eng.last_timing.get("prestaged") is True
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+    # ingest, then aggregate DIFFERENT arrays of the same shapes: must not reuse the staged rows
+    states = strategy.ingest_shared_states("avg_shared_states", paths, PickleSerializer.load)
+    other = [FedAvgSharedState(n_samples=s.n_samples, parameters_update=[a * np.float32(2) for a in s.parameters_update])
+             for s in states]
+    got = strategy.avg_shared_states(other, _skip=True).avg_parameters_update
+    assert not eng.last_timing.get("prestaged")
+    _assert_same(got, fedavg_reference_structure([o.parameters_update for o in other], ns))
+
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    spaths = []
+    for k in range(K):
+        spaths.append(tmp_path / f"s{k}")
+        PickleSerializer.save(ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k],
+                                                  n_samples=ns[k], server_control_variate=c), spaths[-1])
+    sc = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.4)
+    sstates = sc.ingest_shared_states("avg_shared_states", spaths, PickleSerializer.load)
+    assert eng.last_ingest["prestaged_clients"] == K
+    res = sc.avg_shared_states(sstates, _skip=True)
+    assert eng.last_timing.get("prestaged") is True
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.4)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)

@@ -115,3 +115,28 @@ def test_no_cpu_fallback(dummy_algo_class):
     s = [FedAvgSharedState(parameters_update=[np.ones(3, np.float32)], n_samples=1)] * 2
     with pytest.raises(_native.NativeLibraryError, match="no CPU fallback"):
         FedAvg(algo=dummy_algo_class()).avg_shared_states(s, _skip=True)
+
+
+def test_ingest_raises_first_failing_path_in_order(tmp_path):
+    """engine.ingest loads on a thread pool but reports errors like the reference's sequential loop
+    (substratools_methods.py:61-64): the first failing path in list order."""
+    import pickle
+
+    from substrafl_amd.engine import AggregationEngine
+
+    paths = []
+    for k in range(6):
+        p = tmp_path / f"s{k}"
+        p.write_bytes(pickle.dumps({"k": k}))
+        paths.append(p)
+
+    def load(p):
+        if p.name in ("s2", "s4"):
+            raise ValueError(p.name)
+        with open(p, "rb") as f:
+            return pickle.load(f)
+
+    with pytest.raises(ValueError, match="s2"):
+        AggregationEngine(0).ingest(paths, "fedavg", load)
+    good = AggregationEngine(0).ingest(paths[:2], "fedavg", load)  # no GPU here: loads, stages nothing
+    assert [g["k"] for g in good] == [0, 1]
