@@ -257,21 +257,13 @@ class AggregationEngine:
         idx = self._device_index
         return int(os.environ.get("LOCAL_RANK", "0")) if idx is None else idx
 
-    def prewarm(self, strategy: str, input_bytes: int, n_clients: int) -> None:
-        """Start :func:`runtime.prewarm` sized for ``n_clients`` shared states of
-        ``input_bytes`` in total (file sizes are a close upper bound of the bucket bytes)."""
+    def prewarm(self) -> None:
+        """Start :func:`runtime.prewarm` for this engine's GPU (HIP start-up, pinned ring, worker
+        pool, code object) on a background thread; HBM buffers are sized by the first call
+        (``hipMalloc`` is ~0.1 ms, not worth guessing sizes for)."""
         from . import runtime
 
-        if n_clients <= 0 or input_bytes <= 0:
-            return
-        slack = 1 << 20
-        if strategy == "scaffold":  # three buckets (Δ, cv, c copies) in, two fp64 outputs
-            per = input_bytes // 3 + slack
-            out = 2 * (per // n_clients) + slack
-            slots = {self._B_BUCKET: per, self._B_CV: per, self._B_C: per, self._B_OUT: out, self._B_COUT: out}
-        else:
-            slots = {self._B_BUCKET: input_bytes + slack, self._B_OUT: input_bytes // n_clients + slack}
-        runtime.prewarm(self._index(), slots)
+        runtime.prewarm(self._index())
 
     def ingest(self, paths: Sequence, strategy: str, load, max_workers: int = 0) -> List:
         """Load K shared-state files (``load(path)``, e.g. ``PickleSerializer.load``) on a thread

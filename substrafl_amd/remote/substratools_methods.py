@@ -38,6 +38,12 @@ class RemoteMethod:
         self.method_name = method_name
         self.method_parameters = method_parameters
         self.shared_state_serializer = shared_state_serializer
+        # A task process builds exactly one RemoteMethod (remote_struct.py:108-114) right before
+        # substratools calls generic_function: for an aggregation, start the GPU runtime now so
+        # its start-up overlaps the task's own set-up and input loading.
+        warm = getattr(instance, "prewarm_aggregation", None)
+        if callable(warm):
+            warm(method_name, [])
 
     def load_method_inputs(self, inputs: Dict, outputs: Dict) -> Dict:
         loaded: Dict[str, Any] = {}
@@ -71,12 +77,9 @@ class RemoteMethod:
             self.save_shared(method_output, outputs[OutputIdentifiers.shared])
 
     def generic_function(self, inputs: Dict, outputs: Dict, task_properties: Dict) -> None:
-        shared = inputs.get(InputIdentifiers.shared)
         warm = getattr(self.instance, "prewarm_aggregation", None)
-        if callable(warm) and isinstance(shared, Iterable) and not isinstance(shared, (str, Path)):
-            shared = [Path(p) for p in shared]
-            inputs = dict(inputs, **{InputIdentifiers.shared: shared})
-            warm(self.method_name, shared)  # GPU start-up overlaps the unpickling below
+        if callable(warm):
+            warm(self.method_name, [])  # no-op when __init__ already started it
         method_inputs = self.load_method_inputs(inputs, outputs)
         method_inputs["_skip"] = True
         method_output = getattr(self.instance, self.method_name)(**method_inputs, **self.method_parameters)

@@ -7,7 +7,6 @@ Graph building (``build_compute_plan``, ``perform_round``) is Substra control pl
 scope for this engine.
 """
 
-import os
 from abc import abstractmethod
 from typing import Sequence
 
@@ -37,22 +36,16 @@ class Strategy:
     # they use ("fedavg": one bucket; "scaffold": three)
     _aggregation_methods = {"avg_shared_states": "fedavg"}
 
-    def prewarm_aggregation(self, method_name: str, shared_paths: Sequence) -> None:
-        """Called by the task adapter (remote/substratools_methods.py) before it unpickles the
-        shared states: opens and sizes the GPU session on a background thread, overlapped with
-        the unpickling.  Not part of the reference interface; a no-op for other methods."""
-        kind = self._aggregation_methods.get(method_name)
-        if kind is None:
-            return
-        try:
-            total = sum(os.path.getsize(p) for p in shared_paths)
-        except OSError:
+    def prewarm_aggregation(self, method_name: str, shared_paths: Sequence = ()) -> None:
+        """Called by the task adapter (remote/substratools_methods.py) before it loads the shared
+        states: opens and warms the GPU session on a background thread (engine.prewarm), so HIP
+        start-up overlaps the unpickling.  Not part of the reference interface; a no-op for
+        methods that do not aggregate on the engine."""
+        if method_name not in self._aggregation_methods:
             return
         from ..engine import engine_for
 
-        dev = getattr(self, "_device", None)
-        engine = engine_for(dev)
-        engine.prewarm(kind, total, len(shared_paths))
+        engine_for(getattr(self, "_device", None)).prewarm()
 
     def ingest_shared_states(self, method_name: str, shared_paths: Sequence, load):
         """Called by the task adapter instead of its own loading loop: loads the shared states on a

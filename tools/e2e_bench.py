@@ -57,7 +57,7 @@ def main():
     for rep in range(args.reps):
         t0 = time.perf_counter()
         if args.prewarm:
-            eng.prewarm("fedavg", sum(p.stat().st_size for p in paths), len(paths))
+            eng.prewarm()
         states = PickleSerializer.load_many(paths) if args.loader == "threads" else [PickleSerializer.load(p) for p in paths]
         t1 = time.perf_counter()
         updates = [list(s.parameters_update) for s in states]

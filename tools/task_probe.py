@@ -55,10 +55,10 @@ def child(mode: str, d: Path, K: int) -> None:
             strategies = ["Federated Averaging"]
 
         strategy = FedAvg(algo=_Algo())
-        rm = RemoteMethod(strategy, "avg_shared_states", {})
+        if mode == "engine-noprewarm":
+            strategy.prewarm_aggregation = None
         t1 = time.perf_counter()
-        if mode == "engine":
-            strategy.prewarm_aggregation("avg_shared_states", paths)
+        rm = RemoteMethod(strategy, "avg_shared_states", {})  # starts the prewarm (task adapter)
         ta = time.perf_counter()
         inputs = rm.load_method_inputs({"shared": paths}, {})
         tb = time.perf_counter()
