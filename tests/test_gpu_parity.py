@@ -102,6 +102,38 @@ def test_reference_unit_fedavg(torch_gpu, dummy_algo_class, n_samples, factor, g
     assert (factor * np.ones((5, 10)) == got).all() and got[0].dtype == np.float64
 
 
+@pytest.mark.parametrize("n_samples, factor", [([1, 0, 0], 1.0), ([1, 1, 1], 1.0), ([1, 0, 1], 1.5)])
+def test_reference_unit_fedpca(torch_gpu, dummy_algo_class, n_samples, factor):
+    """tests/strategies/test_fed_pca.py:12-33 on the GPU path (float64, exact equality)."""
+    from substrafl_amd.schemas import FedPCASharedState
+    from substrafl_amd.strategies import FedPCA
+
+    states = [
+        FedPCASharedState(parameters_update=[np.ones((5, 10))], n_samples=n_samples[0]),
+        FedPCASharedState(parameters_update=[np.zeros((5, 10))], n_samples=n_samples[1]),
+        FedPCASharedState(parameters_update=[2 * np.ones((5, 10))], n_samples=n_samples[2]),
+    ]
+    got = FedPCA(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    assert (factor * np.ones((5, 10)) == got).all()
+
+
+@pytest.mark.parametrize("shared, expected", [
+    ([(np.array([[0.5, 0, 0], [1, 0, 1.5], [2, 2.5, 3]]), 2), (np.array([[1, 0, 0], [2, 0, 3], [4, 5, 6]]), 1)],
+     np.array([[1, 0, 0], [0, 0, 1], [0, 1, 0]])),
+    ([(np.array([[1, 1, 1, 1], [-1, 4, 4, -1], [4, -2, 2, 0]]), 1)],
+     np.array([[0.5, 0.5, 0.5, 0.5], [-0.5, 0.5, 0.5, -0.5], [0.5, -0.5, 0.5, -0.5]])),
+])
+def test_reference_unit_fedpca_qr(torch_gpu, dummy_algo_class, shared, expected):
+    """tests/strategies/test_fed_pca.py:36-65: each returned row spans the expected direction
+    (rtol 1e-5, tests/conftest.py:345-352)."""
+    from substrafl_amd.schemas import FedPCASharedState
+    from substrafl_amd.strategies import FedPCA
+
+    states = [FedPCASharedState(parameters_update=[x], n_samples=n) for x, n in shared]
+    got = FedPCA(algo=dummy_algo_class()).avg_shared_states_with_qr(states, _skip=True).avg_parameters_update[0]
+    assert all(np.allclose(np.dot(expected[i], row) * row, expected[i], rtol=1e-5) for i, row in enumerate(got))
+
+
 def test_reference_unit_int64_layers(torch_gpu, dummy_algo_class, golden):
     """tests/strategies/test_fed_avg.py:41-54: int64 layers promote to float64."""
     from substrafl_amd.schemas import FedAvgSharedState
