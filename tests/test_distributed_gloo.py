@@ -43,25 +43,28 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mode, q):
+def _worker(rank, world, port, mode, q, on_gpu=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         pus, ns = _data()
+        # on_gpu: every rank reduces its slice with libfedagg on cuda:0 (the ranks share the one
+        # GPU of the test box; the control plane stays gloo, as in bench.py)
+        red = None if on_gpu else oracle_flat_reducer
         if mode == "param":
-            res = param_range_fedavg(pus, ns, reducer=oracle_flat_reducer)
+            res = param_range_fedavg(pus, ns, reducer=red)
         else:
-            res = client_sharded_fedavg(pus, ns, reducer=oracle_flat_reducer, combine=mode)
+            res = client_sharded_fedavg(pus, ns, reducer=red, combine=mode)
         q.put((rank, None if res is None else [np.asarray(a) for a in res]))
     finally:
         dist.destroy_process_group()
 
 
-def _run(mode, world=2):
+def _run(mode, world=2, on_gpu=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, on_gpu)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=120) for _ in procs)
@@ -109,3 +112,15 @@ def test_client_sharded_world2_close(mode):
     assert out[1] is None
     for g, r in zip(out[0], ref):
         np.testing.assert_allclose(g, r, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_param_range_world2_gpu_reducer_bit_exact():
+    """The product reducer (libfedagg per rank) under parameter-range sharding: bit-identical to
+    the reference on every rank."""
+    out = _run("param", on_gpu=True)
+    pus, ns = _data()
+    ref = fedavg_reference_structure(pus, ns)
+    for rank in (0, 1):
+        for g, r in zip(out[rank], ref):
+            assert g.shape == r.shape and np.array_equal(g.view(np.uint32), r.view(np.uint32))
