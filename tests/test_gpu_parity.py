@@ -626,3 +626,37 @@ def test_ingest_overlapped_staging(torch_gpu, dummy_algo_class, tmp_path):
     rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.4)
     _assert_same(res.server_control_variate, rc)
     _assert_same(res.avg_parameters_update, ra)
+
+
+def test_fedavg_layout_edge_cases(torch_gpu, dummy_algo_class):
+    """Fortran-ordered, strided (non-contiguous) and empty layers: same values, shapes and dtypes
+    as the reference's np.sum over the K products."""
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    rng = np.random.default_rng(99)
+    K = 6
+    pus = []
+    for _ in range(K):
+        base = rng.standard_normal((40, 30)).astype(np.float32)
+        pus.append([
+            np.asfortranarray(rng.standard_normal((17, 9)).astype(np.float32)),  # F order
+            base[::2, ::3],  # strided view
+            np.zeros((0,), np.float32),  # empty
+            rng.standard_normal((3, 0, 2)).astype(np.float32),  # empty, 3-d
+            rng.standard_normal((1,)).astype(np.float32),
+        ])
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+
+
+def test_fedavg_only_empty_layers(torch_gpu, dummy_algo_class):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    pus = [[np.zeros((0, 4), np.float32)] for _ in range(3)]
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip([1, 2, 3], pus)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, [1, 2, 3]))
