@@ -311,31 +311,39 @@ class AggregationEngine:
                      ("server_control_variate", self._B_C))
         else:
             lists = (("parameters_update", self._B_BUCKET),)
-        plan = []
-        s = self.session()
+        rows = []
         for field, slot in lists:
             row = list(getattr(state, field, None) or [])
             if not row or not all(isinstance(a, np.ndarray) for a in row):
                 return None
-            dt = row[0].dtype
-            ok = (np.float32,) if strategy == "scaffold" else (np.float16, np.float32, np.float64)
-            if dt not in ok or any(a.dtype != dt for a in row):
-                return None  # grouped / converted layouts are staged by the aggregation call
+            if any(a.dtype != row[0].dtype for a in row) or row[0].dtype.kind not in "biuf":
+                return None  # per-layer dtype groups are staged by the aggregation call
+            rows.append(row)
+        if strategy == "scaffold":  # scaffold engine: fp32 buckets only when every list is fp32
+            all32 = all(r[0].dtype == np.float32 for r in rows)
+            targets = [np.dtype(np.float32 if all32 else np.float64)] * len(rows)
+        else:  # FedAvg: NumPy's product type of the layer (ints -> fp64)
+            targets = [np.result_type(rows[0][0].dtype, 1.0)]
+            if targets[0] not in (np.float16, np.float32, np.float64):
+                return None
+        plan = []
+        s = self.session()
+        for (field, slot), row, dt in zip(lists, rows, targets):
             layout = BucketLayout(list(range(len(row))), [a.shape for a in row], dt)
             ld_bytes = layout.ld * dt.itemsize
             d = s.buffer(slot, K * ld_bytes)
             self._prestaged[slot] = (d, ld_bytes, {})
-            plan.append((field, slot, layout, d, ld_bytes))
+            plan.append((field, slot, layout, d, ld_bytes, row[0].dtype))
         return plan
 
     def _ingest_row(self, plan, k: int, state) -> bool:
         s = self.session()
-        for field, slot, layout, d, ld_bytes in plan:
+        for field, slot, layout, d, ld_bytes, src in plan:
             row = list(getattr(state, field))
             if len(row) != len(layout.segments) or any(
-                    a.dtype != layout.dtype or a.shape != g.shape for a, g in zip(row, layout.segments)):
+                    a.dtype != src or a.shape != g.shape for a, g in zip(row, layout.segments)):
                 return False
-        for field, slot, layout, d, ld_bytes in plan:
+        for field, slot, layout, d, ld_bytes, src in plan:
             row = list(getattr(state, field))
             self._stage_rows(s, [row], layout, d + k * ld_bytes)
             self._prestaged[slot][2][k] = row  # holds the arrays: their ids stay unique
@@ -376,6 +384,17 @@ class AggregationEngine:
             if all(f is not None and f.size == layout.M for f in flats):
                 rows = [[f] for f in flats]  # flat wire format: one segment per client
             s.stage(d_bucket, ld_bytes, rows)
+            return
+        src = {a.dtype for row in rows for a in row}
+        if not prescale and len(src) == 1:
+            # every array has one other dtype (e.g. Scaffold's fp32 deltas next to fp64 control
+            # variates from round 2 on): stage the raw rows with the SAME element stride, then one
+            # exact device cast over the whole [K, ld] block
+            (sdt,) = src
+            K = len(rows)
+            tmp = s.buffer(self._B_TMP, K * layout.ld * sdt.itemsize)
+            s.stage(tmp, layout.ld * sdt.itemsize, rows)
+            s.cast(tmp, sdt, d_bucket, layout.dtype, K * layout.ld)
             return
         for k, row in enumerate(rows):
             for seg, a in zip(layout.segments, row):
@@ -498,7 +517,7 @@ class AggregationEngine:
                                    (control_variate_updates, lay_c, d_cv, self._B_CV),
                                    (server_control_variates, lay_s, d_cc, self._B_C)):
             rows = [list(r) for r in rows]
-            if all_f32 and self._take_prestaged(slot, d, lay.ld * isz, rows):
+            if self._take_prestaged(slot, d, lay.ld * isz, rows):
                 pre += 1
             else:
                 self._stage_rows(s, rows, lay, d)

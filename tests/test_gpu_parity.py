@@ -660,3 +660,50 @@ def test_fedavg_only_empty_layers(torch_gpu, dummy_algo_class):
     states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip([1, 2, 3], pus)]
     got = FedAvg(algo=dummy_algo_class()).avg_shared_states(states, _skip=True).avg_parameters_update
     _assert_same(got, fedavg_reference_structure(pus, [1, 2, 3]))
+
+
+def test_ingest_mixed_dtypes_round2_scaffold_and_int_layers(torch_gpu, dummy_algo_class, tmp_path):
+    """Scaffold from round 2 on ships fp32 deltas with fp64 control variates and fp64 c (the
+    aggregator's fp64 output comes back; tests/golden plumbing call1+): the rows are staged raw
+    and cast once on the device, prestaged by ingest, bit-exact.  Same for int64 FedAvg layers."""
+    from substrafl_amd.engine import engine_for
+    from substrafl_amd.remote import PickleSerializer
+    from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState
+    from substrafl_amd.strategies import FedAvg, Scaffold
+
+    rng = np.random.default_rng(8)
+    shapes = [(64, 9), (1,), (9,), (1, 1), (2049,)]
+    K = 5
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    cvs = [[rng.standard_normal(s) for s in shapes] for _ in range(K)]  # fp64
+    c = [rng.standard_normal(s) for s in shapes]  # fp64
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    paths = []
+    for k in range(K):
+        paths.append(tmp_path / f"s{k}")
+        PickleSerializer.save(ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k],
+                                                  n_samples=ns[k], server_control_variate=c), paths[-1])
+    eng = engine_for(None)
+    sc = Scaffold(algo=dummy_algo_class(), aggregation_lr=1.3)
+    states = sc.ingest_shared_states("avg_shared_states", paths, PickleSerializer.load)
+    assert eng.last_ingest["prestaged_clients"] == K
+    res = sc.avg_shared_states(states, _skip=True)
+    assert eng.last_timing.get("prestaged") is True
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 1.3)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)
+    # the same inputs without ingest (staged by the aggregation call) agree bit for bit
+    res2 = sc.avg_shared_states(states, _skip=True)
+    _assert_same(res2.avg_parameters_update, ra)
+
+    ints = [[rng.integers(-1000, 1000, s) for s in shapes] for _ in range(K)]
+    ipaths = []
+    for k in range(K):
+        ipaths.append(tmp_path / f"i{k}")
+        PickleSerializer.save(FedAvgSharedState(n_samples=ns[k], parameters_update=ints[k]), ipaths[-1])
+    fa = FedAvg(algo=dummy_algo_class())
+    istates = fa.ingest_shared_states("avg_shared_states", ipaths, PickleSerializer.load)
+    assert eng.last_ingest["prestaged_clients"] == K
+    got = fa.avg_shared_states(istates, _skip=True).avg_parameters_update
+    assert eng.last_timing.get("prestaged") is True
+    _assert_same(got, fedavg_reference_structure(ints, ns))
