@@ -65,3 +65,35 @@ def test_missing_library_is_loud(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "LIB_PATH", tmp_path / "nope.so")
     with pytest.raises(_native.NativeLibraryError, match="no CPU fallback"):
         _native.load()
+
+
+def _build_c_demo(tmp_path):
+    """Compile tests/c/fedavg_abi_demo.c with gcc against include/fedagg.h and libfedagg.so: the
+    header is plain C and the library links without any HIP or Python headers."""
+    import shutil
+    import subprocess
+
+    root = HEADER.parents[1]
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("gcc not available")
+    exe = tmp_path / "fedavg_abi_demo"
+    libdir = _native.LIB_PATH.parent
+    subprocess.run([gcc, "-O2", "-ffp-contract=off", "-Wall", "-Werror", f"-I{root / 'include'}",
+                    str(root / "tests" / "c" / "fedavg_abi_demo.c"), f"-L{libdir}", "-lfedagg",
+                    f"-Wl,-rpath,{libdir}", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)], check=True)
+    return exe
+
+
+def test_c_demo_compiles_against_the_header(tmp_path):
+    assert _build_c_demo(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_c_demo_runs_bit_exact(tmp_path):
+    import subprocess
+
+    exe = _build_c_demo(tmp_path)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches=0" in r.stdout
