@@ -38,12 +38,6 @@ class RemoteMethod:
         self.method_name = method_name
         self.method_parameters = method_parameters
         self.shared_state_serializer = shared_state_serializer
-        # A task process builds exactly one RemoteMethod (remote_struct.py:108-114) right before
-        # substratools calls generic_function: for an aggregation, start the GPU runtime now so
-        # its start-up overlaps the task's own set-up and input loading.
-        warm = getattr(instance, "prewarm_aggregation", None)
-        if callable(warm):
-            warm(method_name, [])
 
     def load_method_inputs(self, inputs: Dict, outputs: Dict) -> Dict:
         loaded: Dict[str, Any] = {}
@@ -76,10 +70,26 @@ class RemoteMethod:
         if OutputIdentifiers.shared in outputs:
             self.save_shared(method_output, outputs[OutputIdentifiers.shared])
 
-    def generic_function(self, inputs: Dict, outputs: Dict, task_properties: Dict) -> None:
+    def _prewarm(self) -> None:
         warm = getattr(self.instance, "prewarm_aggregation", None)
         if callable(warm):
-            warm(self.method_name, [])  # no-op when __init__ already started it
+            warm(self.method_name, [])  # idempotent: starts the GPU runtime on a background thread
+
+    def register_substratools_function(self) -> None:
+        """substratools_methods.py:160-166.  Only a task process (function.py) calls this, right
+        before substratools runs generic_function: for an aggregation the GPU runtime starts
+        here, so its start-up overlaps the task's own set-up and input loading.  (Loading a
+        finished model through model_loading builds a RemoteMethod too, but never registers it,
+        so it never touches the GPU.)"""
+        self._prewarm()
+        try:
+            import substratools as tools
+        except ImportError:  # the Substra runtime is not installed here (out of scope)
+            return
+        tools.register(function=self.generic_function, function_name=self.method_name)
+
+    def generic_function(self, inputs: Dict, outputs: Dict, task_properties: Dict) -> None:
+        self._prewarm()  # no-op when register_substratools_function already started it
         method_inputs = self.load_method_inputs(inputs, outputs)
         method_inputs["_skip"] = True
         method_output = getattr(self.instance, self.method_name)(**method_inputs, **self.method_parameters)

@@ -58,7 +58,8 @@ def child(mode: str, d: Path, K: int) -> None:
         if mode == "engine-noprewarm":
             strategy.prewarm_aggregation = None
         t1 = time.perf_counter()
-        rm = RemoteMethod(strategy, "avg_shared_states", {})  # starts the prewarm (task adapter)
+        rm = RemoteMethod(strategy, "avg_shared_states", {})
+        rm.register_substratools_function()  # function.py's next step: starts the prewarm
         ta = time.perf_counter()
         inputs = rm.load_method_inputs({"shared": paths}, {})
         tb = time.perf_counter()
