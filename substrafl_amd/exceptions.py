@@ -12,3 +12,11 @@ class EmptySharedStatesError(Exception):
 
 class IncompatibleAlgoStrategyError(Exception):
     """This algo is not compatible with this strategy."""
+
+
+class LoadMetadataError(Exception):
+    """metadata.json must name the ``model_file`` and ``function_file`` (exceptions.py:129-130)."""
+
+
+class LoadFileNotFoundError(Exception):
+    """The folder must hold function.tar.gz, metadata.json and the model file (exceptions.py:133-135)."""
