@@ -3,21 +3,22 @@
 Two entry levels:
 
 * Device-resident plans (``FedAvgPlan`` / ``ScaffoldPlan``): client buckets already in HBM as
-  one ``[K, ld]`` tensor; ``plan.launch(stream)`` enqueues the bucket kernel and the
-  numel == 1 pairwise patch.  This is what ``bench.py`` times (BASELINE.json metric).
-* Host entry (``AggregationEngine.fedavg`` / ``.scaffold``): the drop-in path behind
-  ``FedAvg.avg_shared_states`` / ``Scaffold.avg_shared_states``.  Shared states arrive as host
-  NumPy arrays (unpickled by ``RemoteMethod.generic_function``,
-  substrafl/remote/substratools_methods.py:54-66), are packed into pinned staging buckets,
-  copied H2D, reduced on the GPU, copied D2H into one owned array and returned as per-layer
-  views.
+  one ``[K, ld]`` tensor or K device pointers; ``plan.launch(stream)`` enqueues the bucket kernel
+  (with the numel == 1 pairwise patch fused in).  This is what ``bench.py`` times
+  (BASELINE.json metric).
+* Host entry (``AggregationEngine.fedavg`` / ``.scaffold``, plus ``.ingest`` and ``.prewarm``):
+  the drop-in path behind ``FedAvg.avg_shared_states`` / ``Scaffold.avg_shared_states``.  Shared
+  states arrive as host NumPy arrays (unpickled by ``RemoteMethod.generic_function``,
+  substrafl/remote/substratools_methods.py:54-66); the native session (:mod:`runtime`) packs
+  them through its pinned ring into HBM, the kernels reduce them, and one D2H copy brings the
+  result home as per-layer views of one owned array.  No PyTorch on this path.
 
-PyTorch is used only for device memory, pinned host memory, streams and events.  Every
-arithmetic step of the reduction runs in libfedagg's HIP kernels; if the library or a GPU is
-missing the engine raises -- there is no CPU fallback.  The engine holds no cross-call state
-(the reference aggregator is stateless per round: strategies/schemas.py:66-68) and initialises
-the GPU lazily on first use (tests fork after import: tests/conftest.py:52-59), so strategies
-that own an engine stay cloudpickle-able for RemoteStruct (remote_struct.py:84-114).
+Every arithmetic step of the reduction runs in libfedagg's HIP kernels; if the library or a GPU
+is missing the engine raises -- there is no CPU fallback.  Results never depend on engine state:
+the only thing kept between calls is the one-shot record of rows staged by :meth:`ingest`, which
+an aggregation uses only for the very same array objects.  The GPU is initialised lazily on
+first use (tests fork after import: tests/conftest.py:52-59), so strategies stay
+cloudpickle-able for RemoteStruct (remote_struct.py:84-114); the engine itself is never pickled.
 """
 
 from __future__ import annotations
