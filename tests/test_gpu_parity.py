@@ -707,3 +707,30 @@ def test_ingest_mixed_dtypes_round2_scaffold_and_int_layers(torch_gpu, dummy_alg
     got = fa.avg_shared_states(istates, _skip=True).avg_parameters_update
     assert eng.last_timing.get("prestaged") is True
     _assert_same(got, fedavg_reference_structure(ints, ns))
+
+
+def test_sharding_over_rccl_world1(torch_gpu):
+    """The RCCL code paths of substrafl_amd.sharding (all_gather of parameter-range slices, reduce
+    of client-block partials) on a one-rank nccl group: with one rank both are exact."""
+    import socket
+
+    import torch.distributed as dist
+
+    from substrafl_amd.sharding import client_sharded_fedavg, param_range_fedavg
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(4)
+        shapes = [(37, 29), (1,), (700,), (1, 1)]
+        pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(6)]
+        ns = [int(v) for v in rng.integers(1, 5000, 6)]
+        ref = fedavg_reference_structure(pus, ns)
+        _assert_same(param_range_fedavg(pus, ns), ref)
+        _assert_same(client_sharded_fedavg(pus, ns, combine="rccl"), ref)
+        _assert_same(client_sharded_fedavg(pus, ns, combine="ordered"), ref)
+    finally:
+        dist.destroy_process_group()
