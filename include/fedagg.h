@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 3
+#define FEDAGG_ABI_VERSION 4
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -210,6 +210,18 @@ int fedagg_session_warm(fedagg_session* s, const uint64_t* slot_bytes, int nslot
  * session stream (the host segments may be released once the call returns). */
 int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
                          const void* const* h_seg, const uint64_t* seg_bytes);
+/* Same, for bytes [byte_lo, byte_hi) of every client's row only (a parameter-range shard,
+ * SURVEY.md §8(e)): written at d_dst + k*ld_bytes.  fedagg_session_stage is the full range. */
+int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
+                               const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
+                               uint64_t byte_hi);
+/* Make the session's GPU the calling thread's current device (kernel entry points launch on
+ * the current device: a thread driving several sessions calls this before each one's launches). */
+int fedagg_session_activate(fedagg_session* s);
+/* number of visible GPUs (0 when none or on error) */
+int fedagg_device_count(void);
+/* hipMemGetInfo of `device`: free and total HBM bytes (sizing of out-of-core shards). */
+int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes);
 /* Copy `bytes` from HBM into (pageable) host memory; returns when the data is in h_dst. */
 int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes);
 int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes);

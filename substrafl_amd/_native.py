@@ -60,13 +60,17 @@ SIGNATURES = {
     "fedagg_session_buffer": (c_int, [c_void, c_int, c_u64, P(c_void)]),
     "fedagg_session_warm": (c_int, [c_void, P(c_u64), c_int]),
     "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
+    "fedagg_session_stage_range": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64]),
+    "fedagg_session_activate": (c_int, [c_void]),
+    "fedagg_device_count": (c_int, []),
+    "fedagg_device_memory": (c_int, [c_int, P(c_u64), P(c_u64)]),
     "fedagg_session_fetch": (c_int, [c_void, c_void, c_void, c_u64]),
     "fedagg_session_memset": (c_int, [c_void, c_void, c_int, c_u64]),
     "fedagg_session_sync": (c_int, [c_void]),
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
@@ -124,7 +128,7 @@ def ptr_array(ptrs) -> ctypes.Array:
 
 def tune(**knobs) -> None:
     """Set launch knobs of the library (``fedagg_tune``): grid_cap, nt_load, nt_store, vpt,
-    fuse_pairwise."""
+    unroll, pipe, tile, fuse_pairwise, sc_vpt, sc_unroll, sc_split, xcd."""
     lib = load()
     for k, v in knobs.items():
         check(lib.fedagg_tune(k.encode(), int(v)), f"fedagg_tune({k})")

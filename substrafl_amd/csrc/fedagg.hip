@@ -65,6 +65,7 @@ int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 4;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8); 4 measured best
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -318,6 +319,18 @@ __device__ __forceinline__ typename E::P fedavg_pairwise_elem(const FaArgs<E, KC
   return (typename E::P)s;
 }
 
+// Tile order.  The dispatcher deals blocks round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// "Workgroup dispatch"), so with the identity order the blocks resident on one XCD are spread
+// over 8x the address span of the grid's in-flight window, in every client stream.  remap = 1
+// gives the blocks of one `b % 8` group a contiguous run of tiles (bijective for any grid size),
+// so each XCD streams one compact window per client.  Speed only: any order is correct.
+__device__ __forceinline__ uint64_t tile_of_block(const int remap) {
+  const uint32_t b = blockIdx.x, G = gridDim.x;
+  if (!remap || G < 16) return b;
+  const uint32_t q = G / 8, r = G % 8, x = b % 8, i = b / 8;
+  return (uint64_t)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // ------------------------------------------------------------------------------------
 // FedAvg bucket kernel (fed_avg.py:217-222)
 // ------------------------------------------------------------------------------------
@@ -442,7 +455,7 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
 __global__ void __launch_bounds__(FA_BLOCK)
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
-                  const uint64_t M, typename E::Out* __restrict__ out) {
+                  const uint64_t M, typename E::Out* __restrict__ out, const int remap) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
@@ -454,7 +467,7 @@ __global__ void __launch_bounds__(FA_BLOCK)
     __shared__ u32x4 stage[WIDE ? FA_BLOCK / 64 : 1][128];
     u32x4* lds_wave = stage[WIDE ? threadIdx.x / 64 : 0];
     const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
-    for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+    for (uint64_t base = tile_of_block(remap) * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
       // wave-uniform: every lane of this wave has all VPT vectors in range
       const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
       if (base + (VPT - 1) * FA_BLOCK < nvec) {
@@ -777,7 +790,7 @@ template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT>
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
-                    double* __restrict__ dout, double* __restrict__ cout) {
+                    double* __restrict__ dout, double* __restrict__ cout, const int remap) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
   const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
@@ -785,7 +798,7 @@ __global__ void __launch_bounds__(FA_BLOCK)
   __shared__ u32x4 stage[FA_BLOCK / 64][128];
   u32x4* lds_wave = stage[threadIdx.x / 64];
   const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
-  for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+  for (uint64_t base = tile_of_block(remap) * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
     const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
     if (base + (VPT - 1) * FA_BLOCK < nvec) {
       uint64_t v[VPT];
@@ -1155,7 +1168,7 @@ template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
   hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE>), dim3(grid), dim3(FA_BLOCK), 0,
-                     s, a, pw, kc, first, nvec, M, out);
+                     s, a, pw, kc, first, nvec, M, out, g_xcd);
 }
 
 // Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
@@ -1327,7 +1340,7 @@ void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FED
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
                              uint64_t M, double* dout, double* cout) {
   hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT>), dim3(grid),
-                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd);
 }
 
 // Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
@@ -1466,6 +1479,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
+  else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

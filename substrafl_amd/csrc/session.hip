@@ -289,13 +289,28 @@ int fedagg_session_warm(fedagg_session* s, const uint64_t* slot_bytes, int nslot
 
 int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
                          const void* const* h_seg, const uint64_t* seg_bytes) {
-  if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes))) return FEDAGG_EINVAL;
+  if (nseg < 0 || (nseg > 0 && !seg_bytes)) return FEDAGG_EINVAL;
+  uint64_t row = 0;
+  for (int i = 0; i < nseg; ++i) row += seg_bytes[i];
+  return fedagg_session_stage_range(s, d_dst, ld_bytes, K, nseg, h_seg, seg_bytes, 0, row);
+}
+
+int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
+                               const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
+                               uint64_t byte_hi) {
+  if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) || byte_hi < byte_lo)
+    return FEDAGG_EINVAL;
   const double t0 = now_s();
   HIP_TRY(hipSetDevice(s->device));
   int rc = s->ensure_ring();
   if (rc) return rc;
-  uint64_t row = 0;
-  for (int i = 0; i < nseg; ++i) row += seg_bytes[i];
+  uint64_t full = 0;
+  for (int i = 0; i < nseg; ++i) full += seg_bytes[i];
+  if (byte_hi > full) {
+    fedagg_internal::set_error("fedagg_session_stage_range: byte range beyond the row");
+    return FEDAGG_EINVAL;
+  }
+  const uint64_t row = byte_hi - byte_lo;  // bytes [byte_lo, byte_hi) of every client's row
   if (row > ld_bytes) {
     fedagg_internal::set_error("fedagg_session_stage: segments exceed the row stride");
     return FEDAGG_EINVAL;
@@ -327,7 +342,7 @@ int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int 
     const void* const* segs = h_seg + (size_t)k * nseg;
     char* dst = static_cast<char*>(s->ring[slot]);
     pool.submit([=, &d] {
-      gather_range(segs, seg_bytes, nseg, a, b, dst);
+      gather_range(segs, seg_bytes, nseg, byte_lo + a, byte_lo + b, dst);
       d.set();
     });
   };
@@ -383,6 +398,28 @@ int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint
   for (int i = 0; i < R; ++i)
     if (pending[i]) done[i].wait();
   s->last_fetch_s = now_s() - t0;
+  return FEDAGG_OK;
+}
+
+int fedagg_session_activate(fedagg_session* s) {
+  if (!s) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(s->device));
+  return FEDAGG_OK;
+}
+
+int fedagg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes) {
+  if (!free_bytes || !total_bytes) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(device));
+  size_t f = 0, t = 0;
+  HIP_TRY(hipMemGetInfo(&f, &t));
+  *free_bytes = f;
+  *total_bytes = t;
   return FEDAGG_OK;
 }
 

@@ -26,7 +26,7 @@ from __future__ import annotations
 import ctypes
 import os
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -35,6 +35,9 @@ from .layout import BucketLayout
 from .wire import flat_of
 
 KINDS = ("f32", "bf16", "f64", "f16")
+
+# GPU selection of the strategies (resolve_devices): an index, several indices, or "all"
+Devices = Optional[Union[int, Sequence[int], str]]
 
 
 def _torch():
@@ -569,15 +572,48 @@ def default_engine() -> AggregationEngine:
     return _default_engine
 
 
-_engines: Dict[int, AggregationEngine] = {}
+_engines: Dict[object, object] = {}
 
 
-def engine_for(device: Optional[int] = None) -> AggregationEngine:
-    """The process-wide engine of ``device`` (``None``: :func:`default_engine`), so rows staged by
-    :meth:`AggregationEngine.ingest` are found by the aggregation call that follows."""
+def _device_count() -> int:
+    n = _native.load().fedagg_device_count()
+    if n <= 0:
+        raise _native.NativeLibraryError("no HIP device visible (the aggregation engine runs on MI355X only)")
+    return n
+
+
+def resolve_devices(device) -> Optional[object]:
+    """``device`` as the strategies take it: ``None`` (``FEDAGG_DEVICES`` if set, else the
+    single default GPU), an int, a sequence of ints, or ``"all"`` (every visible GPU)."""
     if device is None:
+        env = os.environ.get("FEDAGG_DEVICES", "").strip()
+        if not env:
+            return None
+        device = env
+    if isinstance(device, str):
+        if device == "all":
+            return tuple(range(_device_count()))
+        parts = [p for p in device.replace(" ", "").split(",") if p]
+        return int(parts[0]) if len(parts) == 1 else tuple(int(p) for p in parts)
+    if isinstance(device, (list, tuple)):
+        return int(device[0]) if len(device) == 1 else tuple(int(d) for d in device)
+    return int(device)
+
+
+def engine_for(device=None):
+    """The process-wide engine of ``device`` (see :func:`resolve_devices`), so rows staged by
+    :meth:`AggregationEngine.ingest` are found by the aggregation call that follows.  Several
+    devices give a :class:`multi_device.MultiDeviceEngine` (parameter-range shards, bit-exact)."""
+    dev = resolve_devices(device)
+    if dev is None:
         return default_engine()
-    e = _engines.get(int(device))
+    e = _engines.get(dev)
     if e is None:
-        e = _engines[int(device)] = AggregationEngine(int(device))
+        if isinstance(dev, tuple):
+            from .multi_device import MultiDeviceEngine
+
+            e = MultiDeviceEngine(dev)
+        else:
+            e = AggregationEngine(dev)
+        _engines[dev] = e
     return e

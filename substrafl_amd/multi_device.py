@@ -1,0 +1,289 @@
+"""Single-process, multi-device aggregation: parameter-range shards over the node's GPUs.
+
+A Substra aggregate task is ONE OS process (``remote/register/register.py:96-121`` runs one
+``function.py``), so a multi-process ``torch.distributed`` launch does not fit the drop-in path
+("Single process, multi-device").  :class:`MultiDeviceEngine` therefore drives
+several GPUs from one process:
+
+* the flat bucket range ``[0, M)`` is cut into one contiguous shard per device
+  (``sharding.shard_bounds``, 512-element aligned, so every shard row starts 256-B aligned);
+* a thread per shard stages bytes ``[lo, hi)`` of every client's row over that GPU's own PCIe link
+  (``fedagg_session_stage_range``: the pinned-ring pack reads straight from the clients' layer
+  arrays, no host-side re-slicing), runs the same bucket kernel with the same client order on it,
+  and fetches the result straight into its slice of the one output array;
+* a shard too large for its GPU's free HBM (``K x M`` beyond 288 GB, e.g. 256 clients x 350M
+  fp32) is streamed through that GPU in sub-ranges (out-of-core), so any size aggregates.
+
+Each output element is computed by exactly the arithmetic of the single-GPU kernel, so results
+are bit-identical to :class:`engine.AggregationEngine` and to the reference (no collective, no
+re-association).  numel == 1 layers are patched by the shard that owns them.  Layer sets the
+range path does not cover (several dtype groups in one update, dtype conversions, Scaffold lists
+of different shapes) run on the first device's single-GPU engine -- still the HIP path.
+
+Reference behaviour replaced: ``FedAvg.avg_shared_states`` (substrafl/strategies/fed_avg.py:
+207-222) and ``Scaffold.avg_shared_states`` (substrafl/strategies/scaffold.py:297-337).
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native
+from .engine import AggregationEngine, FedAvgPlan, ScaffoldPlan, equal_count, fedavg_weights, kind_of, scaffold_weights
+from .layout import ROW_ALIGN_BYTES, BucketLayout
+from .sharding import SHARD_ALIGN, shard_bounds
+from .wire import flat_of
+
+HBM_HEADROOM = 0.85  # fraction of a device's free HBM one sub-range may use when no cap is given
+
+
+def _ld(n: int, isz: int) -> int:
+    per_row = max(1, ROW_ALIGN_BYTES // isz)
+    return max(per_row, -(-n // per_row) * per_row)
+
+
+def _split(lo: int, hi: int, max_elems: int) -> List[Tuple[int, int]]:
+    """Cut ``[lo, hi)`` into sub-ranges of at most ``max_elems`` (SHARD_ALIGN multiples)."""
+    if hi <= lo:
+        return []
+    step = max(SHARD_ALIGN, (max_elems // SHARD_ALIGN) * SHARD_ALIGN)
+    return [(a, min(hi, a + step)) for a in range(lo, hi, step)]
+
+
+class MultiDeviceEngine:
+    """Drop-in host path over ``devices`` (GPU indices; a repeated index gets its own session,
+    which lets a one-GPU box rehearse the sharded path).  ``max_shard_bytes`` caps the HBM one
+    sub-range of a shard may take (default: 85 % of the device's free HBM)."""
+
+    # HBM buffer slots (same numbering as AggregationEngine)
+    _B_BUCKET, _B_OUT, _B_WS, _B_CV, _B_C, _B_COUT, _B_CNT = 0, 1, 2, 4, 5, 6, 7
+
+    def __init__(self, devices: Sequence[int], max_shard_bytes: Optional[int] = None,
+                 pack_threads: Optional[int] = None):
+        self.devices = [int(d) for d in devices]
+        if not self.devices:
+            raise ValueError("MultiDeviceEngine needs at least one device")
+        self.max_shard_bytes = max_shard_bytes
+        self._pack_threads = pack_threads
+        self._sessions = None
+        self._fallback: Optional[AggregationEngine] = None
+        self.last_timing: Dict[str, object] = {}
+
+    # ----------------------------------------------------------------------------------
+    def sessions(self):
+        """One native session per shard (created on first use)."""
+        if self._sessions is None:
+            from . import runtime
+
+            G = len(self.devices)
+            per = self._pack_threads or max(2, min(16, os.cpu_count() or 1) // G)
+            seen = set()
+            out = []
+            for d in self.devices:
+                if d in seen:
+                    s = runtime.Session(d, threads=per)  # private session: same GPU, second shard
+                else:
+                    s = runtime.session(d)
+                    s.set("threads", per)
+                    seen.add(d)
+                out.append(s)
+            self._sessions = out
+        return self._sessions
+
+    def prewarm(self) -> None:
+        from . import runtime
+
+        for d in sorted(set(self.devices)):
+            runtime.prewarm(d)
+
+    def ingest(self, paths: Sequence, strategy: str, load, max_workers: int = 0) -> List:
+        """Threaded load of the shared-state files (the shards are staged by the aggregation
+        call, each over its own link)."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        paths = list(paths)
+        if not paths:
+            return []
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers or min(len(paths), 16, os.cpu_count() or 1)) as ex:
+            futures = [ex.submit(load, p) for p in paths]
+            states = [f.result() for f in futures]
+        self.last_ingest = {"load_and_stage_s": time.perf_counter() - t0, "prestaged_clients": 0}
+        return states
+
+    def _single(self) -> AggregationEngine:
+        if self._fallback is None:
+            from .engine import engine_for
+
+            self._fallback = engine_for(self.devices[0])
+        return self._fallback
+
+    def _budget(self, g: int) -> int:
+        if self.max_shard_bytes:
+            return int(self.max_shard_bytes)
+        from . import runtime
+
+        free, _ = runtime.device_memory(self.devices[g])
+        return int(free * HBM_HEADROOM)
+
+    def plan_ranges(self, M: int, bytes_per_elem: int) -> List[List[Tuple[int, int]]]:
+        """Per shard, the sub-ranges it streams through its GPU."""
+        bounds = shard_bounds(M, len(self.devices))
+        plan = []
+        for g, (lo, hi) in enumerate(bounds):
+            cap = max(SHARD_ALIGN, self._budget(g) // max(1, bytes_per_elem))
+            plan.append(_split(lo, hi, cap))
+        return plan
+
+    def _run(self, work) -> None:
+        """Run ``work(g, session)`` for every shard on its own thread; re-raise the first error."""
+        sess = self.sessions()
+        errors: List[Optional[BaseException]] = [None] * len(sess)
+
+        def body(g):
+            try:
+                sess[g].activate()
+                work(g, sess[g])
+            except BaseException as e:  # noqa: BLE001 - re-raised on the calling thread
+                errors[g] = e
+
+        threads = [threading.Thread(target=body, args=(g,), name=f"fedagg-shard-{g}") for g in range(len(sess))]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        for e in errors:
+            if e is not None:
+                raise e
+
+    @staticmethod
+    def _rows_direct(rows: List[List[np.ndarray]], dt: np.dtype, M: int) -> Optional[List[List[np.ndarray]]]:
+        """Rows as stageable segments when every array already has dtype ``dt`` (flat wire-format
+        rows as one segment), else None."""
+        if not all(a.dtype == dt for row in rows for a in row):
+            return None
+        flats = [flat_of(row) for row in rows]
+        if all(f is not None and f.size == M for f in flats):
+            return [[f] for f in flats]
+        return [[np.ascontiguousarray(a) for a in row] for row in rows]
+
+    # ----------------------------------------------------------------------------------
+    def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
+               wire: bool = False) -> List[np.ndarray]:
+        """fed_avg.py:217-222 for validated inputs, sharded by parameter range over the devices."""
+        t_start = time.perf_counter()
+        K = len(parameters_updates)
+        L = len(parameters_updates[0])
+        if L == 0:
+            return []
+        dts = {a.dtype for pu in parameters_updates for a in pu}
+        R = np.result_type(next(iter(dts)), 1.0) if len(dts) == 1 else None
+        if R is None or R != next(iter(dts)) or R not in (np.float16, np.float32, np.float64):
+            return self._single().fedavg(parameters_updates, n_samples, wire)  # dtype groups / casts
+        layout = BucketLayout(list(range(L)), [a.shape for a in parameters_updates[0]], R)
+        M, isz = layout.M, R.itemsize
+        rows = self._rows_direct(parameters_updates, R, M)
+        kind = kind_of(R)
+        w = fedavg_weights(n_samples, kind)
+        pw_all = layout.pairwise_idx.astype(np.int64)
+        out = np.empty(M, dtype=R)
+        ranges = self.plan_ranges(M, (K + 1) * isz)
+        ws_bytes = _native.load().fedagg_pairwise_ws_bytes(K, max(1, pw_all.size), 8)
+        timing: List[Dict[str, float]] = [dict() for _ in self.devices]
+
+        def work(g, s):
+            tm = timing[g]
+            for lo, hi in ranges[g]:
+                n = hi - lo
+                ld = _ld(n, isz)
+                t0 = time.perf_counter()
+                d_bucket = s.buffer(self._B_BUCKET, K * ld * isz)
+                s.stage(d_bucket, ld * isz, rows, byte_range=(lo * isz, hi * isz))
+                t1 = time.perf_counter()
+                d_out = s.buffer(self._B_OUT, ld * isz)
+                ws = s.buffer(self._B_WS, ws_bytes)
+                pw = (pw_all[(pw_all >= lo) & (pw_all < hi)] - lo).astype(np.uint64)
+                ptrs = [d_bucket + k * ld * isz for k in range(K)]
+                FedAvgPlan(kind, ptrs, w, n, d_out, pw, ws).launch(s.stream)
+                s.fetch(d_out, out[lo:hi])
+                tm["stage_s"] = tm.get("stage_s", 0.0) + t1 - t0
+                tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
+                tm["ranges"] = tm.get("ranges", 0) + 1
+
+        self._run(work)
+        self.last_timing = {"shards": timing, "total_s": time.perf_counter() - t_start,
+                            "ranges": [r for r in ranges]}
+        results: List[Optional[np.ndarray]] = [None] * L
+        for li, arr in layout.unpack(out, wire):
+            results[li] = arr
+        return results  # type: ignore[return-value]
+
+    # ----------------------------------------------------------------------------------
+    def scaffold(self, parameters_updates, control_variate_updates, server_control_variates, n_samples,
+                 aggregation_lr, wire: bool = False):
+        """scaffold.py:193-196 (c equality, as a mismatch count) and :297-337 (fp64 sums), sharded by
+        parameter range.  Returns ``(mismatches, new_server_control_variate, avg_parameters_update)``."""
+        t_start = time.perf_counter()
+        K = len(parameters_updates)
+        L = len(parameters_updates[0])
+        if L == 0:
+            return 0, [], []
+        lists = (parameters_updates, control_variate_updates, server_control_variates)
+        dts = {a.dtype for lst in lists for client in lst for a in client}
+        shapes = [[a.shape for a in lst[0]] for lst in lists]
+        if len(dts) != 1 or next(iter(dts)) not in (np.float32, np.float64) or not (shapes[0] == shapes[1] == shapes[2]):
+            return self._single().scaffold(*lists, n_samples, aggregation_lr, wire)
+        sdt = next(iter(dts))
+        kind = "f32" if sdt == np.float32 else "f64"
+        isz = sdt.itemsize
+        layout = BucketLayout(list(range(L)), shapes[0], sdt)
+        M = layout.M
+        rows_d = self._rows_direct(parameters_updates, sdt, M)
+        rows_c = self._rows_direct(control_variate_updates, sdt, M)
+        rows_s = self._rows_direct(server_control_variates, sdt, M)
+        w = scaffold_weights(n_samples)
+        lr = float(aggregation_lr)
+        pw_all = layout.pairwise_idx.astype(np.int64)
+        out_d = np.empty(M, np.float64)
+        out_c = np.empty(M, np.float64)
+        mism = [0] * len(self.devices)
+        # per element: K deltas + K control variates + K server-c copies in, two fp64 outputs
+        ranges = self.plan_ranges(M, 3 * K * isz + 16)
+        ws_bytes = _native.load().fedagg_pairwise_ws_bytes(K, max(1, pw_all.size), 8)
+
+        def work(g, s):
+            for lo, hi in ranges[g]:
+                n = hi - lo
+                ld = _ld(n, isz)
+                br = (lo * isz, hi * isz)
+                d_d = s.buffer(self._B_BUCKET, K * ld * isz)
+                d_cv = s.buffer(self._B_CV, K * ld * isz)
+                d_cc = s.buffer(self._B_C, K * ld * isz)
+                s.stage(d_d, ld * isz, rows_d, byte_range=br)
+                s.stage(d_cv, ld * isz, rows_c, byte_range=br)
+                s.stage(d_cc, ld * isz, rows_s, byte_range=br)
+                cnt = s.buffer(self._B_CNT, 8)
+                s.memset(cnt, 0, 8)
+                equal_count(kind, [d_cc + k * ld * isz for k in range(K)], n, cnt, s.stream)
+                dout = s.buffer(self._B_OUT, _ld(n, 8) * 8)
+                cout = s.buffer(self._B_COUT, _ld(n, 8) * 8)
+                ws = s.buffer(self._B_WS, ws_bytes)
+                pw = (pw_all[(pw_all >= lo) & (pw_all < hi)] - lo).astype(np.uint64)
+                ScaffoldPlan(kind, [d_d + k * ld * isz for k in range(K)], [d_cv + k * ld * isz for k in range(K)],
+                             d_cc, w, n, lr, dout, cout, pw, ws).launch(s.stream)
+                m = np.zeros(1, np.int64)
+                s.fetch(cnt, m)
+                s.fetch(dout, out_d[lo:hi])
+                s.fetch(cout, out_c[lo:hi])
+                mism[g] += int(m[0])
+
+        self._run(work)
+        self.last_timing = {"total_s": time.perf_counter() - t_start, "ranges": ranges}
+        avg = [a for _, a in layout.unpack(out_d, wire)]
+        new_c = [a for _, a in layout.unpack(out_c, wire)]
+        return int(sum(mism)), new_c, avg

@@ -87,9 +87,11 @@ class Session:
                       "session_buffer")
         return int(p.value)
 
-    def stage(self, d_dst: int, ld_bytes: int, rows: Sequence[Sequence[np.ndarray]]) -> None:
+    def stage(self, d_dst: int, ld_bytes: int, rows: Sequence[Sequence[np.ndarray]],
+              byte_range: Optional[tuple] = None) -> None:
         """rows[k] = client k's host arrays, in bucket order, each C-contiguous; row k lands at
-        ``d_dst + k * ld_bytes``."""
+        ``d_dst + k * ld_bytes``.  ``byte_range=(lo, hi)`` stages only bytes ``[lo, hi)`` of every
+        row (a parameter-range shard), to ``d_dst + k * ld_bytes`` likewise."""
         K = len(rows)
         nseg = len(rows[0]) if K else 0
         keep: List[np.ndarray] = []
@@ -106,11 +108,21 @@ class Session:
                     sizes[i] = a.nbytes
                 elif a.nbytes != sizes[i]:
                     raise ValueError("segment sizes differ between clients")
-        _native.check(self.lib.fedagg_session_stage(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K, nseg, ptrs,
-                                                    sizes), "session_stage")
+        if byte_range is None:
+            _native.check(self.lib.fedagg_session_stage(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K, nseg,
+                                                        ptrs, sizes), "session_stage")
+        else:
+            lo, hi = (int(v) for v in byte_range)
+            _native.check(self.lib.fedagg_session_stage_range(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K,
+                                                              nseg, ptrs, sizes, lo, hi), "session_stage_range")
+
+    def activate(self) -> None:
+        """Make this session's GPU the calling thread's current device (before kernel launches)."""
+        _native.check(self.lib.fedagg_session_activate(self._h), "session_activate")
 
     def fetch(self, d_src: int, out: np.ndarray) -> np.ndarray:
-        """Copy ``out.nbytes`` from HBM into ``out`` (synchronous)."""
+        """Copy ``out.nbytes`` from HBM into ``out`` (synchronous; ``out`` may be a contiguous
+        slice of a larger array)."""
         if not out.flags.c_contiguous:
             raise ValueError("fetch destination must be C-contiguous")
         _native.check(self.lib.fedagg_session_fetch(self._h, ctypes.c_void_p(d_src),
@@ -138,6 +150,14 @@ class Session:
         _native.check(self.lib.fedagg_scale_cast(ctypes.c_void_p(d_in), kind_code(in_dtype), float(w),
                                                  ctypes.c_void_p(d_out), kind_code(out_dtype), int(n),
                                                  ctypes.c_void_p(self.stream)), "scale_cast")
+
+
+def device_memory(device: int) -> tuple:
+    """``(free, total)`` HBM bytes of ``device`` (``hipMemGetInfo``)."""
+    lib = _native.load()
+    f, t = ctypes.c_uint64(), ctypes.c_uint64()
+    _native.check(lib.fedagg_device_memory(int(device), ctypes.byref(f), ctypes.byref(t)), "device_memory")
+    return int(f.value), int(t.value)
 
 
 _sessions: Dict[int, Session] = {}

@@ -11,7 +11,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from ..engine import engine_for
+from ..engine import Devices, engine_for
 from ..exceptions import EmptySharedStatesError
 from ..remote import remote
 from ..schemas import FedAvgAveragedState, FedAvgSharedState, StrategyName
@@ -34,7 +34,7 @@ def check_same_shapes(per_client_layers: List[List[np.ndarray]]) -> None:
 class FedAvg(Strategy):
     """Federated averaging: ``Δw = Σ_k (n_k / n) Δw_k`` (fed_avg.py:23-52)."""
 
-    def __init__(self, algo, metric_functions=None, device: Optional[int] = None):
+    def __init__(self, algo, metric_functions=None, device: Devices = None):
         if device is None:
             super().__init__(algo=algo, metric_functions=metric_functions)
         else:
@@ -62,7 +62,7 @@ class FedAvg(Strategy):
         return FedAvgAveragedState(avg_parameters_update=averaged_states)
 
 
-def weighted_average(shared_states, state_name: str, device: Optional[int] = None) -> List[np.ndarray]:
+def weighted_average(shared_states, state_name: str, device: Devices = None) -> List[np.ndarray]:
     """fed_avg.py:207-222 (also fed_pca.py:244-257): validation on the host, the weighted sum
     of every layer on the GPU."""
     if len(shared_states) == 0:

@@ -13,6 +13,7 @@ from typing import List, Optional
 
 import numpy as np
 
+from ..engine import Devices
 from ..remote import remote
 from ..schemas import FedPCAAveragedState, FedPCASharedState, StrategyName
 from .fed_avg import weighted_average
@@ -22,7 +23,7 @@ from .strategy import Strategy
 class FedPCA(Strategy):
     _aggregation_methods = {"avg_shared_states": "fedavg", "avg_shared_states_with_qr": "fedavg"}
 
-    def __init__(self, algo, metric_functions=None, device: Optional[int] = None):
+    def __init__(self, algo, metric_functions=None, device: Devices = None):
         if device is None:
             super().__init__(algo=algo, metric_functions=metric_functions)
         else:

@@ -10,7 +10,7 @@ the same ``c`` (scaffold.py:193-196) runs on the GPU too.
 
 from typing import List, Optional
 
-from ..engine import engine_for
+from ..engine import Devices, engine_for
 from ..remote import remote
 from ..schemas import ScaffoldAveragedStates, ScaffoldSharedState, StrategyName
 from .fed_avg import check_same_shapes
@@ -20,7 +20,7 @@ from .strategy import Strategy
 class Scaffold(Strategy):
     _aggregation_methods = {"avg_shared_states": "scaffold"}
 
-    def __init__(self, algo, aggregation_lr: float = 1, metric_functions=None, device: Optional[int] = None):
+    def __init__(self, algo, aggregation_lr: float = 1, metric_functions=None, device: Devices = None):
         if device is None:
             super().__init__(algo=algo, aggregation_lr=aggregation_lr, metric_functions=metric_functions)
         else:

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--kind", default="f32")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--full", action="store_true", help="the whole shape family (nt_store 0/1, grid-strided)")
     args = ap.parse_args()
 
     import torch
@@ -39,11 +40,15 @@ def main():
     plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
 
-    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0)
-    shapes = [dict(), dict(unroll=16), dict(vpt=2, tile=1), dict(vpt=4, tile=1), dict(vpt=4, tile=1, unroll=4),
-              dict(vpt=8, tile=1, unroll=4), dict(vpt=8, tile=1, unroll=2), dict(vpt=4, tile=1, grid_cap=8192),
-              dict(vpt=4, tile=1, grid_cap=2048)]
-    variants = [dict(base, **sh, nt_store=nts) for sh in shapes for nts in (0, 1)]
+    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0)
+    if args.full:
+        shapes = [dict(), dict(unroll=16), dict(vpt=2, tile=1), dict(vpt=4, tile=1), dict(vpt=4, tile=1, unroll=4),
+                  dict(vpt=8, tile=1, unroll=4), dict(vpt=8, tile=1, unroll=2), dict(vpt=4, tile=1, grid_cap=8192),
+                  dict(vpt=4, tile=1, grid_cap=2048)]
+        variants = [dict(base, **sh, nt_store=nts) for sh in shapes for nts in (0, 1)]
+    else:  # contiguous-tile shapes with nt stores, identity vs XCD-contiguous tile order
+        shapes = [dict(vpt=8, unroll=4), dict(vpt=8, unroll=2), dict(vpt=4, unroll=4), dict(vpt=4, unroll=8)]
+        variants = [dict(base, **sh, tile=1, nt_store=1, xcd=x) for sh in shapes for x in (0, 1)]
     times = {i: [] for i in range(len(variants))}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for r in range(args.rounds):
