@@ -199,18 +199,20 @@ def main():
     src = clients if wl["strategy"] == "fedavg" else delta
     nbytes_probe = probe_n * src.element_size()
     floats = nbytes_probe // 4 // 4 * 4
-    pgrid = int(min(floats // 4 // 256, 1 << 20))  # one 16-B vector per thread, like the bucket kernel
-    sink = torch.empty(pgrid, dtype=torch.float32, device=device)
-    for _ in range(3):
-        _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
-                                                stream.cuda_stream), "probe")
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(10):
-        lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid, stream.cuda_stream)
-    e1.record(stream)
-    torch.cuda.synchronize(device)
-    read_ceiling = floats * 4 / (e0.elapsed_time(e1) / 10 / 1e3) / 1e9
+    full = int(min(floats // 4 // 256, 1 << 20))  # one 16-B vector per thread, like the bucket kernel
+    sink = torch.empty(full, dtype=torch.float32, device=device)
+    read_ceiling = 0.0
+    for pgrid in sorted({min(16384, full), min(65536, full), full}):  # best grid = the ceiling
+        for _ in range(3):
+            _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
+                                                    stream.cuda_stream), "probe")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid, stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize(device)
+        read_ceiling = max(read_ceiling, floats * 4 / (e0.elapsed_time(e1) / 10 / 1e3) / 1e9)
 
     # ---- CPU baseline (rank 0, N == 1): the reference call structure timed on host cores ----
     cpu = None
@@ -259,7 +261,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": "fedavg_kernel<F32>" if wl["strategy"] == "fedavg" else "scaffold_kernel<float>",
+                "kernel": (f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>" if wl["strategy"] == "fedavg"
+                           else "scaffold_kernel<float>"),
                 "kernel_ms": round(kern_ms, 5),
                 "read_stream_ceiling_GBps": round(read_ceiling, 1),
                 "frac_of_read_ceiling": round(achieved / read_ceiling, 4),

@@ -1175,16 +1175,19 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
 // type: contiguous tiles of VPT*256 vectors per workgroup step with U-client load groups, the
 // grid-strided single-vector shape, and the pipelined variant; each with plain or
 // non-temporal output stores.  Client loads are non-temporal unless nt_load = 0 (one shape).
-// Measured on MI355X (tools/tune_fedavg.py, profiles/r01_tune_*.log): 8 KiB per wave per client
-// (vpt 8) with 4-client load groups is the best or within noise of it at every size measured
-// (8 x 25M fp32: 6.54 TB/s; 64 x 125M fp32: 6.43 TB/s; 128 x 350M bf16: 6.34 TB/s before the
-// coalesced fp32 stores).  4 KiB x 8 clients ties at 8 clients (box-to-box spread ~3 %).
+// Measured on MI355X (tools/tune_fedavg.py, profiles/r01_tune_*.log, r01_vpt16_*.log): 8 KiB per
+// wave per client (vpt 8) with 4-client load groups is best at 8 clients (8 x 25M fp32: 6.5 TB/s;
+// 16 KiB loses 11 %: half the workgroups); from 32 clients on, 16 KiB per wave per client with
+// 2-client groups wins (32 x 125M: +3 %, 64 x 125M fp32: 6.79 vs 6.65 TB/s, 128 x 350M bf16: +1 %);
+// 16 clients tie.  Box-to-box spread is ~3 %.
 struct Shape {
   int vpt, unroll;
 };
-inline Shape shape_for(int K) {
-  (void)K;
+inline Shape shape_for(int K, uint64_t nvec) {
   if (g_vpt > 0) return {g_vpt, g_unroll};
+  // many client streams over a large bucket: 16 KiB per wave per stream (fewer DRAM row
+  // switches; 64 x 125M fp32 +2 %, 128 x 350M bf16 +1 %), as long as the grid stays >> 256 CUs
+  if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) return Shape{16, 2};
   return Shape{8, 4};
 }
 
@@ -1194,6 +1197,10 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
 #define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
   if (!g_nt_load) return launch_fedavg_variant<E, false, NTS, 1, 8, false, false>(FA_ARGS);
   if (g_tile) {
+    if (sh.vpt >= 16) {  // 16 KiB per wave per client stream (tuning only)
+      if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true>(FA_ARGS);
+      return launch_fedavg_variant<E, true, NTS, 16, 2, false, true>(FA_ARGS);
+    }
     if (sh.vpt >= 8) {
       if (sh.unroll <= 2) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
@@ -1272,7 +1279,7 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
   const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK;
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg: workspace needed for %lld pairwise segments", P);
   const uint64_t nvec = vec ? M / E::L : 0;
-  const Shape sh = shape_for(K);
+  const Shape sh = shape_for(K, nvec);
   const uint64_t per_thread = (g_tile && g_nt_load) ? (uint64_t)sh.vpt : 1;
   const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
@@ -1361,6 +1368,7 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
     return launch_scaffold_variant<TIn, true, true, 4, 4, true>(SC_ARGS);
   }
   if (g_sc_vpt >= 8) {
+    if (g_sc_unroll >= 2 && nts) return launch_scaffold_variant<TIn, true, true, 8, 2>(SC_ARGS);
     if (nts) return launch_scaffold_variant<TIn, true, true, 8, 1>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 8, 1>(SC_ARGS);
   }
@@ -1471,13 +1479,15 @@ int fedagg_tune(const char* key, long long value) {
   if (!strcmp(key, "grid_cap")) g_grid_cap = (int)value;
   else if (!strcmp(key, "nt_load")) g_nt_load = value ? 1 : 0;
   else if (!strcmp(key, "nt_store")) g_nt_store = value < 0 ? -1 : (value ? 1 : 0);
-  else if (!strcmp(key, "vpt")) g_vpt = value <= 0 ? 0 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
-  else if (!strcmp(key, "unroll")) g_unroll = value >= 16 ? 16 : (value <= 2 ? 2 : (value <= 4 ? 4 : 8));
+  else if (!strcmp(key, "vpt"))
+    g_vpt = value <= 0 ? 0 : value >= 16 ? 16 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
+  else if (!strcmp(key, "unroll"))
+    g_unroll = value >= 16 ? 16 : (value <= 1 ? 1 : value <= 2 ? 2 : (value <= 4 ? 4 : 8));
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
   else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
-  else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 2 ? 2 : (value >= 8 ? 8 : 4);
+  else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");

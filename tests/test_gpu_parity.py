@@ -462,7 +462,9 @@ def test_many_numel1_layers_fused_and_separate(torch_gpu, dummy_algo_class, fuse
 @pytest.mark.parametrize("knobs", [dict(vpt=2), dict(nt_load=0), dict(nt_store=1), dict(grid_cap=7),
                                    dict(unroll=4), dict(unroll=16), dict(pipe=1), dict(vpt=2, tile=1),
                                    dict(vpt=4, tile=1, grid_cap=5), dict(vpt=8, unroll=2, tile=1),
-                                   dict(vpt=8, unroll=4, tile=1, grid_cap=3), dict(vpt=1, tile=0)])
+                                   dict(vpt=8, unroll=4, tile=1, grid_cap=3), dict(vpt=1, tile=0),
+                                   dict(vpt=16, unroll=2, tile=1), dict(vpt=16, unroll=1, tile=1, grid_cap=3),
+                                   dict(xcd=1), dict(vpt=16, unroll=2, tile=1, xcd=1)])
 def test_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -472,7 +474,7 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
@@ -483,11 +485,41 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
 
 
+def test_auto_shape_many_clients_bit_identical(torch_gpu):
+    """K >= 32 over a large bucket picks the 16-KiB-per-stream shape (shape_for); it must agree
+    bit for bit with the 8-KiB shape and with the oracle order on sampled elements."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 33, 16 * 256 * 2048 * 4 + 77  # just past the threshold, ragged tail
+    x = torch.randn((K, M + 3), device="cuda")
+    ns = list(range(100, 100 + K))
+    w = fedavg_weights(ns, "f32")
+    outs = []
+    for kn in (dict(vpt=0), dict(vpt=8, unroll=4)):
+        _native.tune(**kn)
+        out = torch.empty(M + 3, device="cuda")
+        FedAvgPlan("f32", x, w, M, out, [5, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append(out[:M].clone())
+    _native.tune(vpt=0, unroll=8)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    idx = np.array([0, 1, 4095, 16 * 256 * 4 * 7 + 3, M // 2, M - 80, M - 2])
+    xs = x[:, torch.from_numpy(idx).cuda()].cpu().numpy()
+    acc = np.zeros(idx.size, np.float32)
+    for k in range(K):
+        acc = (acc + (xs[k] * w[k]).astype(np.float32)).astype(np.float32)
+    assert np.array_equal(acc.view(np.uint32), outs[0][torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint32))
+    del x
+
+
 @pytest.mark.parametrize("knobs", [dict(sc_vpt=1), dict(sc_vpt=2, sc_unroll=2), dict(nt_store=0), dict(nt_load=0),
                                    dict(grid_cap=3), dict(sc_vpt=4, sc_unroll=2), dict(sc_vpt=2, sc_unroll=4),
                                    dict(sc_vpt=8), dict(sc_vpt=8, grid_cap=2), dict(sc_split=1),
                                    dict(sc_split=1, sc_unroll=8), dict(sc_split=1, sc_vpt=8, sc_unroll=2),
-                                   dict(sc_split=1, sc_vpt=8, grid_cap=2)])
+                                   dict(sc_split=1, sc_vpt=8, grid_cap=2), dict(sc_vpt=8, sc_unroll=2),
+                                   dict(xcd=1), dict(sc_vpt=8, sc_unroll=2, xcd=1, grid_cap=5)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -498,7 +530,7 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     cv = torch.randn((K, M + 1), device="cuda")
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
-    default = dict(sc_vpt=4, sc_unroll=4, sc_split=0, nt_store=1, nt_load=1, grid_cap=0)
+    default = dict(sc_vpt=4, sc_unroll=4, sc_split=0, nt_store=1, nt_load=1, grid_cap=0, xcd=0)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)

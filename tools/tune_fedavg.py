@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--full", action="store_true", help="the whole shape family (nt_store 0/1, grid-strided)")
+    ap.add_argument("--xcd", action="store_true", help="each shape also with the XCD-contiguous tile order")
     args = ap.parse_args()
 
     import torch
@@ -46,9 +47,10 @@ def main():
                   dict(vpt=8, tile=1, unroll=4), dict(vpt=8, tile=1, unroll=2), dict(vpt=4, tile=1, grid_cap=8192),
                   dict(vpt=4, tile=1, grid_cap=2048)]
         variants = [dict(base, **sh, nt_store=nts) for sh in shapes for nts in (0, 1)]
-    else:  # contiguous-tile shapes with nt stores, identity vs XCD-contiguous tile order
-        shapes = [dict(vpt=8, unroll=4), dict(vpt=8, unroll=2), dict(vpt=4, unroll=4), dict(vpt=4, unroll=8)]
-        variants = [dict(base, **sh, tile=1, nt_store=1, xcd=x) for sh in shapes for x in (0, 1)]
+    else:  # contiguous-tile shapes with nt stores (--xcd: also the XCD-contiguous tile order)
+        shapes = [dict(vpt=8, unroll=4), dict(vpt=8, unroll=2), dict(vpt=16, unroll=2), dict(vpt=16, unroll=1),
+                  dict(vpt=4, unroll=4), dict(vpt=4, unroll=8)]
+        variants = [dict(base, **sh, tile=1, nt_store=1, xcd=x) for sh in shapes for x in ((0, 1) if args.xcd else (0,))]
     times = {i: [] for i in range(len(variants))}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for r in range(args.rounds):
