@@ -766,3 +766,83 @@ def test_sharding_over_rccl_world1(torch_gpu):
         _assert_same(client_sharded_fedavg(pus, ns, combine="ordered"), ref)
     finally:
         dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------
+# non-finite and extreme values (a diverged client: NaN / Inf updates, overflow, denormals)
+# ------------------------------------------------------------------------------------------
+# Contract: every NaN of the reference is a NaN here and every other value (Inf, max, denormal,
+# signed zero) is bit-exact.  NaN payload and sign bits are NOT part of the reference's
+# behaviour: NumPy's x86 loops keep the first operand's NaN in the scalar path and the second
+# operand's in the SIMD path (fp32: arrays of <= 16 vs >= 17 elements on the box this was
+# measured on), and invalid operations give the negative "indefinite" NaN; the GPU picks its own.
+def _assert_same_nan_aware(got, ref):
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        assert isinstance(g, np.ndarray)
+        assert g.dtype == r.dtype and g.shape == r.shape, (g.dtype, r.dtype, g.shape, r.shape)
+        rn = np.isnan(r)
+        assert np.array_equal(np.isnan(g), rn)
+        assert np.array_equal(_bits(g)[~rn], _bits(r)[~rn])
+
+
+def _nonfinite_updates(dtype, K, rng):
+    info = np.finfo(dtype)
+    bits = {np.float16: np.uint16, np.float32: np.uint32, np.float64: np.uint64}[dtype]
+    specials = [np.nan, -np.nan, np.inf, -np.inf, info.max, -info.max, info.tiny, info.tiny / 4, -0.0, 0.0,
+                info.smallest_subnormal]
+    # NaNs with payloads: quiet with a payload, and signalling (NumPy quiets them in arithmetic)
+    qpay = np.array([np.nan], dtype).view(bits) | bits(5)
+    spay = (np.array([np.inf], dtype).view(bits) | bits(3))
+    specials += [qpay.view(dtype)[0], spay.view(dtype)[0], (qpay | np.array([np.inf], dtype).view(bits) * 0 | (bits(1) << bits(8 * np.dtype(dtype).itemsize - 1))).view(dtype)[0]]
+    specials = np.array(specials, dtype)
+    shapes = [(257,), (1,), (16, 9), (1, 1)]
+    ups = []
+    for k in range(K):
+        row = []
+        for s in shapes:
+            a = (rng.standard_normal(s) * 10.0).astype(dtype)
+            flat = a.reshape(-1)
+            n = flat.size
+            pick = rng.random(n) < 0.3  # 30 % specials, per client
+            flat[pick] = specials[rng.integers(0, specials.size, int(pick.sum()))]
+            row.append(a)
+        ups.append(row)
+    return ups
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.float16])
+@pytest.mark.parametrize("K", [1, 2, 7, 9, 33])
+def test_fedavg_nonfinite_bit_exact(torch_gpu, dummy_algo_class, dtype, K):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    rng = np.random.default_rng(1000 + K)
+    ups = _nonfinite_updates(dtype, K, rng)
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    with np.errstate(all="ignore"):
+        ref = fedavg_reference_structure(ups, ns)
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, ups)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(shared_states=states, _skip=True).avg_parameters_update
+    _assert_same_nan_aware(got, ref)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_scaffold_nonfinite_bit_exact(torch_gpu, dummy_algo_class, dtype):
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    rng = np.random.default_rng(77)
+    K = 6
+    pus = _nonfinite_updates(dtype, K, rng)
+    cvs = _nonfinite_updates(dtype, K, rng)
+    c = [(rng.standard_normal(a.shape) * 3).astype(dtype) for a in pus[0]]
+    c[0].reshape(-1)[:3] = [np.inf, -np.inf, -0.0]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    with np.errstate(all="ignore"):
+        ref_c, ref_avg = scaffold_reference_structure(pus, cvs, c, ns, 0.5)
+    states = [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                  server_control_variate=c) for k in range(K)]
+    got = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.5).avg_shared_states(shared_states=states, _skip=True)
+    _assert_same_nan_aware(got.avg_parameters_update, ref_avg)
+    _assert_same_nan_aware(got.server_control_variate, ref_c)
