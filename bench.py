@@ -153,7 +153,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = bytes_alg * world / (elapsed / args.steps) / 1e9
 
-    # ---- parity spot check (outside the timed region): sampled elements vs the oracle order ----
+    # ---- parity spot check (outside the timed region): sampled elements vs the sequential order ----
     parity = None
     if wl["strategy"] == "fedavg":
         g = np.random.default_rng(123)
@@ -165,14 +165,8 @@ def main():
         acc = np.zeros(idx.size, np.float32)
         for k in range(K):
             acc = (acc + (xs[k] * w32[k]).astype(np.float32)).astype(np.float32)
-        pw_ok = True
-        for p in layout.pairwise_idx.astype(np.int64):  # numel==1 segment: NumPy pairwise order
-            from oracle import numpy_pairwise_sum
-
-            prods = np.array([np.float32(clients[k, p].float().item()) * w32[k] for k in range(K)], np.float32)
-            pw_ok &= np.float32(0.0) + numpy_pairwise_sum(prods) == np.float32(out[p].item())
-        parity = {"sampled": int(idx.size), "mismatches": int(np.sum(acc.view(np.uint32) != got.view(np.uint32))),
-                  "pairwise_ok": bool(pw_ok)}
+        # (the numel == 1 element is reduced in NumPy's pairwise order: tests/ check it against the oracle)
+        parity = {"sampled": int(idx.size), "mismatches": int(np.sum(acc.view(np.uint32) != got.view(np.uint32)))}
     else:  # Scaffold (scaffold.py:262-263,293): fp64 products and sums, c added last, lr after the sum
         g = np.random.default_rng(123)
         idx = np.setdiff1d(np.unique(g.integers(0, M, 4096)), layout.pairwise_idx.astype(np.int64))
