@@ -250,12 +250,38 @@ class AggregationEngine:
     # HBM buffer slots of the session
     _B_BUCKET, _B_OUT, _B_WS, _B_TMP, _B_CV, _B_C, _B_COUT, _B_CNT = range(8)
 
-    def __init__(self, device: Optional[int] = None, pack_threads: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, pack_threads: Optional[int] = None,
+                 max_bucket_bytes: Optional[int] = None):
         self._device_index = device
         self._pack_threads = pack_threads
+        # HBM the staged buckets of one call may take before the call is streamed through the GPU
+        # in parameter ranges (multi_device.MultiDeviceEngine with this one device); default:
+        # 85 % of the device's free HBM at call time
+        self.max_bucket_bytes = max_bucket_bytes
+        self._ooc = None
         self.last_timing: Dict[str, float] = {}
         # rows already on the device from ingest(): slot -> (d_bucket, ld_bytes, {k: row arrays})
         self._prestaged: Dict[int, Tuple[int, int, Dict[int, List[np.ndarray]]]] = {}
+
+    def _out_of_core(self, need_bytes: int):
+        """The range-streaming engine when ``need_bytes`` of buckets exceed this GPU's budget
+        (K x M beyond 288 GB on one MI355X), else None."""
+        from .multi_device import HBM_HEADROOM, MultiDeviceEngine
+
+        if self.max_bucket_bytes is not None:
+            budget = int(self.max_bucket_bytes)
+        else:
+            from . import runtime
+
+            free = runtime.device_memory(self._index())[0] + self.session().held_bytes()
+            budget = int(free * HBM_HEADROOM)
+        if need_bytes <= budget:
+            return None
+        if self._ooc is None:
+            self._ooc = MultiDeviceEngine([self._index()], max_shard_bytes=self.max_bucket_bytes,
+                                          pack_threads=self._pack_threads)
+        self._prestaged = {}
+        return self._ooc
 
     def _index(self) -> int:
         idx = self._device_index
@@ -439,6 +465,16 @@ class AggregationEngine:
             key = (R.str, None if all(d == R for d in pds) else tuple(d.str for d in pds))
             groups.setdefault(key, []).append(li)
 
+        if len(groups) == 1:
+            (rstr, mixed), = groups.keys()
+            R = np.dtype(rstr)
+            direct = mixed is None and all(a.dtype == R for pu in parameters_updates for a in pu)
+            need = (K + 1) * BucketLayout(range(L), [a.shape for a in parameters_updates[0]], R).ld * R.itemsize
+            ooc = self._out_of_core(need) if direct else None
+            if ooc is not None:
+                out = ooc.fedavg(parameters_updates, n_samples, wire)
+                self.last_timing = {"out_of_core": ooc.last_timing}
+                return out
         results: List[Optional[np.ndarray]] = [None] * L
         if len(groups) != 1:
             self._prestaged = {}
@@ -509,6 +545,14 @@ class AggregationEngine:
         lay_d = BucketLayout(lid, [a.shape for a in parameters_updates[0]], sdt)
         lay_c = BucketLayout(lid, [a.shape for a in control_variate_updates[0]], sdt)
         lay_s = BucketLayout(lid, [a.shape for a in server_control_variates[0]], sdt)
+        same = [g.shape for g in lay_d.segments] == [g.shape for g in lay_c.segments] == \
+            [g.shape for g in lay_s.segments]
+        if same and all(a.dtype == sdt for lst in lists for client in lst for a in client):
+            ooc = self._out_of_core(3 * K * lay_d.ld * sdt.itemsize + 2 * lay_d.ld * 8)
+            if ooc is not None:
+                out = ooc.scaffold(*lists, n_samples, aggregation_lr, wire)
+                self.last_timing = {"out_of_core": ooc.last_timing}
+                return out
         w = scaffold_weights(n_samples)
         lr = float(aggregation_lr)
         isz = sdt.itemsize

@@ -129,7 +129,7 @@ class MultiDeviceEngine:
         from . import runtime
 
         free, _ = runtime.device_memory(self.devices[g])
-        return int(free * HBM_HEADROOM)
+        return int((free + self.sessions()[g].held_bytes()) * HBM_HEADROOM)
 
     def plan_ranges(self, M: int, bytes_per_elem: int) -> List[List[Tuple[int, int]]]:
         """Per shard, the sub-ranges it streams through its GPU."""

@@ -52,6 +52,7 @@ class Session:
             )
         self._h = ctypes.c_void_p(h)
         self.device = int(device)
+        self._held: Dict[int, int] = {}
         self.stream = int(self.lib.fedagg_session_stream(self._h) or 0)
         nthreads = threads or int(os.environ.get("FEDAGG_PACK_THREADS", "0")) or min(16, os.cpu_count() or 1)
         self.set("threads", nthreads)
@@ -81,7 +82,12 @@ class Session:
         arr = (ctypes.c_uint64 * n)(*[int(slot_bytes.get(i, 0)) for i in range(n)])
         _native.check(self.lib.fedagg_session_warm(self._h, arr, n), "session_warm")
 
+    def held_bytes(self) -> int:
+        """HBM held by this session's grow-only buffers (reusable by the next call)."""
+        return sum(self._held.values())
+
     def buffer(self, slot: int, nbytes: int) -> int:
+        self._held[int(slot)] = max(self._held.get(int(slot), 0), max(16, int(nbytes)))
         p = ctypes.c_void_p()
         _native.check(self.lib.fedagg_session_buffer(self._h, int(slot), max(16, int(nbytes)), ctypes.byref(p)),
                       "session_buffer")

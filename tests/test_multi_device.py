@@ -190,3 +190,29 @@ def test_strategies_with_device_list(gpu, dummy_algo_class):
         bad = [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
                                    server_control_variate=[a + (k == 1) for a in c]) for k in range(K)]
         Scaffold(algo=dummy_algo_class(), device="0,0").avg_shared_states(shared_states=bad, _skip=True)
+
+
+@pytest.mark.gpu
+def test_single_gpu_engine_streams_oversized_calls(gpu):
+    """AggregationEngine hands a call whose buckets exceed its HBM budget to the range-streaming
+    engine on the same GPU (K x M beyond one MI355X's 288 GB), bit-exact."""
+    from substrafl_amd.engine import AggregationEngine
+
+    rng = np.random.default_rng(21)
+    K = 9
+    pus = _updates(rng, K, SHAPES)
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    eng = AggregationEngine(0, max_bucket_bytes=300_000)
+    _assert_same(eng.fedavg(pus, ns), fedavg_reference_structure(pus, ns))
+    assert "out_of_core" in eng.last_timing and len(eng.last_timing["out_of_core"]["ranges"][0]) > 1
+    cvs = _updates(rng, K, SHAPES)
+    c = [rng.standard_normal(s).astype(np.float32) for s in SHAPES]
+    mism, new_c, avg = eng.scaffold(pus, cvs, [c] * K, ns, 1.5)
+    ref_c, ref_avg = scaffold_reference_structure(pus, cvs, c, ns, 1.5)
+    assert mism == 0 and "out_of_core" in eng.last_timing
+    _assert_same(avg, ref_avg)
+    _assert_same(new_c, ref_c)
+    # a call that fits stays on the plain single-launch path
+    big = AggregationEngine(0)
+    _assert_same(big.fedavg(pus, ns), fedavg_reference_structure(pus, ns))
+    assert "out_of_core" not in big.last_timing
