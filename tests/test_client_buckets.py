@@ -175,3 +175,22 @@ def test_scaffold_client_round_mixed_fp64_vs_torch():
 def _same64(a, b):
     return a.shape == b.shape and a.dtype == b.dtype and torch.equal(a.contiguous().view(torch.int64),
                                                                       b.contiguous().view(torch.int64))
+
+
+def test_export_host_buffer_reused_only_when_released():
+    """export_numpy's host buffer is recycled across rounds (no 100 MB of fresh page faults per
+    export) only when no array of an earlier export is alive."""
+    from substrafl_amd.algorithms import weight_manager as wm
+    from substrafl_amd.wire import bucket_views
+
+    a = wm._host_buffer(100, np.float32)
+    held = bucket_views(a, [(10, 10)])
+    del a
+    b = wm._host_buffer(100, np.float32)
+    assert not np.shares_memory(b, held[0])
+    ptr = b.__array_interface__["data"][0]
+    del b
+    c = wm._host_buffer(64, np.float32)  # smaller request: a prefix of the released buffer
+    assert c.__array_interface__["data"][0] == ptr
+    other = wm._host_buffer(8, np.float64)  # per dtype
+    assert not np.shares_memory(other, c)
