@@ -19,7 +19,6 @@ for a Python scalar); ``increment_parameters`` is ``w += fl32(multiplier) * u``.
 from __future__ import annotations
 
 import ctypes
-import sys
 from typing import Generator, List, Optional, Sequence
 
 import numpy as np
@@ -281,26 +280,9 @@ def export_numpy(tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
     from .. import runtime
 
     # one D2H through the native session's pinned ring (chunked, copied out by its worker pool)
-    host = _host_buffer(flat.numel(), torch.empty(0, dtype=flat.dtype).numpy().dtype)  # bf16 raises, as .numpy()
+    host = runtime.reusable_host_array(flat.numel(), torch.empty(0, dtype=flat.dtype).numpy().dtype,
+                                       "export")  # bf16 raises, as .numpy()
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
     runtime.session(flat.device.index).fetch(flat.data_ptr(), host)
     return bucket_views(host, [tuple(t.shape) for t in tensors])
 
-
-_host_cache: dict = {}
-
-
-def _host_buffer(n: int, dtype) -> np.ndarray:
-    """A host array of ``n`` elements for :func:`export_numpy`.  A fresh 100 MB allocation costs
-    ~8 ms of first-touch page faults (glibc maps every block above 32 MiB anew), more than the D2H
-    itself, so the previous round's buffer is reused -- but only when nothing references it any
-    more (every array handed out earlier was a view holding it), so no caller ever sees its data
-    change."""
-    dtype = np.dtype(dtype)
-    buf = _host_cache.get(dtype)
-    # references: the cache dict, the local name and getrefcount's argument; a live view adds one
-    if buf is not None and buf.size >= n and sys.getrefcount(buf) <= 3:
-        return buf[:n]
-    buf = np.empty(n, dtype=dtype)
-    _host_cache[dtype] = buf
-    return buf

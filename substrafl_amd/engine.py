@@ -30,7 +30,7 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
-from . import _native
+from . import _native, runtime
 from .layout import BucketLayout
 from .wire import flat_of
 
@@ -503,7 +503,7 @@ class AggregationEngine:
             ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
             t1 = time.perf_counter()
             FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
-            out = np.empty(layout.M, dtype=R)
+            out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}")
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
             tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
             for li, arr in layout.unpack(out, wire):
@@ -593,8 +593,8 @@ class AggregationEngine:
                          ws).launch(s.stream)
             ScaffoldPlan(kind, rows_c, rows_c, d_cc, w, lay_c.M, lr, scratch, cout, lay_c.pairwise_idx,
                          ws).launch(s.stream)
-        out_d = np.empty(lay_d.M, np.float64)
-        out_c = np.empty(lay_c.M, np.float64)
+        out_d = runtime.reusable_host_array(lay_d.M, np.float64, "scaffold-delta")
+        out_c = runtime.reusable_host_array(lay_c.M, np.float64, "scaffold-c")
         mism = np.zeros(1, np.int64)
         s.fetch(cnt, mism)
         s.fetch(dout, out_d)

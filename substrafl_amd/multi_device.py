@@ -33,7 +33,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import _native
+from . import _native, runtime
 from .engine import AggregationEngine, FedAvgPlan, ScaffoldPlan, equal_count, fedavg_weights, kind_of, scaffold_weights
 from .layout import ROW_ALIGN_BYTES, BucketLayout
 from .sharding import SHARD_ALIGN, shard_bounds
@@ -191,7 +191,7 @@ class MultiDeviceEngine:
         kind = kind_of(R)
         w = fedavg_weights(n_samples, kind)
         pw_all = layout.pairwise_idx.astype(np.int64)
-        out = np.empty(M, dtype=R)
+        out = runtime.reusable_host_array(M, R, "multi-fedavg")
         ranges = self.plan_ranges(M, (K + 1) * isz)
         ws_bytes = _native.load().fedagg_pairwise_ws_bytes(K, max(1, pw_all.size), 8)
         timing: List[Dict[str, float]] = [dict() for _ in self.devices]
@@ -249,8 +249,8 @@ class MultiDeviceEngine:
         w = scaffold_weights(n_samples)
         lr = float(aggregation_lr)
         pw_all = layout.pairwise_idx.astype(np.int64)
-        out_d = np.empty(M, np.float64)
-        out_c = np.empty(M, np.float64)
+        out_d = runtime.reusable_host_array(M, np.float64, "multi-scaffold-delta")
+        out_c = runtime.reusable_host_array(M, np.float64, "multi-scaffold-c")
         mism = [0] * len(self.devices)
         # per element: K deltas + K control variates + K server-c copies in, two fp64 outputs
         ranges = self.plan_ranges(M, 3 * K * isz + 16)

@@ -158,6 +158,27 @@ class Session:
                                                  ctypes.c_void_p(self.stream)), "scale_cast")
 
 
+_host_cache: Dict[tuple, np.ndarray] = {}
+
+
+def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
+    """A host array of ``n`` elements for a D2H result (``tag`` names the call site).  A fresh
+    100 MB allocation costs ~8 ms of first-touch page faults (glibc maps every block above 32 MiB
+    anew), three times the D2H itself, so the previous call's buffer is recycled -- but only when
+    nothing references it any more (every array handed out from it was a view holding it), so no
+    caller ever sees its data change."""
+    import sys
+
+    key = (tag, np.dtype(dtype))
+    buf = _host_cache.get(key)
+    # references: the cache dict, the local name and getrefcount's argument; a live view adds one
+    if buf is not None and buf.size >= n and sys.getrefcount(buf) <= 3:
+        return buf[:n]
+    buf = np.empty(n, dtype=key[1])
+    _host_cache[key] = buf
+    return buf
+
+
 def device_memory(device: int) -> tuple:
     """``(free, total)`` HBM bytes of ``device`` (``hipMemGetInfo``)."""
     lib = _native.load()

@@ -177,20 +177,24 @@ def _same64(a, b):
                                                                       b.contiguous().view(torch.int64))
 
 
-def test_export_host_buffer_reused_only_when_released():
-    """export_numpy's host buffer is recycled across rounds (no 100 MB of fresh page faults per
-    export) only when no array of an earlier export is alive."""
-    from substrafl_amd.algorithms import weight_manager as wm
+def test_host_result_buffer_reused_only_when_released():
+    """D2H result buffers (export_numpy, the engine's outputs) are recycled across calls (no 100 MB
+    of fresh page faults per call) only when no array handed out from them is alive."""
+    from substrafl_amd.runtime import reusable_host_array
     from substrafl_amd.wire import bucket_views
 
-    a = wm._host_buffer(100, np.float32)
+    a = reusable_host_array(100, np.float32, "t")
     held = bucket_views(a, [(10, 10)])
     del a
-    b = wm._host_buffer(100, np.float32)
+    b = reusable_host_array(100, np.float32, "t")
     assert not np.shares_memory(b, held[0])
     ptr = b.__array_interface__["data"][0]
     del b
-    c = wm._host_buffer(64, np.float32)  # smaller request: a prefix of the released buffer
+    c = reusable_host_array(64, np.float32, "t")  # smaller request: a prefix of the released buffer
     assert c.__array_interface__["data"][0] == ptr
-    other = wm._host_buffer(8, np.float64)  # per dtype
-    assert not np.shares_memory(other, c)
+    assert not np.shares_memory(reusable_host_array(8, np.float32, "other"), c)  # per call site
+    assert not np.shares_memory(reusable_host_array(8, np.float64, "t"), c)  # per dtype
+    views = [c[:10].reshape(2, 5), c[10:20]]  # plain views (the engine's per-layer outputs) hold it too
+    del c
+    d = reusable_host_array(64, np.float32, "t")
+    assert not any(np.shares_memory(d, v) for v in views)
