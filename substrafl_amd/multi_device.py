@@ -236,7 +236,8 @@ class MultiDeviceEngine:
         lists = (parameters_updates, control_variate_updates, server_control_variates)
         dts = {a.dtype for lst in lists for client in lst for a in client}
         shapes = [[a.shape for a in lst[0]] for lst in lists]
-        if len(dts) != 1 or next(iter(dts)) not in (np.float32, np.float64) or not (shapes[0] == shapes[1] == shapes[2]):
+        uniform = len(dts) == 1 and next(iter(dts)) in (np.float32, np.float64)
+        if not uniform or not shapes[0] == shapes[1] == shapes[2]:
             return self._single().scaffold(*lists, n_samples, aggregation_lr, wire)
         sdt = next(iter(dts))
         kind = "f32" if sdt == np.float32 else "f64"
