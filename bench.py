@@ -153,6 +153,16 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = bytes_alg * world / (elapsed / args.steps) / 1e9
 
+    # ---- per-launch distribution (after the timed region): one event pair per launch ----
+    n_each = max(5, min(args.steps, 20))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_each)]
+    for a, b in evs:
+        a.record(stream)
+        plan.launch(stream)
+        b.record(stream)
+    torch.cuda.synchronize(device)
+    each_ms = np.array([a.elapsed_time(b) for a, b in evs])
+
     # ---- parity spot check (outside the timed region): sampled elements vs the sequential order ----
     parity = None
     if wl["strategy"] == "fedavg":
@@ -258,6 +268,8 @@ def main():
                 "kernel": (f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>" if wl["strategy"] == "fedavg"
                            else "scaffold_kernel<float>"),
                 "kernel_ms": round(kern_ms, 5),
+                "kernel_ms_median": round(float(np.median(each_ms)), 5),
+                "kernel_ms_min": round(float(each_ms.min()), 5),
                 "read_stream_ceiling_GBps": round(read_ceiling, 1),
                 "frac_of_read_ceiling": round(achieved / read_ceiling, 4),
             },
