@@ -846,3 +846,29 @@ def test_scaffold_nonfinite_bit_exact(torch_gpu, dummy_algo_class, dtype):
     got = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.5).avg_shared_states(shared_states=states, _skip=True)
     _assert_same_nan_aware(got.avg_parameters_update, ref_avg)
     _assert_same_nan_aware(got.server_control_variate, ref_c)
+
+
+@pytest.mark.parametrize("ns", [[5, -3, 7], [0, 0, 9, 0], [-1, -2, -4], [2**62, 3, 2**61 + 1], [1, 10**18, 7, 10**18 - 5],
+                                [True, 3, 4]])
+def test_n_samples_edge_values(torch_gpu, dummy_algo_class, ns):
+    """negative and zero n_k are accepted, totals are exact Python ints (so huge
+    counts keep their exact double ratio), True counts as 1 -- weights computed as the reference."""
+    from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState
+    from substrafl_amd.strategies import FedAvg, Scaffold
+
+    rng = np.random.default_rng(len(ns))
+    K = len(ns)
+    shapes = [(33, 5), (1,), (1000,)]
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    nsi = [s.n_samples for s in states]  # after the schema's coercion
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(shared_states=states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, nsi))
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    sst = [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                               server_control_variate=c) for k in range(K)]
+    sg = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.3).avg_shared_states(shared_states=sst, _skip=True)
+    ref_c, ref_avg = scaffold_reference_structure(pus, cvs, c, nsi, 0.3)
+    _assert_same(sg.avg_parameters_update, ref_avg)
+    _assert_same(sg.server_control_variate, ref_c)
