@@ -872,3 +872,82 @@ def test_n_samples_edge_values(torch_gpu, dummy_algo_class, ns):
     ref_c, ref_avg = scaffold_reference_structure(pus, cvs, c, nsi, 0.3)
     _assert_same(sg.avg_parameters_update, ref_avg)
     _assert_same(sg.server_control_variate, ref_c)
+
+
+# ------------------------------------------------------------------------------------------
+# seeded random sweep: client counts, layer lists, dtypes and counts drawn together
+# ------------------------------------------------------------------------------------------
+def _random_case(seed):
+    rng = np.random.default_rng(9000 + seed)
+    K = int(rng.choice([1, 2, 3, 5, 8, 9, 16, 17, 31, 64, 127, 128, 129, 200, 257]))
+    L = int(rng.integers(1, 10))
+    shapes = []
+    for _ in range(L):
+        kind = rng.integers(0, 6)
+        if kind == 0:
+            shapes.append((1,))
+        elif kind == 1:
+            shapes.append((int(rng.integers(0, 3)), int(rng.integers(1, 40))))  # may be empty
+        elif kind == 2:
+            shapes.append((int(rng.integers(1, 9000)),))
+        elif kind == 3:
+            shapes.append(tuple(int(v) for v in rng.integers(1, 12, 3)))
+        else:
+            shapes.append((int(rng.integers(1, 300)), int(rng.integers(1, 300))))
+    base = rng.choice([np.float32, np.float32, np.float64, np.float16])
+    mixed = rng.random() < 0.2
+    pus = []
+    for _ in range(K):
+        row = []
+        for li, s in enumerate(shapes):
+            dt = np.float64 if (mixed and li == 0) else base
+            if mixed and li == 1 and len(shapes) > 1:
+                row.append(rng.integers(-50, 50, s).astype(np.int64))
+            else:
+                row.append((rng.standard_normal(s) * 10.0 ** rng.integers(-3, 3)).astype(dt))
+        pus.append(row)
+    ns = [int(v) for v in rng.integers(0, 3000, K)]
+    if sum(ns) == 0:
+        ns[0] = 1
+    return pus, ns
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_sweep_fedavg(torch_gpu, dummy_algo_class, seed):
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    pus, ns = _random_case(seed)
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    got = FedAvg(algo=dummy_algo_class()).avg_shared_states(shared_states=states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_sweep_scaffold(torch_gpu, dummy_algo_class, seed):
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    pus, ns = _random_case(100 + seed)
+    rng = np.random.default_rng(seed)
+    pus = [[np.asarray(a, dtype=np.float64 if seed % 3 == 0 else np.float32) for a in row] for row in pus]
+    cvs = [[(rng.standard_normal(a.shape)).astype(a.dtype) for a in row] for row in pus]
+    c = [rng.standard_normal(a.shape).astype(a.dtype) for a in pus[0]]
+    lr = float(rng.choice([0.0, 0.5, 1.0, 2.5]))
+    states = [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                  server_control_variate=c) for k in range(len(ns))]
+    got = Scaffold(algo=dummy_algo_class(), aggregation_lr=lr).avg_shared_states(shared_states=states, _skip=True)
+    ref_c, ref_avg = scaffold_reference_structure(pus, cvs, c, ns, lr)
+    _assert_same(got.avg_parameters_update, ref_avg)
+    _assert_same(got.server_control_variate, ref_c)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_sweep_multi_device(torch_gpu, seed):
+    from substrafl_amd.multi_device import MultiDeviceEngine
+
+    pus, ns = _random_case(300 + seed)
+    devices = (0,) * (1 + seed % 4)
+    cap = [None, 20_000, 150_000, 1_000_000][seed % 4]
+    got = MultiDeviceEngine(devices, max_shard_bytes=cap).fedavg(pus, ns)
+    _assert_same(got, fedavg_reference_structure(pus, ns))
