@@ -24,6 +24,7 @@ cloudpickle-able for RemoteStruct (remote_struct.py:84-114); the engine itself i
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple, Union
@@ -241,6 +242,24 @@ def _row_pointers(clients) -> List[int]:
 # ======================================================================================
 # host entry (drop-in path)
 # ======================================================================================
+def serialized(method):
+    """Run an engine call under the locks of the engine's devices (``runtime.device_lock``), taken
+    in device order, so concurrent callers never share a session's buffers mid-call."""
+
+    @functools.wraps(method)
+    def wrapper(self, *args, **kwargs):
+        locks = [runtime.device_lock(d) for d in sorted(set(self.lock_devices()))]
+        for lk in locks:
+            lk.acquire()
+        try:
+            return method(self, *args, **kwargs)
+        finally:
+            for lk in reversed(locks):
+                lk.release()
+
+    return wrapper
+
+
 class AggregationEngine:
     """Drop-in host path bound to one GPU (``device``, else ``LOCAL_RANK``, else 0).
 
@@ -283,6 +302,9 @@ class AggregationEngine:
         self._prestaged = {}
         return self._ooc
 
+    def lock_devices(self) -> List[int]:
+        return [self._index()]
+
     def _index(self) -> int:
         idx = self._device_index
         return int(os.environ.get("LOCAL_RANK", "0")) if idx is None else idx
@@ -295,6 +317,7 @@ class AggregationEngine:
 
         runtime.prewarm(self._index())
 
+    @serialized
     def ingest(self, paths: Sequence, strategy: str, load, max_workers: int = 0) -> List:
         """Load K shared-state files (``load(path)``, e.g. ``PickleSerializer.load``) on a thread
         pool and stage each client's bucket rows to HBM as soon as that client is loaded, so the
@@ -441,6 +464,7 @@ class AggregationEngine:
                 s.sync()  # tmp is reused by the next segment's stage
 
     # ----------------------------------------------------------------------------------
+    @serialized
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
                wire: bool = False) -> List[np.ndarray]:
         """GPU equivalent of fed_avg.py:217-222 for validated inputs (same layer count and shapes
@@ -513,6 +537,7 @@ class AggregationEngine:
         return results  # type: ignore[return-value]
 
     # ----------------------------------------------------------------------------------
+    @serialized
     def scaffold(
         self,
         parameters_updates: List[List[np.ndarray]],

@@ -34,7 +34,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native, runtime
-from .engine import AggregationEngine, FedAvgPlan, ScaffoldPlan, equal_count, fedavg_weights, kind_of, scaffold_weights
+from .engine import (AggregationEngine, FedAvgPlan, ScaffoldPlan, equal_count, fedavg_weights, kind_of,
+                     scaffold_weights, serialized)
 from .layout import ROW_ALIGN_BYTES, BucketLayout
 from .sharding import SHARD_ALIGN, shard_bounds
 from .wire import flat_of
@@ -73,6 +74,9 @@ class MultiDeviceEngine:
         self._sessions = None
         self._fallback: Optional[AggregationEngine] = None
         self.last_timing: Dict[str, object] = {}
+
+    def lock_devices(self) -> List[int]:
+        return list(self.devices)
 
     # ----------------------------------------------------------------------------------
     def sessions(self):
@@ -173,6 +177,7 @@ class MultiDeviceEngine:
         return [[np.ascontiguousarray(a) for a in row] for row in rows]
 
     # ----------------------------------------------------------------------------------
+    @serialized
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
                wire: bool = False) -> List[np.ndarray]:
         """fed_avg.py:217-222 for validated inputs, sharded by parameter range over the devices."""
@@ -224,6 +229,7 @@ class MultiDeviceEngine:
         return results  # type: ignore[return-value]
 
     # ----------------------------------------------------------------------------------
+    @serialized
     def scaffold(self, parameters_updates, control_variate_updates, server_control_variates, n_samples,
                  aggregation_lr, wire: bool = False):
         """scaffold.py:193-196 (c equality, as a mismatch count) and :297-337 (fp64 sums), sharded by

@@ -158,6 +158,20 @@ class Session:
                                                  ctypes.c_void_p(self.stream)), "scale_cast")
 
 
+_device_locks: Dict[int, threading.RLock] = {}
+
+
+def device_lock(device: int) -> threading.RLock:
+    """The lock that serialises aggregation calls on ``device``: its session's buffers and stream
+    are shared by every engine of the process (the reference runs one aggregation at a time;
+    this keeps concurrent callers correct rather than racing on the HBM buffers)."""
+    with _lock:
+        lk = _device_locks.get(int(device))
+        if lk is None:
+            lk = _device_locks[int(device)] = threading.RLock()
+        return lk
+
+
 _host_cache: Dict[tuple, np.ndarray] = {}
 
 

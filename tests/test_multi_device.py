@@ -216,3 +216,35 @@ def test_single_gpu_engine_streams_oversized_calls(gpu):
     big = AggregationEngine(0)
     _assert_same(big.fedavg(pus, ns), fedavg_reference_structure(pus, ns))
     assert "out_of_core" not in big.last_timing
+
+
+@pytest.mark.gpu
+def test_concurrent_calls_are_serialized(gpu):
+    """Several threads aggregating at once on one GPU (shared session buffers) all get their own
+    exact result: engine calls are serialised per device."""
+    import threading
+
+    from substrafl_amd.engine import engine_for
+    from substrafl_amd.multi_device import MultiDeviceEngine
+
+    cases = []
+    for t in range(6):
+        rng = np.random.default_rng(500 + t)
+        K = int(rng.integers(2, 20))
+        pus = _updates(rng, K, SHAPES)
+        cases.append((pus, [int(v) for v in rng.integers(1, 5000, K)]))
+    results = [None] * len(cases)
+
+    def run(i):
+        pus, ns = cases[i]
+        eng = engine_for(0) if i % 2 == 0 else MultiDeviceEngine((0, 0))
+        for _ in range(3):
+            results[i] = [np.array(a, copy=True) for a in eng.fedavg(pus, ns)]
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(len(cases))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for (pus, ns), got in zip(cases, results):
+        _assert_same(got, fedavg_reference_structure(pus, ns))
