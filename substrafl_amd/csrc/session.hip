@@ -29,12 +29,17 @@
 #include <vector>
 
 #include "fedagg.h"
+#include "host_pool.h"
 
 // defined in fedagg.hip
 extern "C" const char* fedagg_last_error(void);
 namespace fedagg_internal {
 void set_error(const char* msg);
 }
+
+using fedagg_host::Done;
+using fedagg_host::gather_range;
+using fedagg_host::Pool;
 
 namespace {
 
@@ -50,67 +55,6 @@ int hip_fail(const char* what, hipError_t e) {
     hipError_t e_ = (call);                               \
     if (e_ != hipSuccess) return hip_fail(#call, e_);     \
   } while (0)
-
-class Pool {
- public:
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  void submit(std::function<void()> f) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      q_.push_back(std::move(f));
-    }
-    cv_.notify_one();
-  }
-  int size() const { return (int)th_.size(); }
-
- private:
-  void run() {
-    for (;;) {
-      std::function<void()> f;
-      {
-        std::unique_lock<std::mutex> l(m_);
-        cv_.wait(l, [this] { return stop_ || !q_.empty(); });
-        if (stop_ && q_.empty()) return;
-        f = std::move(q_.front());
-        q_.pop_front();
-      }
-      f();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::deque<std::function<void()>> q_;
-  std::mutex m_;
-  std::condition_variable cv_;
-  bool stop_ = false;
-};
-
-// completion flag for one packed chunk
-struct Done {
-  std::mutex m;
-  std::condition_variable cv;
-  bool done = false;
-  void set() {
-    {
-      std::lock_guard<std::mutex> g(m);
-      done = true;
-    }
-    cv.notify_all();
-  }
-  void wait() {
-    std::unique_lock<std::mutex> l(m);
-    cv.wait(l, [this] { return done; });
-  }
-};
 
 }  // namespace
 
@@ -163,17 +107,6 @@ struct fedagg_session {
 
 namespace {
 
-// Copy bytes [a, b) of the concatenation of segments (ptr[i], len[i]) into dst.
-void gather_range(const void* const* ptr, const uint64_t* len, int nseg, uint64_t a, uint64_t b, char* dst) {
-  uint64_t off = 0;
-  for (int i = 0; i < nseg && off < b; ++i) {
-    const uint64_t s0 = off, s1 = off + len[i];
-    off = s1;
-    const uint64_t lo = std::max(a, s0), hi = std::min(b, s1);
-    if (lo >= hi) continue;
-    memcpy(dst + (lo - a), static_cast<const char*>(ptr[i]) + (lo - s0), hi - lo);
-  }
-}
 
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
