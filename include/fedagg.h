@@ -48,12 +48,14 @@ const char* fedagg_last_error(void);
 /* Process-wide launch knobs (defaults are the values measured best on MI355X):
  *   "grid_cap"      workgroups per launch before the kernels grid-stride (<= 0: no cap)
  *   "nt_load"       non-temporal client loads (0/1)      "nt_store"  non-temporal output stores
- *   "vpt"           16-B vectors per thread per step (0 = auto by K, 1/2/4/8)
- *   "unroll"        clients per load group (2/4/8/16, with an explicit vpt)
+ *   "vpt"           16-B vectors per thread per step (0 = auto by K, size and type; 1/2/4/8/16)
+ *   "unroll"        clients per load group (1/2/4/8/16, with an explicit vpt)
+ *   "xcd"           1 = blocks sharing an XCD take adjacent tiles (measured slower; default 0)
  *   "tile"          a workgroup step covers vpt*256 contiguous vectors (0/1)
  *   "pipe"          software-pipelined client groups (0/1, vpt 1 only)
  *   "fuse_pairwise" patch numel==1 tensors inside the bucket launch (0/1)
- *   "sc_vpt"        Scaffold: 16-B vectors per thread per step (1/2/4/8)
+ *   "sc_vpt"        Scaffold: 16-B vectors per thread per step (0 = auto by K; 1/2/4/8)
+ *   "sc_pipe"       Scaffold: software-pipelined client groups (0/1)
  *   "sc_unroll"     Scaffold: clients per load group (2/4/8)
  *   "sc_split"      Scaffold: 1 = stream all delta vectors, then all control-variate vectors
  * Returns FEDAGG_EINVAL for an unknown key. */

@@ -25,6 +25,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -62,9 +64,10 @@ int g_unroll = 8;       // clients per load group (ignored when vpt is auto)
 int g_pipe = 0;         // software-pipelined client groups
 int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
-int g_sc_vpt = 4;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8); 4 measured best
-int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8)
+int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
+int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -556,9 +559,50 @@ __device__ __forceinline__ void scaffold_pairwise_elem(const ScArgs<TIn, KC>& a,
   *cval = 0.0 + pw_leaf<double>(gc, 0, K + 1);
 }
 
+// Loads of one group of SU clients, both buckets, for the N vectors v[].
+template <typename TIn, int KC, bool NT, int N, int SU>
+__device__ __forceinline__ void scaffold_load_group(const ScArgs<TIn, KC>& a, const int k, const uint64_t* v,
+                                                    u32x4 (&rd)[N][SU], u32x4 (&rc)[N][SU]) {
+  constexpr int L = 16 / sizeof(TIn);
+#pragma unroll
+  for (int u = 0; u < SU; ++u)
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      rd[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
+      rc[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+    }
+}
+
+// fp64 products and in-order adds of one loaded group (scaffold.py:262,293: w_k * x_k summed in
+// list order).
+template <typename TIn, int N, int SU>
+__device__ __forceinline__ void scaffold_accumulate(const u32x4 (&rd)[N][SU], const u32x4 (&rc)[N][SU],
+                                                    const double* w, double (*ad)[16 / sizeof(TIn)],
+                                                    double (*ac)[16 / sizeof(TIn)]) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const double wu = w[u];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      double xd[L], xc[L];
+      unpack_d<TIn>(rd[n][u], xd);
+      unpack_d<TIn>(rc[n][u], xc);
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const double pd = wu * xd[j];
+        const double pc = wu * xc[j];
+        ad[n][j] = ad[n][j] + pd;
+        ac[n][j] = ac[n][j] + pc;
+      }
+    }
+  }
+}
+
 // N 16-byte vectors of both buckets: in-order fp64 sums over the K clients, then (last chunk)
-// + c and * lr, the fused numel==1 patch, and the fp64 stores.
-template <typename TIn, int KC, bool NT, bool NTS, int N, int SU>
+// + c and * lr, the fused numel==1 patch, and the fp64 stores.  PIPE: software-pipelined groups.
+template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, bool PIPE = false>
 __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                  const int first, const int last, const TIn* __restrict__ c,
                                                  const double lr, const uint64_t* v, double* __restrict__ dout,
@@ -575,31 +619,29 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
     }
   }
   int k = 0;
-  for (; k + SU <= K; k += SU) {
-    u32x4 rd[N][SU], rc[N][SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u)
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        rd[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
-        rc[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+  if constexpr (PIPE) {
+    // the next group's loads are issued before this group's fp64 products and adds
+    if (K >= SU) {
+      u32x4 da[N][SU], ca[N][SU], db[N][SU], cb[N][SU];
+      scaffold_load_group<TIn, KC, NT, N, SU>(a, 0, v, da, ca);
+      for (;;) {
+        const bool mb = k + 2 * SU <= K;
+        if (mb) scaffold_load_group<TIn, KC, NT, N, SU>(a, k + SU, v, db, cb);
+        scaffold_accumulate<TIn, N, SU>(da, ca, a.w + k, ad, ac);
+        k += SU;
+        if (!mb) break;
+        const bool ma = k + 2 * SU <= K;
+        if (ma) scaffold_load_group<TIn, KC, NT, N, SU>(a, k + SU, v, da, ca);
+        scaffold_accumulate<TIn, N, SU>(db, cb, a.w + k, ad, ac);
+        k += SU;
+        if (!ma) break;
       }
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const double w = a.w[k + u];
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        double xd[L], xc[L];
-        unpack_d<TIn>(rd[n][u], xd);
-        unpack_d<TIn>(rc[n][u], xc);
-#pragma unroll
-        for (int j = 0; j < L; ++j) {
-          const double pd = w * xd[j];
-          const double pc = w * xc[j];
-          ad[n][j] = ad[n][j] + pd;
-          ac[n][j] = ac[n][j] + pc;
-        }
-      }
+    }
+  } else {
+    for (; k + SU <= K; k += SU) {
+      u32x4 rd[N][SU], rc[N][SU];
+      scaffold_load_group<TIn, KC, NT, N, SU>(a, k, v, rd, rc);
+      scaffold_accumulate<TIn, N, SU>(rd, rc, a.w + k, ad, ac);
     }
   }
   for (; k < K; ++k) {
@@ -786,7 +828,7 @@ __device__ __forceinline__ void scaffold_vectors_split(const ScArgs<TIn, KC>& a,
 }
 
 // Same tiling as fedavg_kernel: a workgroup step covers VPT*256 contiguous vectors.
-template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT>
+template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, bool PIPE = false>
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
@@ -808,8 +850,8 @@ __global__ void __launch_bounds__(FA_BLOCK)
         scaffold_vectors_split<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
                                                            lds_wave);
       else
-        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
-                                                     lds_wave);
+        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU, PIPE>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
+                                                           lds_wave);
     } else {
       for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
         scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout, false, lds_wave);
@@ -1182,13 +1224,21 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
 // 16 clients tie.  Box-to-box spread is ~3 %.
 struct Shape {
   int vpt, unroll;
+  bool pipe;
 };
+template <typename E>
 inline Shape shape_for(int K, uint64_t nvec) {
-  if (g_vpt > 0) return {g_vpt, g_unroll};
+  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0};
+  // fp64: the adds of a client group take long enough that the HBM idles unless the next
+  // group's loads are already in flight (software-pipelined tiles: 8 x 25M fp64 6.0 vs 5.1 TB/s,
+  // 64 x 62.5M 6.1 vs 4.9; profiles/r01_tune2_f64_*.log)
+  if constexpr (std::is_same<E, F64>::value) return Shape{4, 4, true};
   // many client streams over a large bucket: 16 KiB per wave per stream (fewer DRAM row
-  // switches; 64 x 125M fp32 +2 %, 128 x 350M bf16 +1 %), as long as the grid stays >> 256 CUs
-  if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) return Shape{16, 2};
-  return Shape{8, 4};
+  // switches; 64 x 125M fp32 +2 %, 128 x 350M bf16 +1 %, 64 x 125M fp16 +1 %), as long as the
+  // grid stays >> 256 CUs
+  if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) return Shape{16, 2, false};
+  if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false};  // 8 x 25M fp16: +5 % over 8 KiB
+  return Shape{8, 4, false};
 }
 
 template <typename E, bool NTS>
@@ -1197,7 +1247,11 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
 #define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
   if (!g_nt_load) return launch_fedavg_variant<E, false, NTS, 1, 8, false, false>(FA_ARGS);
   if (g_tile) {
-    if (sh.vpt >= 16) {  // 16 KiB per wave per client stream (tuning only)
+    if (sh.pipe) {  // contiguous tiles with the next client group's loads issued before this group's adds
+      if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
+      return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
+    }
+    if (sh.vpt >= 16) {  // 16 KiB per wave per client stream
       if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 16, 2, false, true>(FA_ARGS);
     }
@@ -1279,7 +1333,7 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
   const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK;
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg: workspace needed for %lld pairwise segments", P);
   const uint64_t nvec = vec ? M / E::L : 0;
-  const Shape sh = shape_for(K, nvec);
+  const Shape sh = shape_for<E>(K, nvec);
   const uint64_t per_thread = (g_tile && g_nt_load) ? (uint64_t)sh.vpt : 1;
   const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
@@ -1342,11 +1396,11 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
   return FEDAGG_OK;
 }
 
-template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false>
+template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false>
 void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
                              uint64_t M, double* dout, double* cout) {
-  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT>), dim3(grid),
+  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT, PIPE>), dim3(grid),
                      dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd);
 }
 
@@ -1355,33 +1409,37 @@ void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FED
 template <typename TIn>
 void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
                      int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
-                     double* cout) {
+                     double* cout, const int sv, const int su) {
 #define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
   const bool nts = g_nt_store != 0;
   if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
+  if (g_sc_pipe && nts && !g_sc_split) {  // software-pipelined client groups
+    if (sv >= 4) return launch_scaffold_variant<TIn, true, true, 4, 2, false, true>(SC_ARGS);
+    return launch_scaffold_variant<TIn, true, true, 2, 4, false, true>(SC_ARGS);
+  }
   if (g_sc_split && nts) {  // phase-split walk (nt stores)
-    if (g_sc_vpt >= 8) {
-      if (g_sc_unroll <= 2) return launch_scaffold_variant<TIn, true, true, 8, 2, true>(SC_ARGS);
+    if (sv >= 8) {
+      if (su <= 2) return launch_scaffold_variant<TIn, true, true, 8, 2, true>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, true, 8, 4, true>(SC_ARGS);
     }
-    if (g_sc_unroll >= 8) return launch_scaffold_variant<TIn, true, true, 4, 8, true>(SC_ARGS);
+    if (su >= 8) return launch_scaffold_variant<TIn, true, true, 4, 8, true>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, true, 4, 4, true>(SC_ARGS);
   }
-  if (g_sc_vpt >= 8) {
-    if (g_sc_unroll >= 2 && nts) return launch_scaffold_variant<TIn, true, true, 8, 2>(SC_ARGS);
+  if (sv >= 8) {
+    if (su >= 2 && nts) return launch_scaffold_variant<TIn, true, true, 8, 2>(SC_ARGS);
     if (nts) return launch_scaffold_variant<TIn, true, true, 8, 1>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 8, 1>(SC_ARGS);
   }
-  if (g_sc_vpt >= 4) {
-    if (g_sc_unroll <= 2) {
+  if (sv >= 4) {
+    if (su <= 2) {
       if (nts) return launch_scaffold_variant<TIn, true, true, 4, 2>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, false, 4, 2>(SC_ARGS);
     }
     if (nts) return launch_scaffold_variant<TIn, true, true, 4, 4>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 4, 4>(SC_ARGS);
   }
-  if (g_sc_vpt >= 2) {
-    if (g_sc_unroll <= 2) {
+  if (sv >= 2) {
+    if (su <= 2) {
       if (nts) return launch_scaffold_variant<TIn, true, true, 2, 2>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, false, 2, 2>(SC_ARGS);
     }
@@ -1411,7 +1469,11 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "scaffold: workspace needed for %lld pairwise segments", P);
   constexpr int L = 16 / sizeof(TIn);
   const uint64_t nvec = vec ? M / L : 0;
-  const uint64_t per_thread = g_nt_load ? (uint64_t)g_sc_vpt : 1;
+  // launch shape: 8 vectors x 2-client groups from 32 clients on (64 x 25M: 6.69 vs 6.28 TB/s),
+  // 4 x 4 below (16 x 25M: 6.23 vs 6.16); profiles/r01_tune3_*.log
+  const int sv = g_sc_vpt > 0 ? g_sc_vpt : (K >= 32 ? 8 : 4);
+  const int su = g_sc_vpt > 0 ? g_sc_unroll : (K >= 32 ? 2 : 4);
+  const uint64_t per_thread = g_nt_load ? (uint64_t)sv : 1;
   const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
     const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
@@ -1429,7 +1491,7 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0, last = (k0 + kc) == K;
-    launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+    launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     int rc = check_launch("scaffold_kernel");
     if (rc) return rc;
   }
@@ -1486,10 +1548,11 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
   else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
-  else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
+  else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value <= 0 ? 0 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
+  else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

@@ -464,7 +464,8 @@ def test_many_numel1_layers_fused_and_separate(torch_gpu, dummy_algo_class, fuse
                                    dict(vpt=4, tile=1, grid_cap=5), dict(vpt=8, unroll=2, tile=1),
                                    dict(vpt=8, unroll=4, tile=1, grid_cap=3), dict(vpt=1, tile=0),
                                    dict(vpt=16, unroll=2, tile=1), dict(vpt=16, unroll=1, tile=1, grid_cap=3),
-                                   dict(xcd=1), dict(vpt=16, unroll=2, tile=1, xcd=1)])
+                                   dict(xcd=1), dict(vpt=16, unroll=2, tile=1, xcd=1),
+                                   dict(vpt=4, unroll=4, tile=1, pipe=1), dict(vpt=8, tile=1, pipe=1, grid_cap=3)])
 def test_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -517,9 +518,10 @@ def test_auto_shape_many_clients_bit_identical(torch_gpu):
 @pytest.mark.parametrize("knobs", [dict(sc_vpt=1), dict(sc_vpt=2, sc_unroll=2), dict(nt_store=0), dict(nt_load=0),
                                    dict(grid_cap=3), dict(sc_vpt=4, sc_unroll=2), dict(sc_vpt=2, sc_unroll=4),
                                    dict(sc_vpt=8), dict(sc_vpt=8, grid_cap=2), dict(sc_split=1),
-                                   dict(sc_split=1, sc_unroll=8), dict(sc_split=1, sc_vpt=8, sc_unroll=2),
+                                   dict(sc_split=1, sc_vpt=4, sc_unroll=8), dict(sc_split=1, sc_vpt=8, sc_unroll=2),
                                    dict(sc_split=1, sc_vpt=8, grid_cap=2), dict(sc_vpt=8, sc_unroll=2),
-                                   dict(xcd=1), dict(sc_vpt=8, sc_unroll=2, xcd=1, grid_cap=5)])
+                                   dict(xcd=1), dict(sc_vpt=8, sc_unroll=2, xcd=1, grid_cap=5),
+                                   dict(sc_pipe=1), dict(sc_pipe=1, sc_vpt=2, sc_unroll=4, grid_cap=3)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -530,7 +532,7 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     cv = torch.randn((K, M + 1), device="cuda")
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
-    default = dict(sc_vpt=4, sc_unroll=4, sc_split=0, nt_store=1, nt_load=1, grid_cap=0, xcd=0)
+    default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0, xcd=0)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)

@@ -32,11 +32,12 @@ def main():
 
     shapes = synthetic_state_dict_shapes(args.M)
     lay = BucketLayout(range(len(shapes)), shapes, np.float32)
-    dt = torch.bfloat16 if args.kind == "bf16" else torch.float32
+    dt = {"bf16": torch.bfloat16, "f32": torch.float32, "f64": torch.float64, "f16": torch.float16}[args.kind]
+    out_dt = {"bf16": torch.float32, "f32": torch.float32, "f64": torch.float64, "f16": torch.float16}[args.kind]
     x = torch.empty((args.K, lay.ld), device="cuda", dtype=dt)
     for k in range(args.K):  # row by row: a full fp32 temporary of C5 would not fit
         x[k].copy_(torch.randn(lay.ld, device="cuda"))
-    out = torch.empty(lay.ld, device="cuda")
+    out = torch.empty(lay.ld, device="cuda", dtype=out_dt)
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
     plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
@@ -48,9 +49,11 @@ def main():
                   dict(vpt=4, tile=1, grid_cap=2048)]
         variants = [dict(base, **sh, nt_store=nts) for sh in shapes for nts in (0, 1)]
     else:  # contiguous-tile shapes with nt stores (--xcd: also the XCD-contiguous tile order)
-        shapes = [dict(vpt=8, unroll=4), dict(vpt=8, unroll=2), dict(vpt=16, unroll=2), dict(vpt=16, unroll=1),
-                  dict(vpt=4, unroll=4), dict(vpt=4, unroll=8)]
-        variants = [dict(base, **sh, tile=1, nt_store=1, xcd=x) for sh in shapes for x in ((0, 1) if args.xcd else (0,))]
+        shapes = [dict(vpt=0), dict(vpt=8, unroll=4), dict(vpt=8, unroll=2), dict(vpt=16, unroll=2), dict(vpt=16, unroll=1),
+                  dict(vpt=4, unroll=4), dict(vpt=4, unroll=8), dict(vpt=2, unroll=8),
+                  dict(vpt=4, unroll=4, pipe=1), dict(vpt=8, unroll=2, pipe=1), dict(vpt=1, unroll=8, tile=0, pipe=1)]
+        variants = [dict(base, **dict(dict(tile=1), **sh), nt_store=1, xcd=x) for sh in shapes
+                    for x in ((0, 1) if args.xcd else (0,))]
     times = {i: [] for i in range(len(variants))}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for r in range(args.rounds):

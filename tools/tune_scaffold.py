@@ -34,10 +34,12 @@ def main():
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
     plan = ScaffoldPlan("f32", d, cv, c, scaffold_weights(ns), args.M, 1.0, dout, cout, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
-    variants = [dict(sc_split=0, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=x)
-                for v, u in ((2, 4), (4, 2), (4, 4), (8, 1), (8, 2)) for x in (0,)]
-    variants += [dict(sc_split=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=x)
-                 for v, u in ((4, 4), (8, 2)) for x in (0,)]
+    variants = [dict(sc_split=0, sc_pipe=0, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
+                for v, u in ((0, 4), (2, 4), (4, 2), (4, 4), (8, 1), (8, 2))]  # sc_vpt 0: the auto shape
+    variants += [dict(sc_split=0, sc_pipe=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
+                 for v, u in ((4, 2), (2, 4))]
+    variants += [dict(sc_split=1, sc_pipe=0, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
+                 for v, u in ((4, 4), (8, 2))]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {i: [] for i in range(len(variants))}
     for _ in range(args.rounds):
