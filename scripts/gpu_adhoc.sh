@@ -1,7 +1,7 @@
 set -u
 mkdir -p gpurun_out
-FILES=tests SMOKE=1 bash scripts/gpu_check.sh || exit $?
-timeout -k 10 300 python tools/tune_fedavg.py --K 8 --M 25000000 --kind f64 > gpurun_out/tune4_f64_k8.log 2>&1 || exit $?
-timeout -k 10 300 python tools/tune_scaffold.py --K 64 --M 25000000 --rounds 3 > gpurun_out/tune4_sc_k64.log 2>&1 || exit $?
-for f in tune4_f64_k8 tune4_sc_k64; do grep -h '"median_us"' gpurun_out/$f.log | grep -v probe | head -3; done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider -k "equal_count or scaffold" --timeout 120 --timeout-method thread > gpurun_out/eq.log 2>&1 || { tail -30 gpurun_out/eq.log; exit 1; }
+tail -2 gpurun_out/eq.log
+timeout -k 10 300 python tools/tune_scaffold.py --K 16 --M 25000000 > gpurun_out/tune6_c4.log 2>&1 || exit $?
+grep -h equal_count gpurun_out/tune6_c4.log
 echo done

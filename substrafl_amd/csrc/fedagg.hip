@@ -67,6 +67,7 @@ int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
 int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
@@ -967,6 +968,67 @@ __global__ void __launch_bounds__(FA_BLOCK)
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(cnt, bad);
 }
 
+// Vectorised form (16-B loads, contiguous tiles of VPT*256 vectors per workgroup step, client
+// copies in groups of 4), used when every pointer is 16-B aligned.  Same per-element test.
+template <typename T>
+__device__ __forceinline__ unsigned eq_mismatches(u32x4 x, u32x4 r) {
+  constexpr int L = 16 / sizeof(T);
+  T xv[L], rv[L];
+  __builtin_memcpy(xv, &x, 16);
+  __builtin_memcpy(rv, &r, 16);
+  unsigned bad = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) bad += !((xv[j] == rv[j]) || (xv[j] != xv[j] && rv[j] != rv[j]));
+  return bad;
+}
+
+template <typename T, int KC, int VPT>
+__global__ void __launch_bounds__(FA_BLOCK)
+    equal_count_vec_kernel(const EqArgs<T, KC> a, const int K, const T* __restrict__ ref, const uint64_t nvec,
+                           const uint64_t M, unsigned long long* __restrict__ cnt) {
+  constexpr int L = 16 / sizeof(T);
+  constexpr int U = 4;
+  unsigned long long bad = 0;
+  const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+  for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+    u32x4 r[VPT];
+    bool in[VPT];
+#pragma unroll
+    for (int n = 0; n < VPT; ++n) {
+      in[n] = base + (uint64_t)n * FA_BLOCK < nvec;
+      if (in[n]) r[n] = ld16<true>(ref + (base + (uint64_t)n * FA_BLOCK) * L);
+    }
+    int k = 0;
+    for (; k + U <= K; k += U) {
+      u32x4 x[VPT][U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int n = 0; n < VPT; ++n)
+          if (in[n]) x[n][u] = ld16<true>(a.x[k + u] + (base + (uint64_t)n * FA_BLOCK) * L);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int n = 0; n < VPT; ++n)
+          if (in[n]) bad += eq_mismatches<T>(x[n][u], r[n]);
+    }
+    for (; k < K; ++k)
+#pragma unroll
+      for (int n = 0; n < VPT; ++n)
+        if (in[n]) bad += eq_mismatches<T>(ld16<true>(a.x[k] + (base + (uint64_t)n * FA_BLOCK) * L), r[n]);
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
+  for (uint64_t i = nvec * L + (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x; i < M; i += stride) {
+    const T rr = ref[i];
+    for (int k = 0; k < K; ++k) {
+      const T v = a.x[k][i];
+      bad += !((v == rr) || (v != v && rr != rr));
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(cnt, bad);
+}
+
 // ------------------------------------------------------------------------------------
 // dtype plumbing on the device (exact widening casts; per-client pre-scaling for layers whose
 // clients do not share one dtype) -- NumPy semantics: int/bool -> float64 is the C cast
@@ -1503,14 +1565,25 @@ template <typename T>
 int equal_launch(const T* const* x, int K, uint64_t M, unsigned long long* cnt, hipStream_t s) {
   if (K <= 0 || !x || !cnt) return fail(FEDAGG_EINVAL, "equal_count: invalid argument (K=%lld)", K);
   if (M == 0 || K == 1) return FEDAGG_OK;
-  const unsigned grid = grid_for(M);
+  bool vec = g_eq_vec != 0;
+  for (int k = 0; k < K; ++k) {
+    if (!x[k]) return fail(FEDAGG_EINVAL, "equal_count: client pointer %lld is NULL", k);
+    vec = vec && aligned16(x[k]);
+  }
+  constexpr int EQ_VPT = 4;
+  const uint64_t nvec = vec ? M / (16 / sizeof(T)) : 0;
+  const unsigned grid = vec ? grid_for((nvec + EQ_VPT - 1) / EQ_VPT) : grid_for(M);
   for (int k0 = 1; k0 < K; k0 += FEDAGG_KCHUNK) {
     const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
     EqArgs<T, FEDAGG_KCHUNK> a;
     memset(&a, 0, sizeof(a));
     for (int k = 0; k < kc; ++k) a.x[k] = x[k0 + k];
-    hipLaunchKernelGGL((equal_count_kernel<T, FEDAGG_KCHUNK>), dim3(grid), dim3(FA_BLOCK), 0, s, a, kc, x[0], M,
-                       cnt);
+    if (vec)
+      hipLaunchKernelGGL((equal_count_vec_kernel<T, FEDAGG_KCHUNK, EQ_VPT>), dim3(grid), dim3(FA_BLOCK), 0, s, a, kc,
+                         x[0], nvec, M, cnt);
+    else
+      hipLaunchKernelGGL((equal_count_kernel<T, FEDAGG_KCHUNK>), dim3(grid), dim3(FA_BLOCK), 0, s, a, kc, x[0], M,
+                         cnt);
     int rc = check_launch("equal_count_kernel");
     if (rc) return rc;
   }
@@ -1553,6 +1626,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
+  else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

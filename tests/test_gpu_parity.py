@@ -373,6 +373,39 @@ def test_scaffold_full_size_vs_torch_fp64(torch_gpu, K, M):
     assert torch.equal(co[:M].view(torch.int64), ac.view(torch.int64))
 
 
+@pytest.mark.parametrize("M", [100_000, 100_003, 4096 * 4 * 256 + 37])
+@pytest.mark.parametrize("kind", ["f32", "f64"])
+@pytest.mark.parametrize("vec", [1, 0])
+def test_equal_count_variants(torch_gpu, M, kind, vec):
+    """scaffold.py:193-196 assert_array_equal semantics (+0 == -0, NaN == NaN) on the vectorised
+    and the scalar check, aligned and unaligned rows, tails, and a differing reference copy."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import equal_count
+
+    dt = torch.float32 if kind == "f32" else torch.float64
+    K = 13
+    c = torch.randn(M, device="cuda", dtype=dt)
+    c[11] = 0.0
+    c[5] = float("nan")
+    copies = c.repeat(K, 1)
+    copies[4, 11] = -0.0  # equal
+    copies[3, 17] = 1e9  # 1
+    copies[12, M - 1] = float("nan")  # 1 (NaN vs number)
+    copies[9, M - 2] = -copies[9, M - 2]  # 1 (tail element)
+    copies[0, 100] = 7.0  # reference copy differs: every other copy mismatches there (K - 1)
+    copies[6, :5] = 1e30  # 5
+    expected = 1 + 1 + 1 + (K - 1) + 5
+    _native.tune(eq_vec=vec)
+    try:
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        equal_count(kind, copies, M, cnt)
+        torch.cuda.synchronize()
+    finally:
+        _native.tune(eq_vec=1)
+    assert int(cnt.item()) == expected
+
+
 def test_equal_count_kernel(torch_gpu):
     torch = torch_gpu
     from substrafl_amd.engine import equal_count

@@ -52,6 +52,26 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[i].append(ev[0].elapsed_time(ev[1]) / args.iters)
+    # the c-equality check of the same call (scaffold.py:193-196): K copies of c, scalar vs 16-B
+    from substrafl_amd.engine import equal_count
+
+    cc = c.repeat(args.K, 1)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for vec in (0, 1):
+        _native.tune(eq_vec=vec)
+        tt = []
+        for _ in range(args.rounds):
+            equal_count("f32", cc, lay.M, cnt)
+            ev[0].record()
+            for _ in range(args.iters):
+                equal_count("f32", cc, lay.M, cnt)
+            ev[1].record()
+            torch.cuda.synchronize()
+            tt.append(ev[0].elapsed_time(ev[1]) / args.iters)
+        nb = args.K * lay.M * 4
+        print(json.dumps(dict(equal_count=True, eq_vec=vec, K=args.K, M=args.M, median_us=round(float(np.median(tt)) * 1e3, 2),
+                              GBps=round(nb / (np.median(tt) / 1e3) / 1e9, 1))))
+    _native.tune(eq_vec=1)
     res = []
     for i, kn in enumerate(variants):
         t = np.array(times[i])
