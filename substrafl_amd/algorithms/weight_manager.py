@@ -23,6 +23,7 @@ from typing import Generator, List, Optional, Sequence
 
 import numpy as np
 import torch
+from torch._utils import _unflatten_dense_tensors
 
 from .. import _native
 from ..wire import bucket_views, flat_of
@@ -74,13 +75,20 @@ def _kind(tensors: Sequence[torch.Tensor], device=None) -> Optional[int]:
     if not tensors:
         return None
     t0 = tensors[0]
-    dev = t0.device if device is None else torch.device(device)
     if not (t0.is_cuda and t0.dtype in _KIND):
         return None
-    for t in tensors:
-        if not (t.is_cuda and t.dtype == t0.dtype and t.is_contiguous() and t.device == dev):
+    if device is None:
+        idx = t0.get_device()
+    else:
+        d = torch.device(device)
+        if d.type != "cuda":
             return None
-    return _KIND[t0.dtype]
+        idx = d.index if d.index is not None else torch.cuda.current_device()
+    dt = t0.dtype
+    for t in tensors:  # get_device() is -1 on the CPU: one int compare covers device and placement
+        if t.dtype != dt or t.get_device() != idx or not t.is_contiguous():
+            return None
+    return _KIND[dt]
 
 
 def _fast(tensors: Sequence[torch.Tensor]) -> bool:
@@ -92,12 +100,9 @@ def _numel_array(tensors):
 
 
 def _views(flat: torch.Tensor, like: Sequence[torch.Tensor]) -> List[torch.Tensor]:
-    out, off = [], 0
-    for t in like:
-        n = t.numel()
-        out.append(flat.narrow(0, off, n).view(t.shape))
-        off += n
-    return out
+    """Per-layer views of ``flat`` shaped like ``like`` (one C++ call: per-layer ``narrow().view()``
+    from Python cost ≈10 µs a layer, more than the flat kernels themselves on a 300-layer model)."""
+    return list(_unflatten_dense_tensors(flat, list(like)))
 
 
 def _stream(device) -> int:

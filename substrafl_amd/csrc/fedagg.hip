@@ -67,6 +67,7 @@ int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand is fp32
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
 int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
@@ -1187,6 +1188,67 @@ __global__ void __launch_bounds__(FA_BLOCK) flat_seg_kernel(const SegArgs a, voi
   }
 }
 
+// All-fp32 form of flat_seg_kernel: 16-B accesses (4 elements per lane).  Layer tensors are
+// 16-B aligned, but a layer's slice of the flat bucket starts wherever the previous layers end,
+// so the accesses are declared 4-B aligned: gfx950 serves unaligned dwordx4 loads and stores,
+// a wave still touches one contiguous KiB (plus at most one extra line).  Same per-element
+// arithmetic as the scalar kernel's fp32 branches.
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int OP>
+__global__ void __launch_bounds__(FA_BLOCK) flat_seg_vec_kernel(const SegArgs a, float* __restrict__ flat) {
+#pragma clang fp contract(off)
+  const int l = seg_of_block(a, blockIdx.x);
+  const uint64_t base = (uint64_t)(blockIdx.x - a.block_start[l]) * SEG_CHUNK;
+  const uint64_t n = a.n[l];
+  const uint64_t end = base + SEG_CHUNK < n ? base + SEG_CHUNK : n;
+  float* f = flat + a.flat_off[l];
+  float cf[FEDAGG_FLAT_MAX_LISTS];
+#pragma unroll
+  for (int j = 0; j < FEDAGG_FLAT_MAX_LISTS; ++j) cf[j] = (float)a.coeff[j];  // torch rounds the scalar
+  for (uint64_t i = base + 4 * (uint64_t)threadIdx.x; i < end; i += 4 * (uint64_t)FA_BLOCK) {
+    if (i + 4 <= end) {
+      if constexpr (OP == 0) {
+        *reinterpret_cast<f32x4u*>(f + i) = *reinterpret_cast<const f32x4u*>(static_cast<const float*>(a.p[0][l]) + i);
+      } else if constexpr (OP == 1) {
+        *reinterpret_cast<f32x4u*>(const_cast<float*>(static_cast<const float*>(a.p[0][l])) + i) =
+            *reinterpret_cast<const f32x4u*>(f + i);
+      } else if constexpr (OP == 2) {
+        const f32x4u t0 = *reinterpret_cast<const f32x4u*>(static_cast<const float*>(a.p[0][l]) + i) * cf[0];
+        f32x4u acc = f32x4u(0.0f) + t0;  // Python sum() starts from int 0
+        for (int j = 1; j < a.nlists; ++j) {
+          const f32x4u t = *reinterpret_cast<const f32x4u*>(static_cast<const float*>(a.p[j][l]) + i) * cf[j];
+          acc = acc + t;
+        }
+        *reinterpret_cast<f32x4u*>(f + i) = acc;
+      } else {
+        float* w = const_cast<float*>(static_cast<const float*>(a.p[0][l])) + i;
+        const f32x4u t = cf[0] * *reinterpret_cast<const f32x4u*>(f + i);
+        *reinterpret_cast<f32x4u*>(w) = *reinterpret_cast<const f32x4u*>(w) + t;
+      }
+    } else {
+      for (uint64_t e = i; e < end; ++e) {
+        if constexpr (OP == 0) {
+          f[e] = static_cast<const float*>(a.p[0][l])[e];
+        } else if constexpr (OP == 1) {
+          const_cast<float*>(static_cast<const float*>(a.p[0][l]))[e] = f[e];
+        } else if constexpr (OP == 2) {
+          float acc = 0.0f + static_cast<const float*>(a.p[0][l])[e] * cf[0];
+          for (int j = 1; j < a.nlists; ++j) {
+            const float t = static_cast<const float*>(a.p[j][l])[e] * cf[j];
+            acc = acc + t;
+          }
+          f[e] = acc;
+        } else {
+          float* w = const_cast<float*>(static_cast<const float*>(a.p[0][l]));
+          const float t = cf[0] * f[e];
+          w[e] = w[e] + t;
+        }
+      }
+    }
+  }
+}
+
 template <int OP>
 int flat_seg_launch(const void* const* ptrs, const int* kinds, int nlists, const double* coeffs,
                     const uint64_t* numel, int L, void* flat, int flat_kind, hipStream_t s) {
@@ -1230,7 +1292,11 @@ int flat_seg_launch(const void* const* ptrs, const int* kinds, int nlists, const
     }
     a.block_start[nl] = (uint32_t)blocks;
     if (blocks == 0) continue;
-    hipLaunchKernelGGL((flat_seg_kernel<OP>), dim3((unsigned)blocks), dim3(FA_BLOCK), 0, s, a, flat);
+    if (mask == 0 && g_flat_vec)
+      hipLaunchKernelGGL((flat_seg_vec_kernel<OP>), dim3((unsigned)blocks), dim3(FA_BLOCK), 0, s, a,
+                         static_cast<float*>(flat));
+    else
+      hipLaunchKernelGGL((flat_seg_kernel<OP>), dim3((unsigned)blocks), dim3(FA_BLOCK), 0, s, a, flat);
     int rc = check_launch("flat_seg_kernel");
     if (rc) return rc;
   }
@@ -1627,6 +1693,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
   else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
+  else if (!strcmp(key, "flat_vec")) g_flat_vec = value ? 1 : 0;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

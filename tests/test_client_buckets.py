@@ -57,8 +57,18 @@ def test_host_flat_detects_engine_style_views():
     assert wm._host_flat([flat[0:6].reshape(2, 3), flat[8:9]]) is None
 
 
+@pytest.fixture(params=[1, 0], ids=["vec16", "scalar"])
+def flat_path(request):
+    """Run a client-op test on the 16-B fp32 kernel and on the generic scalar kernel."""
+    from substrafl_amd import _native
+
+    _native.tune(flat_vec=request.param)
+    yield request.param
+    _native.tune(flat_vec=1)
+
+
 @pytest.mark.gpu
-def test_flat_ops_bit_exact_vs_torch_semantics():
+def test_flat_ops_bit_exact_vs_torch_semantics(flat_path):
     assert torch.cuda.is_available()
     m = _model("cuda")
     old = wm.get_parameters(m, True)
@@ -102,7 +112,7 @@ def test_flat_ops_bit_exact_vs_torch_semantics():
 
 
 @pytest.mark.gpu
-def test_flat_ops_many_layers():
+def test_flat_ops_many_layers(flat_path):
     """> 32 layers (several launches of the segmented kernel) and layers > 8192 elements."""
     torch.manual_seed(3)
     a = [torch.randn(int(n), device="cuda") for n in np.random.default_rng(0).integers(1, 40000, 75)]
