@@ -86,3 +86,26 @@ def test_pairwise_restatement_equals_numpy_sum(n, seed, dt):
     got = numpy_pairwise_sum(x) if n else dt(0.0)
     ref = np.add.reduce(x) if n else dt(0.0)
     assert np.asarray(dt(0.0) + got).tobytes() == np.asarray(ref).tobytes()
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.integers(0, 5_000_000), st.integers(1, 9), st.integers(1, 64), st.one_of(st.none(), st.integers(1, 10**8)))
+def test_multi_device_plan_partitions_the_bucket(M, G, bytes_per_elem, cap):
+    """MultiDeviceEngine.plan_ranges: the sub-ranges of all shards tile [0, M) in order, every
+    boundary except M is 512-element aligned, and no sub-range exceeds the HBM cap (or the
+    512-element minimum step)."""
+    from substrafl_amd.multi_device import MultiDeviceEngine
+    from substrafl_amd.sharding import SHARD_ALIGN
+
+    eng = MultiDeviceEngine(list(range(G)), max_shard_bytes=cap or 10**15)
+    plan = eng.plan_ranges(M, bytes_per_elem)
+    assert len(plan) == G
+    flat = [r for shard in plan for r in shard]
+    if M == 0:
+        assert flat == []
+        return
+    assert flat[0][0] == 0 and flat[-1][1] == M
+    for (a, b), (c, _) in zip(flat, flat[1:]):
+        assert b == c and b % SHARD_ALIGN == 0
+    limit = max(SHARD_ALIGN, (cap or 10**15) // bytes_per_elem)
+    assert all(0 < b - a <= limit for a, b in flat)
