@@ -70,6 +70,7 @@ int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then a
 int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand is fp32
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
 int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
+int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per workgroup)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -336,6 +337,18 @@ __device__ __forceinline__ uint64_t tile_of_block(const int remap) {
   return (uint64_t)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// it-th tile of this block: the grid-stride order above (tpb == 1), or tpb consecutive tiles
+// per block (tpb > 1; the caller divides the grid by tpb).  Speed only.
+__device__ __forceinline__ bool block_tile(const int remap, const int tpb, const uint64_t it, uint64_t* t) {
+  if (tpb > 1) {
+    if (it >= (uint64_t)tpb) return false;
+    *t = (uint64_t)blockIdx.x * tpb + it;
+  } else {
+    *t = tile_of_block(remap) + it * gridDim.x;
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------------------------
 // FedAvg bucket kernel (fed_avg.py:217-222)
 // ------------------------------------------------------------------------------------
@@ -460,7 +473,7 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
 __global__ void __launch_bounds__(FA_BLOCK)
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
-                  const uint64_t M, typename E::Out* __restrict__ out, const int remap) {
+                  const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
@@ -472,7 +485,9 @@ __global__ void __launch_bounds__(FA_BLOCK)
     __shared__ u32x4 stage[WIDE ? FA_BLOCK / 64 : 1][128];
     u32x4* lds_wave = stage[WIDE ? threadIdx.x / 64 : 0];
     const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
-    for (uint64_t base = tile_of_block(remap) * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+    uint64_t t;
+    for (uint64_t it = 0; block_tile(remap, tpb, it, &t) && t * tile < nvec; ++it) {
+      const uint64_t base = t * tile + threadIdx.x;
       // wave-uniform: every lane of this wave has all VPT vectors in range
       const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
       if (base + (VPT - 1) * FA_BLOCK < nvec) {
@@ -834,7 +849,7 @@ template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, 
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
-                    double* __restrict__ dout, double* __restrict__ cout, const int remap) {
+                    double* __restrict__ dout, double* __restrict__ cout, const int remap, const int tpb) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
   const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
@@ -842,7 +857,9 @@ __global__ void __launch_bounds__(FA_BLOCK)
   __shared__ u32x4 stage[FA_BLOCK / 64][128];
   u32x4* lds_wave = stage[threadIdx.x / 64];
   const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
-  for (uint64_t base = tile_of_block(remap) * tile + threadIdx.x; base < nvec; base += (uint64_t)gridDim.x * tile) {
+  uint64_t t;
+  for (uint64_t it = 0; block_tile(remap, tpb, it, &t) && t * tile < nvec; ++it) {
+    const uint64_t base = t * tile + threadIdx.x;
     const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
     if (base + (VPT - 1) * FA_BLOCK < nvec) {
       uint64_t v[VPT];
@@ -1338,7 +1355,7 @@ template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
   hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE>), dim3(grid), dim3(FA_BLOCK), 0,
-                     s, a, pw, kc, first, nvec, M, out, g_xcd);
+                     s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb);
 }
 
 // Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
@@ -1463,7 +1480,9 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
   const uint64_t nvec = vec ? M / E::L : 0;
   const Shape sh = shape_for<E>(K, nvec);
   const uint64_t per_thread = (g_tile && g_nt_load) ? (uint64_t)sh.vpt : 1;
-  const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
+  unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
+  if (g_tpb > 1 && g_tile && nvec)  // every tile exactly once: no grid cap with tpb
+    grid = (unsigned)(((nvec + per_thread - 1) / per_thread + g_tpb - 1) / g_tpb);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
     const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
     FaArgs<E, FEDAGG_KCHUNK> a;
@@ -1529,7 +1548,7 @@ void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FED
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
                              uint64_t M, double* dout, double* cout) {
   hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT, PIPE>), dim3(grid),
-                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd);
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd, g_tpb);
 }
 
 // Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
@@ -1602,7 +1621,9 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   const int sv = g_sc_vpt > 0 ? g_sc_vpt : (K >= 32 ? 8 : 4);
   const int su = g_sc_vpt > 0 ? g_sc_unroll : (K >= 32 ? 2 : 4);
   const uint64_t per_thread = g_nt_load ? (uint64_t)sv : 1;
-  const unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
+  unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
+  if (g_tpb > 1 && nvec)  // every tile exactly once: no grid cap with tpb
+    grid = (unsigned)(((nvec + per_thread - 1) / per_thread + g_tpb - 1) / g_tpb);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
     const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
     ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a;
@@ -1694,6 +1715,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
   else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
   else if (!strcmp(key, "flat_vec")) g_flat_vec = value ? 1 : 0;
+  else if (!strcmp(key, "tpb")) g_tpb = value < 1 ? 1 : (value > 64 ? 64 : (int)value);
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

@@ -498,7 +498,8 @@ def test_many_numel1_layers_fused_and_separate(torch_gpu, dummy_algo_class, fuse
                                    dict(vpt=8, unroll=4, tile=1, grid_cap=3), dict(vpt=1, tile=0),
                                    dict(vpt=16, unroll=2, tile=1), dict(vpt=16, unroll=1, tile=1, grid_cap=3),
                                    dict(xcd=1), dict(vpt=16, unroll=2, tile=1, xcd=1),
-                                   dict(vpt=4, unroll=4, tile=1, pipe=1), dict(vpt=8, tile=1, pipe=1, grid_cap=3)])
+                                   dict(vpt=4, unroll=4, tile=1, pipe=1), dict(vpt=8, tile=1, pipe=1, grid_cap=3),
+                                   dict(tpb=3), dict(tpb=7, grid_cap=5), dict(vpt=16, unroll=2, tile=1, tpb=2)])
 def test_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -508,7 +509,7 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
@@ -554,7 +555,8 @@ def test_auto_shape_many_clients_bit_identical(torch_gpu):
                                    dict(sc_split=1, sc_vpt=4, sc_unroll=8), dict(sc_split=1, sc_vpt=8, sc_unroll=2),
                                    dict(sc_split=1, sc_vpt=8, grid_cap=2), dict(sc_vpt=8, sc_unroll=2),
                                    dict(xcd=1), dict(sc_vpt=8, sc_unroll=2, xcd=1, grid_cap=5),
-                                   dict(sc_pipe=1), dict(sc_pipe=1, sc_vpt=2, sc_unroll=4, grid_cap=3)])
+                                   dict(sc_pipe=1), dict(sc_pipe=1, sc_vpt=2, sc_unroll=4, grid_cap=3),
+                                   dict(tpb=3), dict(tpb=5, grid_cap=2, sc_vpt=8, sc_unroll=2)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -565,7 +567,7 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     cv = torch.randn((K, M + 1), device="cuda")
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
-    default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0, xcd=0)
+    default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0, xcd=0, tpb=1)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)

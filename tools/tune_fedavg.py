@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--full", action="store_true", help="the whole shape family (nt_store 0/1, grid-strided)")
     ap.add_argument("--xcd", action="store_true", help="each shape also with the XCD-contiguous tile order")
+    ap.add_argument("--tpb", type=int, nargs="*", default=[2, 4, 8], help="auto shape with N consecutive tiles per block")
     args = ap.parse_args()
 
     import torch
@@ -42,7 +43,7 @@ def main():
     plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
 
-    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0)
+    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1)
     if args.full:
         shapes = [dict(), dict(unroll=16), dict(vpt=2, tile=1), dict(vpt=4, tile=1), dict(vpt=4, tile=1, unroll=4),
                   dict(vpt=8, tile=1, unroll=4), dict(vpt=8, tile=1, unroll=2), dict(vpt=4, tile=1, grid_cap=8192),
@@ -52,8 +53,9 @@ def main():
         shapes = [dict(vpt=0), dict(vpt=8, unroll=4), dict(vpt=8, unroll=2), dict(vpt=16, unroll=2), dict(vpt=16, unroll=1),
                   dict(vpt=4, unroll=4), dict(vpt=4, unroll=8), dict(vpt=2, unroll=8),
                   dict(vpt=4, unroll=4, pipe=1), dict(vpt=8, unroll=2, pipe=1), dict(vpt=1, unroll=8, tile=0, pipe=1)]
-        variants = [dict(base, **dict(dict(tile=1), **sh), nt_store=1, xcd=x) for sh in shapes
+        variants = [dict(base, **dict(dict(tile=1), **sh), nt_store=1, xcd=x, tpb=1) for sh in shapes
                     for x in ((0, 1) if args.xcd else (0,))]
+        variants += [dict(base, vpt=0, tile=1, nt_store=1, xcd=0, tpb=t) for t in args.tpb]
     times = {i: [] for i in range(len(variants))}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for r in range(args.rounds):
