@@ -248,3 +248,51 @@ def test_concurrent_calls_are_serialized(gpu):
         t.join()
     for (pus, ns), got in zip(cases, results):
         _assert_same(got, fedavg_reference_structure(pus, ns))
+
+
+class _PicklableAlgo:
+    strategies = ["Federated Averaging", "Scaffold"]
+
+
+@pytest.mark.gpu
+def test_task_process_with_device_list(gpu, tmp_path):
+    """Subprocess mode (substratools_methods.py:94-118 contract): a strategy built with
+    device=[0, 0] is cloudpickled into RemoteStruct, re-created in a fresh process, loads the
+    shared-state pickles and aggregates on the multi-device engine, bit-exact."""
+    import pickle
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    import cloudpickle
+
+    from substrafl_amd.remote import PickleSerializer
+    from substrafl_amd.schemas import FedAvgSharedState
+    from substrafl_amd.strategies import FedAvg
+
+    root = Path(__file__).resolve().parents[1]
+    rng = np.random.default_rng(77)
+    pus = _updates(rng, 4, SHAPES)
+    ns = [31, 7, 1000, 2]
+    paths = []
+    for k in range(4):
+        p = tmp_path / f"shared_{k}"
+        PickleSerializer.save(FedAvgSharedState(n_samples=ns[k], parameters_update=pus[k]), p)
+        paths.append(str(p))
+    cloudpickle.register_pickle_by_value(sys.modules[__name__])
+    FedAvg(algo=_PicklableAlgo(), device=[0, 0]).avg_shared_states(shared_states=paths).remote_struct.save(tmp_path)
+    out = tmp_path / "out_shared"
+    script = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from substrafl_amd.remote import RemoteStruct\n"
+        "from substrafl_amd.engine import engine_for\n"
+        "rs = RemoteStruct.load(__import__('pathlib').Path(%r))\n"
+        "inst = rs.get_remote_instance()\n"
+        "inst.generic_function({'shared': %r}, {'shared': %r}, {})\n"
+        "eng = engine_for([0, 0])\n"
+        "assert type(eng).__name__ == 'MultiDeviceEngine' and eng.last_timing['ranges'], eng.last_timing\n"
+    ) % (str(root), str(tmp_path), paths, str(out))
+    subprocess.run([sys.executable, "-c", script], check=True, timeout=300)
+    with open(out, "rb") as f:
+        res = pickle.load(f)
+    _assert_same(res.avg_parameters_update, fedavg_reference_structure(pus, ns))
