@@ -23,6 +23,17 @@ class PickleSerializer:
             return pickle.load(f)
 
     @staticmethod
+    def load_mapped(path: Path) -> Any:
+        """``load`` with the NumPy array payloads left in a private mapping of the file (no copy,
+        no fresh pages: mapped_pickle.py); used by the aggregate task's ingest, whose inputs are
+        read-only task inputs.  Same objects as ``load``."""
+        if os.environ.get("FEDAGG_MAPPED_LOAD", "1") == "0":  # measurement switch: the copying load
+            return PickleSerializer.load(path)
+        from .mapped_pickle import load_mapped
+
+        return load_mapped(path)
+
+    @staticmethod
     def load_many(paths: Sequence[Path], max_workers: int = 0) -> List[Any]:
         """``[load(p) for p in paths]`` with the K file reads overlapped on a thread pool (the
         read syscalls, where page faulting of the fresh buffers happens, release the GIL).

@@ -55,7 +55,8 @@ class RemoteMethod:
                 states = None
                 ingest = getattr(self.instance, "ingest_shared_states", None)
                 if callable(ingest):  # load + stage to the GPU, overlapped (engine.ingest)
-                    states = ingest(self.method_name, paths, self.shared_state_serializer.load)
+                    load = getattr(self.shared_state_serializer, "load_mapped", self.shared_state_serializer.load)
+                    states = ingest(self.method_name, paths, load)
                 if states is None:
                     loader = getattr(self.shared_state_serializer, "load_many", None)
                     states = loader(paths) if loader else [self.load_shared(p) for p in paths]

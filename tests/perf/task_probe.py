@@ -7,6 +7,7 @@ per task that unpickles K shared-state files, aggregates and pickles the result.
   child --mode engine:    substrafl_amd's RemoteMethod.generic_function (prewarm + threaded load +
                           GPU engine), exactly the drop-in task path.
   child --mode engine-noprewarm: same, with the prewarm hook disabled.
+  child --mode engine-copyload: same, loading with pickle.load instead of the mapped loader.
   child --mode numpy:     the reference's own sequence (sequential pickle.load, NumPy FedAvg in the
                           reference call structure from oracle/, pickle.dump) -- the CPU baseline.
 """
@@ -57,6 +58,8 @@ def child(mode: str, d: Path, K: int) -> None:
         strategy = FedAvg(algo=_Algo())
         if mode == "engine-noprewarm":
             strategy.prewarm_aggregation = None
+        if mode == "engine-copyload":  # pickle.load instead of the mapped loader
+            os.environ["FEDAGG_MAPPED_LOAD"] = "0"
         t1 = time.perf_counter()
         rm = RemoteMethod(strategy, "avg_shared_states", {})
         rm.register_substratools_function()  # function.py's next step: starts the prewarm
@@ -106,7 +109,7 @@ def main():
         with open(d / f"shared_{k}", "wb") as f:
             pickle.dump(st, f)
     for rep in range(args.reps):
-        for mode in ("numpy", "engine", "engine-noprewarm"):
+        for mode in ("numpy", "engine", "engine-noprewarm", "engine-copyload"):
             t0 = time.perf_counter()
             r = subprocess.run([sys.executable, __file__, "--child", mode, "--dir", str(d), "--K", str(args.K)],
                                capture_output=True, text=True, timeout=600)
