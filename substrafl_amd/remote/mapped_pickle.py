@@ -11,9 +11,11 @@ no copy, no zeroed pages.  Everything else in the pickle is unpickled as usual, 
 library's own unpickler (``pickle._Unpickler``) with two hooks:
 
 * the file object hands out payloads of >= 1 MiB as ``memoryview`` slices of the mapping;
-* ``BUILD`` of a plain ``ndarray`` whose raw data is such a slice (NumPy's protocol 2-4
+* ``BUILD`` of a plain ``ndarray`` whose raw data is such a slice (NumPy's protocol 3-4
   reduction ``_reconstruct`` + ``__setstate__``) becomes ``np.frombuffer(slice).reshape(...)``,
-  replacing the placeholder on the stack and in the memo.
+  replacing the placeholder on the stack and in the memo;
+* protocol 5 in-band buffers (``BYTEARRAY8``: NumPy's ``PickleBuffer`` reduction, the flat wire
+  bucket) of >= 1 MiB are handed to their reduction as writable views of the mapping.
 
 The arrays are writable (copy-on-write), C- or F-ordered as pickled, and equal to what
 ``pickle.load`` returns.  If any large payload is consumed by something else (a ``bytes`` field,
@@ -27,12 +29,17 @@ from __future__ import annotations
 
 import mmap
 import pickle
+import struct
 from pathlib import Path
 from typing import Any, List
 
 import numpy as np
 
 BIG = 1 << 20  # payloads handed out as views of the mapping
+# callables a pickle may hand such a payload to, that build an array viewing it (protocol 5 arrays,
+# the flat wire format)
+_VIEW_CONSUMERS = {("numpy._core.numeric", "_frombuffer"), ("numpy.core.numeric", "_frombuffer"),
+                   ("substrafl_amd.wire", "_bucket_from_buffer")}
 
 
 class _MappedFile:
@@ -79,15 +86,32 @@ class _MappedUnpickler(pickle._Unpickler):  # the pure-Python unpickler: its dis
 
     def find_class(self, module, name):
         obj = super().find_class(module, name)
-        if module == "substrafl_amd.wire" and name == "_bucket_from_buffer":  # flat wire format
+        if (module, name) in _VIEW_CONSUMERS:  # reductions that take a buffer and keep a view of it
 
-            def bucket_from_buffer(buf, _f=obj):
+            def consume(buf, *args, _f=obj):
                 if isinstance(buf, memoryview):
                     self.consumed += 1  # a writable view of the mapping: np.frombuffer keeps it
-                return _f(buf)
+                return _f(buf, *args)
 
-            return bucket_from_buffer
+            return consume
         return obj
+
+    def load_bytearray8(self):
+        # protocol 5 in-band buffers (NumPy's PickleBuffer reduction, the wire bucket): a view of
+        # the mapping instead of a fresh bytearray, for payloads written outside a frame
+        n, = struct.unpack("<Q", self.read(8))
+        f = self._mapped
+        if n >= BIG and not self._unframer.current_frame and f.pos + n <= f.size:
+            v = f.view[f.pos : f.pos + n]
+            f.pos += n
+            f.views.append(v)
+            self.append(v)
+            return
+        b = bytearray(n)
+        self.readinto(b)
+        self.append(b)
+
+    dispatch[pickle.BYTEARRAY8[0]] = load_bytearray8
 
     def load_build(self):
         stack = self.stack

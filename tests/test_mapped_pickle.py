@@ -61,7 +61,7 @@ def test_equal_to_pickle_load(tmp_path, protocol):
     ref = pickle.loads(p.read_bytes())
     got = load_mapped(p)
     _same(got, ref)
-    if protocol in (3, 4):  # NumPy's _reconstruct + __setstate__ with a BINBYTES payload: mapped
+    if protocol in (3, 4, 5):  # BINBYTES (3, 4) or in-band PickleBuffer (5) payloads: mapped
         big = got.parameters_update[0]
         assert isinstance(_root(big), memoryview)  # a view of the file mapping, not a copy
         big[0] = 123.0  # copy-on-write: the file is untouched
@@ -82,12 +82,13 @@ def test_shared_references_and_scaffold(tmp_path):
     assert got.parameters_update[0] is got.control_variate_update[0]
 
 
-def test_wire_format_mapped(tmp_path):
+@pytest.mark.parametrize("protocol", [4, 5])
+def test_wire_format_mapped(tmp_path, protocol):
     rng = np.random.default_rng(4)
     layers = _layers(rng)
     st = FedAvgSharedState(n_samples=3, parameters_update=wire.pack([layers[0], layers[2]]))  # one dtype
     p = tmp_path / "s"
-    p.write_bytes(pickle.dumps(st))
+    p.write_bytes(pickle.dumps(st, protocol=protocol))
     got = load_mapped(p)
     _same([np.asarray(a) for a in got.parameters_update],
           [np.asarray(a) for a in pickle.loads(p.read_bytes()).parameters_update])
