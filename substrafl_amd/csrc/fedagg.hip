@@ -1590,9 +1590,11 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
       if (nts) return launch_scaffold_variant<TIn, true, true, 2, 2>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, false, 2, 2>(SC_ARGS);
     }
+    if (su >= 8 && nts) return launch_scaffold_variant<TIn, true, true, 2, 8>(SC_ARGS);
     if (nts) return launch_scaffold_variant<TIn, true, true, 2, 4>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 2, 4>(SC_ARGS);
   }
+  if (su >= 8 && nts) return launch_scaffold_variant<TIn, true, true, 1, 8>(SC_ARGS);
   if (nts) return launch_scaffold_variant<TIn, true, true, 1, 4>(SC_ARGS);
   return launch_scaffold_variant<TIn, true, false, 1, 4>(SC_ARGS);
 #undef SC_ARGS

@@ -556,7 +556,8 @@ def test_auto_shape_many_clients_bit_identical(torch_gpu):
                                    dict(sc_split=1, sc_vpt=8, grid_cap=2), dict(sc_vpt=8, sc_unroll=2),
                                    dict(xcd=1), dict(sc_vpt=8, sc_unroll=2, xcd=1, grid_cap=5),
                                    dict(sc_pipe=1), dict(sc_pipe=1, sc_vpt=2, sc_unroll=4, grid_cap=3),
-                                   dict(tpb=3), dict(tpb=5, grid_cap=2, sc_vpt=8, sc_unroll=2)])
+                                   dict(tpb=3), dict(tpb=5, grid_cap=2, sc_vpt=8, sc_unroll=2),
+                                   dict(sc_vpt=2, sc_unroll=8), dict(sc_vpt=1, sc_unroll=8, grid_cap=4)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native

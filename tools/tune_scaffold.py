@@ -35,7 +35,7 @@ def main():
     plan = ScaffoldPlan("f32", d, cv, c, scaffold_weights(ns), args.M, 1.0, dout, cout, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
     variants = [dict(sc_split=0, sc_pipe=0, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
-                for v, u in ((0, 4), (2, 4), (4, 2), (4, 4), (8, 1), (8, 2))]  # sc_vpt 0: the auto shape
+                for v, u in ((0, 4), (2, 4), (2, 8), (1, 8), (4, 2), (4, 4), (8, 1), (8, 2))]  # sc_vpt 0: auto
     variants += [dict(sc_split=0, sc_pipe=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
                  for v, u in ((4, 2), (2, 4))]
     variants += [dict(sc_split=1, sc_pipe=0, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
