@@ -11,12 +11,15 @@ Two entry levels:
   states arrive as host NumPy arrays (unpickled by ``RemoteMethod.generic_function``,
   substrafl/remote/substratools_methods.py:54-66); the native session (:mod:`runtime`) packs
   them through its pinned ring into HBM, the kernels reduce them, and one D2H copy brings the
-  result home as per-layer views of one owned array.  No PyTorch on this path.
+  result home as per-layer views of one owned array.  No PyTorch on this path.  A call whose
+  buckets exceed the GPU's HBM budget is streamed through it in parameter ranges
+  (:mod:`multi_device`), and ``engine_for`` with several devices returns that module's engine.
 
 Every arithmetic step of the reduction runs in libfedagg's HIP kernels; if the library or a GPU
 is missing the engine raises -- there is no CPU fallback.  Results never depend on engine state:
-the only thing kept between calls is the one-shot record of rows staged by :meth:`ingest`, which
-an aggregation uses only for the very same array objects.  The GPU is initialised lazily on
+what is kept between calls is the one-shot record of rows staged by :meth:`ingest` (used only for
+the very same array objects), grow-only HBM buffers and result host buffers that are recycled
+only once nothing references them.  Calls are serialised per GPU.  The GPU is initialised lazily on
 first use (tests fork after import: tests/conftest.py:52-59), so strategies stay
 cloudpickle-able for RemoteStruct (remote_struct.py:84-114); the engine itself is never pickled.
 """
