@@ -588,10 +588,15 @@ class AggregationEngine:
         d_d = s.buffer(self._B_BUCKET, K * lay_d.ld * isz)
         d_cv = s.buffer(self._B_CV, K * lay_c.ld * isz)
         d_cc = s.buffer(self._B_C, K * lay_s.ld * isz)
+        # every client holding the very same c arrays (simulation mode: the server's broadcast):
+        # assert_array_equal holds by identity, so one copy is staged and the check is skipped
+        same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
+                     for row in server_control_variates[1:])
         pre = 0
         for rows, lay, d, slot in ((parameters_updates, lay_d, d_d, self._B_BUCKET),
                                    (control_variate_updates, lay_c, d_cv, self._B_CV),
-                                   (server_control_variates, lay_s, d_cc, self._B_C)):
+                                   (server_control_variates[:1] if same_c else server_control_variates, lay_s, d_cc,
+                                    self._B_C)):
             rows = [list(r) for r in rows]
             if self._take_prestaged(slot, d, lay.ld * isz, rows):
                 pre += 1
@@ -599,11 +604,13 @@ class AggregationEngine:
                 self._stage_rows(s, rows, lay, d)
         self._prestaged = {}
         tm["prestaged"] = pre == 3
+        tm["c_check"] = "identity" if same_c else "device"
         tm["stage_s"] = time.perf_counter() - t0
         t1 = time.perf_counter()
         cnt = s.buffer(self._B_CNT, 8)
         s.memset(cnt, 0, 8)
-        equal_count(kind, [d_cc + k * lay_s.ld * isz for k in range(K)], lay_s.M, cnt, s.stream)
+        if not same_c:
+            equal_count(kind, [d_cc + k * lay_s.ld * isz for k in range(K)], lay_s.M, cnt, s.stream)
         dout = s.buffer(self._B_OUT, lay_d.ld * 8)
         cout = s.buffer(self._B_COUT, lay_c.ld * 8)
         ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, max(1, lay_d.pairwise_idx.size), 8))

@@ -252,7 +252,10 @@ class MultiDeviceEngine:
         M = layout.M
         rows_d = self._rows_direct(parameters_updates, sdt, M)
         rows_c = self._rows_direct(control_variate_updates, sdt, M)
-        rows_s = self._rows_direct(server_control_variates, sdt, M)
+        same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
+                     for row in server_control_variates[1:])
+        rows_s = self._rows_direct(server_control_variates[:1] if same_c else server_control_variates, sdt, M)
+        Kc = 1 if same_c else K  # identical c objects: one staged copy, no check (see engine.scaffold)
         w = scaffold_weights(n_samples)
         lr = float(aggregation_lr)
         pw_all = layout.pairwise_idx.astype(np.int64)
@@ -260,7 +263,7 @@ class MultiDeviceEngine:
         out_c = runtime.reusable_host_array(M, np.float64, "multi-scaffold-c")
         mism = [0] * len(self.devices)
         # per element: K deltas + K control variates + K server-c copies in, two fp64 outputs
-        ranges = self.plan_ranges(M, 3 * K * isz + 16)
+        ranges = self.plan_ranges(M, (2 * K + Kc) * isz + 16)
         ws_bytes = _native.load().fedagg_pairwise_ws_bytes(K, max(1, pw_all.size), 8)
 
         def work(g, s):
@@ -270,13 +273,14 @@ class MultiDeviceEngine:
                 br = (lo * isz, hi * isz)
                 d_d = s.buffer(self._B_BUCKET, K * ld * isz)
                 d_cv = s.buffer(self._B_CV, K * ld * isz)
-                d_cc = s.buffer(self._B_C, K * ld * isz)
+                d_cc = s.buffer(self._B_C, Kc * ld * isz)
                 s.stage(d_d, ld * isz, rows_d, byte_range=br)
                 s.stage(d_cv, ld * isz, rows_c, byte_range=br)
                 s.stage(d_cc, ld * isz, rows_s, byte_range=br)
                 cnt = s.buffer(self._B_CNT, 8)
                 s.memset(cnt, 0, 8)
-                equal_count(kind, [d_cc + k * ld * isz for k in range(K)], n, cnt, s.stream)
+                if not same_c:
+                    equal_count(kind, [d_cc + k * ld * isz for k in range(K)], n, cnt, s.stream)
                 dout = s.buffer(self._B_OUT, _ld(n, 8) * 8)
                 cout = s.buffer(self._B_COUT, _ld(n, 8) * 8)
                 ws = s.buffer(self._B_WS, ws_bytes)

@@ -271,6 +271,34 @@ def test_scaffold_fp64_inputs_and_c_check(torch_gpu, dummy_algo_class):
         Scaffold(algo=dummy_algo_class()).avg_shared_states(shared_states=states, _skip=True)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_scaffold_shared_c_objects_staged_once(torch_gpu, dtype):
+    """All clients holding the very same c arrays (simulation mode) stage one copy and skip the
+    device check; equal-valued copies, and one copy that differs, still take the device check."""
+    from substrafl_amd.engine import AggregationEngine
+
+    rng = np.random.default_rng(21)
+    K = 5
+    shapes = [(300, 7), (1,), (4096,)]
+    mk = lambda: [rng.standard_normal(s).astype(dtype) for s in shapes]  # noqa: E731
+    pus, cvs, c = [mk() for _ in range(K)], [mk() for _ in range(K)], mk()
+    c[0][3, 3] = np.nan
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.9)
+    eng = AggregationEngine(0)
+    for rows, check in (([c] * K, "identity"), ([list(c) for _ in range(K)], "identity"),
+                        ([[a.copy() for a in c] for _ in range(K)], "device")):
+        mism, new_c, avg = eng.scaffold(pus, cvs, rows, ns, 0.9)
+        assert mism == 0 and eng.last_timing["c_check"] == check
+        _assert_same(new_c, rc)
+        _assert_same(avg, ra)
+    rows = [list(c) for _ in range(K)]
+    rows[K - 1][2] = c[2].copy()
+    rows[K - 1][2][-1] += 1
+    mism, _, _ = eng.scaffold(pus, cvs, rows, ns, 0.9)
+    assert mism == 1 and eng.last_timing["c_check"] == "device"
+
+
 # ------------------------------------------------------------------------------------------
 # device-resident plans through the C ABI (bf16, unaligned rows, full size)
 # ------------------------------------------------------------------------------------------
