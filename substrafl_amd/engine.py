@@ -293,8 +293,6 @@ class AggregationEngine:
         if self.max_bucket_bytes is not None:
             budget = int(self.max_bucket_bytes)
         else:
-            from . import runtime
-
             free = runtime.device_memory(self._index())[0] + self.session().held_bytes()
             budget = int(free * HBM_HEADROOM)
         if need_bytes <= budget:
@@ -316,8 +314,6 @@ class AggregationEngine:
         """Start :func:`runtime.prewarm` for this engine's GPU (HIP start-up, pinned ring, worker
         pool, code object) on a background thread; HBM buffers are sized by the first call
         (``hipMalloc`` is ~0.1 ms, not worth guessing sizes for)."""
-        from . import runtime
-
         runtime.prewarm(self._index())
 
     @serialized
@@ -417,8 +413,6 @@ class AggregationEngine:
         return True
 
     def session(self):
-        from . import runtime
-
         s = runtime.session(self._index())
         if self._pack_threads:
             s.set("threads", self._pack_threads)

@@ -82,8 +82,6 @@ class MultiDeviceEngine:
     def sessions(self):
         """One native session per shard (created on first use)."""
         if self._sessions is None:
-            from . import runtime
-
             G = len(self.devices)
             per = self._pack_threads or max(2, min(16, os.cpu_count() or 1) // G)
             seen = set()
@@ -100,8 +98,6 @@ class MultiDeviceEngine:
         return self._sessions
 
     def prewarm(self) -> None:
-        from . import runtime
-
         for d in sorted(set(self.devices)):
             runtime.prewarm(d)
 
@@ -130,7 +126,6 @@ class MultiDeviceEngine:
     def _budget(self, g: int) -> int:
         if self.max_shard_bytes:
             return int(self.max_shard_bytes)
-        from . import runtime
 
         free, _ = runtime.device_memory(self.devices[g])
         return int((free + self.sessions()[g].held_bytes()) * HBM_HEADROOM)
