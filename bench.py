@@ -206,7 +206,7 @@ def main():
     full = int(min(floats // 4 // 256, 1 << 20))  # one 16-B vector per thread, like the bucket kernel
     sink = torch.empty(full, dtype=torch.float32, device=device)
     read_ceiling = 0.0
-    for pgrid in sorted({min(16384, full), min(65536, full), full}):  # best grid = the ceiling
+    for pgrid in sorted({min(g, full) for g in (2048, 4096, 8192, 16384, 65536)} | {full}):  # best grid = the ceiling
         for _ in range(3):
             _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
                                                     stream.cuda_stream), "probe")
