@@ -13,6 +13,12 @@ import numpy as np
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
+def x_isz(dt):
+    import torch
+
+    return torch.empty(0, dtype=dt).element_size()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--K", type=int, default=8)
@@ -23,6 +29,10 @@ def main():
     ap.add_argument("--full", action="store_true", help="the whole shape family (nt_store 0/1, grid-strided)")
     ap.add_argument("--xcd", action="store_true", help="each shape also with the XCD-contiguous tile order")
     ap.add_argument("--tpb", type=int, nargs="*", default=[2, 4, 8], help="auto shape with N consecutive tiles per block")
+    ap.add_argument("--pads", type=int, nargs="*", default=[],
+                    help="row-pitch paddings (elements) to time the auto shape with instead of the shape sweep")
+    ap.add_argument("--gridstride", action="store_true",
+                    help="grid-strided and tile shapes under grid caps (the read probe's walk), next to the auto shape")
     args = ap.parse_args()
 
     import torch
@@ -42,9 +52,43 @@ def main():
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
     plan = FedAvgPlan(args.kind, x, fedavg_weights(ns, args.kind), args.M, out, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
+    if args.pads:  # client rows at pitch ld + pad: do the clients' same offsets collide in the HBM channels?
+        del x
+        plans = []
+        for pad in args.pads:
+            xp = torch.empty((args.K, lay.ld + pad), device="cuda", dtype=dt)
+            xp.normal_()
+            plans.append((pad, FedAvgPlan(args.kind, xp[:, :lay.ld], fedavg_weights(ns, args.kind), args.M, out,
+                                          lay.pairwise_idx), xp))
+        _native.tune(vpt=0, tile=1, nt_store=1, grid_cap=0, xcd=0, tpb=1, pipe=0)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        tt = {pad: [] for pad, _, _ in plans}
+        for r in range(args.rounds):
+            for pad, pl, _ in plans:
+                for _ in range(3):
+                    pl.launch()
+                ev[0].record()
+                for _ in range(args.iters):
+                    pl.launch()
+                ev[1].record()
+                torch.cuda.synchronize()
+                tt[pad].append(ev[0].elapsed_time(ev[1]) / args.iters)
+        for pad in tt:
+            m = float(np.median(tt[pad]))
+            print(json.dumps(dict(pad_elems=pad, pad_bytes=pad * x_isz(dt), kind=args.kind, K=args.K, M=args.M,
+                                  median_us=round(m * 1e3, 2), GBps=round(nbytes / (m / 1e3) / 1e9, 1))))
+        return
 
     base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1)
-    if args.full:
+    if args.gridstride:
+        shapes = [dict(vpt=1, unroll=8), dict(vpt=1, unroll=4), dict(vpt=2, unroll=8), dict(vpt=1, unroll=8, pipe=1),
+                  dict(vpt=1, unroll=16)]
+        variants = [dict(base, vpt=0, tile=1, nt_store=1)]
+        variants += [dict(base, **sh, tile=0, nt_store=1, grid_cap=g) for sh in shapes
+                     for g in (0, 2048, 4096, 8192, 16384)]
+        variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, grid_cap=g) for v, u in ((8, 4), (4, 4))
+                     for g in (1024, 2048, 4096)]
+    elif args.full:
         shapes = [dict(), dict(unroll=16), dict(vpt=2, tile=1), dict(vpt=4, tile=1), dict(vpt=4, tile=1, unroll=4),
                   dict(vpt=8, tile=1, unroll=4), dict(vpt=8, tile=1, unroll=2), dict(vpt=4, tile=1, grid_cap=8192),
                   dict(vpt=4, tile=1, grid_cap=2048)]
@@ -72,7 +116,7 @@ def main():
     # read-stream probe ceiling at several grid sizes (same process, same buffer)
     sink = torch.empty(1 << 20, device="cuda")
     nfl = x.numel() * x.element_size() // 4 // 4 * 4
-    for g in (4096, 16384, 65536, int(min(nfl // 4 // 256, 1 << 20))):
+    for g in (2048, 4096, 8192, 16384, 65536, int(min(nfl // 4 // 256, 1 << 20))):
         tt = []
         for _ in range(args.rounds):
             ev[0].record()
