@@ -373,7 +373,42 @@ def test_full_size_vs_torch_sequential(torch_gpu, K, M, kind):
         assert _bits(np.float32(0.0) + numpy_pairwise_sum(prods)) == _bits(out[p].cpu().numpy())
 
 
-@pytest.mark.parametrize("K, M", [(16, 5_000_011), (3, 2_000_000)])
+@pytest.mark.parametrize("K, M, kind", [(64, 125_000_000, "f32"), (128, 350_000_000, "bf16")])
+def test_baseline_config_sizes_vs_torch_sequential(torch_gpu, K, M, kind):
+    """BASELINE.json configs C3 (64 x 125M fp32, 32.5 GB) and C5 (128 x 350M bf16, 91 GB) on one
+    GPU: bit-exact against torch eager ops applied client by client in list order (one rounded
+    IEEE op each), built row by row so no fp32 copy of the whole bucket is made."""
+    torch = torch_gpu
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+
+    shapes = synthetic_state_dict_shapes(M)
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    dt = torch.bfloat16 if kind == "bf16" else torch.float32
+    x = torch.empty((K, lay.ld), device="cuda", dtype=dt)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for k in range(K):
+        x[k].copy_(torch.randn(lay.ld, generator=g, device="cuda"))
+    ns = [int(v) for v in np.random.default_rng(11).integers(100, 10000, K)]
+    w = fedavg_weights(ns, "f32")
+    out = torch.empty(lay.ld, device="cuda")
+    FedAvgPlan(kind, x, w, M, out, lay.pairwise_idx).launch()
+    acc = torch.zeros(M, device="cuda")
+    for k in range(K):
+        acc = acc + x[k, :M].float() * torch.tensor(w[k], device="cuda")
+    torch.cuda.synchronize()
+    mask = torch.ones(M, dtype=torch.bool, device="cuda")
+    mask[torch.from_numpy(lay.pairwise_idx.astype(np.int64)).cuda()] = False
+    same = torch.equal(out[:M][mask].view(torch.int32), acc[mask].view(torch.int32))
+    for p in lay.pairwise_idx.astype(np.int64):
+        prods = (x[:, p].float().cpu().numpy() * w).astype(np.float32)
+        same = same and _bits(np.float32(0.0) + numpy_pairwise_sum(prods)) == _bits(out[p].cpu().numpy())
+    del x, acc, mask, out
+    torch.cuda.empty_cache()
+    assert same
+
+
+@pytest.mark.parametrize("K, M", [(16, 25_000_000), (16, 5_000_011), (3, 2_000_000)])
 def test_scaffold_full_size_vs_torch_fp64(torch_gpu, K, M):
     """Scaffold at size: bit-exact against torch fp64 eager ops (w*x, +, c last, lr*) on the device."""
     torch = torch_gpu
