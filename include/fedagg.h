@@ -197,7 +197,8 @@ fedagg_session* fedagg_session_create(int device);
 void fedagg_session_destroy(fedagg_session* s);
 /* the session's hipStream_t, to pass as `stream` to the kernel entry points */
 void* fedagg_session_stream(fedagg_session* s);
-/* knobs: "threads" (pack workers), "chunk_bytes" (pinned slot size), "slots" (ring length) */
+/* knobs: "threads" (pack workers), "chunk_bytes" (pinned slot size), "slots" (ring length),
+ * "copy_streams" (1 or 2 H2D queues for staging; default 2) */
 int fedagg_session_set(fedagg_session* s, const char* key, long long value);
 /* grow-only device buffer number `slot` (0..FEDAGG_SESSION_BUFFERS-1) of at least `bytes` */
 int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr);

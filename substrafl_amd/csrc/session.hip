@@ -61,6 +61,12 @@ int hip_fail(const char* what, hipError_t e) {
 struct fedagg_session {
   int device = 0;
   hipStream_t stream = nullptr;
+  // second H2D queue: staging alternates its chunks over `stream` and `xstream`, so one chunk's
+  // copy is set up while the other's is on the link (4 MiB pinned chunks: 49 GB/s on one queue,
+  // 56 GB/s over two on MI355X, profiles/r01_h2d_probe.log); the tail of a stage joins `stream`
+  hipStream_t xstream = nullptr;
+  hipEvent_t join_ev = nullptr;
+  int copy_streams = 2;
   int threads = 8;
   uint64_t chunk_bytes = 4ull << 20;  // 4 MiB: same staging rate as 16 MiB, a third of the cold ring cost
   int slots = 12;
@@ -133,8 +139,12 @@ fedagg_session* fedagg_session_create(int device) {
   }
   auto* s = new fedagg_session();
   s->device = device;
-  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) {
-    hip_fail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&s->join_ev, hipEventDisableTiming)) != hipSuccess) {
+    hip_fail("fedagg_session_create: stream/event", e);
+    if (s->xstream) (void)hipStreamDestroy(s->xstream);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return nullptr;
   }
@@ -145,9 +155,12 @@ void fedagg_session_destroy(fedagg_session* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   (void)hipStreamSynchronize(s->stream);
+  (void)hipStreamSynchronize(s->xstream);
   s->release_ring();
   for (int i = 0; i < FEDAGG_SESSION_BUFFERS; ++i)
     if (s->dbuf[i]) (void)hipFree(s->dbuf[i]);
+  (void)hipEventDestroy(s->join_ev);
+  (void)hipStreamDestroy(s->xstream);
   (void)hipStreamDestroy(s->stream);
   delete s->pool;
   delete s;
@@ -166,6 +179,8 @@ int fedagg_session_set(fedagg_session* s, const char* key, long long value) {
   } else if (!strcmp(key, "chunk_bytes") && value >= (1 << 16)) {
     s->release_ring();
     s->chunk_bytes = (uint64_t)value;
+  } else if (!strcmp(key, "copy_streams") && (value == 1 || value == 2)) {
+    s->copy_streams = (int)value;
   } else if (!strcmp(key, "slots") && value >= 2 && value <= 1024) {
     s->release_ring();
     s->slots = (int)std::max<long long>(value, s->threads + 1);
@@ -259,6 +274,11 @@ int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes
   const uint64_t units = per_row * (uint64_t)K;
   const int R = (int)s->ring.size();
   Pool& pool = s->workers();
+  const bool two = s->copy_streams > 1 && units > 1;
+  if (two) {  // the second queue starts after everything already enqueued on the session stream
+    HIP_TRY(hipEventRecord(s->join_ev, s->stream));
+    HIP_TRY(hipStreamWaitEvent(s->xstream, s->join_ev, 0));
+  }
   std::vector<Done> done(units ? std::min<uint64_t>(units, (uint64_t)R) : 1);
   // In-order window: unit u lives in slot u % R.  R-1 packs run ahead of the copy being
   // enqueued; a slot is refilled only after the copy that read it completed, while the next
@@ -286,10 +306,15 @@ int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes
     const int k = (int)(u / per_row);
     const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
     char* dst = static_cast<char*>(d_dst) + (uint64_t)k * ld_bytes + a;
-    HIP_TRY(hipMemcpyAsync(dst, s->ring[slot], b - a, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(hipEventRecord(s->ring_ev[slot], s->stream));
+    hipStream_t q = (two && (u & 1)) ? s->xstream : s->stream;
+    HIP_TRY(hipMemcpyAsync(dst, s->ring[slot], b - a, hipMemcpyHostToDevice, q));
+    HIP_TRY(hipEventRecord(s->ring_ev[slot], q));
     s->ring_used[slot] = true;
     if (next_submit < units) submit(next_submit++);
+  }
+  if (two) {  // work enqueued on the session stream after this call sees every staged byte
+    HIP_TRY(hipEventRecord(s->join_ev, s->xstream));
+    HIP_TRY(hipStreamWaitEvent(s->stream, s->join_ev, 0));
   }
   s->last_stage_s = now_s() - t0;
   return FEDAGG_OK;

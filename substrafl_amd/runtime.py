@@ -56,6 +56,8 @@ class Session:
         self.stream = int(self.lib.fedagg_session_stream(self._h) or 0)
         nthreads = threads or int(os.environ.get("FEDAGG_PACK_THREADS", "0")) or min(16, os.cpu_count() or 1)
         self.set("threads", nthreads)
+        if os.environ.get("FEDAGG_COPY_STREAMS"):  # measurement switch: 1 or 2 H2D queues (default 2)
+            self.set("copy_streams", int(os.environ["FEDAGG_COPY_STREAMS"]))
 
     def close(self) -> None:
         if getattr(self, "_h", None):
