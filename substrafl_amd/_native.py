@@ -128,7 +128,7 @@ def ptr_array(ptrs) -> ctypes.Array:
 
 def tune(**knobs) -> None:
     """Set launch knobs of the library (``fedagg_tune``): grid_cap, nt_load, nt_store, vpt,
-    unroll, pipe, tile, fuse_pairwise, sc_vpt, sc_unroll, sc_split, xcd."""
+    unroll, pipe, tile, fuse_pairwise, sc_vpt, sc_unroll, sc_split, sc_bsplit, xcd."""
     lib = load()
     for k, v in knobs.items():
         check(lib.fedagg_tune(k.encode(), int(v)), f"fedagg_tune({k})")

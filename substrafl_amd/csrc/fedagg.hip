@@ -67,6 +67,7 @@ int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_sc_bsplit = 0;    // Scaffold: bucket-split workgroup pairs (delta / control variate per workgroup)
 int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand is fp32
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
 int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
@@ -896,6 +897,67 @@ __global__ void __launch_bounds__(FA_BLOCK)
   }
 }
 
+// Bucket-split variant (fedagg_tune "sc_bsplit"): workgroup pairs (2t, 2t+1) own the same tile,
+// the even one streams the K delta rows, the odd one the K control-variate rows (+ c).  A thread
+// then holds one bucket's loads and accumulators (half the registers of the fused walk), so the
+// launch can give a wave 8 KiB per stream like the FedAvg kernel, while both buckets stay in
+// flight chip-wide at once (unlike sc_split, which walks them one after the other per thread).
+// Same per-element arithmetic and order as scaffold_kernel.  Vector path only (16-B aligned
+// operands, nvec = M / L); the grid is even.
+template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU>
+__global__ void __launch_bounds__(FA_BLOCK)
+    scaffold_bsplit_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
+                           const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
+                           double* __restrict__ dout, double* __restrict__ cout) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+  __shared__ u32x4 stage[FA_BLOCK / 64][128];
+  u32x4* lds_wave = stage[threadIdx.x / 64];
+  const int ph = blockIdx.x & 1;
+  const uint64_t pairs = gridDim.x / 2, pb = blockIdx.x >> 1;
+  const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+  for (uint64_t t = pb; t * tile < nvec; t += pairs) {
+    const uint64_t base = t * tile + threadIdx.x;
+    const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
+    if (base + (VPT - 1) * FA_BLOCK < nvec) {
+      uint64_t v[VPT];
+#pragma unroll
+      for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+      if (ph == 0)
+        scaffold_phase<TIn, KC, NT, NTS, VPT, SU, 0>(a, pw, K, first, last, c, lr, v, dout, wave_full, lds_wave);
+      else
+        scaffold_phase<TIn, KC, NT, NTS, VPT, SU, 1>(a, pw, K, first, last, c, lr, v, cout, wave_full, lds_wave);
+    } else {
+      for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK) {
+        if (ph == 0)
+          scaffold_phase<TIn, KC, NT, NTS, 1, SU, 0>(a, pw, K, first, last, c, lr, &v0, dout, false, lds_wave);
+        else
+          scaffold_phase<TIn, KC, NT, NTS, 1, SU, 1>(a, pw, K, first, last, c, lr, &v0, cout, false, lds_wave);
+      }
+    }
+  }
+  // scalar remainder (M % L elements): the even workgroups, both buckets
+  if (ph) return;
+  for (uint64_t i = nvec * L + pb * FA_BLOCK + threadIdx.x; i < M; i += pairs * FA_BLOCK) {
+    double ad = first ? 0.0 : dout[i];
+    double ac = first ? 0.0 : cout[i];
+    for (int k = 0; k < K; ++k) {
+      const double pd = a.w[k] * (double)a.d[k][i];
+      const double pc = a.w[k] * (double)a.cv[k][i];
+      ad = ad + pd;
+      ac = ac + pc;
+    }
+    if (last) {
+      ac = ac + (double)c[i];
+      ad = lr * ad;
+    }
+    for (int p = 0; p < pw.n; ++p)
+      if (pw.idx[p] == i) scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, i, &ad, &ac);
+    dout[i] = ad;
+    cout[i] = ac;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Separate numel==1 path (K > one chunk, or more indices than fit the kernel arguments)
 // ------------------------------------------------------------------------------------
@@ -1553,6 +1615,32 @@ void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FED
 
 // Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
 
+template <typename TIn, int VPT, int SU>
+void launch_scaffold_bsplit_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
+                                    const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr,
+                                    uint64_t nvec, uint64_t M, double* dout, double* cout) {
+  hipLaunchKernelGGL((scaffold_bsplit_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, true, VPT, SU>), dim3(grid),
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+}
+
+// Bucket-split shapes (sc_vpt x sc_unroll); grid = 2 x the tile count (even).
+template <typename TIn>
+void launch_scaffold_bsplit(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
+                            const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
+                            uint64_t M, double* dout, double* cout, const int sv, const int su) {
+#define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
+  if (sv >= 8) {
+    if (su >= 4) return launch_scaffold_bsplit_variant<TIn, 8, 4>(SC_ARGS);
+    return launch_scaffold_bsplit_variant<TIn, 8, 2>(SC_ARGS);
+  }
+  if (sv >= 4) {
+    if (su >= 8) return launch_scaffold_bsplit_variant<TIn, 4, 8>(SC_ARGS);
+    return launch_scaffold_bsplit_variant<TIn, 4, 4>(SC_ARGS);
+  }
+  return launch_scaffold_bsplit_variant<TIn, 2, 8>(SC_ARGS);
+#undef SC_ARGS
+}
+
 template <typename TIn>
 void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
                      int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
@@ -1624,7 +1712,10 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   const int su = g_sc_vpt > 0 ? g_sc_unroll : (K >= 32 ? 2 : 4);
   const uint64_t per_thread = g_nt_load ? (uint64_t)sv : 1;
   unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
-  if (g_tpb > 1 && nvec)  // every tile exactly once: no grid cap with tpb
+  // bucket-split pairs: vector path with nt loads/stores only (the tail is in-kernel)
+  const bool bsplit = g_sc_bsplit && nvec && g_nt_load && g_nt_store != 0;
+  if (bsplit) grid *= 2;
+  else if (g_tpb > 1 && nvec)  // every tile exactly once: no grid cap with tpb
     grid = (unsigned)(((nvec + per_thread - 1) / per_thread + g_tpb - 1) / g_tpb);
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
     const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
@@ -1642,7 +1733,10 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0, last = (k0 + kc) == K;
-    launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+    if (bsplit)
+      launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+    else
+      launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     int rc = check_launch("scaffold_kernel");
     if (rc) return rc;
   }
@@ -1713,6 +1807,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value <= 0 ? 0 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
+  else if (!strcmp(key, "sc_bsplit")) g_sc_bsplit = value ? 1 : 0;
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
   else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
