@@ -67,6 +67,7 @@ int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_fa_occ = 0;       // FedAvg: register-capped occupancy variants (0: off; 2-4 with the 8/16-KiB shapes)
 int g_sc_bsplit = 0;    // Scaffold: bucket-split workgroup pairs (delta / control variate per workgroup)
 int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand is fp32
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
@@ -471,8 +472,10 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 // step; U clients per load group; PIPE software-pipelined client groups; TILE: a workgroup owns
 // VPT*256 CONTIGUOUS vectors per step (a wave reads VPT KiB contiguous per client) instead of
 // VPT grid-strided vectors.
-template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
-__global__ void __launch_bounds__(FA_BLOCK)
+// OCC (fedagg_tune "fa_occ"): minimum waves per SIMD the register allocation must allow
+// (amdgpu_waves_per_eu; 1 = no constraint beyond the launch bound).
+template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1>
+__global__ void __launch_bounds__(FA_BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
                   const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb) {
 #pragma clang fp contract(off)
@@ -1413,10 +1416,10 @@ inline unsigned grid_for(uint64_t work) {
   return (unsigned)g;
 }
 
-template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE>
+template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
-  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE>), dim3(grid), dim3(FA_BLOCK), 0,
+  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC>), dim3(grid), dim3(FA_BLOCK), 0,
                      s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb);
 }
 
@@ -1432,20 +1435,28 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
 struct Shape {
   int vpt, unroll;
   bool pipe;
+  int occ;  // > 1: the register-capped (amdgpu_waves_per_eu) build of the 8/16-KiB tile
 };
 template <typename E>
 inline Shape shape_for(int K, uint64_t nvec) {
-  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0};
+  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0, g_fa_occ};
   // fp64: the adds of a client group take long enough that the HBM idles unless the next
   // group's loads are already in flight (software-pipelined tiles: 8 x 25M fp64 6.0 vs 5.1 TB/s,
   // 64 x 62.5M 6.1 vs 4.9; profiles/r01_tune2_f64_*.log)
-  if constexpr (std::is_same<E, F64>::value) return Shape{4, 4, true};
+  if constexpr (std::is_same<E, F64>::value) return Shape{4, 4, true, 0};
   // many client streams over a large bucket: 16 KiB per wave per stream (fewer DRAM row
   // switches; 64 x 125M fp32 +2 %, 128 x 350M bf16 +1 %, 64 x 125M fp16 +1 %), as long as the
   // grid stays >> 256 CUs
-  if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) return Shape{16, 2, false};
-  if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false};  // 8 x 25M fp16: +5 % over 8 KiB
-  return Shape{8, 4, false};
+  if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) {
+    // bf16: single-client groups (128 x 350M: +0.4-1 % over pairs; profiles/r01_occ_c5.log);
+    // fp32: client pairs built for 2 waves per SIMD (247 VGPRs, no spill; the uncapped build
+    // takes 257 registers and runs 1 wave; 64 x 125M: -1.4 %, profiles/r01_occ_c3.log)
+    if constexpr (std::is_same<E, BF16>::value) return Shape{16, 1, false, g_fa_occ};
+    if constexpr (std::is_same<E, F32>::value) return Shape{16, 2, false, g_fa_occ > 1 ? g_fa_occ : 2};
+    return Shape{16, 2, false, g_fa_occ};
+  }
+  if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false, 0};  // 8 x 25M fp16: +5 % over 8 KiB
+  return Shape{8, 4, false, g_fa_occ};
 }
 
 template <typename E, bool NTS>
@@ -1457,6 +1468,18 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
     if (sh.pipe) {  // contiguous tiles with the next client group's loads issued before this group's adds
       if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
+    }
+    if constexpr (NTS && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
+      if (sh.occ > 1) {  // register-capped occupancy variants of the 8- and 16-KiB shapes
+        if (sh.vpt >= 16) {
+          if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 3>(FA_ARGS);
+          return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 2>(FA_ARGS);
+        }
+        if (sh.vpt >= 8 && sh.unroll > 2) {
+          if (sh.occ >= 4) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 4>(FA_ARGS);
+          return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 3>(FA_ARGS);
+        }
+      }
     }
     if (sh.vpt >= 16) {  // 16 KiB per wave per client stream
       if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true>(FA_ARGS);
@@ -1808,6 +1831,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
   else if (!strcmp(key, "sc_bsplit")) g_sc_bsplit = value ? 1 : 0;
+  else if (!strcmp(key, "fa_occ")) g_fa_occ = value <= 1 ? 0 : (value >= 4 ? 4 : (int)value);
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
   else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;

@@ -572,11 +572,38 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
         FedAvgPlan("f32", x, fedavg_weights(ns, "f32"), M, out, [0, 17, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append(out[:M].clone())
+    _native.tune(**default)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
+@pytest.mark.parametrize("kind", ["f32", "bf16"])
+@pytest.mark.parametrize("knobs", [dict(vpt=8, unroll=4, fa_occ=3), dict(vpt=8, unroll=4, fa_occ=4, grid_cap=3),
+                                   dict(vpt=16, unroll=2, fa_occ=2), dict(vpt=16, unroll=1, fa_occ=3),
+                                   dict(vpt=0, fa_occ=2)])
+def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
+    """Register-capped (amdgpu_waves_per_eu) builds of the 8/16-KiB shapes: same bits as the
+    default launch, for fp32 and bf16 inputs, with numel==1 patches and a ragged tail."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 13, 2_000_011
+    dt = torch.float32 if kind == "f32" else torch.bfloat16
+    x = torch.randn((K, M + 5), device="cuda").to(dt)
+    ns = list(range(7, 7 + K))
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0)
+    outs = []
+    for kn in (default, dict(default, **knobs)):
+        _native.tune(**kn)
+        out = torch.empty(M + 5, device="cuda")
+        FedAvgPlan(kind, x, fedavg_weights(ns, kind), M, out, [0, 9, M - 1]).launch()
         torch.cuda.synchronize()
         outs.append(out[:M].clone())
     _native.tune(**default)

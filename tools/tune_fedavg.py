@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--tpb", type=int, nargs="*", default=[2, 4, 8], help="auto shape with N consecutive tiles per block")
     ap.add_argument("--pads", type=int, nargs="*", default=[],
                     help="row-pitch paddings (elements) to time the auto shape with instead of the shape sweep")
+    ap.add_argument("--occ", action="store_true",
+                    help="register-capped occupancy variants (fa_occ 2-4) of the 8/16-KiB shapes beside the uncapped ones")
     ap.add_argument("--gridstride", action="store_true",
                     help="grid-strided and tile shapes under grid caps (the read probe's walk), next to the auto shape")
     args = ap.parse_args()
@@ -79,8 +81,12 @@ def main():
                                   median_us=round(m * 1e3, 2), GBps=round(nbytes / (m / 1e3) / 1e9, 1))))
         return
 
-    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1)
-    if args.gridstride:
+    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1, fa_occ=0)
+    if args.occ:
+        variants = [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_occ=o)
+                    for v, u, occs in ((8, 4, (0, 3, 4)), (16, 2, (0, 2)), (16, 1, (0, 3))) for o in occs]
+        variants.insert(0, dict(base, vpt=0, tile=1, nt_store=1))
+    elif args.gridstride:
         shapes = [dict(vpt=1, unroll=8), dict(vpt=1, unroll=4), dict(vpt=2, unroll=8), dict(vpt=1, unroll=8, pipe=1),
                   dict(vpt=1, unroll=16)]
         variants = [dict(base, vpt=0, tile=1, nt_store=1)]
