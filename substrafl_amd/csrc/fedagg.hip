@@ -67,6 +67,7 @@ int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+int g_buf = 0;          // FedAvg: buffer-descriptor client loads (8/16-KiB tiles, fp32/bf16)
 int g_fa_occ = 0;       // FedAvg: register-capped occupancy variants (0: off; 2-4 with the 8/16-KiB shapes)
 int g_sc_bsplit = 0;    // Scaffold: bucket-split workgroup pairs (delta / control variate per workgroup)
 int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand is fp32
@@ -376,22 +377,42 @@ __device__ __forceinline__ void fedavg_accumulate(const u32x4 (&raw)[N][U], cons
   }
 }
 
-template <typename E, int KC, bool NT, int N, int U>
+// BUF: raw buffer loads through one descriptor per client based at this workgroup's tile (byte
+// offset tb, scalar): every load addresses with the same 32-bit lane offset plus a scalar n*4 KiB,
+// instead of one 64-bit VGPR address per (client, vector).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* row, uint64_t tb) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(static_cast<const char*>(row)) + tb, 0, 0x7FFFFFFF,
+                                           0x00020000);
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16_buf(__amdgpu_buffer_rsrc_t r, int n) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(threadIdx.x * 16u), n * FA_BLOCK * 16, NT ? 2 : 0);
+}
+
+template <typename E, int KC, bool NT, int N, int U, bool BUF = false>
 __device__ __forceinline__ void fedavg_load_group(const FaArgs<E, KC>& a, int k, const uint64_t* v,
-                                                  u32x4 (&raw)[N][U]) {
+                                                  u32x4 (&raw)[N][U], uint64_t tb = 0) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+  for (int u = 0; u < U; ++u) {
+    if constexpr (BUF) {
+      const __amdgpu_buffer_rsrc_t r = tile_rsrc(a.x[k + u], tb);
 #pragma unroll
-    for (int n = 0; n < N; ++n) raw[n][u] = ld16<NT>(a.x[k + u] + v[n] * E::L);
+      for (int n = 0; n < N; ++n) raw[n][u] = ld16_buf<NT>(r, n);
+    } else {
+#pragma unroll
+      for (int n = 0; n < N; ++n) raw[n][u] = ld16<NT>(a.x[k + u] + v[n] * E::L);
+    }
+  }
 }
 
 // acc[n][:] = sum over the K clients (in order) for the N 16-byte vectors v[n].
 // PIPE: the loads of client group g+1 are issued before the adds of group g (two register
 // buffers), so a wave keeps 2*U*N loads in flight across the add chain.
-template <typename E, int KC, bool NT, int N, int U, bool PIPE>
+template <typename E, int KC, bool NT, int N, int U, bool PIPE, bool BUF = false>
 __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int K, const int first,
                                                const uint64_t* v, typename E::P (*acc)[E::L],
-                                               const typename E::Out* out) {
+                                               const typename E::Out* out, const uint64_t tb = 0) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
@@ -425,7 +446,7 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
   } else {
     for (; k + U <= K; k += U) {
       u32x4 raw[N][U];
-      fedavg_load_group<E, KC, NT, N, U>(a, k, v, raw);
+      fedavg_load_group<E, KC, NT, N, U, BUF>(a, k, v, raw, tb);
       fedavg_accumulate<E, N, U>(raw, a.w + k, acc);
     }
   }
@@ -434,7 +455,8 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       P xs[L];
-      E::unpack(ld16<NT>(a.x[k] + v[n] * L), xs);
+      if constexpr (BUF) E::unpack(ld16_buf<NT>(tile_rsrc(a.x[k], tb), n), xs);
+      else E::unpack(ld16<NT>(a.x[k] + v[n] * L), xs);
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const P p = xs[j] * w;
@@ -474,7 +496,7 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 // VPT grid-strided vectors.
 // OCC (fedagg_tune "fa_occ"): minimum waves per SIMD the register allocation must allow
 // (amdgpu_waves_per_eu; 1 = no constraint beyond the launch bound).
-template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1>
+template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false>
 __global__ void __launch_bounds__(FA_BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
                   const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb) {
@@ -499,7 +521,7 @@ __global__ void __launch_bounds__(FA_BLOCK) __attribute__((amdgpu_waves_per_eu(O
 #pragma unroll
         for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
         P acc[VPT][L];
-        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, acc, out);
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE, BUF>(a, K, first, v, acc, out, t * tile * 16);
         if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
 #pragma unroll
         for (int n = 0; n < VPT; ++n) store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
@@ -1416,10 +1438,11 @@ inline unsigned grid_for(uint64_t work) {
   return (unsigned)g;
 }
 
-template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1>
+template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
-  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC>), dim3(grid), dim3(FA_BLOCK), 0,
+  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF>), dim3(grid),
+                     dim3(FA_BLOCK), 0,
                      s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb);
 }
 
@@ -1436,10 +1459,11 @@ struct Shape {
   int vpt, unroll;
   bool pipe;
   int occ;  // > 1: the register-capped (amdgpu_waves_per_eu) build of the 8/16-KiB tile
+  bool buf;  // buffer-descriptor client loads
 };
 template <typename E>
 inline Shape shape_for(int K, uint64_t nvec) {
-  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0, g_fa_occ};
+  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0, g_fa_occ, g_buf != 0};
   // fp64: the adds of a client group take long enough that the HBM idles unless the next
   // group's loads are already in flight (software-pipelined tiles: 8 x 25M fp64 6.0 vs 5.1 TB/s,
   // 64 x 62.5M 6.1 vs 4.9; profiles/r01_tune2_f64_*.log)
@@ -1448,15 +1472,16 @@ inline Shape shape_for(int K, uint64_t nvec) {
   // switches; 64 x 125M fp32 +2 %, 128 x 350M bf16 +1 %, 64 x 125M fp16 +1 %), as long as the
   // grid stays >> 256 CUs
   if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) {
-    // bf16: single-client groups (128 x 350M: +0.4-1 % over pairs; profiles/r01_occ_c5.log);
+    // bf16: client pairs with buffer-descriptor loads (128 x 350M: 12.64 vs 12.96 ms with global
+    // loads, 64 x 125M: -7.7 %; profiles/r01_buf2_*.log; slower for fp32, r01_buf_c{2,3}.log);
     // fp32: client pairs built for 2 waves per SIMD (247 VGPRs, no spill; the uncapped build
     // takes 257 registers and runs 1 wave; 64 x 125M: -1.4 %, profiles/r01_occ_c3.log)
-    if constexpr (std::is_same<E, BF16>::value) return Shape{16, 1, false, g_fa_occ};
-    if constexpr (std::is_same<E, F32>::value) return Shape{16, 2, false, g_fa_occ > 1 ? g_fa_occ : 2};
-    return Shape{16, 2, false, g_fa_occ};
+    if constexpr (std::is_same<E, BF16>::value) return Shape{16, 2, false, g_fa_occ, true};
+    if constexpr (std::is_same<E, F32>::value) return Shape{16, 2, false, g_fa_occ > 1 ? g_fa_occ : 2, false};
+    return Shape{16, 2, false, g_fa_occ, false};
   }
   if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false, 0};  // 8 x 25M fp16: +5 % over 8 KiB
-  return Shape{8, 4, false, g_fa_occ};
+  return Shape{8, 4, false, g_fa_occ, g_buf != 0};
 }
 
 template <typename E, bool NTS>
@@ -1470,9 +1495,27 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
       return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
     }
     if constexpr (NTS && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
+      if (sh.buf && !sh.pipe) {  // buffer-descriptor loads (one lane offset for every client stream)
+        if (sh.vpt >= 16) {
+          if (sh.unroll <= 1) {
+            if (sh.occ > 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 2, true>(FA_ARGS);
+            return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 1, true>(FA_ARGS);
+          }
+          if (sh.occ > 1) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 2, true>(FA_ARGS);
+          return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, true>(FA_ARGS);
+        }
+        if (sh.vpt >= 8 && sh.unroll > 2) {
+          if (sh.occ >= 4) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 4, true>(FA_ARGS);
+          if (sh.occ == 3) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 3, true>(FA_ARGS);
+          return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 1, true>(FA_ARGS);
+        }
+      }
       if (sh.occ > 1) {  // register-capped occupancy variants of the 8- and 16-KiB shapes
         if (sh.vpt >= 16) {
-          if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 3>(FA_ARGS);
+          if (sh.unroll <= 1) {
+            if (sh.occ <= 2) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 2>(FA_ARGS);
+            return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 3>(FA_ARGS);
+          }
           return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 2>(FA_ARGS);
         }
         if (sh.vpt >= 8 && sh.unroll > 2) {
@@ -1831,6 +1874,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
   else if (!strcmp(key, "sc_bsplit")) g_sc_bsplit = value ? 1 : 0;
+  else if (!strcmp(key, "buf")) g_buf = value ? 1 : 0;
   else if (!strcmp(key, "fa_occ")) g_fa_occ = value <= 1 ? 0 : (value >= 4 ? 4 : (int)value);
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;

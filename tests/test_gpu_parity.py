@@ -572,7 +572,7 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
@@ -586,7 +586,10 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
 @pytest.mark.parametrize("kind", ["f32", "bf16"])
 @pytest.mark.parametrize("knobs", [dict(vpt=8, unroll=4, fa_occ=3), dict(vpt=8, unroll=4, fa_occ=4, grid_cap=3),
                                    dict(vpt=16, unroll=2, fa_occ=2), dict(vpt=16, unroll=1, fa_occ=3),
-                                   dict(vpt=0, fa_occ=2)])
+                                   dict(vpt=0, fa_occ=2), dict(vpt=0, buf=1), dict(vpt=8, unroll=4, buf=1),
+                                   dict(vpt=8, unroll=4, fa_occ=3, buf=1, grid_cap=5), dict(vpt=16, unroll=2, buf=1),
+                                   dict(vpt=16, unroll=2, fa_occ=2, buf=1), dict(vpt=16, unroll=1, buf=1),
+                                   dict(vpt=16, unroll=1, fa_occ=2, buf=1, grid_cap=3)])
 def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     """Register-capped (amdgpu_waves_per_eu) builds of the 8/16-KiB shapes: same bits as the
     default launch, for fp32 and bf16 inputs, with numel==1 patches and a ragged tail."""
@@ -598,7 +601,7 @@ def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     dt = torch.float32 if kind == "f32" else torch.bfloat16
     x = torch.randn((K, M + 5), device="cuda").to(dt)
     ns = list(range(7, 7 + K))
-    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0)
     outs = []
     for kn in (default, dict(default, **knobs)):
         _native.tune(**kn)
@@ -635,6 +638,36 @@ def test_auto_shape_many_clients_bit_identical(torch_gpu):
     acc = np.zeros(idx.size, np.float32)
     for k in range(K):
         acc = (acc + (xs[k] * w[k]).astype(np.float32)).astype(np.float32)
+    assert np.array_equal(acc.view(np.uint32), outs[0][torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint32))
+    del x
+
+
+def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
+    """bf16 from 32 clients over a large bucket: the auto shape (16-KiB tiles, client pairs,
+    buffer-descriptor loads) against the 8-KiB global-load shape and the oracle order (exact
+    upcast, fp32 products and client-order sums, N8)."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 34, 16 * 256 * 2048 * 8 + 45  # bf16: 8 elements per 16-B vector; just past the threshold
+    x = torch.randn((K, M + 3), device="cuda").to(torch.bfloat16)
+    ns = list(range(50, 50 + K))
+    w = fedavg_weights(ns, "bf16")
+    outs = []
+    for kn in (dict(vpt=0, buf=0), dict(vpt=8, unroll=4, buf=0)):
+        _native.tune(**kn)
+        out = torch.empty(M + 3, device="cuda")
+        FedAvgPlan("bf16", x, w, M, out, [2, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append(out[:M].clone())
+    _native.tune(vpt=0, unroll=8)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    idx = np.array([0, 1, 8191, 16 * 256 * 8 * 5 + 7, M // 3, M - 40, M - 2])
+    xs = x[:, torch.from_numpy(idx).cuda()].float().cpu().numpy()
+    acc = np.zeros(idx.size, np.float32)
+    for k in range(K):
+        acc = (acc + (xs[k] * np.float32(w[k])).astype(np.float32)).astype(np.float32)
     assert np.array_equal(acc.view(np.uint32), outs[0][torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint32))
     del x
 
