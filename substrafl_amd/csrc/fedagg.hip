@@ -69,6 +69,7 @@ int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an expl
 int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
 int g_buf = 0;          // FedAvg: buffer-descriptor client loads (8/16-KiB tiles, fp32/bf16)
 int g_fa_occ = 0;       // FedAvg: register-capped occupancy variants (0: off; 2-4 with the 8/16-KiB shapes)
+int g_sc_buf = 0;       // Scaffold: buffer-descriptor client loads (fp32 inputs, 4- and 8-vector tiles)
 int g_sc_bsplit = 0;    // Scaffold: bucket-split workgroup pairs (delta / control variate per workgroup)
 int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand is fp32
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
@@ -603,17 +604,27 @@ __device__ __forceinline__ void scaffold_pairwise_elem(const ScArgs<TIn, KC>& a,
 }
 
 // Loads of one group of SU clients, both buckets, for the N vectors v[].
-template <typename TIn, int KC, bool NT, int N, int SU>
+template <typename TIn, int KC, bool NT, int N, int SU, bool BUF = false>
 __device__ __forceinline__ void scaffold_load_group(const ScArgs<TIn, KC>& a, const int k, const uint64_t* v,
-                                                    u32x4 (&rd)[N][SU], u32x4 (&rc)[N][SU]) {
+                                                    u32x4 (&rd)[N][SU], u32x4 (&rc)[N][SU], uint64_t tb = 0) {
   constexpr int L = 16 / sizeof(TIn);
 #pragma unroll
-  for (int u = 0; u < SU; ++u)
+  for (int u = 0; u < SU; ++u) {
+    if constexpr (BUF) {  // buffer descriptors based at the tile (see fedavg_load_group)
+      const __amdgpu_buffer_rsrc_t r_d = tile_rsrc(a.d[k + u], tb), r_c = tile_rsrc(a.cv[k + u], tb);
 #pragma unroll
-    for (int n = 0; n < N; ++n) {
-      rd[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
-      rc[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+      for (int n = 0; n < N; ++n) {
+        rd[n][u] = ld16_buf<NT>(r_d, n);
+        rc[n][u] = ld16_buf<NT>(r_c, n);
+      }
+    } else {
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        rd[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
+        rc[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+      }
     }
+  }
 }
 
 // fp64 products and in-order adds of one loaded group (scaffold.py:262,293: w_k * x_k summed in
@@ -645,11 +656,12 @@ __device__ __forceinline__ void scaffold_accumulate(const u32x4 (&rd)[N][SU], co
 
 // N 16-byte vectors of both buckets: in-order fp64 sums over the K clients, then (last chunk)
 // + c and * lr, the fused numel==1 patch, and the fp64 stores.  PIPE: software-pipelined groups.
-template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, bool PIPE = false>
+template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, bool PIPE = false, bool BUF = false>
 __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                  const int first, const int last, const TIn* __restrict__ c,
                                                  const double lr, const uint64_t* v, double* __restrict__ dout,
-                                                 double* __restrict__ cout, bool wave_full, u32x4* lds_wave) {
+                                                 double* __restrict__ cout, bool wave_full, u32x4* lds_wave,
+                                                 const uint64_t tb = 0) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
   double ad[N][L], ac[N][L];
@@ -683,7 +695,7 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
   } else {
     for (; k + SU <= K; k += SU) {
       u32x4 rd[N][SU], rc[N][SU];
-      scaffold_load_group<TIn, KC, NT, N, SU>(a, k, v, rd, rc);
+      scaffold_load_group<TIn, KC, NT, N, SU, BUF>(a, k, v, rd, rc, tb);
       scaffold_accumulate<TIn, N, SU>(rd, rc, a.w + k, ad, ac);
     }
   }
@@ -692,8 +704,13 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       double xd[L], xc[L];
-      unpack_d<TIn>(ld16<NT>(a.d[k] + v[n] * L), xd);
-      unpack_d<TIn>(ld16<NT>(a.cv[k] + v[n] * L), xc);
+      if constexpr (BUF) {
+        unpack_d<TIn>(ld16_buf<NT>(tile_rsrc(a.d[k], tb), n), xd);
+        unpack_d<TIn>(ld16_buf<NT>(tile_rsrc(a.cv[k], tb), n), xc);
+      } else {
+        unpack_d<TIn>(ld16<NT>(a.d[k] + v[n] * L), xd);
+        unpack_d<TIn>(ld16<NT>(a.cv[k] + v[n] * L), xc);
+      }
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const double pd = w * xd[j];
@@ -871,7 +888,7 @@ __device__ __forceinline__ void scaffold_vectors_split(const ScArgs<TIn, KC>& a,
 }
 
 // Same tiling as fedavg_kernel: a workgroup step covers VPT*256 contiguous vectors.
-template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, bool PIPE = false>
+template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, bool PIPE = false, bool BUF = false>
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
@@ -895,8 +912,8 @@ __global__ void __launch_bounds__(FA_BLOCK)
         scaffold_vectors_split<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
                                                            lds_wave);
       else
-        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU, PIPE>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
-                                                           lds_wave);
+        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU, PIPE, BUF>(a, pw, K, first, last, c, lr, v, dout, cout,
+                                                                wave_full, lds_wave, t * tile * 16);
     } else {
       for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
         scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout, false, lds_wave);
@@ -1671,11 +1688,11 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
   return FEDAGG_OK;
 }
 
-template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false>
+template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false, bool BUF = false>
 void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
                              uint64_t M, double* dout, double* cout) {
-  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT, PIPE>), dim3(grid),
+  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT, PIPE, BUF>), dim3(grid),
                      dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd, g_tpb);
 }
 
@@ -1714,6 +1731,16 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
 #define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
   const bool nts = g_nt_store != 0;
   if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
+  if (g_sc_buf && nts && !g_sc_split && !g_sc_pipe && sizeof(TIn) == 4) {  // buffer-descriptor loads
+    if (sv >= 8) {
+      if (su >= 4) return launch_scaffold_variant<TIn, true, true, 8, 4, false, false, true>(SC_ARGS);
+      return launch_scaffold_variant<TIn, true, true, 8, 2, false, false, true>(SC_ARGS);
+    }
+    if (sv >= 4) {
+      if (su <= 2) return launch_scaffold_variant<TIn, true, true, 4, 2, false, false, true>(SC_ARGS);
+      return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, true>(SC_ARGS);
+    }
+  }
   if (g_sc_pipe && nts && !g_sc_split) {  // software-pipelined client groups
     if (sv >= 4) return launch_scaffold_variant<TIn, true, true, 4, 2, false, true>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, true, 2, 4, false, true>(SC_ARGS);
@@ -1873,6 +1900,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value <= 0 ? 0 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
+  else if (!strcmp(key, "sc_buf")) g_sc_buf = value ? 1 : 0;
   else if (!strcmp(key, "sc_bsplit")) g_sc_bsplit = value ? 1 : 0;
   else if (!strcmp(key, "buf")) g_buf = value ? 1 : 0;
   else if (!strcmp(key, "fa_occ")) g_fa_occ = value <= 1 ? 0 : (value >= 4 ? 4 : (int)value);

@@ -684,7 +684,9 @@ def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
                                    dict(sc_bsplit=1), dict(sc_bsplit=1, sc_vpt=8, sc_unroll=4),
                                    dict(sc_bsplit=1, sc_vpt=8, sc_unroll=2, grid_cap=3),
                                    dict(sc_bsplit=1, sc_vpt=4, sc_unroll=8), dict(sc_bsplit=1, sc_vpt=2, sc_unroll=8),
-                                   dict(sc_bsplit=1, nt_store=0)])
+                                   dict(sc_bsplit=1, nt_store=0), dict(sc_buf=1), dict(sc_buf=1, sc_vpt=4, sc_unroll=2),
+                                   dict(sc_buf=1, sc_vpt=8, sc_unroll=2, grid_cap=3), dict(sc_buf=1, sc_vpt=8, sc_unroll=4),
+                                   dict(sc_buf=1, sc_vpt=2), dict(sc_buf=1, nt_store=0)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -695,8 +697,8 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     cv = torch.randn((K, M + 1), device="cuda")
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
-    default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_bsplit=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0, xcd=0,
-                   tpb=1)
+    default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_bsplit=0, sc_buf=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0,
+                   xcd=0, tpb=1)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)

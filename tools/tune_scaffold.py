@@ -44,7 +44,9 @@ def main():
                  for t in (2, 4, 8)]
     variants += [dict(sc_split=0, sc_pipe=0, sc_bsplit=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
                  for v, u in ((8, 4), (8, 2), (4, 4), (4, 8), (2, 8))]
-    variants = [dict(dict(tpb=1, sc_bsplit=0), **v) for v in variants]
+    variants += [dict(sc_split=0, sc_pipe=0, sc_buf=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
+                 for v, u in ((4, 4), (4, 2), (8, 2), (8, 4))]
+    variants = [dict(dict(tpb=1, sc_bsplit=0, sc_buf=0), **v) for v in variants]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {i: [] for i in range(len(variants))}
     for _ in range(args.rounds):
