@@ -1727,11 +1727,11 @@ void launch_scaffold_bsplit(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDA
 template <typename TIn>
 void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
                      int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
-                     double* cout, const int sv, const int su) {
+                     double* cout, const int sv, const int su, const bool buf) {
 #define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
   const bool nts = g_nt_store != 0;
   if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
-  if (g_sc_buf && nts && !g_sc_split && !g_sc_pipe && sizeof(TIn) == 4) {  // buffer-descriptor loads
+  if (buf && nts && !g_sc_split && !g_sc_pipe && sizeof(TIn) == 4) {  // buffer-descriptor loads
     if (sv >= 8) {
       if (su >= 4) return launch_scaffold_variant<TIn, true, true, 8, 4, false, false, true>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, true, 8, 2, false, false, true>(SC_ARGS);
@@ -1799,10 +1799,14 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "scaffold: workspace needed for %lld pairwise segments", P);
   constexpr int L = 16 / sizeof(TIn);
   const uint64_t nvec = vec ? M / L : 0;
-  // launch shape: 8 vectors x 2-client groups from 32 clients on (64 x 25M: 6.69 vs 6.28 TB/s),
-  // 4 x 4 below (16 x 25M: 6.23 vs 6.16); profiles/r01_tune3_*.log
-  const int sv = g_sc_vpt > 0 ? g_sc_vpt : (K >= 32 ? 8 : 4);
-  const int su = g_sc_vpt > 0 ? g_sc_unroll : (K >= 32 ? 2 : 4);
+  // launch shape: from 32 clients on (fp32 inputs), 8 vectors x 4-client groups over buffer
+  // descriptors (252 VGPRs, 2 waves/SIMD; 64 x 25M 2.00 vs 2.04 ms for 8 x 2 global loads,
+  // 48 x 12M 763 vs > 789 us, 32 x 25M 1.113 vs 1.120 ms; profiles/r01_scbuf2_*.log), 4 x 4 global
+  // loads below (16 x 25M: 6.23 vs 6.16 TB/s for 8 x 2; profiles/r01_tune3_*.log)
+  const bool wide = K >= 32;
+  const int sv = g_sc_vpt > 0 ? g_sc_vpt : (wide ? 8 : 4);
+  const int su = g_sc_vpt > 0 ? g_sc_unroll : (wide ? (sizeof(TIn) == 4 ? 4 : 2) : 4);
+  const bool buf = g_sc_vpt > 0 ? g_sc_buf != 0 : (wide && sizeof(TIn) == 4);
   const uint64_t per_thread = g_nt_load ? (uint64_t)sv : 1;
   unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   // bucket-split pairs: vector path with nt loads/stores only (the tail is in-kernel)
@@ -1829,7 +1833,7 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
     if (bsplit)
       launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     else
-      launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+      launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, buf);
     int rc = check_launch("scaffold_kernel");
     if (rc) return rc;
   }

@@ -727,6 +727,33 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
         assert _bits(rc[0].reshape(-1)[0]) == _bits(outs[0][1][i].cpu().numpy())
 
 
+@pytest.mark.parametrize("K", [32, 40, 70])
+def test_scaffold_auto_shape_many_clients_bit_identical(torch_gpu, K):
+    """From 32 clients the Scaffold auto shape is 8 x 4 over buffer descriptors (two launch chunks
+    at 70); it must agree bit for bit with the 4 x 4 global-load shape."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import ScaffoldPlan, scaffold_weights
+
+    M = 1_000_003
+    d = torch.randn((K, M + 1), device="cuda")
+    cv = torch.randn((K, M + 1), device="cuda")
+    c = torch.randn(M + 1, device="cuda")
+    w = scaffold_weights(list(range(9, 9 + K)))
+    outs = []
+    for kn in (dict(sc_vpt=0), dict(sc_vpt=4, sc_unroll=4, sc_buf=0)):
+        _native.tune(**kn)
+        do = torch.empty(M + 1, dtype=torch.float64, device="cuda")
+        co = torch.empty(M + 1, dtype=torch.float64, device="cuda")
+        ScaffoldPlan("f32", [d[k].data_ptr() for k in range(K)], [cv[k].data_ptr() for k in range(K)], c, w, M, 0.7,
+                     do, co, [1, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append((do[:M].clone(), co[:M].clone()))
+    _native.tune(sc_vpt=0, sc_unroll=4, sc_buf=0)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+
+
 def test_golden_fedpca(golden, torch_gpu, dummy_algo_class):
     """FedPCA average (bit-exact, same kernel as FedAvg) and the QR variant (fed_pca.py:210-299)."""
     from substrafl_amd.schemas import FedPCASharedState
