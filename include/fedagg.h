@@ -58,6 +58,13 @@ const char* fedagg_last_error(void);
  *   "sc_pipe"       Scaffold: software-pipelined client groups (0/1)
  *   "sc_unroll"     Scaffold: clients per load group (2/4/8)
  *   "sc_split"      Scaffold: 1 = stream all delta vectors, then all control-variate vectors
+ *   "sc_bsplit"     Scaffold: 1 = workgroup pairs, one streams the delta rows, one the control variates
+ *   "sc_buf"        Scaffold: buffer-descriptor client loads with an explicit sc_vpt (auto: from 32
+ *                   fp32 clients)
+ *   "fa_occ"        FedAvg: 2-4 = register-capped (waves per SIMD) build of the 8/16-KiB tiles
+ *                   (auto: 2 for fp32 from 32 clients)
+ *   "buf"           FedAvg: buffer-descriptor client loads with an explicit vpt (auto: bf16 from
+ *                   32 clients)
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);
 
