@@ -1497,7 +1497,7 @@ inline Shape shape_for(int K, uint64_t nvec) {
     if constexpr (std::is_same<E, F32>::value) return Shape{16, 2, false, g_fa_occ > 1 ? g_fa_occ : 2, false};
     return Shape{16, 2, false, g_fa_occ, false};
   }
-  if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false, 0};  // 8 x 25M fp16: +5 % over 8 KiB
+  if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false, 0, g_buf != 0};  // 8 x 25M: +5 % over 8 KiB
   return Shape{8, 4, false, g_fa_occ, g_buf != 0};
 }
 
@@ -1510,6 +1510,16 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
     if (sh.pipe) {  // contiguous tiles with the next client group's loads issued before this group's adds
       if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
+    }
+    if constexpr (NTS && std::is_same<E, F16>::value) {
+      if (sh.buf && !sh.pipe) {  // fp16: buffer-descriptor loads, uncapped builds only
+        if (sh.vpt >= 16) {
+          if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 1, true>(FA_ARGS);
+          return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, true>(FA_ARGS);
+        }
+        if (sh.vpt >= 8 && sh.unroll > 2) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 1, true>(FA_ARGS);
+        if (sh.vpt >= 4 && sh.unroll >= 4) return launch_fedavg_variant<E, true, NTS, 4, 4, false, true, 1, true>(FA_ARGS);
+      }
     }
     if constexpr (NTS && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
       if (sh.buf && !sh.pipe) {  // buffer-descriptor loads (one lane offset for every client stream)

@@ -613,6 +613,30 @@ def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
 
 
+@pytest.mark.parametrize("knobs", [dict(vpt=0, buf=1), dict(vpt=4, unroll=4, buf=1), dict(vpt=8, unroll=4, buf=1),
+                                   dict(vpt=16, unroll=2, buf=1, grid_cap=3), dict(vpt=16, unroll=1, buf=1)])
+def test_fp16_buffer_load_variants_bit_identical(torch_gpu, knobs):
+    """fp16 FedAvg (fp16 products and sums, N4) over buffer-descriptor loads: same bits as the
+    default global-load launch, numel==1 patches and a ragged tail included."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 11, 1_500_013
+    x = torch.randn((K, M + 5), device="cuda").to(torch.float16)
+    ns = list(range(20, 20 + K))
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0)
+    outs = []
+    for kn in (default, dict(default, **knobs)):
+        _native.tune(**kn)
+        out = torch.empty(M + 5, device="cuda", dtype=torch.float16)
+        FedAvgPlan("f16", x, fedavg_weights(ns, "f16"), M, out, [4, M - 1]).launch()
+        torch.cuda.synchronize()
+        outs.append(out[:M].clone())
+    _native.tune(**default)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
 def test_auto_shape_many_clients_bit_identical(torch_gpu):
     """K >= 32 over a large bucket picks the 16-KiB-per-stream shape (shape_for); it must agree
     bit for bit with the 8-KiB shape and with the oracle order on sampled elements."""
