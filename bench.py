@@ -2,24 +2,38 @@
 """Device-resident aggregation throughput (BASELINE.json metric:
 "aggregated-param GB/s (device-resident) FedAvg reduce, N clients x M params").
 
-One step = one pass of the hot path (the FedAvg bucket kernel + the numel == 1 pairwise
-patch) over one batch of synthetic client buckets already resident in HBM.  Default workload
-is BASELINE.json configs[1]: FedAvg, 8 clients x 25M fp32 params on one MI355X.
+One step = one pass of the hot path over one batch of synthetic client buckets already resident
+in HBM.  The default workload is BASELINE.json configs[2] on one MI355X: FedAvg, 64 clients x
+125M fp32 params (C3) -- the configuration north_star's ">= 80 % of the single-GPU HBM-read
+roofline" target is stated on.
 
-N > 1 (torchrun, one process per GPU): the buckets are sharded by PARAMETER RANGE (SURVEY.md
-§8(e) primary mode): every rank owns its own 25M-param slice of an N x 25M-param model for all
-8 clients, so there is no data-path collective and results are bit-identical to one GPU
-(weak scaling).  value = algorithmic bytes of all ranks / max-over-ranks time.
+Multi-GPU (one process per GPU).  ``--gpus N`` from a plain ``python3 bench.py`` starts the N rank
+processes itself (before anything touches a GPU); under torchrun the ranks come from the
+environment, and a WORLD_SIZE that differs from --gpus is an error.  Modes:
 
-Algorithmic bytes: FedAvg K*M*s_in + M*s_out; Scaffold
-2*K*M*s_in + M*s_in + 2*M*8.
+* ``--mode param-range`` (default; SURVEY.md §8(e) primary, bit-exact): every rank reduces its own
+  parameter range of all K clients -- no data-path collective.  ``--scaling weak`` (default): each
+  rank owns a full M-param slice of an N*M-param model; ``--scaling strong``: the workload's own M
+  is split over the N ranks (C3 at 64 x 125M over 8 GPUs = 15.6M params per GPU).
+* ``--mode client-shard --combine relay|rccl|ordered`` (the north-star mode): the K clients are
+  split over the ranks, partial sums stay in HBM and are combined over RCCL/xGMI on the root
+  (``relay`` bit-exact; see substrafl_amd/sharding.py).  Needs one GPU per rank.
+* ``--engine multi-device``: the drop-in's own multi-GPU path, ONE process driving N GPUs
+  (MultiDeviceEngine: host buckets staged over each GPU's PCIe link, per-shard kernel time from
+  HIP events on the session streams) -- an end-to-end line, not the device-resident metric.
+
+value = algorithmic bytes of the whole job / max-over-ranks time.  Algorithmic bytes (SURVEY.md
+§8(d)): FedAvg K*M*s_in + M*s_out; Scaffold 2*K*M*s_in + M*s_in + 2*M*8.
 """
 
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -44,50 +58,145 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--mode", default="param-range", choices=["param-range", "client-shard"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered"])
+    ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--grid-cap", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1)
     ap.add_argument("--traffic", default="", help="JSON with PMC-derived bytes per launch (profiles/)")
+    ap.add_argument("--rehearse-cpu", action="store_true",
+                    help="tests only: run the launcher / rank / timing plumbing with no GPU (no measurement)")
     return ap.parse_args()
 
 
-def synth_clients(torch, K, ld, M, kind, device, rank):
-    """Client k's bucket: N(0,1) from torch's device Philox stream seeded 20241016 + k (+rank salt)."""
+# ======================================================================================
+# launcher: --gpus N from a plain `python3 bench.py`
+# ======================================================================================
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """Start ranks 0..n-1 of this very command as child processes (torchrun's environment
+    contract: RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT), before any GPU call in this
+    process; wait for all of them and return the first failure's code (0 if all succeeded).
+    A failed rank takes the others down (exact PIDs, no pattern kill)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            alive.discard(r)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for o in alive:
+                    procs[o].terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ======================================================================================
+# synthetic device-resident buckets
+# ======================================================================================
+def synth_clients(torch, K, ld, M, kind, device, seed0):
+    """Client k's bucket: N(0,1) from torch's device Philox stream seeded seed0 + k."""
     dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}[kind]
-    buf = torch.empty((K, ld), dtype=dt, device=device)
+    buf = torch.empty((max(1, K), ld), dtype=dt, device=device)
     g = torch.Generator(device=device)
     for k in range(K):
-        g.manual_seed(20241016 + k + 1_000_003 * rank)
+        g.manual_seed(seed0 + k)
         if kind == "bf16":
             buf[k, :M].copy_(torch.randn(M, generator=g, device=device, dtype=torch.float32))
         else:
             buf[k, :M].normal_(generator=g)
         buf[k, M:].zero_()
-    return buf
+    return buf[:K]
 
 
+def lib_sha256() -> str:
+    p = ROOT / "substrafl_amd" / "libfedagg.so"
+    return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else ""
+
+
+def read_traffic(args, sha):
+    """PMC-derived HBM bytes per launch from a rocprofv3 --pmc session (tools/pmc_traffic.py),
+    with its source file and whether it was collected on this very build of libfedagg.so."""
+    tpath = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_{args.workload}.json"
+    if not tpath.exists():
+        return None, None
+    try:
+        tj = json.loads(tpath.read_text())
+    except Exception:  # noqa: BLE001
+        return None, None
+    src = {"file": str(tpath.relative_to(ROOT)) if tpath.is_relative_to(ROOT) else str(tpath),
+           "lib_sha256": tj.get("lib_sha256"), "same_build": tj.get("lib_sha256") == sha,
+           "collected": tj.get("collected", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes")}
+    return tj.get("hbm_bytes_per_launch"), src
+
+
+# ======================================================================================
+# the rank path (device-resident metric)
+# ======================================================================================
 def main():
     args = parse()
+    if args.engine == "multi-device":
+        return multi_device_bench(args)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report a mislabelled line",
+              file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if args.rehearse_cpu:
+        return rehearse(args, world, rank)
+
     import torch
     import torch.distributed as dist
 
     from substrafl_amd import _native
     from substrafl_amd.engine import FedAvgPlan, ScaffoldPlan, fedavg_weights, scaffold_weights
     from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+    from substrafl_amd.sharding import (DistTransport, FedAvgShard, GpuShardOps, ScaffoldShard, block_of,
+                                        client_blocks, client_shard_fedavg, client_shard_scaffold, shard_bounds)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # Parameter-range sharding has no data-path collective: the process group only carries
-        # the barrier and the max-over-ranks timing, on the host (gloo).
-        dist.init_process_group("gloo")
     ndev = torch.cuda.device_count()
-    local = local % max(1, ndev)  # lets a 1-GPU box rehearse N > 1 (ranks then share the GPU)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if ndev == 0:
+        print("bench.py: no GPU visible", file=sys.stderr)
+        sys.exit(3)
+    client_shard = args.mode == "client-shard"
+    if client_shard and world > ndev:
+        print(f"bench.py: --mode client-shard needs one GPU per rank (RCCL); {world} ranks, {ndev} GPUs",
+              file=sys.stderr)
+        sys.exit(2)
+    dev_index = local % ndev  # param-range: a 1-GPU box can rehearse N > 1 (the ranks share the GPU)
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    if world > 1:
+        if client_shard:  # the exchange is RCCL over xGMI
+            dist.init_process_group("nccl", device_id=device)
+        else:  # parameter ranges need no data-path collective: barrier + max-over-ranks only
+            dist.init_process_group("gloo")
     lib = _native.load()
     if args.grid_cap:
         _native.tune(grid_cap=args.grid_cap)
@@ -95,145 +204,165 @@ def main():
         _native.tune(nt_load=args.nontemporal)
 
     wl = WORKLOADS[args.workload]
-    K, M, kind = wl["K"], wl["M"], wl["kind"]
-    shapes = synthetic_state_dict_shapes(M)
+    K, M_glob, kind = wl["K"], wl["M"], wl["kind"]
+    scaffold = wl["strategy"] == "scaffold"
+    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    s_in = 2 if kind == "bf16" else 4
+
+    # ---- this rank's share of the job ----
+    if client_shard:
+        M = M_glob
+        k0, k1 = client_blocks(K, world)[block_of(rank, world)]
+        parallelism = f"client-shard x{world} ({args.combine})" if world > 1 else "single-gpu"
+        scaling = "strong"
+    elif args.scaling == "strong":
+        lo, hi = shard_bounds(M_glob, world)[rank]
+        M = hi - lo
+        k0, k1 = 0, K
+        parallelism = f"param-range x{world} (strong)" if world > 1 else "single-gpu"
+        scaling = "strong"
+    else:
+        M = M_glob
+        k0, k1 = 0, K
+        parallelism = f"param-range x{world}" if world > 1 else "single-gpu"
+        scaling = "weak"
+    Kr = k1 - k0
+    shapes = synthetic_state_dict_shapes(M_glob if client_shard else max(M, 1))
     layout = BucketLayout(list(range(len(shapes))), shapes, np.float32)
     ld = layout.ld
-    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    pw = layout.pairwise_idx
+    seed0 = 20241016 + k0 + (1_000_003 * rank if not client_shard else 0)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    if wl["strategy"] == "fedavg":
-        clients = synth_clients(torch, K, ld, M, kind, device, rank)
+    stream = torch.cuda.current_stream(device)
+    if not scaffold:
+        clients = synth_clients(torch, Kr, ld, M, kind, device, seed0)
         out = torch.empty(ld, dtype=torch.float32, device=device)
-        w = fedavg_weights(n_samples, kind)
-        plan = FedAvgPlan(kind, clients, w, M, out, layout.pairwise_idx)
-        s_in = 2 if kind == "bf16" else 4
+        w_all = fedavg_weights(n_samples, kind)
+        if client_shard:
+            sh = FedAvgShard(kind, clients, w_all[k0:k1], k0, K, M, pw)
+            ops, tr = GpuShardOps(), DistTransport() if world > 1 else None
+            ws = torch.zeros((max(1, pw.size), K), dtype=torch.float32, device=device)
+
+            def step():
+                if world > 1:
+                    client_shard_fedavg(sh, out, tr, ops, args.combine, ws=ws)
+                else:
+                    FedAvgPlan(kind, clients, w_all, M, out, pw).launch(stream)
+
+            kplan = FedAvgPlan(kind, clients, w_all[k0:k1], M, out, None)  # this block's partial kernel
+        else:
+            plan = FedAvgPlan(kind, clients, w_all, M, out, pw)
+            kplan = plan
+
+            def step():
+                plan.launch(stream)
+        bytes_job = K * M_glob * s_in + M_glob * 4
+        bytes_kernel = kplan.bytes_alg()
     else:
-        delta = synth_clients(torch, K, ld, M, kind, device, rank)
-        cv = synth_clients(torch, K, ld, M, kind, device, rank + 7919)
-        c = torch.randn(ld, dtype=torch.float32, device=device)
+        delta = synth_clients(torch, Kr, ld, M, kind, device, seed0)
+        cv = synth_clients(torch, Kr, ld, M, kind, device, seed0 + 7919)
+        gc = torch.Generator(device=device)
+        gc.manual_seed(4242)
+        c = torch.randn(ld, dtype=torch.float32, device=device, generator=gc)
         dout = torch.empty(ld, dtype=torch.float64, device=device)
         cout = torch.empty(ld, dtype=torch.float64, device=device)
-        w = scaffold_weights(n_samples)
-        plan = ScaffoldPlan(kind, delta, cv, c, w, M, 1.0, dout, cout, layout.pairwise_idx)
-        s_in = 4
-    bytes_alg = plan.bytes_alg()
-    stream = torch.cuda.current_stream(device)
+        w_all = scaffold_weights(n_samples)
+        if client_shard:
+            sh = ScaffoldShard(kind, delta, cv, c, w_all[k0:k1], k0, K, M, 1.0, pw)
+            ops, tr = GpuShardOps(), DistTransport() if world > 1 else None
+
+            def step():
+                if world > 1:
+                    client_shard_scaffold(sh, dout, cout, tr, ops, args.combine)
+                else:
+                    ScaffoldPlan(kind, delta, cv, c, w_all, M, 1.0, dout, cout, pw).launch(stream)
+
+            kplan = ScaffoldPlan(kind, delta, cv, c, w_all[k0:k1], M, 1.0, dout, cout, None)
+        else:
+            plan = ScaffoldPlan(kind, delta, cv, c, w_all, M, 1.0, dout, cout, pw)
+            kplan = plan
+
+            def step():
+                plan.launch(stream)
+        bytes_job = 2 * K * M_glob * 4 + M_glob * 4 + 2 * M_glob * 8
+        bytes_kernel = kplan.bytes_alg()
+    if not client_shard and args.scaling == "weak":  # every rank reduces a full M-param slice
+        bytes_job = bytes_kernel * world
 
     # ---- warmup (untimed) ----
     for _ in range(args.warmup):
-        plan.launch(stream)
+        step()
     torch.cuda.synchronize(device)
 
     # ---- timed region: exactly `steps` steps, barrier + sync on both sides ----
-    # HIP events on the launch stream bracket the region: kern_ms = region / steps is the
-    # average launch duration of the bucket kernel (back-to-back launches, so it includes the
-    # ~1-2 us inter-kernel boundary: an upper bound; rocprofv3 gives the exact duration).
     ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     ev_start.record(stream)
     for _ in range(args.steps):
-        plan.launch(stream)
+        step()
     ev_end.record(stream)
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0  # this rank's region; the job's time is the max over ranks
     barrier()
-    kern_ms = ev_start.elapsed_time(ev_end) / args.steps
+    step_ms_dev = ev_start.elapsed_time(ev_end) / args.steps
 
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = bytes_alg * world / (elapsed / args.steps) / 1e9
-
-    # ---- per-launch distribution (after the timed region): one event pair per launch ----
+    # ---- the dominant kernel alone, HIP events on its launch stream (after the timed region) ----
     n_each = max(5, min(args.steps, 20))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_each)]
     for a, b in evs:
         a.record(stream)
-        plan.launch(stream)
+        kplan.launch(stream)
         b.record(stream)
     torch.cuda.synchronize(device)
     each_ms = np.array([a.elapsed_time(b) for a, b in evs])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(max(5, min(args.steps, 50))):
+        kplan.launch(stream)
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    kern_ms = e0.elapsed_time(e1) / max(5, min(args.steps, 50))
+    if not client_shard:  # the step IS the one kernel, launched back to back: region / steps
+        kern_ms = step_ms_dev
 
-    # ---- parity spot check (outside the timed region): sampled elements vs the sequential order ----
-    parity = None
-    if wl["strategy"] == "fedavg":
-        g = np.random.default_rng(123)
-        idx = np.setdiff1d(np.unique(g.integers(0, M, 4096)), layout.pairwise_idx.astype(np.int64))
-        tidx = torch.from_numpy(idx).to(device)
-        xs = clients[:, tidx].float().cpu().numpy()  # exact upcast for bf16
-        got = out[tidx].cpu().numpy()
-        w32 = fedavg_weights(n_samples, "f32")
-        acc = np.zeros(idx.size, np.float32)
-        for k in range(K):
-            acc = (acc + (xs[k] * w32[k]).astype(np.float32)).astype(np.float32)
-        # (the numel == 1 element is reduced in NumPy's pairwise order: tests/ check it against the oracle)
-        parity = {"sampled": int(idx.size), "mismatches": int(np.sum(acc.view(np.uint32) != got.view(np.uint32)))}
-    else:  # Scaffold (scaffold.py:262-263,293): fp64 products and sums, c added last, lr after the sum
-        g = np.random.default_rng(123)
-        idx = np.setdiff1d(np.unique(g.integers(0, M, 4096)), layout.pairwise_idx.astype(np.int64))
-        tidx = torch.from_numpy(idx).to(device)
-        xd = delta[:, tidx].double().cpu().numpy()
-        xc = cv[:, tidx].double().cpu().numpy()
-        cc = c[tidx].double().cpu().numpy()
-        w64 = scaffold_weights(n_samples)
-        ad = np.zeros(idx.size, np.float64)
-        ac = np.zeros(idx.size, np.float64)
-        for k in range(K):
-            ad = ad + xd[k] * w64[k]
-            ac = ac + xc[k] * w64[k]
-        ad = 1.0 * ad
-        ac = ac + cc
-        gd = dout[tidx].cpu().numpy()
-        gc = cout[tidx].cpu().numpy()
-        parity = {"sampled": int(idx.size),
-                  "mismatches": int(np.sum(ad.view(np.uint64) != gd.view(np.uint64))
-                                    + np.sum(ac.view(np.uint64) != gc.view(np.uint64)))}
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                         device=device if client_shard else torch.device("cpu"))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+    ms_per_step = elapsed / args.steps * 1e3
+    value = bytes_job / (elapsed / args.steps) / 1e9
+
+    # ---- parity spot check (outside the timed region) ----
+    step()  # the kernel-alone launches above overwrote the outputs with a block's partial
+    torch.cuda.synchronize(device)
+    parity = spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, layout, n_samples, kind,
+                        device, locals())
 
     # ---- read-stream ceiling on the same box (same 16-B nt load path) ----
-    probe_n = min(clients.numel() if wl["strategy"] == "fedavg" else delta.numel(), 2_000_000_000)
-    src = clients if wl["strategy"] == "fedavg" else delta
-    nbytes_probe = probe_n * src.element_size()
-    floats = nbytes_probe // 4 // 4 * 4
-    full = int(min(floats // 4 // 256, 1 << 20))  # one 16-B vector per thread, like the bucket kernel
-    sink = torch.empty(full, dtype=torch.float32, device=device)
-    read_ceiling = 0.0
-    for pgrid in sorted({min(g, full) for g in (2048, 4096, 8192, 16384, 65536)} | {full}):  # best grid = the ceiling
-        for _ in range(3):
-            _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
-                                                    stream.cuda_stream), "probe")
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(10):
-            lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid, stream.cuda_stream)
-        e1.record(stream)
-        torch.cuda.synchronize(device)
-        read_ceiling = max(read_ceiling, floats * 4 / (e0.elapsed_time(e1) / 10 / 1e3) / 1e9)
+    src = clients if not scaffold else delta
+    read_ceiling = read_probe(torch, lib, src, stream, device, _native)
 
     # ---- CPU baseline (rank 0, N == 1): the reference call structure timed on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, args.cpu_seconds)
 
-    traffic = None
-    tpath = Path(args.traffic) if args.traffic else ROOT / "profiles" / f"traffic_{args.workload}.json"
-    if tpath.exists():
-        try:
-            tj = json.loads(tpath.read_text())
-            traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
+    sha = lib_sha256()
+    traffic, tsrc = read_traffic(args, sha) if (world == 1 or args.scaling == "weak") and not client_shard \
+        else (None, None)
 
-    achieved = bytes_alg / (kern_ms / 1e3) / 1e9
+    achieved = bytes_kernel / (kern_ms / 1e3) / 1e9
     if rank == 0:
+        kname = (f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>" if not scaffold else "scaffold_kernel<float>")
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -243,20 +372,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "bf16-in/f32-acc" if kind == "bf16" else ("f32-in/f64-acc" if wl["strategy"] == "scaffold" else "f32"),
+            "dtype": "bf16-in/f32-acc" if kind == "bf16" else ("f32-in/f64-acc" if scaffold else "f32"),
             "data": "synthetic (N(0,1) client buckets generated on device, torch Philox seeds 20241016+k; "
                     "n_samples = default_rng(7).integers(100, 10000, K))",
             "config": {
                 "workload": wl["name"],
                 "strategy": wl["strategy"],
                 "clients": K,
+                "clients_per_gpu": Kr,
                 "params_per_gpu": M,
-                "global_params": M * world,
+                "global_params": M_glob if (client_shard or args.scaling == "strong") else M * world,
                 "layers": len(shapes),
-                "parallelism": f"param-range x{world}" if world > 1 else "single-gpu",
-                "bytes_alg_per_step_per_gpu": bytes_alg,
+                "parallelism": parallelism,
+                "bytes_alg_per_step_job": bytes_job,
+                "bytes_alg_per_launch_rank0": bytes_kernel,
             },
             "roofline": {
                 "bound": "hbm",
@@ -265,18 +396,212 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": (f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>" if wl["strategy"] == "fedavg"
-                           else "scaffold_kernel<float>"),
+                "traffic_source": tsrc,
+                "kernel": kname,
                 "kernel_ms": round(kern_ms, 5),
+                "kernel_ms_max_over_ranks": round(kern_ms_max, 5),
                 "kernel_ms_median": round(float(np.median(each_ms)), 5),
                 "kernel_ms_min": round(float(each_ms.min()), 5),
-                "read_stream_ceiling_GBps": round(read_ceiling, 1),
-                "frac_of_read_ceiling": round(achieved / read_ceiling, 4),
+                "kernel_timing": "HIP events on the launch stream: timed region / steps" if not client_shard else
+                                 "HIP events on the launch stream: this rank's block kernel alone, back to back",
+                "read_stream_ceiling_GBps": round(read_ceiling, 1) if read_ceiling > 0 else None,
+                "frac_of_read_ceiling": round(achieved / read_ceiling, 4) if read_ceiling > 0 else None,
             },
             "cpu_baseline": cpu,
             "parity": parity,
+            "build": {"lib_sha256": sha},
         }
+        if client_shard and world > 1:
+            line["combine"] = {"mode": args.combine, "step_ms": round(ms_per_step, 5),
+                               "block_kernel_ms": round(kern_ms_max, 5),
+                               "exchange_and_final_ms": round(max(0.0, ms_per_step - kern_ms_max), 5),
+                               "bit_exact_by_construction": args.combine == "relay"}
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, layout, n_samples, kind, device, env):
+    """Sampled output elements against the reference's sequential order (fp32 FedAvg chain /
+    fp64 Scaffold with c last and lr after the sum); client-sharded: every rank's sampled
+    columns are gathered on the root.  numel == 1 elements are excluded here (pairwise order:
+    tests/ check them against the oracle)."""
+    from substrafl_amd.engine import fedavg_weights, scaffold_weights
+
+    g = np.random.default_rng(123)
+    idx = np.setdiff1d(np.unique(g.integers(0, M, 4096)), layout.pairwise_idx.astype(np.int64))
+    tidx = torch.from_numpy(idx).to(device)
+    Kr = k1 - k0
+
+    def cols(x):  # [Kr, S] sampled columns of this rank's rows, gathered on the root in block order
+        xs = x[:, tidx].to(torch.float64) if Kr else torch.zeros((0, idx.size), dtype=torch.float64, device=device)
+        if not (client_shard and world > 1):
+            return xs.cpu().numpy()
+        from substrafl_amd.sharding import chain_rank, client_blocks
+
+        per = -(-K // world)
+        pad = torch.zeros((per, idx.size), dtype=torch.float64, device=device)
+        pad[:Kr] = xs
+        got = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad, gather_list=got, dst=0)
+        if rank != 0:
+            return None
+        blocks = client_blocks(K, world)
+        return np.concatenate([got[chain_rank(b, world)][: blocks[b][1] - blocks[b][0]].cpu().numpy()
+                               for b in range(world)], axis=0)
+
+    if not scaffold:
+        xs = cols(env["clients"])
+        if rank != 0 or xs is None:
+            return None
+        got = env["out"][tidx].cpu().numpy()
+        w32 = fedavg_weights(n_samples, "f32")
+        acc = np.zeros(idx.size, np.float32)
+        for k in range(K if client_shard else xs.shape[0]):
+            acc = (acc + (xs[k].astype(np.float32) * w32[k]).astype(np.float32)).astype(np.float32)
+        bad = acc.view(np.uint32) != got.view(np.uint32)
+        res = {"sampled": int(idx.size), "mismatches": int(np.sum(bad))}
+        if bad.any():
+            ia, ib = acc.view(np.int32).astype(np.int64), got.view(np.int32).astype(np.int64)
+            res["max_ulp"] = int(np.max(np.abs(ia - ib)))
+        return res
+    xd, xc = cols(env["delta"]), cols(env["cv"])
+    if rank != 0 or xd is None:
+        return None
+    cc = env["c"][tidx].double().cpu().numpy()
+    w64 = scaffold_weights(n_samples)
+    ad = np.zeros(idx.size)
+    ac = np.zeros(idx.size)
+    for k in range(xd.shape[0]):
+        ad = ad + xd[k] * w64[k]
+        ac = ac + xc[k] * w64[k]
+    ad = 1.0 * ad
+    ac = ac + cc
+    gd = env["dout"][tidx].cpu().numpy()
+    gcv = env["cout"][tidx].cpu().numpy()
+    return {"sampled": int(idx.size),
+            "mismatches": int(np.sum(ad.view(np.uint64) != gd.view(np.uint64))
+                              + np.sum(ac.view(np.uint64) != gcv.view(np.uint64)))}
+
+
+def read_probe(torch, lib, src, stream, device, _native) -> float:
+    """Best single-stream 16-B non-temporal read rate over the client buckets (2K..64K grids)."""
+    probe_n = min(src.numel(), 2_000_000_000)
+    if probe_n < 4096:
+        return 0.0
+    nbytes_probe = probe_n * src.element_size()
+    floats = nbytes_probe // 4 // 4 * 4
+    full = int(min(floats // 4 // 256, 1 << 20))
+    sink = torch.empty(max(1, full), dtype=torch.float32, device=device)
+    best = 0.0
+    for pgrid in sorted({min(g, full) for g in (2048, 4096, 8192, 16384, 65536)} | {full}):
+        if pgrid <= 0:
+            continue
+        for _ in range(3):
+            _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
+                                                    stream.cuda_stream), "probe")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid, stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize(device)
+        best = max(best, floats * 4 / (e0.elapsed_time(e1) / 10 / 1e3) / 1e9)
+    return best
+
+
+# ======================================================================================
+# --engine multi-device: the drop-in's one-process multi-GPU path (end-to-end line)
+# ======================================================================================
+def multi_device_bench(args):
+    """MultiDeviceEngine over --gpus devices of ONE process (indices repeat on a box with fewer
+    GPUs, one native session each): host buckets -> per-GPU pinned-ring staging over its PCIe
+    link -> the bucket kernel -> D2H into the one output array.  Reports the PCIe-inclusive rate
+    and, per shard, the stage / kernel / fetch split with the kernel timed by HIP events on the
+    shard's session stream."""
+    from substrafl_amd import _native
+    from substrafl_amd.layout import synthetic_state_dict_shapes
+    from substrafl_amd.multi_device import MultiDeviceEngine
+
+    ndev = _native.load().fedagg_device_count()
+    if ndev <= 0:
+        print("bench.py: no GPU visible", file=sys.stderr)
+        sys.exit(3)
+    wl = WORKLOADS[args.workload]
+    if wl["strategy"] != "fedavg" or wl["kind"] != "f32":
+        print("bench.py: --engine multi-device runs the fp32 FedAvg workloads (c2, c3)", file=sys.stderr)
+        sys.exit(2)
+    K, M = wl["K"], wl["M"]
+    devices = [g % ndev for g in range(args.gpus)]
+    shapes = synthetic_state_dict_shapes(M)
+    rng = np.random.default_rng(1)
+    base = [rng.standard_normal(int(np.prod(s)), dtype=np.float32).reshape(s) for s in shapes]
+    pus = [[(a * np.float32(1 + 0.01 * k)).astype(np.float32) for a in base] for k in range(K)]
+    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    eng = MultiDeviceEngine(devices)
+    eng.kernel_events = True
+    for _ in range(max(1, args.warmup)):
+        eng.fedavg(pus, n_samples)
+    walls, shards = [], []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        eng.fedavg(pus, n_samples)
+        walls.append(time.perf_counter() - t0)
+        shards.append(eng.last_timing["shards"])
+    wall = float(np.median(walls))
+    bytes_alg = K * M * 4 + M * 4
+    per_shard = []
+    for g in range(len(devices)):
+        st = [s[g] for s in shards]
+        lo, hi = eng.last_timing["ranges"][g][0][0], eng.last_timing["ranges"][g][-1][1]
+        kms = float(np.median([s.get("kernel_ms", float("nan")) for s in st]))
+        b = K * (hi - lo) * 4 + (hi - lo) * 4
+        per_shard.append({"device": devices[g], "params": hi - lo,
+                          "stage_s": round(float(np.median([s["stage_s"] for s in st])), 5),
+                          "kernel_fetch_s": round(float(np.median([s["kernel_fetch_s"] for s in st])), 5),
+                          "kernel_ms": round(kms, 4),
+                          "kernel_GBps_device_resident": round(b / (kms / 1e3) / 1e9, 1) if kms == kms else None})
+    print(json.dumps({
+        "metric": "aggregated-param GB/s (host buckets, PCIe-inclusive) FedAvg reduce, one process x N GPUs",
+        "value": round(bytes_alg / wall / 1e9, 2), "unit": "GB/s", "n_gpus": len(devices),
+        "distinct_gpus": len(set(devices)), "steps": args.steps, "warmup": args.warmup,
+        "ms_per_call_median": round(wall * 1e3, 3), "higher_is_better": True, "dtype": "f32",
+        "data": "synthetic host NumPy client states (per-layer arrays, N(0,1) scaled per client)",
+        "config": {"workload": wl["name"], "clients": K, "params": M, "layers": len(shapes),
+                   "engine": "MultiDeviceEngine (one process, one thread + native session per GPU)"},
+        "shards": per_shard,
+        "note": "end-to-end (pinned-ring pack + H2D + kernel + D2H); not the device-resident metric",
+    }), flush=True)
+
+
+# ======================================================================================
+# --rehearse-cpu (tests): the launcher / rank / timing plumbing without a GPU
+# ======================================================================================
+def rehearse(args, world, rank):
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = np.ones(1 << 16, np.float32)
+    for _ in range(args.warmup):
+        x = x * np.float32(1.0)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = x * np.float32(1.0)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank == 0:
+        print(json.dumps({"metric": METRIC + " [CPU rehearsal of the launcher: not a measurement]",
+                          "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 6),
+                          "rehearsal": True, "ranks_seen": world}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 4
+#define FEDAGG_ABI_VERSION 5
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -133,6 +133,68 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
                            void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Client-sharded building blocks (sharding.py).  The K clients are
+ * cut into contiguous blocks, each block's buckets live on one GPU; the reference's
+ * sequential client sum (fed_avg.py:221-222, scaffold.py:262-263,293) is then either
+ *   - CHAINED: block b continues the accumulator of blocks 0..b-1 (received from the
+ *     previous rank over xGMI) -- bit-identical to one pass, or
+ *   - re-associated: every block sums from +0.0, the partial sums are combined on the
+ *     root (RCCL reduce, or a gather + rank-order sum) -- a few ulp off the reference.
+ * The numel==1 elements (NumPy pairwise order over ALL K products) cannot be chained:
+ * every block writes its products into columns kbase.. of a [P][stride] workspace, the
+ * root reduces the workspaces and runs the tree.
+ *
+ * fedavg_chain: acc = seed ? +0.0 : d_out[i];  acc = fl(acc + fl(x_k[i] * h_w[k])) for the K
+ *   clients of this block, in order; d_out[i] = acc (no numel==1 patch; h_w are the GLOBAL
+ *   weights fl(n_k / n)).  bf16 buckets accumulate into fp32 d_out, fp16 weights as bits.
+ * -------------------------------------------------------------------------*/
+int fedagg_fedavg_chain_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
+                            float* d_out, void* stream);
+int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
+                             float* d_out, void* stream);
+int fedagg_fedavg_chain_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, int seed,
+                            double* d_out, void* stream);
+int fedagg_fedavg_chain_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, uint64_t M, int seed,
+                            uint16_t* d_out, void* stream);
+/* d_ws[p * stride + kbase + k] = fl(x_k[h_idx[p]] * h_w[k]) in the pairwise-sum type (fp32 for
+ * f32/bf16/f16 -- NumPy's HALF_pairwise_sum adds in fp32 -- fp64 for f64). */
+int fedagg_pairwise_products_f32(const float* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,
+                                 int P, int64_t stride, int kbase, float* d_ws, void* stream);
+int fedagg_pairwise_products_bf16(const uint16_t* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,
+                                  int P, int64_t stride, int kbase, float* d_ws, void* stream);
+int fedagg_pairwise_products_f64(const double* const* d_clients, const double* h_w, int K, const uint64_t* h_idx,
+                                 int P, int64_t stride, int kbase, double* d_ws, void* stream);
+int fedagg_pairwise_products_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, const uint64_t* h_idx,
+                                 int P, int64_t stride, int kbase, float* d_ws, void* stream);
+/* d_out[h_idx[p]] = +0.0 + pairwise_sum(d_ws[p * stride .. p * stride + n)) (fed_avg.py:222 on a
+ * numel == 1 tensor).  _f32 also serves bf16 buckets (fp32 output). */
+int fedagg_pairwise_finish_f32(const float* d_ws, int64_t n, int64_t stride, const uint64_t* h_idx, int P,
+                               float* d_out, void* stream);
+int fedagg_pairwise_finish_f64(const double* d_ws, int64_t n, int64_t stride, const uint64_t* h_idx, int P,
+                               double* d_out, void* stream);
+int fedagg_pairwise_finish_f16(const float* d_ws, int64_t n, int64_t stride, const uint64_t* h_idx, int P,
+                               uint16_t* d_out, void* stream);
+/* Scaffold (fp64): seed ? +0.0 : d_*_out as the accumulators; finish = 1 on the LAST block only:
+ * then + c (scaffold.py:262-263) and * lr (scaffold.py:293), d_c read; finish = 0: plain sums,
+ * d_c may be NULL. */
+int fedagg_scaffold_chain_f32(const float* const* d_delta, const float* const* d_cv, const float* d_c,
+                              const double* h_w, int K, uint64_t M, int seed, int finish, double lr,
+                              double* d_delta_out, double* d_c_out, void* stream);
+int fedagg_scaffold_chain_f64(const double* const* d_delta, const double* const* d_cv, const double* d_c,
+                              const double* h_w, int K, uint64_t M, int seed, int finish, double lr,
+                              double* d_delta_out, double* d_c_out, void* stream);
+/* Scaffold numel==1 workspace: P * (2 * Ktot + 1) doubles = delta terms [P][Ktot], then
+ * control-variate terms [P][Ktot + 1] (column Ktot = c, written by _finish). */
+int fedagg_scaffold_products_f32(const float* const* d_delta, const float* const* d_cv, const double* h_w, int K,
+                                 int kbase, int Ktot, const uint64_t* h_idx, int P, double* d_ws, void* stream);
+int fedagg_scaffold_products_f64(const double* const* d_delta, const double* const* d_cv, const double* h_w, int K,
+                                 int kbase, int Ktot, const uint64_t* h_idx, int P, double* d_ws, void* stream);
+int fedagg_scaffold_finish_f32(double* d_ws, int Ktot, const float* d_c, const uint64_t* h_idx, int P, double lr,
+                               double* d_delta_out, double* d_c_out, void* stream);
+int fedagg_scaffold_finish_f64(double* d_ws, int Ktot, const double* d_c, const uint64_t* h_idx, int P, double lr,
+                               double* d_delta_out, double* d_c_out, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Client-side flat-bucket ops (the producer / consumer of the buckets, SURVEY.md §8(a)
  * a5-a7).  A model's L parameter tensors (device pointers d_layers[l], numel[l] fp32 elements
  * each, in weight_manager.model_parameters order, weight_manager.py:53-76) map onto one flat
@@ -198,6 +260,7 @@ int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid,
  * pickled back, :82-86) without PyTorch on the task's critical path.
  * -------------------------------------------------------------------------*/
 #define FEDAGG_SESSION_BUFFERS 16
+#define FEDAGG_SESSION_EVENTS 8
 typedef struct fedagg_session fedagg_session;
 /* NULL on failure (no device, ...): see fedagg_last_error(). */
 fedagg_session* fedagg_session_create(int device);
@@ -205,7 +268,8 @@ void fedagg_session_destroy(fedagg_session* s);
 /* the session's hipStream_t, to pass as `stream` to the kernel entry points */
 void* fedagg_session_stream(fedagg_session* s);
 /* knobs: "threads" (pack workers), "chunk_bytes" (pinned slot size), "slots" (ring length),
- * "copy_streams" (1 or 2 H2D queues for staging; default 2) */
+ * "copy_streams" (1 or 2 H2D queues for staging; default 2), "fail_copy_after" (tests: the n-th
+ * copy enqueued from now on fails with FEDAGG_EHIP; 0 = never) */
 int fedagg_session_set(fedagg_session* s, const char* key, long long value);
 /* grow-only device buffer number `slot` (0..FEDAGG_SESSION_BUFFERS-1) of at least `bytes` */
 int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr);
@@ -225,6 +289,16 @@ int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int 
 int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
                                const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
                                uint64_t byte_hi);
+/* Scaffold's server-control-variate check on the host, during staging (scaffold.py:193-196,
+ * np.testing.assert_array_equal(c_0, c_k)): K clients' c rows (nseg host segments each, as
+ * fedagg_session_stage); ONE copy -- bytes [byte_lo, byte_hi) of row 0 -- is staged to d_dst, the
+ * same bytes of rows 1..K-1 are compared with it by value on the pack workers (+0 == -0,
+ * NaN == NaN; byte-identical stretches skipped) and the number of mismatching elements is written
+ * to *mismatches.  kind: FEDAGG_F32 or FEDAGG_F64 (every segment of that element type; the range
+ * element-aligned).  Replaces K-1 PCIe copies plus the device check (fedagg_equal_count_*). */
+int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, const void* const* h_seg,
+                               const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, int kind,
+                               uint64_t* mismatches);
 /* Make the session's GPU the calling thread's current device (kernel entry points launch on
  * the current device: a thread driving several sessions calls this before each one's launches). */
 int fedagg_session_activate(fedagg_session* s);
@@ -236,6 +310,11 @@ int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes
 int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes);
 int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes);
 int fedagg_session_sync(fedagg_session* s);
+/* timing events on the session stream (0 <= ev < FEDAGG_SESSION_EVENTS): record, and the time
+ * between two recorded events in ms (waits for ev1) -- per-shard kernel time of the one-process
+ * multi-GPU engine (bench.py --engine multi-device) */
+int fedagg_session_event_record(fedagg_session* s, int ev);
+int fedagg_session_event_elapsed(fedagg_session* s, int ev0, int ev1, float* ms);
 /* wall time of the last stage / fetch call, seconds */
 int fedagg_session_timing(fedagg_session* s, double* stage_s, double* fetch_s);
 

@@ -17,6 +17,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("FEDAGG_LIB", str(_HERE / "libfedagg.so")))
 
 c_u64 = ctypes.c_uint64
+c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_void = ctypes.c_void_p
 c_dbl = ctypes.c_double
@@ -53,6 +54,32 @@ SIGNATURES = {
     "fedagg_flat_wsum": (c_int, [P(c_void), P(c_int), c_int, P(c_dbl), P(c_u64), c_int, c_void, c_int, c_void]),
     "fedagg_flat_increment": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_int, c_dbl, c_void]),
     "fedagg_scale_cast": (c_int, [c_void, c_int, c_dbl, c_void, c_int, c_u64, c_void]),
+    # client-sharded building blocks (chain / split pairwise trees)
+    "fedagg_fedavg_chain_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_pairwise_products_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_i64, c_int,
+                                             c_void, c_void]),
+    "fedagg_pairwise_products_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_i64, c_int,
+                                              c_void, c_void]),
+    "fedagg_pairwise_products_f64": (c_int, [P(c_void), P(c_dbl), c_int, P(c_u64), c_int, c_i64, c_int, c_void,
+                                             c_void]),
+    "fedagg_pairwise_products_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, P(c_u64), c_int, c_i64, c_int,
+                                             c_void, c_void]),
+    "fedagg_pairwise_finish_f32": (c_int, [c_void, c_i64, c_i64, P(c_u64), c_int, c_void, c_void]),
+    "fedagg_pairwise_finish_f64": (c_int, [c_void, c_i64, c_i64, P(c_u64), c_int, c_void, c_void]),
+    "fedagg_pairwise_finish_f16": (c_int, [c_void, c_i64, c_i64, P(c_u64), c_int, c_void, c_void]),
+    "fedagg_scaffold_chain_f32": (c_int, [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, c_int, c_int, c_dbl,
+                                          c_void, c_void, c_void]),
+    "fedagg_scaffold_chain_f64": (c_int, [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, c_int, c_int, c_dbl,
+                                          c_void, c_void, c_void]),
+    "fedagg_scaffold_products_f32": (c_int, [P(c_void), P(c_void), P(c_dbl), c_int, c_int, c_int, P(c_u64), c_int,
+                                             c_void, c_void]),
+    "fedagg_scaffold_products_f64": (c_int, [P(c_void), P(c_void), P(c_dbl), c_int, c_int, c_int, P(c_u64), c_int,
+                                             c_void, c_void]),
+    "fedagg_scaffold_finish_f32": (c_int, [c_void, c_int, c_void, P(c_u64), c_int, c_dbl, c_void, c_void, c_void]),
+    "fedagg_scaffold_finish_f64": (c_int, [c_void, c_int, c_void, P(c_u64), c_int, c_dbl, c_void, c_void, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),
@@ -61,6 +88,10 @@ SIGNATURES = {
     "fedagg_session_warm": (c_int, [c_void, P(c_u64), c_int]),
     "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
     "fedagg_session_stage_range": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64]),
+    "fedagg_session_stage_check": (c_int, [c_void, c_void, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64, c_int,
+                                           P(c_u64)]),
+    "fedagg_session_event_record": (c_int, [c_void, c_int]),
+    "fedagg_session_event_elapsed": (c_int, [c_void, c_int, c_int, P(ctypes.c_float)]),
     "fedagg_session_activate": (c_int, [c_void]),
     "fedagg_device_count": (c_int, []),
     "fedagg_device_memory": (c_int, [c_int, P(c_u64), P(c_u64)]),
@@ -70,13 +101,14 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
 FEDAGG_MAX_PAIRWISE = 64
 FEDAGG_FLAT_MAX_LISTS = 4
 FEDAGG_SESSION_BUFFERS = 16
+FEDAGG_SESSION_EVENTS = 8
 FEDAGG_F16 = 0  # kinds (include/fedagg.h enum)
 FEDAGG_F32 = 1
 FEDAGG_F64 = 2

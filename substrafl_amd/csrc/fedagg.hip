@@ -1033,15 +1033,15 @@ __global__ void __launch_bounds__(FA_BLOCK)
   ws_c[p * (K + 1) + kbase + k] = a.w[k] * (double)a.cv[k][i];
 }
 
-// Stage 2: out[idx_p] = (+0.0 + pairwise(ws[p]))
+// Stage 2: out[idx_p] = (+0.0 + pairwise(ws[p * stride .. p * stride + n)))
 template <typename E>
-__global__ void pairwise_tree_kernel(const typename E::W* __restrict__ ws, const int64_t n, const IdxArgs ix,
-                                     const int P, typename E::Out* __restrict__ out) {
+__global__ void pairwise_tree_kernel(const typename E::W* __restrict__ ws, const int64_t n, const int64_t stride,
+                                     const IdxArgs ix, const int P, typename E::Out* __restrict__ out) {
 #pragma clang fp contract(off)
   using W = typename E::W;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  const W* row = ws + p * n;
+  const W* row = ws + p * stride;
   auto get = [&](int64_t i) -> W { return row[i]; };
   const W s = W(0.0f) + pw_sum<W>(get, n);
   out[ix.idx[p]] = E::out((typename E::P)s);
@@ -1609,16 +1609,72 @@ int fedavg_pairwise_launch(const typename E::In* const* x, const typename E::P* 
       int rc = check_launch("pairwise_gather_kernel");
       if (rc) return rc;
     }
-    hipLaunchKernelGGL((pairwise_tree_kernel<E>), dim3(1), dim3(64), 0, s, (const W*)wsT, (int64_t)K, ix, pc, out);
+    hipLaunchKernelGGL((pairwise_tree_kernel<E>), dim3(1), dim3(64), 0, s, (const W*)wsT, (int64_t)K, (int64_t)K, ix,
+                       pc, out);
     int rc = check_launch("pairwise_tree_kernel");
     if (rc) return rc;
   }
   return FEDAGG_OK;
 }
 
+// Products of a client block at the numel==1 indices, for a pairwise tree over clients held by
+// several launches (or ranks): ws[p * stride + kbase + k] = fl(x_k[idx_p] * w_k) in type W.
+template <typename E>
+int pairwise_products_launch(const typename E::In* const* x, const typename E::P* w, int K, const uint64_t* idx,
+                             int P, int64_t stride, int kbase, typename E::W* ws, hipStream_t s) {
+  if (P == 0) return FEDAGG_OK;
+  if (K <= 0 || P < 0 || !x || !w || !idx || !ws || kbase < 0 || stride < (int64_t)kbase + K)
+    return fail(FEDAGG_EINVAL, "pairwise_products: invalid argument (K=%lld)", K);
+  for (int k = 0; k < K; ++k)
+    if (!x[k]) return fail(FEDAGG_EINVAL, "pairwise_products: client pointer %lld is NULL", k);
+  for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
+    const int pc = (P - p0) < FEDAGG_MAX_PAIRWISE ? (P - p0) : FEDAGG_MAX_PAIRWISE;
+    IdxArgs ix;
+    memset(&ix, 0, sizeof(ix));
+    for (int p = 0; p < pc; ++p) ix.idx[p] = idx[p0 + p];
+    for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
+      const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
+      FaArgs<E, FEDAGG_KCHUNK> a;
+      memset(&a, 0, sizeof(a));
+      for (int k = 0; k < kc; ++k) {
+        a.x[k] = x[k0 + k];
+        a.w[k] = w[k0 + k];
+      }
+      const unsigned g = (unsigned)((pc * kc + FA_BLOCK - 1) / FA_BLOCK);
+      hipLaunchKernelGGL((pairwise_gather_kernel<E, FEDAGG_KCHUNK>), dim3(g), dim3(FA_BLOCK), 0, s, a, kc, kbase + k0,
+                         ix, pc, stride, ws + (int64_t)p0 * stride);
+      int rc = check_launch("pairwise_gather_kernel");
+      if (rc) return rc;
+    }
+  }
+  return FEDAGG_OK;
+}
+
+// out[idx_p] = +0.0 + pairwise(ws[p * stride .. p * stride + n)) for p < P.
+template <typename E>
+int pairwise_finish_launch(const typename E::W* ws, int64_t n, int64_t stride, const uint64_t* idx, int P,
+                           typename E::Out* out, hipStream_t s) {
+  if (P == 0) return FEDAGG_OK;
+  if (n <= 0 || P < 0 || stride < n || !ws || !idx || !out)
+    return fail(FEDAGG_EINVAL, "pairwise_finish: invalid argument (n=%lld)", n);
+  for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
+    const int pc = (P - p0) < FEDAGG_MAX_PAIRWISE ? (P - p0) : FEDAGG_MAX_PAIRWISE;
+    IdxArgs ix;
+    memset(&ix, 0, sizeof(ix));
+    for (int p = 0; p < pc; ++p) ix.idx[p] = idx[p0 + p];
+    hipLaunchKernelGGL((pairwise_tree_kernel<E>), dim3(1), dim3(64), 0, s, ws + (int64_t)p0 * stride, n, stride, ix,
+                       pc, out);
+    int rc = check_launch("pairwise_tree_kernel");
+    if (rc) return rc;
+  }
+  return FEDAGG_OK;
+}
+
+// seed = false: the accumulator starts from d_out (a partial sum over the clients before this
+// block, e.g. received from the previous rank of a client-sharded chain) instead of +0.0.
 template <typename E>
 int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K, uint64_t M, const uint64_t* idx,
-                  int P, void* ws, typename E::Out* out, hipStream_t s) {
+                  int P, void* ws, typename E::Out* out, hipStream_t s, bool seed = true) {
   if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg: K must be > 0 (got %lld)", K);
   if (!x || !w || !out) return fail(FEDAGG_EINVAL, "fedavg: NULL argument");
   if (P < 0 || (P > 0 && !idx)) return fail(FEDAGG_EINVAL, "fedavg: bad pairwise index list (P=%lld)", P);
@@ -1653,7 +1709,7 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const bool nts = g_nt_store < 0 ? K >= NT_STORE_MIN_K : g_nt_store != 0;
-    launch_fedavg<E>(grid, s, a, pw, kc, k0 == 0 ? 1 : 0, nvec, M, out, nts, sh);
+    launch_fedavg<E>(grid, s, a, pw, kc, (k0 == 0 && seed) ? 1 : 0, nvec, M, out, nts, sh);
     int rc = check_launch("fedavg_kernel");
     if (rc) return rc;
   }
@@ -1692,6 +1748,66 @@ int scaffold_pairwise_launch(const TIn* const* d, const TIn* const* cv, const TI
     }
     hipLaunchKernelGGL((scaffold_tree_kernel<TIn>), dim3(1), dim3(64), 0, s, (const double*)ws_d, ws_c, c,
                        (int64_t)K, ix, pc, lr, dout, cout);
+    int rc = check_launch("scaffold_tree_kernel");
+    if (rc) return rc;
+  }
+  return FEDAGG_OK;
+}
+
+// Client-block products for a Scaffold pairwise tree held by several launches / ranks.  ws layout:
+// delta terms [P][Ktot] doubles, then control-variate terms [P][Ktot + 1] (the last column is c,
+// written by the finish step); this block's clients go to columns kbase .. kbase + K - 1.
+template <typename TIn>
+int scaffold_products_launch(const TIn* const* d, const TIn* const* cv, const double* w, int K, int kbase, int Ktot,
+                             const uint64_t* idx, int P, double* ws, hipStream_t s) {
+  if (P == 0) return FEDAGG_OK;
+  if (K <= 0 || P < 0 || !d || !cv || !w || !idx || !ws || kbase < 0 || kbase + K > Ktot)
+    return fail(FEDAGG_EINVAL, "scaffold_products: invalid argument (K=%lld)", K);
+  for (int k = 0; k < K; ++k)
+    if (!d[k] || !cv[k]) return fail(FEDAGG_EINVAL, "scaffold_products: client pointer %lld is NULL", k);
+  double* ws_d = ws;
+  double* ws_c = ws + (size_t)P * Ktot;
+  for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
+    const int pc = (P - p0) < FEDAGG_MAX_PAIRWISE ? (P - p0) : FEDAGG_MAX_PAIRWISE;
+    IdxArgs ix;
+    memset(&ix, 0, sizeof(ix));
+    for (int p = 0; p < pc; ++p) ix.idx[p] = idx[p0 + p];
+    for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
+      const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
+      ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a;
+      memset(&a, 0, sizeof(a));
+      for (int k = 0; k < kc; ++k) {
+        a.d[k] = d[k0 + k];
+        a.cv[k] = cv[k0 + k];
+        a.w[k] = w[k0 + k];
+      }
+      const unsigned g = (unsigned)((pc * kc + FA_BLOCK - 1) / FA_BLOCK);
+      hipLaunchKernelGGL((scaffold_gather_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD>), dim3(g), dim3(FA_BLOCK), 0, s, a,
+                         kc, kbase + k0, ix, pc, (int64_t)Ktot, ws_d + (size_t)p0 * Ktot,
+                         ws_c + (size_t)p0 * (Ktot + 1));
+      int rc = check_launch("scaffold_gather_kernel");
+      if (rc) return rc;
+    }
+  }
+  return FEDAGG_OK;
+}
+
+// dout[idx_p] = lr * (0 + pairwise(delta terms)), cout[idx_p] = 0 + pairwise(cv terms, c last).
+template <typename TIn>
+int scaffold_finish_launch(double* ws, int Ktot, const TIn* c, const uint64_t* idx, int P, double lr, double* dout,
+                           double* cout, hipStream_t s) {
+  if (P == 0) return FEDAGG_OK;
+  if (Ktot <= 0 || P < 0 || !ws || !c || !idx || !dout || !cout)
+    return fail(FEDAGG_EINVAL, "scaffold_finish: invalid argument (K=%lld)", Ktot);
+  double* ws_d = ws;
+  double* ws_c = ws + (size_t)P * Ktot;
+  for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
+    const int pc = (P - p0) < FEDAGG_MAX_PAIRWISE ? (P - p0) : FEDAGG_MAX_PAIRWISE;
+    IdxArgs ix;
+    memset(&ix, 0, sizeof(ix));
+    for (int p = 0; p < pc; ++p) ix.idx[p] = idx[p0 + p];
+    hipLaunchKernelGGL((scaffold_tree_kernel<TIn>), dim3(1), dim3(64), 0, s, (const double*)(ws_d + (size_t)p0 * Ktot),
+                       ws_c + (size_t)p0 * (Ktot + 1), c, (int64_t)Ktot, ix, pc, lr, dout, cout);
     int rc = check_launch("scaffold_tree_kernel");
     if (rc) return rc;
   }
@@ -1791,16 +1907,20 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
 #undef SC_ARGS
 }
 
+// seed = false: both accumulators start from d_dout / d_cout (partial sums of the clients before
+// this block); finish = false: the sums are left as they are (no + c, no lr), c is not read.
 template <typename TIn>
 int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, const double* w, int K, uint64_t M,
-                    const uint64_t* idx, int P, void* ws, double lr, double* dout, double* cout, hipStream_t s) {
+                    const uint64_t* idx, int P, void* ws, double lr, double* dout, double* cout, hipStream_t s,
+                    bool seed = true, bool finish = true) {
   if (K <= 0) return fail(FEDAGG_EINVAL, "scaffold: K must be > 0 (got %lld)", K);
-  if (!d || !cv || !c || !w || !dout || !cout) return fail(FEDAGG_EINVAL, "scaffold: NULL argument");
+  if (!d || !cv || (finish && !c) || !w || !dout || !cout) return fail(FEDAGG_EINVAL, "scaffold: NULL argument");
   if (P < 0 || (P > 0 && !idx)) return fail(FEDAGG_EINVAL, "scaffold: bad pairwise index list (P=%lld)", P);
+  if (P > 0 && !(seed && finish)) return fail(FEDAGG_EINVAL, "scaffold: pairwise patch needs a whole chain (P=%lld)", P);
   for (int p = 0; p < P; ++p)
     if (idx[p] >= M) return fail(FEDAGG_EINVAL, "scaffold: pairwise index %lld out of range", (long long)idx[p]);
   if (M == 0) return FEDAGG_OK;
-  bool vec = aligned16(c) && aligned16(dout) && aligned16(cout);
+  bool vec = (!finish || aligned16(c)) && aligned16(dout) && aligned16(cout);
   for (int k = 0; k < K; ++k) {
     if (!d[k] || !cv[k]) return fail(FEDAGG_EINVAL, "scaffold: client pointer %lld is NULL", k);
     vec = vec && aligned16(d[k]) && aligned16(cv[k]);
@@ -1839,7 +1959,7 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       pw.n = P;
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
-    const int first = k0 == 0, last = (k0 + kc) == K;
+    const int first = k0 == 0 && seed, last = (k0 + kc) == K && finish;
     if (bsplit)
       launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     else
@@ -2028,6 +2148,86 @@ int fedagg_scale_cast(const void* d_in, int in_kind, double w, void* d_out, int 
   hipLaunchKernelGGL(scale_cast_kernel, dim3(grid_for(n)), dim3(FA_BLOCK), 0, (hipStream_t)stream, d_in, in_kind, w,
                      d_out, out_kind, n);
   return check_launch("scale_cast_kernel");
+}
+
+// ---- client-sharded building blocks (chain / partial sums / split pairwise trees) ----
+int fedagg_fedavg_chain_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
+                            float* d_out, void* stream) {
+  return fedavg_launch<F32>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
+}
+int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
+                             float* d_out, void* stream) {
+  return fedavg_launch<BF16>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
+}
+int fedagg_fedavg_chain_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, int seed,
+                            double* d_out, void* stream) {
+  return fedavg_launch<F64>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
+}
+int fedagg_fedavg_chain_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, uint64_t M, int seed,
+                            uint16_t* d_out, void* stream) {
+  if (!h_w || K <= 0) return fail(FEDAGG_EINVAL, "fedavg_chain_f16: invalid weights (K=%lld)", K);
+  return fedavg_launch<F16>(d_clients, reinterpret_cast<const _Float16*>(h_w), K, M, nullptr, 0, nullptr, d_out,
+                            (hipStream_t)stream, seed != 0);
+}
+
+int fedagg_pairwise_products_f32(const float* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,
+                                 int P, int64_t stride, int kbase, float* d_ws, void* stream) {
+  return pairwise_products_launch<F32>(d_clients, h_w, K, h_idx, P, stride, kbase, d_ws, (hipStream_t)stream);
+}
+int fedagg_pairwise_products_bf16(const uint16_t* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,
+                                  int P, int64_t stride, int kbase, float* d_ws, void* stream) {
+  return pairwise_products_launch<BF16>(d_clients, h_w, K, h_idx, P, stride, kbase, d_ws, (hipStream_t)stream);
+}
+int fedagg_pairwise_products_f64(const double* const* d_clients, const double* h_w, int K, const uint64_t* h_idx,
+                                 int P, int64_t stride, int kbase, double* d_ws, void* stream) {
+  return pairwise_products_launch<F64>(d_clients, h_w, K, h_idx, P, stride, kbase, d_ws, (hipStream_t)stream);
+}
+int fedagg_pairwise_products_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, const uint64_t* h_idx,
+                                 int P, int64_t stride, int kbase, float* d_ws, void* stream) {
+  if (!h_w || K <= 0) return fail(FEDAGG_EINVAL, "pairwise_products_f16: invalid weights (K=%lld)", K);
+  return pairwise_products_launch<F16>(d_clients, reinterpret_cast<const _Float16*>(h_w), K, h_idx, P, stride, kbase,
+                                       d_ws, (hipStream_t)stream);
+}
+int fedagg_pairwise_finish_f32(const float* d_ws, int64_t n, int64_t stride, const uint64_t* h_idx, int P,
+                               float* d_out, void* stream) {
+  return pairwise_finish_launch<F32>(d_ws, n, stride, h_idx, P, d_out, (hipStream_t)stream);
+}
+int fedagg_pairwise_finish_f64(const double* d_ws, int64_t n, int64_t stride, const uint64_t* h_idx, int P,
+                               double* d_out, void* stream) {
+  return pairwise_finish_launch<F64>(d_ws, n, stride, h_idx, P, d_out, (hipStream_t)stream);
+}
+int fedagg_pairwise_finish_f16(const float* d_ws, int64_t n, int64_t stride, const uint64_t* h_idx, int P,
+                               uint16_t* d_out, void* stream) {
+  return pairwise_finish_launch<F16>(d_ws, n, stride, h_idx, P, d_out, (hipStream_t)stream);
+}
+
+int fedagg_scaffold_chain_f32(const float* const* d_delta, const float* const* d_cv, const float* d_c,
+                              const double* h_w, int K, uint64_t M, int seed, int finish, double lr,
+                              double* d_delta_out, double* d_c_out, void* stream) {
+  return scaffold_launch<float>(d_delta, d_cv, d_c, h_w, K, M, nullptr, 0, nullptr, lr, d_delta_out, d_c_out,
+                                (hipStream_t)stream, seed != 0, finish != 0);
+}
+int fedagg_scaffold_chain_f64(const double* const* d_delta, const double* const* d_cv, const double* d_c,
+                              const double* h_w, int K, uint64_t M, int seed, int finish, double lr,
+                              double* d_delta_out, double* d_c_out, void* stream) {
+  return scaffold_launch<double>(d_delta, d_cv, d_c, h_w, K, M, nullptr, 0, nullptr, lr, d_delta_out, d_c_out,
+                                 (hipStream_t)stream, seed != 0, finish != 0);
+}
+int fedagg_scaffold_products_f32(const float* const* d_delta, const float* const* d_cv, const double* h_w, int K,
+                                 int kbase, int Ktot, const uint64_t* h_idx, int P, double* d_ws, void* stream) {
+  return scaffold_products_launch<float>(d_delta, d_cv, h_w, K, kbase, Ktot, h_idx, P, d_ws, (hipStream_t)stream);
+}
+int fedagg_scaffold_products_f64(const double* const* d_delta, const double* const* d_cv, const double* h_w, int K,
+                                 int kbase, int Ktot, const uint64_t* h_idx, int P, double* d_ws, void* stream) {
+  return scaffold_products_launch<double>(d_delta, d_cv, h_w, K, kbase, Ktot, h_idx, P, d_ws, (hipStream_t)stream);
+}
+int fedagg_scaffold_finish_f32(double* d_ws, int Ktot, const float* d_c, const uint64_t* h_idx, int P, double lr,
+                               double* d_delta_out, double* d_c_out, void* stream) {
+  return scaffold_finish_launch<float>(d_ws, Ktot, d_c, h_idx, P, lr, d_delta_out, d_c_out, (hipStream_t)stream);
+}
+int fedagg_scaffold_finish_f64(double* d_ws, int Ktot, const double* d_c, const uint64_t* h_idx, int P, double lr,
+                               double* d_delta_out, double* d_c_out, void* stream) {
+  return scaffold_finish_launch<double>(d_ws, Ktot, d_c, h_idx, P, lr, d_delta_out, d_c_out, (hipStream_t)stream);
 }
 
 int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid, void* stream) {

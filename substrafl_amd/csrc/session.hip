@@ -37,9 +37,8 @@ namespace fedagg_internal {
 void set_error(const char* msg);
 }
 
-using fedagg_host::Done;
-using fedagg_host::gather_range;
 using fedagg_host::Pool;
+using fedagg_host::Ring;
 
 namespace {
 
@@ -72,29 +71,41 @@ struct fedagg_session {
   int slots = 12;
   void* ring_base = nullptr;  // one pinned block: slot i at ring_base + i * chunk_bytes, so
                               // adjacent slots can take one larger DMA (fetch super-chunks)
-  std::vector<void*> ring;
+  Ring ring;
   std::vector<hipEvent_t> ring_ev;
-  std::vector<bool> ring_used;
   void* dbuf[FEDAGG_SESSION_BUFFERS] = {};
   uint64_t dbytes[FEDAGG_SESSION_BUFFERS] = {};
+  hipEvent_t tev[FEDAGG_SESSION_EVENTS] = {};  // timing events (fedagg_session_event_*)
   Pool* pool = nullptr;
   double last_stage_s = 0, last_fetch_s = 0;
+  uint64_t fail_copy_after = 0;  // test knob: the n-th copy of the session fails (0 = never)
+  uint64_t copies = 0;
 
   int ensure_ring() {
-    if ((int)ring.size() == slots) return FEDAGG_OK;
+    if (ring.size() == slots && ring.chunk_bytes == chunk_bytes) return FEDAGG_OK;
     release_ring();
-    ring.assign(slots, nullptr);
+    ring.slot.assign(slots, nullptr);
     ring_ev.assign(slots, nullptr);
-    ring_used.assign(slots, false);
-    HIP_TRY(hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocDefault));
+    ring.used.assign(slots, false);
+    ring.chunk_bytes = chunk_bytes;
+    hipError_t e = hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      ring_base = nullptr;
+      release_ring();
+      return hip_fail("hipHostMalloc(staging ring)", e);
+    }
     for (int i = 0; i < slots; ++i) {
-      ring[i] = static_cast<char*>(ring_base) + (size_t)i * chunk_bytes;
-      HIP_TRY(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming));
+      ring.slot[i] = static_cast<char*>(ring_base) + (size_t)i * chunk_bytes;
+      if ((e = hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming)) != hipSuccess) {
+        ring_ev[i] = nullptr;
+        release_ring();
+        return hip_fail("hipEventCreate(staging ring)", e);
+      }
     }
     return FEDAGG_OK;
   }
   void release_ring() {
-    for (size_t i = 0; i < ring.size(); ++i) {
+    for (size_t i = 0; i < ring_ev.size(); ++i) {
       if (ring_ev[i]) {
         (void)hipEventSynchronize(ring_ev[i]);
         (void)hipEventDestroy(ring_ev[i]);
@@ -102,9 +113,10 @@ struct fedagg_session {
     }
     if (ring_base) (void)hipHostFree(ring_base);
     ring_base = nullptr;
-    ring.clear();
+    ring.slot.clear();
+    ring.used.clear();
+    ring.chunk_bytes = 0;
     ring_ev.clear();
-    ring_used.clear();
   }
   Pool& workers() {
     if (!pool || pool->size() != threads) {
@@ -117,10 +129,31 @@ struct fedagg_session {
 
 namespace {
 
-
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+
+// The copy engine of host_pool.h's pipelines on HIP: queue 0 = the session stream, queue 1 = the
+// second H2D queue; one event per ring slot.
+struct HipEngine {
+  fedagg_session* s;
+  bool injected() { return s->fail_copy_after && ++s->copies >= s->fail_copy_after; }
+  int h2d(int q, void* d, const void* h, uint64_t n) {
+    if (injected()) return hip_fail("hipMemcpyAsync(H2D) [injected by the fail_copy_after knob]", hipErrorUnknown);
+    hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, q ? s->xstream : s->stream);
+    return e == hipSuccess ? FEDAGG_OK : hip_fail("hipMemcpyAsync(H2D)", e);
+  }
+  int d2h(void* h, const void* d, uint64_t n) {
+    if (injected()) return hip_fail("hipMemcpyAsync(D2H) [injected by the fail_copy_after knob]", hipErrorUnknown);
+    hipError_t e = hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s->stream);
+    return e == hipSuccess ? FEDAGG_OK : hip_fail("hipMemcpyAsync(D2H)", e);
+  }
+  int mark(int slot, int q) {
+    hipError_t e = hipEventRecord(s->ring_ev[slot], q ? s->xstream : s->stream);
+    return e == hipSuccess ? FEDAGG_OK : hip_fail("hipEventRecord(ring)", e);
+  }
+  void wait(int slot) { (void)hipEventSynchronize(s->ring_ev[slot]); }
+};
 
 }  // namespace
 
@@ -163,6 +196,8 @@ void fedagg_session_destroy(fedagg_session* s) {
   s->release_ring();
   for (int i = 0; i < FEDAGG_SESSION_BUFFERS; ++i)
     if (s->dbuf[i]) (void)hipFree(s->dbuf[i]);
+  for (int i = 0; i < FEDAGG_SESSION_EVENTS; ++i)
+    if (s->tev[i]) (void)hipEventDestroy(s->tev[i]);
   (void)hipEventDestroy(s->join_ev);
   (void)hipStreamDestroy(s->xstream);
   (void)hipStreamDestroy(s->stream);
@@ -188,6 +223,9 @@ int fedagg_session_set(fedagg_session* s, const char* key, long long value) {
   } else if (!strcmp(key, "slots") && value >= 2 && value <= 1024) {
     s->release_ring();
     s->slots = (int)std::max<long long>(value, s->threads + 1);
+  } else if (!strcmp(key, "fail_copy_after") && value >= 0) {  // tests: error paths of stage/fetch
+    s->fail_copy_after = (uint64_t)value;
+    s->copies = 0;
   } else {
     fedagg_internal::set_error("fedagg_session_set: unknown key or bad value");
     return FEDAGG_EINVAL;
@@ -247,12 +285,13 @@ int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int 
   return fedagg_session_stage_range(s, d_dst, ld_bytes, K, nseg, h_seg, seg_bytes, 0, row);
 }
 
-int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
-                               const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
-                               uint64_t byte_hi) {
+namespace {
+
+// shared argument checks and set-up of the staging entry points; returns the row length in bytes
+int stage_prepare(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg, const void* const* h_seg,
+                  const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, uint64_t* row_out) {
   if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) || byte_hi < byte_lo)
     return FEDAGG_EINVAL;
-  const double t0 = now_s();
   HIP_TRY(hipSetDevice(s->device));
   int rc = s->ensure_ring();
   if (rc) return rc;
@@ -273,55 +312,63 @@ int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes
         fedagg_internal::set_error("fedagg_session_stage: NULL host segment");
         return FEDAGG_EINVAL;
       }
-  const uint64_t cb = s->chunk_bytes;
-  const uint64_t per_row = row ? (row + cb - 1) / cb : 0;
-  const uint64_t units = per_row * (uint64_t)K;
-  const int R = (int)s->ring.size();
-  Pool& pool = s->workers();
-  const bool two = s->copy_streams > 1 && units > 1;
+  *row_out = row;
+  return FEDAGG_OK;
+}
+
+int stage_run(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg, const void* const* h_seg,
+              const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t row, int check_esz, uint64_t* mismatches) {
+  const double t0 = now_s();
+  const bool two = s->copy_streams > 1;
   if (two) {  // the second queue starts after everything already enqueued on the session stream
     HIP_TRY(hipEventRecord(s->join_ev, s->stream));
     HIP_TRY(hipStreamWaitEvent(s->xstream, s->join_ev, 0));
   }
-  std::vector<Done> done(units ? std::min<uint64_t>(units, (uint64_t)R) : 1);
-  // In-order window: unit u lives in slot u % R.  R-1 packs run ahead of the copy being
-  // enqueued; a slot is refilled only after the copy that read it completed, while the next
-  // copy is already in flight, so the link never waits on the main thread.
-  uint64_t next_submit = 0;
-  auto submit = [&](uint64_t u) {
-    const int slot = (int)(u % R);
-    if (s->ring_used[slot]) (void)hipEventSynchronize(s->ring_ev[slot]);  // H2D of unit u-R done
-    s->ring_used[slot] = false;
-    Done& d = done[slot];
-    d.done = false;
-    const int k = (int)(u / per_row);
-    const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
-    const void* const* segs = h_seg + (size_t)k * nseg;
-    char* dst = static_cast<char*>(s->ring[slot]);
-    pool.submit([=, &d] {
-      gather_range(segs, seg_bytes, nseg, byte_lo + a, byte_lo + b, dst);
-      d.set();
-    });
-  };
-  for (; next_submit < units && next_submit + 1 < (uint64_t)R; ++next_submit) submit(next_submit);
-  for (uint64_t u = 0; u < units; ++u) {
-    const int slot = (int)(u % R);
-    done[slot].wait();
-    const int k = (int)(u / per_row);
-    const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
-    char* dst = static_cast<char*>(d_dst) + (uint64_t)k * ld_bytes + a;
-    hipStream_t q = (two && (u & 1)) ? s->xstream : s->stream;
-    HIP_TRY(hipMemcpyAsync(dst, s->ring[slot], b - a, hipMemcpyHostToDevice, q));
-    HIP_TRY(hipEventRecord(s->ring_ev[slot], q));
-    s->ring_used[slot] = true;
-    if (next_submit < units) submit(next_submit++);
-  }
+  HipEngine eng{s};
+  int rc = fedagg_host::stage_pipeline(eng, s->workers(), s->ring, h_seg, seg_bytes, nseg, K, byte_lo, row,
+                                       static_cast<char*>(d_dst), ld_bytes, two, check_esz, mismatches);
   if (two) {  // work enqueued on the session stream after this call sees every staged byte
-    HIP_TRY(hipEventRecord(s->join_ev, s->xstream));
-    HIP_TRY(hipStreamWaitEvent(s->stream, s->join_ev, 0));
+    hipError_t e = hipEventRecord(s->join_ev, s->xstream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s->stream, s->join_ev, 0);
+    if (e != hipSuccess && !rc) rc = hip_fail("fedagg_session_stage: join of the copy queues", e);
   }
   s->last_stage_s = now_s() - t0;
-  return FEDAGG_OK;
+  return rc;
+}
+
+}  // namespace
+
+int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
+                               const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
+                               uint64_t byte_hi) {
+  uint64_t row = 0;
+  int rc = stage_prepare(s, d_dst, ld_bytes, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row);
+  if (rc) return rc;
+  return stage_run(s, d_dst, ld_bytes, K, nseg, h_seg, seg_bytes, byte_lo, row, 0, nullptr);
+}
+
+int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, const void* const* h_seg,
+                               const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, int kind,
+                               uint64_t* mismatches) {
+  if (!mismatches || (kind != FEDAGG_F32 && kind != FEDAGG_F64)) {
+    fedagg_internal::set_error("fedagg_session_stage_check: kind must be FEDAGG_F32 or FEDAGG_F64");
+    return FEDAGG_EINVAL;
+  }
+  const int esz = kind == FEDAGG_F64 ? 8 : 4;
+  for (int i = 0; i < nseg && seg_bytes; ++i)
+    if (seg_bytes[i] % esz) {
+      fedagg_internal::set_error("fedagg_session_stage_check: segment not a whole number of elements");
+      return FEDAGG_EINVAL;
+    }
+  if (byte_lo % esz || byte_hi % esz) {
+    fedagg_internal::set_error("fedagg_session_stage_check: byte range not element-aligned");
+    return FEDAGG_EINVAL;
+  }
+  uint64_t row = 0;
+  int rc = stage_prepare(s, d_dst, byte_hi - byte_lo, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row);
+  if (rc) return rc;
+  *mismatches = 0;
+  return stage_run(s, d_dst, row, K, nseg, h_seg, seg_bytes, byte_lo, row, esz, mismatches);
 }
 
 int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes) {
@@ -330,48 +377,29 @@ int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint
   HIP_TRY(hipSetDevice(s->device));
   int rc = s->ensure_ring();
   if (rc) return rc;
-  const uint64_t cb = s->chunk_bytes;
-  const int R = (int)s->ring.size();
-  // D2H in super-chunks of G adjacent slots (one DMA of G * chunk_bytes: 16 MiB copies run at
-  // 55 GB/s where 4 MiB ones reach 49, profiles/r01_h2d_probe.log); each slot of a super-chunk is
-  // then copied out by its own worker once the DMA's event completes.  Groups rotate over the ring.
-  const int G = std::max(1, std::min(4, R / 2));
-  const int NG = R / G;
-  const uint64_t sb = cb * (uint64_t)G;
-  const uint64_t units = (bytes + sb - 1) / sb;
-  Pool& pool = s->workers();
-  std::vector<Done> done(R);
-  std::vector<bool> pending(R, false);
-  for (uint64_t u = 0; u < units; ++u) {
-    const int g0 = (int)(u % (uint64_t)NG) * G;  // first slot of this group
-    for (int i = 0; i < G; ++i)
-      if (pending[g0 + i]) done[g0 + i].wait();
-    const uint64_t a = u * sb, b = std::min(bytes, a + sb);
-    HIP_TRY(hipMemcpyAsync(s->ring[g0], static_cast<const char*>(d_src) + a, b - a, hipMemcpyDeviceToHost,
-                           s->stream));
-    HIP_TRY(hipEventRecord(s->ring_ev[g0], s->stream));
-    hipEvent_t ev = s->ring_ev[g0];
-    for (int i = 0; i < G; ++i) {
-      const uint64_t pa = a + (uint64_t)i * cb;
-      if (pa >= b) break;
-      const uint64_t pb = std::min(b, pa + cb);
-      const int slot = g0 + i;
-      s->ring_used[slot] = i == 0;
-      done[slot].done = false;
-      pending[slot] = true;
-      char* src = static_cast<char*>(s->ring[slot]);
-      char* dst = static_cast<char*>(h_dst) + pa;
-      Done* d = &done[slot];
-      pool.submit([=] {
-        (void)hipEventSynchronize(ev);
-        memcpy(dst, src, pb - pa);
-        d->set();
-      });
-    }
-  }
-  for (int i = 0; i < R; ++i)
-    if (pending[i]) done[i].wait();
+  // D2H in super-chunks of adjacent slots (16 MiB copies run at 55 GB/s where 4 MiB ones reach
+  // 49, profiles/r01_h2d_probe.log), copied out of the ring by the workers (host_pool.h)
+  HipEngine eng{s};
+  rc = fedagg_host::fetch_pipeline(eng, s->workers(), s->ring, static_cast<const char*>(d_src),
+                                   static_cast<char*>(h_dst), bytes);
   s->last_fetch_s = now_s() - t0;
+  return rc;
+}
+
+int fedagg_session_event_record(fedagg_session* s, int ev) {
+  if (!s || ev < 0 || ev >= FEDAGG_SESSION_EVENTS) return FEDAGG_EINVAL;
+  HIP_TRY(hipSetDevice(s->device));
+  if (!s->tev[ev]) HIP_TRY(hipEventCreate(&s->tev[ev]));
+  HIP_TRY(hipEventRecord(s->tev[ev], s->stream));
+  return FEDAGG_OK;
+}
+
+int fedagg_session_event_elapsed(fedagg_session* s, int ev0, int ev1, float* ms) {
+  if (!s || !ms || ev0 < 0 || ev1 < 0 || ev0 >= FEDAGG_SESSION_EVENTS || ev1 >= FEDAGG_SESSION_EVENTS ||
+      !s->tev[ev0] || !s->tev[ev1])
+    return FEDAGG_EINVAL;
+  HIP_TRY(hipEventSynchronize(s->tev[ev1]));
+  HIP_TRY(hipEventElapsedTime(ms, s->tev[ev0], s->tev[ev1]));
   return FEDAGG_OK;
 }
 

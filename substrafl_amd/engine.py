@@ -273,27 +273,34 @@ class AggregationEngine:
     _B_BUCKET, _B_OUT, _B_WS, _B_TMP, _B_CV, _B_C, _B_COUT, _B_CNT = range(8)
 
     def __init__(self, device: Optional[int] = None, pack_threads: Optional[int] = None,
-                 max_bucket_bytes: Optional[int] = None):
+                 max_bucket_bytes: Optional[int] = None, c_check: str = "host"):
         self._device_index = device
         self._pack_threads = pack_threads
+        if c_check not in ("host", "device"):
+            raise ValueError("c_check must be 'host' or 'device'")
+        # where Scaffold's server-control-variate equality check runs (scaffold.py:193-196)
+        self.c_check = os.environ.get("FEDAGG_C_CHECK", c_check)
         # HBM the staged buckets of one call may take before the call is streamed through the GPU
         # in parameter ranges (multi_device.MultiDeviceEngine with this one device); default:
         # 85 % of the device's free HBM at call time
         self.max_bucket_bytes = max_bucket_bytes
         self._ooc = None
         self.last_timing: Dict[str, float] = {}
-        # rows already on the device from ingest(): slot -> (d_bucket, ld_bytes, {k: row arrays})
-        self._prestaged: Dict[int, Tuple[int, int, Dict[int, List[np.ndarray]]]] = {}
+        # rows already on the device from ingest(): slot -> (d_bucket, ld_bytes, {k: row arrays},
+        # write generation of the slot after the ingest) -- valid only while nothing else (another
+        # engine on this GPU's shared session, or this engine's own other paths) wrote the slot
+        self._prestaged: Dict[int, list] = {}
 
-    def _out_of_core(self, need_bytes: int):
+    def _out_of_core(self, need_bytes: int, slots: Sequence[int]):
         """The range-streaming engine when ``need_bytes`` of buckets exceed this GPU's budget
-        (K x M beyond 288 GB on one MI355X), else None."""
+        (K x M beyond 288 GB on one MI355X), else None.  ``slots``: the session buffers the
+        in-core call would (re)use; only their bytes count as available besides the free HBM."""
         from .multi_device import HBM_HEADROOM, MultiDeviceEngine
 
         if self.max_bucket_bytes is not None:
             budget = int(self.max_bucket_bytes)
         else:
-            free = runtime.device_memory(self._index())[0] + self.session().held_bytes()
+            free = runtime.device_memory(self._index())[0] + self.session().held_bytes(slots)
             budget = int(free * HBM_HEADROOM)
         if need_bytes <= budget:
             return None
@@ -353,14 +360,18 @@ class AggregationEngine:
                     plan = False
                     self._prestaged = {}
             states = [f.result() for f in futures]
+        s = getattr(self, "_prestaged_session", None)
+        for slot, rec in self._prestaged.items():  # seal: the slots as this ingest left them
+            rec.append(s.generation(slot) if s is not None else -1)
         self.last_ingest = {"load_and_stage_s": time.perf_counter() - t0, "prestaged_clients": staged}
         return states
 
     def _ingest_plan(self, state, strategy: str, K: int):
         """Layouts and buffers for staging rows shaped like ``state``'s (None: do not prestage)."""
         if strategy == "scaffold":
-            lists = (("parameters_update", self._B_BUCKET), ("control_variate_update", self._B_CV),
-                     ("server_control_variate", self._B_C))
+            # the server control variates are not prestaged: the aggregation stages ONE copy and
+            # checks the others against it on the host (Session.stage_check)
+            lists = (("parameters_update", self._B_BUCKET), ("control_variate_update", self._B_CV))
         else:
             lists = (("parameters_update", self._B_BUCKET),)
         rows = []
@@ -372,7 +383,9 @@ class AggregationEngine:
                 return None  # per-layer dtype groups are staged by the aggregation call
             rows.append(row)
         if strategy == "scaffold":  # scaffold engine: fp32 buckets only when every list is fp32
-            all32 = all(r[0].dtype == np.float32 for r in rows)
+            c_row = list(getattr(state, "server_control_variate", None) or [])
+            all32 = all(r[0].dtype == np.float32 for r in rows) and all(
+                isinstance(a, np.ndarray) and a.dtype == np.float32 for a in c_row)
             targets = [np.dtype(np.float32 if all32 else np.float64)] * len(rows)
         else:  # FedAvg: NumPy's product type of the layer (ints -> fp64)
             targets = [np.result_type(rows[0][0].dtype, 1.0)]
@@ -384,8 +397,9 @@ class AggregationEngine:
             layout = BucketLayout(list(range(len(row))), [a.shape for a in row], dt)
             ld_bytes = layout.ld * dt.itemsize
             d = s.buffer(slot, K * ld_bytes)
-            self._prestaged[slot] = (d, ld_bytes, {})
+            self._prestaged[slot] = [d, ld_bytes, {}]
             plan.append((field, slot, layout, d, ld_bytes, row[0].dtype))
+        self._prestaged_session = s
         return plan
 
     def _ingest_row(self, plan, k: int, state) -> bool:
@@ -404,7 +418,9 @@ class AggregationEngine:
     def _take_prestaged(self, slot: int, d_bucket: int, ld_bytes: int, rows) -> bool:
         """True when every row was staged by :meth:`ingest` from these very arrays."""
         rec = self._prestaged.pop(slot, None)
-        if rec is None or rec[0] != d_bucket or rec[1] != ld_bytes or len(rec[2]) != len(rows):
+        if rec is None or len(rec) != 4 or rec[0] != d_bucket or rec[1] != ld_bytes or len(rec[2]) != len(rows):
+            return False
+        if rec[3] != self.session().generation(slot):  # the slot was written since the ingest
             return False
         for k, row in enumerate(rows):
             got = rec[2].get(k)
@@ -491,7 +507,7 @@ class AggregationEngine:
             R = np.dtype(rstr)
             direct = mixed is None and all(a.dtype == R for pu in parameters_updates for a in pu)
             need = (K + 1) * BucketLayout(range(L), [a.shape for a in parameters_updates[0]], R).ld * R.itemsize
-            ooc = self._out_of_core(need) if direct else None
+            ooc = self._out_of_core(need, (self._B_BUCKET, self._B_OUT, self._B_WS)) if direct else None
             if ooc is not None:
                 out = ooc.fedavg(parameters_updates, n_samples, wire)
                 self.last_timing = {"out_of_core": ooc.last_timing}
@@ -570,7 +586,9 @@ class AggregationEngine:
         same = [g.shape for g in lay_d.segments] == [g.shape for g in lay_c.segments] == \
             [g.shape for g in lay_s.segments]
         if same and all(a.dtype == sdt for lst in lists for client in lst for a in client):
-            ooc = self._out_of_core(3 * K * lay_d.ld * sdt.itemsize + 2 * lay_d.ld * 8)
+            ooc = self._out_of_core(3 * K * lay_d.ld * sdt.itemsize + 2 * lay_d.ld * 8,
+                                    (self._B_BUCKET, self._B_CV, self._B_C, self._B_OUT, self._B_COUT, self._B_WS,
+                                     self._B_CNT))
             if ooc is not None:
                 out = ooc.scaffold(*lists, n_samples, aggregation_lr, wire)
                 self.last_timing = {"out_of_core": ooc.last_timing}
@@ -586,28 +604,44 @@ class AggregationEngine:
         # assert_array_equal holds by identity, so one copy is staged and the check is skipped
         same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
                      for row in server_control_variates[1:])
+        # otherwise (task process: K separately unpickled copies) the check runs on the host while
+        # the bytes are staged: ONE copy crosses PCIe, the others are compared with it on the pack
+        # workers (Session.stage_check); the device check over K staged copies stays as a knob
+        # (c_check="device") and for c lists of another dtype than the buckets
+        host_c = (not same_c and self.c_check == "host"
+                  and all(a.dtype == sdt for row in server_control_variates for a in row))
         pre = 0
+        host_mism = 0
         for rows, lay, d, slot in ((parameters_updates, lay_d, d_d, self._B_BUCKET),
-                                   (control_variate_updates, lay_c, d_cv, self._B_CV),
-                                   (server_control_variates[:1] if same_c else server_control_variates, lay_s, d_cc,
-                                    self._B_C)):
+                                   (control_variate_updates, lay_c, d_cv, self._B_CV)):
             rows = [list(r) for r in rows]
             if self._take_prestaged(slot, d, lay.ld * isz, rows):
                 pre += 1
             else:
                 self._stage_rows(s, rows, lay, d)
+        c_rows = [list(r) for r in server_control_variates]
+        if same_c:
+            self._stage_rows(s, c_rows[:1], lay_s, d_cc)
+        elif host_c:
+            flats = [flat_of(r) for r in c_rows]
+            if all(f is not None and f.size == lay_s.M for f in flats):
+                c_rows = [[f] for f in flats]  # flat wire format: one segment per client
+            host_mism = s.stage_check(d_cc, c_rows, sdt)
+        else:
+            self._stage_rows(s, c_rows, lay_s, d_cc)
         self._prestaged = {}
-        tm["prestaged"] = pre == 3
-        tm["c_check"] = "identity" if same_c else "device"
+        tm["prestaged"] = pre == 2
+        tm["c_check"] = "identity" if same_c else ("host" if host_c else "device")
         tm["stage_s"] = time.perf_counter() - t0
         t1 = time.perf_counter()
         cnt = s.buffer(self._B_CNT, 8)
         s.memset(cnt, 0, 8)
-        if not same_c:
+        if not same_c and not host_c:
             equal_count(kind, [d_cc + k * lay_s.ld * isz for k in range(K)], lay_s.M, cnt, s.stream)
         dout = s.buffer(self._B_OUT, lay_d.ld * 8)
         cout = s.buffer(self._B_COUT, lay_c.ld * 8)
-        ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, max(1, lay_d.pairwise_idx.size), 8))
+        ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(
+            K, max(1, lay_d.pairwise_idx.size, lay_c.pairwise_idx.size), 8))
         rows_d = [d_d + k * lay_d.ld * isz for k in range(K)]
         rows_c = [d_cv + k * lay_c.ld * isz for k in range(K)]
         if [g.shape for g in lay_d.segments] == [g.shape for g in lay_c.segments]:
@@ -632,7 +666,7 @@ class AggregationEngine:
         avg = [a for _, a in lay_d.unpack(out_d, wire)]
         new_c = [a for _, a in lay_c.unpack(out_c, wire)]
         tm["total_s"] = time.perf_counter() - t_start
-        return int(mism[0]), new_c, avg
+        return int(mism[0]) + host_mism, new_c, avg
 
 
 _default_engine: Optional[AggregationEngine] = None

@@ -74,6 +74,9 @@ class MultiDeviceEngine:
         self._sessions = None
         self._fallback: Optional[AggregationEngine] = None
         self.last_timing: Dict[str, object] = {}
+        # measurement switch (bench.py --engine multi-device): time each shard's kernel with HIP
+        # events on its session stream (adds one event pair per sub-range)
+        self.kernel_events = False
 
     def lock_devices(self) -> List[int]:
         return list(self.devices)
@@ -123,19 +126,25 @@ class MultiDeviceEngine:
             self._fallback = engine_for(self.devices[0])
         return self._fallback
 
-    def _budget(self, g: int) -> int:
+    _FEDAVG_SLOTS = (0, 1, 2)
+    _SCAFFOLD_SLOTS = (0, 1, 2, 4, 5, 6, 7)
+
+    def _budget(self, g: int, slots: Sequence[int]) -> int:
+        """HBM one sub-range may take on shard ``g``: free HBM plus the session buffers the call
+        reuses (``slots``; buffers of other calls stay allocated and are not counted)."""
         if self.max_shard_bytes:
             return int(self.max_shard_bytes)
 
         free, _ = runtime.device_memory(self.devices[g])
-        return int((free + self.sessions()[g].held_bytes()) * HBM_HEADROOM)
+        return int((free + self.sessions()[g].held_bytes(slots)) * HBM_HEADROOM)
 
-    def plan_ranges(self, M: int, bytes_per_elem: int) -> List[List[Tuple[int, int]]]:
+    def plan_ranges(self, M: int, bytes_per_elem: int, slots: Sequence[int] = _SCAFFOLD_SLOTS
+                    ) -> List[List[Tuple[int, int]]]:
         """Per shard, the sub-ranges it streams through its GPU."""
         bounds = shard_bounds(M, len(self.devices))
         plan = []
         for g, (lo, hi) in enumerate(bounds):
-            cap = max(SHARD_ALIGN, self._budget(g) // max(1, bytes_per_elem))
+            cap = max(SHARD_ALIGN, self._budget(g, slots) // max(1, bytes_per_elem))
             plan.append(_split(lo, hi, cap))
         return plan
 
@@ -192,7 +201,7 @@ class MultiDeviceEngine:
         w = fedavg_weights(n_samples, kind)
         pw_all = layout.pairwise_idx.astype(np.int64)
         out = runtime.reusable_host_array(M, R, "multi-fedavg")
-        ranges = self.plan_ranges(M, (K + 1) * isz)
+        ranges = self.plan_ranges(M, (K + 1) * isz, self._FEDAVG_SLOTS)
         ws_bytes = _native.load().fedagg_pairwise_ws_bytes(K, max(1, pw_all.size), 8)
         timing: List[Dict[str, float]] = [dict() for _ in self.devices]
 
@@ -209,8 +218,14 @@ class MultiDeviceEngine:
                 ws = s.buffer(self._B_WS, ws_bytes)
                 pw = (pw_all[(pw_all >= lo) & (pw_all < hi)] - lo).astype(np.uint64)
                 ptrs = [d_bucket + k * ld * isz for k in range(K)]
+                if self.kernel_events:
+                    s.event_record(0)
                 FedAvgPlan(kind, ptrs, w, n, d_out, pw, ws).launch(s.stream)
+                if self.kernel_events:
+                    s.event_record(1)
                 s.fetch(d_out, out[lo:hi])
+                if self.kernel_events:
+                    tm["kernel_ms"] = tm.get("kernel_ms", 0.0) + s.event_elapsed_ms(0, 1)
                 tm["stage_s"] = tm.get("stage_s", 0.0) + t1 - t0
                 tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
                 tm["ranges"] = tm.get("ranges", 0) + 1
@@ -250,7 +265,10 @@ class MultiDeviceEngine:
         same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
                      for row in server_control_variates[1:])
         rows_s = self._rows_direct(server_control_variates[:1] if same_c else server_control_variates, sdt, M)
-        Kc = 1 if same_c else K  # identical c objects: one staged copy, no check (see engine.scaffold)
+        # identical c objects: one staged copy, no check; otherwise one staged copy and the check of
+        # the others on the host while staging (Session.stage_check; see engine.scaffold)
+        host_c = not same_c and self._single().c_check == "host"
+        Kc = 1 if same_c or host_c else K
         w = scaffold_weights(n_samples)
         lr = float(aggregation_lr)
         pw_all = layout.pairwise_idx.astype(np.int64)
@@ -258,7 +276,7 @@ class MultiDeviceEngine:
         out_c = runtime.reusable_host_array(M, np.float64, "multi-scaffold-c")
         mism = [0] * len(self.devices)
         # per element: K deltas + K control variates + K server-c copies in, two fp64 outputs
-        ranges = self.plan_ranges(M, (2 * K + Kc) * isz + 16)
+        ranges = self.plan_ranges(M, (2 * K + Kc) * isz + 16, self._SCAFFOLD_SLOTS)
         ws_bytes = _native.load().fedagg_pairwise_ws_bytes(K, max(1, pw_all.size), 8)
 
         def work(g, s):
@@ -271,10 +289,13 @@ class MultiDeviceEngine:
                 d_cc = s.buffer(self._B_C, Kc * ld * isz)
                 s.stage(d_d, ld * isz, rows_d, byte_range=br)
                 s.stage(d_cv, ld * isz, rows_c, byte_range=br)
-                s.stage(d_cc, ld * isz, rows_s, byte_range=br)
+                if host_c:
+                    mism[g] += s.stage_check(d_cc, rows_s, sdt, byte_range=br)
+                else:
+                    s.stage(d_cc, ld * isz, rows_s, byte_range=br)
                 cnt = s.buffer(self._B_CNT, 8)
                 s.memset(cnt, 0, 8)
-                if not same_c:
+                if not same_c and not host_c:
                     equal_count(kind, [d_cc + k * ld * isz for k in range(K)], n, cnt, s.stream)
                 dout = s.buffer(self._B_OUT, _ld(n, 8) * 8)
                 cout = s.buffer(self._B_COUT, _ld(n, 8) * 8)

@@ -53,6 +53,11 @@ class Session:
         self._h = ctypes.c_void_p(h)
         self.device = int(device)
         self._held: Dict[int, int] = {}
+        self._ptr: Dict[int, int] = {}
+        # write generation per buffer slot: bumped by every call that writes into the slot
+        # (stage, cast, memset, regrowth), so a record of rows staged earlier (engine.ingest) can
+        # tell whether any engine sharing this session has written the slot since
+        self._gen: Dict[int, int] = {}
         self.stream = int(self.lib.fedagg_session_stream(self._h) or 0)
         nthreads = threads or int(os.environ.get("FEDAGG_PACK_THREADS", "0")) or min(16, os.cpu_count() or 1)
         self.set("threads", nthreads)
@@ -84,16 +89,39 @@ class Session:
         arr = (ctypes.c_uint64 * n)(*[int(slot_bytes.get(i, 0)) for i in range(n)])
         _native.check(self.lib.fedagg_session_warm(self._h, arr, n), "session_warm")
 
-    def held_bytes(self) -> int:
-        """HBM held by this session's grow-only buffers (reusable by the next call)."""
-        return sum(self._held.values())
+    def held_bytes(self, slots: Optional[Sequence[int]] = None) -> int:
+        """HBM held by this session's grow-only buffers (all, or only ``slots``: the buffers a
+        call will reuse -- the others stay allocated and are not free for it)."""
+        if slots is None:
+            return sum(self._held.values())
+        return sum(self._held.get(int(k), 0) for k in set(slots))
 
     def buffer(self, slot: int, nbytes: int) -> int:
-        self._held[int(slot)] = max(self._held.get(int(slot), 0), max(16, int(nbytes)))
+        slot = int(slot)
+        self._held[slot] = max(self._held.get(slot, 0), max(16, int(nbytes)))
         p = ctypes.c_void_p()
-        _native.check(self.lib.fedagg_session_buffer(self._h, int(slot), max(16, int(nbytes)), ctypes.byref(p)),
+        _native.check(self.lib.fedagg_session_buffer(self._h, slot, max(16, int(nbytes)), ctypes.byref(p)),
                       "session_buffer")
+        if self._ptr.get(slot) != int(p.value):
+            self._ptr[slot] = int(p.value)
+            self._bump(int(p.value))
         return int(p.value)
+
+    # ----------------------------------------------------------------------------------
+    def _slot_of(self, d: int) -> Optional[int]:
+        for slot, base in self._ptr.items():
+            if base <= d < base + self._held.get(slot, 0):
+                return slot
+        return None
+
+    def _bump(self, d: int) -> None:
+        slot = self._slot_of(int(d))
+        if slot is not None:
+            self._gen[slot] = self._gen.get(slot, 0) + 1
+
+    def generation(self, slot: int) -> int:
+        """Write generation of buffer ``slot`` (see ``_gen``)."""
+        return self._gen.get(int(slot), 0)
 
     def stage(self, d_dst: int, ld_bytes: int, rows: Sequence[Sequence[np.ndarray]],
               byte_range: Optional[tuple] = None) -> None:
@@ -101,21 +129,8 @@ class Session:
         ``d_dst + k * ld_bytes``.  ``byte_range=(lo, hi)`` stages only bytes ``[lo, hi)`` of every
         row (a parameter-range shard), to ``d_dst + k * ld_bytes`` likewise."""
         K = len(rows)
-        nseg = len(rows[0]) if K else 0
-        keep: List[np.ndarray] = []
-        ptrs = (ctypes.c_void_p * max(1, K * nseg))()
-        sizes = (ctypes.c_uint64 * max(1, nseg))()
-        for k, row in enumerate(rows):
-            if len(row) != nseg:
-                raise ValueError("every client row needs the same segments")
-            for i, a in enumerate(row):
-                a = np.ascontiguousarray(a)
-                keep.append(a)
-                ptrs[k * nseg + i] = a.ctypes.data if a.nbytes else None
-                if k == 0:
-                    sizes[i] = a.nbytes
-                elif a.nbytes != sizes[i]:
-                    raise ValueError("segment sizes differ between clients")
+        nseg, ptrs, sizes, keep = _segments(rows)
+        self._bump(d_dst)
         if byte_range is None:
             _native.check(self.lib.fedagg_session_stage(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K, nseg,
                                                         ptrs, sizes), "session_stage")
@@ -123,6 +138,35 @@ class Session:
             lo, hi = (int(v) for v in byte_range)
             _native.check(self.lib.fedagg_session_stage_range(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K,
                                                               nseg, ptrs, sizes, lo, hi), "session_stage_range")
+
+    def stage_check(self, d_dst: int, rows: Sequence[Sequence[np.ndarray]], dtype,
+                    byte_range: Optional[tuple] = None) -> int:
+        """Stage ``rows[0]`` (bytes ``byte_range`` of it, default all) to ``d_dst`` and compare the
+        same bytes of every other row with it by value on the host
+        (``fedagg_session_stage_check``: Scaffold's server-control-variate check,
+        scaffold.py:193-196).  Returns the number of mismatching elements."""
+        kind = {np.dtype(np.float32): _native.FEDAGG_F32, np.dtype(np.float64): _native.FEDAGG_F64}[np.dtype(dtype)]
+        nseg, ptrs, sizes, keep = _segments(rows)
+        for row in rows:
+            for a in row:
+                if a.dtype != dtype:
+                    raise ValueError("stage_check: every array must have the checked dtype")
+        lo, hi = (0, sum(int(sizes[i]) for i in range(nseg))) if byte_range is None else byte_range
+        self._bump(d_dst)
+        mism = ctypes.c_uint64(0)
+        _native.check(self.lib.fedagg_session_stage_check(self._h, ctypes.c_void_p(d_dst), len(rows), nseg, ptrs,
+                                                          sizes, int(lo), int(hi), kind, ctypes.byref(mism)),
+                      "session_stage_check")
+        return int(mism.value)
+
+    def event_record(self, ev: int) -> None:
+        _native.check(self.lib.fedagg_session_event_record(self._h, int(ev)), "session_event_record")
+
+    def event_elapsed_ms(self, ev0: int, ev1: int) -> float:
+        ms = ctypes.c_float()
+        _native.check(self.lib.fedagg_session_event_elapsed(self._h, int(ev0), int(ev1), ctypes.byref(ms)),
+                      "session_event_elapsed")
+        return float(ms.value)
 
     def activate(self) -> None:
         """Make this session's GPU the calling thread's current device (before kernel launches)."""
@@ -138,6 +182,7 @@ class Session:
         return out
 
     def memset(self, d: int, value: int, nbytes: int) -> None:
+        self._bump(d)
         _native.check(self.lib.fedagg_session_memset(self._h, ctypes.c_void_p(d), int(value), int(nbytes)),
                       "session_memset")
 
@@ -151,13 +196,36 @@ class Session:
 
     # ----------------------------------------------------------------------------------
     def cast(self, d_in: int, in_dtype, d_out: int, out_dtype, n: int) -> None:
+        self._bump(d_out)
         _native.check(self.lib.fedagg_cast(ctypes.c_void_p(d_in), kind_code(in_dtype), ctypes.c_void_p(d_out),
                                            kind_code(out_dtype), int(n), ctypes.c_void_p(self.stream)), "cast")
 
     def scale_cast(self, d_in: int, in_dtype, w: float, d_out: int, out_dtype, n: int) -> None:
+        self._bump(d_out)
         _native.check(self.lib.fedagg_scale_cast(ctypes.c_void_p(d_in), kind_code(in_dtype), float(w),
                                                  ctypes.c_void_p(d_out), kind_code(out_dtype), int(n),
                                                  ctypes.c_void_p(self.stream)), "scale_cast")
+
+
+def _segments(rows: Sequence[Sequence[np.ndarray]]):
+    """ctypes tables of K rows of nseg C-contiguous host arrays: (nseg, pointers, sizes, keep)."""
+    K = len(rows)
+    nseg = len(rows[0]) if K else 0
+    keep: List[np.ndarray] = []
+    ptrs = (ctypes.c_void_p * max(1, K * nseg))()
+    sizes = (ctypes.c_uint64 * max(1, nseg))()
+    for k, row in enumerate(rows):
+        if len(row) != nseg:
+            raise ValueError("every client row needs the same segments")
+        for i, a in enumerate(row):
+            a = np.ascontiguousarray(a)
+            keep.append(a)
+            ptrs[k * nseg + i] = a.ctypes.data if a.nbytes else None
+            if k == 0:
+                sizes[i] = a.nbytes
+            elif a.nbytes != sizes[i]:
+                raise ValueError("segment sizes differ between clients")
+    return nseg, ptrs, sizes, keep
 
 
 _device_locks: Dict[int, threading.RLock] = {}

@@ -14,6 +14,7 @@
 using fedagg_host::Done;
 using fedagg_host::gather_range;
 using fedagg_host::Pool;
+using fedagg_host::Ring;
 
 static int check_gather(std::mt19937_64& rng) {
   const int nseg = (int)(rng() % 9);
@@ -70,6 +71,155 @@ static long pipeline(Pool& pool, int R, int units, int unit_bytes, std::mt19937_
   return bad;
 }
 
+// ------------------------------------------------------------------------------------------
+// The session's real staging / fetch pipelines (fedagg_host::stage_pipeline / fetch_pipeline)
+// over a fake copy engine: one "DMA" thread executes the enqueued copies in order, slot events
+// complete when the DMA passed them, and the n-th copy can be made to fail (the HIP error path:
+// ADVICE r01 -- pending pack / copy-out tasks must be drained before the call returns).
+// ------------------------------------------------------------------------------------------
+struct FakeDma {
+  struct Job {
+    char* dst;
+    const char* src;
+    uint64_t n;
+    uint64_t seq;
+  };
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<Job> q;
+  uint64_t enq = 0, doneseq = 0;
+  std::vector<uint64_t> ev;  // per slot: sequence number the slot's event waits for
+  bool stop = false;
+  uint64_t fail_at = 0, calls = 0;
+  std::thread th;
+  explicit FakeDma(int slots) : ev(slots, 0) {
+    th = std::thread([this] {
+      for (;;) {
+        Job j;
+        {
+          std::unique_lock<std::mutex> l(m);
+          cv.wait(l, [this] { return stop || !q.empty(); });
+          if (q.empty()) return;
+          j = q.front();
+          q.pop_front();
+        }
+        memcpy(j.dst, j.src, j.n);
+        std::lock_guard<std::mutex> g(m);
+        doneseq = j.seq;
+        cv.notify_all();
+      }
+    });
+  }
+  ~FakeDma() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  int copy(void* d, const void* s, uint64_t n) {
+    if (fail_at && ++calls >= fail_at) return -2;
+    std::lock_guard<std::mutex> g(m);
+    q.push_back({static_cast<char*>(d), static_cast<const char*>(s), n, ++enq});
+    cv.notify_all();
+    return 0;
+  }
+  int h2d(int, void* d, const void* s, uint64_t n) { return copy(d, s, n); }
+  int d2h(void* h, const void* d, uint64_t n) { return copy(h, d, n); }
+  int mark(int slot, int) {
+    std::lock_guard<std::mutex> g(m);
+    ev[slot] = enq;
+    return 0;
+  }
+  void wait(int slot) {
+    std::unique_lock<std::mutex> l(m);
+    const uint64_t want = ev[slot];
+    cv.wait(l, [&] { return doneseq >= want; });
+  }
+  void drain() {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [&] { return doneseq >= enq; });
+  }
+};
+
+// K client rows of random segments staged through a ring into a "device" buffer and fetched
+// back; with fail_at, the fail_at-th copy fails and the call must return the error cleanly.
+static int staging_round_trip(Pool& pool, std::mt19937_64& rng, uint64_t fail_at, bool check) {
+  const int K = 1 + (int)(rng() % 6), nseg = 1 + (int)(rng() % 5), R = pool.size() + 2 + (int)(rng() % 3);
+  const uint64_t cb = 64 * (1 + rng() % 8);  // small chunks: many units
+  std::vector<uint64_t> len(nseg);
+  uint64_t row = 0;
+  for (auto& l : len) row += (l = 4 * (rng() % 200));  // whole floats
+  std::vector<std::vector<std::vector<float>>> data(K, std::vector<std::vector<float>>(nseg));
+  std::vector<const void*> segs((size_t)K * nseg);
+  for (int k = 0; k < K; ++k)
+    for (int i = 0; i < nseg; ++i) {
+      auto& v = data[k][i];
+      v.resize(len[i] / 4);
+      for (auto& f : v) f = (float)(int)(rng() % 7) - 3.0f;
+      if (check && k > 0 && rng() % 2) v = data[0][i];  // mostly identical copies of c
+      if (check && k > 0 && !v.empty() && rng() % 3 == 0) v[0] = -v[0] + 1.0f;
+      segs[(size_t)k * nseg + i] = v.data();
+    }
+  std::vector<char> ring_mem((size_t)R * cb);
+  Ring ring;
+  ring.chunk_bytes = cb;
+  for (int i = 0; i < R; ++i) ring.slot.push_back(ring_mem.data() + (size_t)i * cb);
+  ring.used.assign(R, false);
+  const uint64_t ld = row + 16;
+  std::vector<char> dev((size_t)K * ld, 0), back(dev.size(), 0);
+  FakeDma dma(R);
+  dma.fail_at = fail_at;
+  uint64_t mism = 0;
+  int rc = fedagg_host::stage_pipeline(dma, pool, ring, segs.data(), len.data(), nseg, K, 0, row, dev.data(), ld,
+                                       true, check ? 4 : 0, &mism);
+  dma.drain();
+  if (fail_at) {
+    const uint64_t units = (row ? (row + cb - 1) / cb : 0) * (check ? 1 : K);
+    return (fail_at <= units) == (rc != 0) ? 0 : 1;  // an error exactly when the failing copy was reached
+  }
+  if (rc) return 1;
+  if (check) {  // row 0 staged, the mismatch count is the value comparison of the others
+    uint64_t want = 0;
+    for (int k = 1; k < K; ++k)
+      for (int i = 0; i < nseg; ++i)
+        for (size_t e = 0; e < data[k][i].size(); ++e) want += data[k][i][e] != data[0][i][e];
+    if (want != mism) return 1;
+  }
+  for (int k = 0; k < (check ? 1 : K); ++k) {
+    uint64_t off = 0;
+    for (int i = 0; i < nseg; ++i) {
+      if (len[i] && memcmp(dev.data() + (size_t)k * ld + off, data[k][i].data(), len[i])) return 1;
+      off += len[i];
+    }
+  }
+  rc = fedagg_host::fetch_pipeline(dma, pool, ring, dev.data(), back.data(), dev.size());
+  dma.drain();
+  if (rc) return 1;
+  return memcmp(back.data(), dev.data(), dev.size()) ? 1 : 0;
+}
+
+static int fetch_with_failure(Pool& pool, std::mt19937_64& rng) {
+  const int R = pool.size() + 2;
+  const uint64_t cb = 256;
+  std::vector<char> ring_mem((size_t)R * cb);
+  Ring ring;
+  ring.chunk_bytes = cb;
+  for (int i = 0; i < R; ++i) ring.slot.push_back(ring_mem.data() + (size_t)i * cb);
+  ring.used.assign(R, false);
+  const uint64_t bytes = 1 + rng() % 20000;
+  std::vector<char> dev(bytes), host(bytes);
+  for (auto& c : dev) c = (char)rng();
+  FakeDma dma(R);
+  dma.fail_at = 1 + rng() % 6;
+  int rc = fedagg_host::fetch_pipeline(dma, pool, ring, dev.data(), host.data(), bytes);
+  dma.drain();
+  const int G = std::max(1, std::min(4, R / 2));
+  const uint64_t units = (bytes + cb * G - 1) / (cb * G);
+  return (dma.fail_at <= units) == (rc != 0) ? 0 : 1;
+}
+
 int main() {
   std::mt19937_64 rng(20241016);
   for (int t = 0; t < 4000; ++t)
@@ -84,6 +234,22 @@ int main() {
       const long bad = pipeline(pool, R, 1 + (int)(rng() % 40), 64 + (int)(rng() % 4096), rng);
       if (bad) {
         fprintf(stderr, "pipeline: %ld wrong bytes (threads %d, rep %d)\n", bad, threads, rep);
+        return 1;
+      }
+    }
+  }
+  for (int threads : {1, 4}) {
+    Pool pool(threads);
+    for (int rep = 0; rep < 80; ++rep) {
+      const bool check = rep % 2 == 1;
+      const uint64_t fail_at = rep % 3 == 2 ? 1 + rng() % 12 : 0;
+      if (staging_round_trip(pool, rng, fail_at, check)) {
+        fprintf(stderr, "stage/fetch pipeline failed (threads %d, rep %d, fail_at %llu)\n", threads, rep,
+                (unsigned long long)fail_at);
+        return 1;
+      }
+      if (fetch_with_failure(pool, rng)) {
+        fprintf(stderr, "fetch pipeline error path failed (threads %d, rep %d)\n", threads, rep);
         return 1;
       }
     }

@@ -1,0 +1,53 @@
+"""bench.py's multi-rank contract on CPU: ``python3 bench.py --gpus N`` (no torchrun) starts N rank
+processes itself and the line reports ``"n_gpus": N``; a WORLD_SIZE that disagrees with --gpus
+exits non-zero.  ``--rehearse-cpu`` runs the launcher / rank / barrier / max-over-ranks plumbing
+with no GPU and reports no value (the driver's plain command must not silently run
+one rank)."""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, env=env,
+                          timeout=240, cwd=str(ROOT))
+
+
+def _line(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_plain_gpus_2_launches_two_ranks():
+    r = _run(["--gpus", "2", "--rehearse-cpu", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _line(r.stdout)
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["rehearsal"] is True
+    assert line["value"] is None  # a rehearsal is never a measurement
+
+
+def test_plain_gpus_3_launches_three_ranks():
+    r = _run(["--gpus", "3", "--rehearse-cpu", "--steps", "2", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _line(r.stdout)["n_gpus"] == 3
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _run(["--gpus", "2", "--rehearse-cpu"], {"WORLD_SIZE": "3", "RANK": "0"})
+    assert r.returncode == 2
+    assert "refusing" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_single_rank_default():
+    r = _run(["--rehearse-cpu", "--steps", "2", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _line(r.stdout)["n_gpus"] == 1

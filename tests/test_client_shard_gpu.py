@@ -1,0 +1,232 @@
+"""GPU tests of the client-sharded (north-star) mode with the product arithmetic (libfedagg's chain
+/ partial / pairwise kernels, substrafl_amd.sharding.GpuShardOps):
+
+* G ranks as threads on the one GPU of the test box (LoopbackGroup: each rank on its own HIP
+  stream, messages ordered by events) -- the relay combine bit-identical to the reference oracle
+  for FedAvg fp32 / bf16 and Scaffold, also with empty client blocks; the re-associating
+  combines close, their numel == 1 elements exact;
+* the host entry points over a real RCCL process group of world size 1."""
+
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import fedavg_reference_structure, scaffold_reference_structure
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(37, 29), (1,), (3000,), (1, 1), (3, 3, 3), (1,), (257,)]
+
+
+def _data(K, seed=0, shapes=SHAPES):
+    rng = np.random.default_rng(seed)
+    pus = [[(rng.standard_normal(s) * 10.0 ** rng.integers(-2, 3)).astype(np.float32) for s in shapes]
+           for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    return pus, ns
+
+
+def _loopback(G, fn):
+    import torch
+
+    from substrafl_amd.sharding import LoopbackGroup
+
+    grp = LoopbackGroup(G)
+    res, err = [None] * G, [None] * G
+
+    def body(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                res[r] = fn(r, grp.transport(r))
+            s.synchronize()
+        except BaseException as e:  # noqa: BLE001
+            err[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+        assert not t.is_alive(), "loopback rank hung"
+    for e in err:
+        if e is not None:
+            raise e
+    return res
+
+
+def _rows(torch, lists, layout, dtype=np.float32, tdtype=None):
+    rows = np.zeros((max(1, len(lists)), layout.ld), dtype)
+    for k, lay in enumerate(lists):
+        layout.pack_row(lay, rows[k])
+    t = torch.from_numpy(rows).cuda()
+    if tdtype is not None:
+        t = t.to(tdtype)
+    return t[: len(lists)]
+
+
+def _fedavg(G, K, combine, kind="f32", chunk_elems=4096):
+    import torch
+
+    from substrafl_amd.engine import fedavg_weights
+    from substrafl_amd.layout import BucketLayout
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, block_of, client_blocks, client_shard_fedavg)
+
+    pus, ns = _data(K)
+    if kind == "bf16":  # bf16-representable values: the reference runs on the exact upcast
+        pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
+    layout = BucketLayout(range(len(SHAPES)), SHAPES, np.float32)
+    w = fedavg_weights(ns, kind)
+
+    def rank_fn(r, tr):
+        k0, k1 = client_blocks(K, G)[block_of(r, G)]
+        rows = _rows(torch, pus[k0:k1], layout, tdtype=torch.bfloat16 if kind == "bf16" else None)
+        out = torch.zeros(layout.ld, dtype=torch.float32, device="cuda")
+        sh = FedAvgShard(kind, rows, w[k0:k1], k0, K, layout.M, layout.pairwise_idx)
+        if client_shard_fedavg(sh, out, tr, GpuShardOps(), combine, chunk_elems=chunk_elems):
+            torch.cuda.current_stream().synchronize()
+            return out[: layout.M].cpu().numpy().copy()
+        return None
+
+    res = _loopback(G, rank_fn)
+    assert all(x is None for x in res[1:])
+    got = [a for _, a in layout.unpack(res[0])]
+    return got, fedavg_reference_structure(pus, ns)
+
+
+@pytest.mark.parametrize("G,K", [(2, 7), (3, 3), (4, 2), (8, 20)])
+def test_relay_fedavg_bit_exact(G, K):
+    got, ref = _fedavg(G, K, "relay")
+    for g, r in zip(got, ref):
+        assert g.shape == r.shape and np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+def test_relay_fedavg_bf16_bit_exact():
+    got, ref = _fedavg(4, 9, "relay", kind="bf16")
+    for g, r in zip(got, ref):
+        assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+@pytest.mark.parametrize("combine", ["ordered", "rccl"])
+def test_reassociating_combines_close(combine):
+    got, ref = _fedavg(4, 13, combine)
+    for g, r in zip(got, ref):
+        np.testing.assert_allclose(g, r, rtol=2e-5, atol=1e-5)
+        if g.size == 1:  # the numel == 1 tensors are exact in every mode (pairwise tree on the root)
+            assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+def _scaffold(G, K, combine, lr=0.7, chunk_elems=4096):
+    import torch
+
+    from substrafl_amd.engine import scaffold_weights
+    from substrafl_amd.layout import BucketLayout
+    from substrafl_amd.sharding import (GpuShardOps, ScaffoldShard, block_of, client_blocks, client_shard_scaffold)
+
+    pus, ns = _data(K, seed=1)
+    rng = np.random.default_rng(9)
+    cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+    c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+    layout = BucketLayout(range(len(SHAPES)), SHAPES, np.float32)
+    w = scaffold_weights(ns)
+
+    def rank_fn(r, tr):
+        k0, k1 = client_blocks(K, G)[block_of(r, G)]
+        d = _rows(torch, pus[k0:k1], layout)
+        v = _rows(torch, cvs[k0:k1], layout)
+        ct = _rows(torch, [c], layout)[0]
+        dout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+        cout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+        sh = ScaffoldShard("f32", d, v, ct, w[k0:k1], k0, K, layout.M, lr, layout.pairwise_idx)
+        if client_shard_scaffold(sh, dout, cout, tr, GpuShardOps(), combine, chunk_elems=chunk_elems):
+            torch.cuda.current_stream().synchronize()
+            return dout[: layout.M].cpu().numpy().copy(), cout[: layout.M].cpu().numpy().copy()
+        return None
+
+    res = _loopback(G, rank_fn)
+    lay64 = BucketLayout(range(len(SHAPES)), SHAPES, np.float64)
+    d, cc = res[0]
+    got = [a for _, a in lay64.unpack(cc)] + [a for _, a in lay64.unpack(d)]
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
+    return got, rc + ra
+
+
+@pytest.mark.parametrize("G,K", [(2, 5), (3, 2), (8, 17)])
+def test_relay_scaffold_bit_exact(G, K):
+    """c added last and lr applied on the root, inside its last kernel (or, for an empty last
+    block, by the final-step launch) -- fp64 bit-exact."""
+    got, ref = _scaffold(G, K, "relay")
+    for g, r in zip(got, ref):
+        assert g.dtype == np.float64 and np.array_equal(g.view(np.uint64), r.view(np.uint64))
+
+
+@pytest.mark.parametrize("combine", ["ordered", "rccl"])
+def test_scaffold_reassociating_combines_close(combine):
+    got, ref = _scaffold(3, 10, combine)
+    for g, r in zip(got, ref):
+        np.testing.assert_allclose(g, r, rtol=1e-12, atol=1e-13)
+        if g.size == 1:
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+
+
+# ---- host entry points over RCCL, world size 1 ----
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _nccl_world1(q, port):
+    import torch
+    import torch.distributed as dist
+
+    from substrafl_amd.sharding import client_sharded_fedavg, client_sharded_scaffold
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pus, ns = _data(6, seed=3)
+        out = {"fedavg": {m: client_sharded_fedavg(pus, ns, combine=m) for m in ("relay", "ordered", "rccl")}}
+        rng = np.random.default_rng(2)
+        cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+        c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+        cs = [[a.copy() for a in c] for _ in pus]  # separately unpickled copies: checked on the host
+        out["scaffold"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5)
+        cs[3][2][17] += 1.0
+        out["scaffold_bad"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5)[0]
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_entry_points_nccl_world1():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1, args=(q, _free_port()))
+    p.start()
+    out = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    pus, ns = _data(6, seed=3)
+    ref = fedavg_reference_structure(pus, ns)
+    for mode, got in out["fedavg"].items():
+        for g, r in zip(got, ref):
+            assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), mode
+    rng = np.random.default_rng(2)
+    cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+    c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.5)
+    mism, new_c, avg = out["scaffold"]
+    assert mism == 0
+    for g, r in zip(new_c + avg, rc + ra):
+        assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+    assert out["scaffold_bad"] == 1

@@ -9,9 +9,15 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from oracle import fedavg_reference_structure, numpy_pairwise_sum
+import torch
+
+from oracle import fedavg_reference_structure, numpy_pairwise_sum, scaffold_reference_structure
+from substrafl_amd.engine import fedavg_weights, scaffold_weights
 from substrafl_amd.layout import BucketLayout
-from substrafl_amd.sharding import client_sharded_fedavg, pack_range, param_range_fedavg, shard_bounds
+from substrafl_amd.sharding import (DistTransport, FedAvgShard, ScaffoldShard, block_of, chain_rank, client_blocks,
+                                    client_shard_fedavg, client_shard_scaffold, pack_range, param_range_fedavg,
+                                    relay_chunks, shard_bounds)
+from shard_cpu_ops import CpuShardOps
 
 
 def oracle_flat_reducer(rows, n_samples, pairwise_idx):
@@ -43,28 +49,63 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mode, q, on_gpu=False):
+def _flat_rows(lists, layout, dtype):
+    rows = np.zeros((len(lists), layout.ld), dtype)
+    for k, lay in enumerate(lists):
+        layout.pack_row(lay, rows[k])
+    return rows
+
+
+def _client_shard_cpu(rank, world, mode, K, strategy, chunk_elems):
+    """This rank's block of the client-sharded FedAvg / Scaffold over gloo with the NumPy ops."""
+    pus, ns = _data(K=K)
+    layout = BucketLayout(range(len(pus[0])), [a.shape for a in pus[0]], np.float32)
+    k0, k1 = client_blocks(K, world)[block_of(rank, world)]
+    tr = DistTransport()
+    if strategy == "fedavg":
+        rows = torch.from_numpy(_flat_rows(pus[k0:k1], layout, np.float32))
+        sh = FedAvgShard("f32", rows, fedavg_weights(ns, "f32")[k0:k1], k0, K, layout.M, layout.pairwise_idx)
+        out = torch.zeros(layout.ld, dtype=torch.float32)
+        root = client_shard_fedavg(sh, out, tr, CpuShardOps(), combine=mode, chunk_elems=chunk_elems)
+        return [a for _, a in layout.unpack(out[: layout.M].numpy().copy())] if root else None
+    rng = np.random.default_rng(5)
+    cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+    c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+    delta = torch.from_numpy(_flat_rows(pus[k0:k1], layout, np.float32))
+    cv = torch.from_numpy(_flat_rows(cvs[k0:k1], layout, np.float32))
+    ct = torch.from_numpy(_flat_rows([c], layout, np.float32)[0])
+    sh = ScaffoldShard("f32", delta, cv, ct, scaffold_weights(ns)[k0:k1], k0, K, layout.M, 0.7, layout.pairwise_idx)
+    dout = torch.zeros(layout.ld, dtype=torch.float64)
+    cout = torch.zeros(layout.ld, dtype=torch.float64)
+    root = client_shard_scaffold(sh, dout, cout, tr, CpuShardOps(), combine=mode, chunk_elems=chunk_elems)
+    if not root:
+        return None
+    lay64 = BucketLayout(range(len(pus[0])), [a.shape for a in pus[0]], np.float64)
+    return ([a for _, a in lay64.unpack(cout[: layout.M].numpy().copy())]
+            + [a for _, a in lay64.unpack(dout[: layout.M].numpy().copy())])
+
+
+def _worker(rank, world, port, mode, q, on_gpu=False, K=5, strategy="fedavg", chunk_elems=512):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pus, ns = _data()
-        # on_gpu: every rank reduces its slice with libfedagg on cuda:0 (the ranks share the one
-        # GPU of the test box; the control plane stays gloo, as in bench.py)
-        red = None if on_gpu else oracle_flat_reducer
         if mode == "param":
-            res = param_range_fedavg(pus, ns, reducer=red)
+            pus, ns = _data()
+            # on_gpu: every rank stages and reduces its slice with libfedagg on cuda:0 (the ranks
+            # share the one GPU of the test box; the control plane stays gloo, as in bench.py)
+            res = param_range_fedavg(pus, ns, reducer=None if on_gpu else oracle_flat_reducer)
         else:
-            res = client_sharded_fedavg(pus, ns, reducer=red, combine=mode)
+            res = _client_shard_cpu(rank, world, mode, K, strategy, chunk_elems)
         q.put((rank, None if res is None else [np.asarray(a) for a in res]))
     finally:
         dist.destroy_process_group()
 
 
-def _run(mode, world=2, on_gpu=False):
+def _run(mode, world=2, on_gpu=False, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, on_gpu)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, on_gpu), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=120) for _ in procs)
@@ -103,15 +144,63 @@ def test_param_range_world2_bit_exact():
             assert g.shape == r.shape and np.array_equal(g.view(np.uint32), r.view(np.uint32))
 
 
+def test_client_blocks_and_chain():
+    for K in (1, 2, 3, 5, 64, 65):
+        for G in (1, 2, 3, 8):
+            blocks = client_blocks(K, G)
+            assert blocks[0][0] == 0 and blocks[-1][1] == K and len(blocks) == G
+            assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+            assert sorted(chain_rank(b, G) for b in range(G)) == list(range(G))
+            assert chain_rank(G - 1, G) == 0  # the last block (final step) is on the root
+            assert all(block_of(chain_rank(b, G), G) == b for b in range(G))
+    for M in (0, 1, 511, 513, 10_000):
+        ch = relay_chunks(M, 1000)
+        assert ch[0][0] == 0 and ch[-1][1] == M and all(a[1] == b[0] for a, b in zip(ch, ch[1:]))
+
+
+@pytest.mark.parametrize("world,K", [(2, 5), (3, 5), (3, 2), (4, 9)])
+def test_client_sharded_relay_bit_exact(world, K):
+    """North-star client sharding with the relay combine: the chain of blocks reproduces the
+    reference's sequential client sum exactly (numel == 1 layers via the gathered pairwise
+    products), also with empty blocks (K < world) and several pipelining chunks."""
+    pus, ns = _data(K=K)
+    ref = fedavg_reference_structure(pus, ns)
+    out = _run("relay", world=world, K=K)
+    assert all(out[r] is None for r in range(1, world))
+    for g, r in zip(out[0], ref):
+        assert g.shape == r.shape and np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
 @pytest.mark.parametrize("mode", ["ordered", "rccl"])
 def test_client_sharded_world2_close(mode):
-    """North-star mode re-associates the client sum: close, not bit-exact."""
+    """The re-associating combines: close, not bit-exact (numel == 1 layers stay exact)."""
     pus, ns = _data()
     ref = fedavg_reference_structure(pus, ns)
     out = _run(mode)
     assert out[1] is None
     for g, r in zip(out[0], ref):
         np.testing.assert_allclose(g, r, rtol=1e-5, atol=1e-6)
+        if g.size == 1:
+            assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+@pytest.mark.parametrize("mode,world,K", [("relay", 2, 5), ("relay", 3, 2), ("ordered", 2, 5), ("rccl", 3, 7)])
+def test_client_sharded_scaffold(mode, world, K):
+    """Scaffold over client blocks: c added last and aggregation_lr applied on the root
+    (scaffold.py:262-263, 293); relay bit-exact in fp64."""
+    pus, ns = _data(K=K)
+    rng = np.random.default_rng(5)
+    cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+    c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.7)
+    out = _run(mode, world=world, K=K, strategy="scaffold")
+    assert all(out[r] is None for r in range(1, world))
+    for g, r in zip(out[0], rc + ra):
+        assert g.dtype == np.float64 and g.shape == r.shape
+        if mode == "relay":
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+        else:
+            np.testing.assert_allclose(g, r, rtol=1e-12, atol=1e-14)
 
 
 @pytest.mark.gpu

@@ -272,9 +272,12 @@ def test_scaffold_fp64_inputs_and_c_check(torch_gpu, dummy_algo_class):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_scaffold_shared_c_objects_staged_once(torch_gpu, dtype):
+@pytest.mark.parametrize("c_check", ["host", "device"])
+def test_scaffold_shared_c_objects_staged_once(torch_gpu, dtype, c_check):
     """All clients holding the very same c arrays (simulation mode) stage one copy and skip the
-    device check; equal-valued copies, and one copy that differs, still take the device check."""
+    check; equal-valued copies (separately unpickled, the task-process case) are checked on the
+    host while ONE copy is staged (default) or, with the knob, staged K times and checked on the
+    device -- the same mismatch count either way."""
     from substrafl_amd.engine import AggregationEngine
 
     rng = np.random.default_rng(21)
@@ -285,9 +288,9 @@ def test_scaffold_shared_c_objects_staged_once(torch_gpu, dtype):
     c[0][3, 3] = np.nan
     ns = [int(v) for v in rng.integers(1, 5000, K)]
     rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.9)
-    eng = AggregationEngine(0)
+    eng = AggregationEngine(0, c_check=c_check)
     for rows, check in (([c] * K, "identity"), ([list(c) for _ in range(K)], "identity"),
-                        ([[a.copy() for a in c] for _ in range(K)], "device")):
+                        ([[a.copy() for a in c] for _ in range(K)], c_check)):
         mism, new_c, avg = eng.scaffold(pus, cvs, rows, ns, 0.9)
         assert mism == 0 and eng.last_timing["c_check"] == check
         _assert_same(new_c, rc)
@@ -295,8 +298,41 @@ def test_scaffold_shared_c_objects_staged_once(torch_gpu, dtype):
     rows = [list(c) for _ in range(K)]
     rows[K - 1][2] = c[2].copy()
     rows[K - 1][2][-1] += 1
+    rows[1] = [a.copy() for a in c]
+    rows[1][0][0, 0] = -rows[1][0][0, 0] if rows[1][0][0, 0] != 0 else 1.0
+    rows[1][0][3, 3] = -np.nan  # NaN == NaN for assert_array_equal
     mism, _, _ = eng.scaffold(pus, cvs, rows, ns, 0.9)
-    assert mism == 1 and eng.last_timing["c_check"] == "device"
+    assert mism == 2 and eng.last_timing["c_check"] == c_check
+
+
+def test_scaffold_host_c_check_signed_zero_and_flat_rows(torch_gpu):
+    """+0 == -0 and NaN == NaN on the host check too; flat wire-format c rows (one buffer per
+    client) are checked as one segment."""
+    from substrafl_amd.engine import AggregationEngine
+    from substrafl_amd.wire import BucketArray, pack
+
+    rng = np.random.default_rng(3)
+    K = 4
+    shapes = [(2000,), (1,), (33, 3)]
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    c[0][:10] = 0.0
+    c[2][0, 0] = np.nan
+    ns = [4, 1, 7, 2]
+    rows = []
+    for k in range(K):
+        ck = [a.copy() for a in c]
+        if k % 2:
+            ck[0][:10] = -0.0
+        rows.append(pack(ck) if k == 2 else ck)
+    eng = AggregationEngine(0)
+    mism, new_c, avg = eng.scaffold(pus, cvs, rows, ns, 1.1)
+    assert mism == 0 and eng.last_timing["c_check"] == "host"
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 1.1)
+    _assert_same_nan_aware(new_c, rc)
+    _assert_same(avg, ra)
+    assert isinstance(rows[2][0], BucketArray)
 
 
 # ------------------------------------------------------------------------------------------
