@@ -65,6 +65,9 @@ const char* fedagg_last_error(void);
  *                   (auto: 2 for fp32 from 32 clients)
  *   "buf"           FedAvg: buffer-descriptor client loads with an explicit vpt (auto: bf16 from
  *                   32 clients)
+ *   "sc_cpf"        Scaffold 4x4 tile: load c with the last client group (0/1)
+ *   "sc_occ"        Scaffold 4x4 tile: register-capped build, waves per SIMD (0 = uncapped)
+ *   "sc_blk"        Scaffold 4x4 tile: threads per workgroup (256 / 512)
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);
 

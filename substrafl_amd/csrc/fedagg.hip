@@ -75,6 +75,9 @@ int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand i
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
 int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
 int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per workgroup)
+int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
+int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
+int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -656,7 +659,10 @@ __device__ __forceinline__ void scaffold_accumulate(const u32x4 (&rd)[N][SU], co
 
 // N 16-byte vectors of both buckets: in-order fp64 sums over the K clients, then (last chunk)
 // + c and * lr, the fused numel==1 patch, and the fp64 stores.  PIPE: software-pipelined groups.
-template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, bool PIPE = false, bool BUF = false>
+// CPF: the server c vectors of the last chunk are loaded together with the last client group's
+// loads instead of after the client walk (one dependent HBM round trip less per tile).
+template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, bool PIPE = false, bool BUF = false,
+          bool CPF = false>
 __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                  const int first, const int last, const TIn* __restrict__ c,
                                                  const double lr, const uint64_t* v, double* __restrict__ dout,
@@ -674,6 +680,8 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
     }
   }
   int k = 0;
+  u32x4 craw[CPF ? N : 1];
+  bool pre_c = false;
   if constexpr (PIPE) {
     // the next group's loads are issued before this group's fp64 products and adds
     if (K >= SU) {
@@ -695,6 +703,13 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
   } else {
     for (; k + SU <= K; k += SU) {
       u32x4 rd[N][SU], rc[N][SU];
+      if constexpr (CPF) {
+        if (last && k + SU == K && !pre_c) {
+#pragma unroll
+          for (int n = 0; n < N; ++n) craw[n] = ld16<NT>(c + v[n] * L);
+          pre_c = true;
+        }
+      }
       scaffold_load_group<TIn, KC, NT, N, SU, BUF>(a, k, v, rd, rc, tb);
       scaffold_accumulate<TIn, N, SU>(rd, rc, a.w + k, ad, ac);
     }
@@ -724,7 +739,8 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
   for (int n = 0; n < N; ++n) {
     if (last) {
       double xcc[L];
-      unpack_d<TIn>(ld16<NT>(c + v[n] * L), xcc);
+      if constexpr (CPF) unpack_d<TIn>(pre_c ? craw[n] : ld16<NT>(c + v[n] * L), xcc);
+      else unpack_d<TIn>(ld16<NT>(c + v[n] * L), xcc);
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         ac[n][j] = ac[n][j] + xcc[j];  // server c appended LAST (scaffold.py:262-263)
@@ -887,35 +903,40 @@ __device__ __forceinline__ void scaffold_vectors_split(const ScArgs<TIn, KC>& a,
   scaffold_phase<TIn, KC, NT, NTS, N, SU, 1>(a, pw, K, first, last, c, lr, v, cout, wave_full, lds_wave);
 }
 
-// Same tiling as fedavg_kernel: a workgroup step covers VPT*256 contiguous vectors.
-template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, bool PIPE = false, bool BUF = false>
-__global__ void __launch_bounds__(FA_BLOCK)
+// Same tiling as fedavg_kernel: a workgroup step covers VPT*BLK contiguous vectors.
+// OCC (fedagg_tune "sc_occ"): minimum waves per SIMD for the register allocation; BLK
+// ("sc_blk"): threads per workgroup (256, or 512: 32 KiB per stream per workgroup step at VPT 4);
+// CPF ("sc_cpf"): c loaded with the last client group.
+template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, bool PIPE = false, bool BUF = false,
+          bool CPF = false, int OCC = 1, int BLK = FA_BLOCK>
+__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                     const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
                     double* __restrict__ dout, double* __restrict__ cout, const int remap, const int tpb) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
-  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
-  const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
-  __shared__ u32x4 stage[FA_BLOCK / 64][128];
+  static_assert(!BUF || BLK == FA_BLOCK, "buffer-descriptor tiles assume 256-thread workgroups");
+  const uint64_t stride = (uint64_t)gridDim.x * BLK;
+  const uint64_t gid = (uint64_t)blockIdx.x * BLK + threadIdx.x;
+  __shared__ u32x4 stage[BLK / 64][128];
   u32x4* lds_wave = stage[threadIdx.x / 64];
-  const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+  const uint64_t tile = (uint64_t)VPT * BLK;
   uint64_t t;
   for (uint64_t it = 0; block_tile(remap, tpb, it, &t) && t * tile < nvec; ++it) {
     const uint64_t base = t * tile + threadIdx.x;
-    const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
-    if (base + (VPT - 1) * FA_BLOCK < nvec) {
+    const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * BLK < nvec;
+    if (base + (VPT - 1) * BLK < nvec) {
       uint64_t v[VPT];
 #pragma unroll
-      for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+      for (int n = 0; n < VPT; ++n) v[n] = base + n * BLK;
       if constexpr (SPLIT)
         scaffold_vectors_split<TIn, KC, NT, NTS, VPT, SU>(a, pw, K, first, last, c, lr, v, dout, cout, wave_full,
                                                            lds_wave);
       else
-        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU, PIPE, BUF>(a, pw, K, first, last, c, lr, v, dout, cout,
-                                                                wave_full, lds_wave, t * tile * 16);
+        scaffold_vectors<TIn, KC, NT, NTS, VPT, SU, PIPE, BUF, CPF>(a, pw, K, first, last, c, lr, v, dout, cout,
+                                                                     wave_full, lds_wave, t * tile * 16);
     } else {
-      for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
+      for (uint64_t v0 = base; v0 < nvec; v0 += BLK)
         scaffold_vectors<TIn, KC, NT, NTS, 1, SU>(a, pw, K, first, last, c, lr, &v0, dout, cout, false, lds_wave);
     }
   }
@@ -1814,12 +1835,14 @@ int scaffold_finish_launch(double* ws, int Ktot, const TIn* c, const uint64_t* i
   return FEDAGG_OK;
 }
 
-template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false, bool BUF = false>
+template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false, bool BUF = false,
+          bool CPF = false, int OCC = 1, int BLK = FA_BLOCK>
 void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
                              uint64_t M, double* dout, double* cout) {
-  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT, PIPE, BUF>), dim3(grid),
-                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd, g_tpb);
+  if (BLK != FA_BLOCK) grid = (grid + BLK / FA_BLOCK - 1) / (BLK / FA_BLOCK);  // the caller sized it for 256
+  hipLaunchKernelGGL((scaffold_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, NT, NTS, VPT, SU, SPLIT, PIPE, BUF, CPF, OCC, BLK>),
+                     dim3(grid), dim3(BLK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, g_xcd, g_tpb);
 }
 
 // Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
@@ -1888,6 +1911,18 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
     if (su <= 2) {
       if (nts) return launch_scaffold_variant<TIn, true, true, 4, 2>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, false, 4, 2>(SC_ARGS);
+    }
+    if (nts && (g_sc_cpf || g_sc_occ > 1 || g_sc_blk > FA_BLOCK)) {  // 4 x 4 experiments (fedagg_tune)
+      const int v = (g_sc_cpf ? 1 : 0) | (g_sc_occ > 1 ? 2 : 0) | (g_sc_blk > FA_BLOCK ? 4 : 0);
+      switch (v) {
+        case 1: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, true>(SC_ARGS);
+        case 2: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, false, 4>(SC_ARGS);
+        case 3: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, true, 4>(SC_ARGS);
+        case 4: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, false, 1, 512>(SC_ARGS);
+        case 5: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, true, 1, 512>(SC_ARGS);
+        case 6: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, false, 2, 512>(SC_ARGS);
+        default: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, true, 2, 512>(SC_ARGS);
+      }
     }
     if (nts) return launch_scaffold_variant<TIn, true, true, 4, 4>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 4, 4>(SC_ARGS);
@@ -2043,6 +2078,9 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
   else if (!strcmp(key, "flat_vec")) g_flat_vec = value ? 1 : 0;
   else if (!strcmp(key, "tpb")) g_tpb = value < 1 ? 1 : (value > 64 ? 64 : (int)value);
+  else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
+  else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
+  else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

@@ -746,19 +746,25 @@ def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
                                    dict(sc_bsplit=1, sc_vpt=4, sc_unroll=8), dict(sc_bsplit=1, sc_vpt=2, sc_unroll=8),
                                    dict(sc_bsplit=1, nt_store=0), dict(sc_buf=1), dict(sc_buf=1, sc_vpt=4, sc_unroll=2),
                                    dict(sc_buf=1, sc_vpt=8, sc_unroll=2, grid_cap=3), dict(sc_buf=1, sc_vpt=8, sc_unroll=4),
-                                   dict(sc_buf=1, sc_vpt=2), dict(sc_buf=1, nt_store=0)])
+                                   dict(sc_buf=1, sc_vpt=2), dict(sc_buf=1, nt_store=0),
+                                   dict(sc_vpt=4, sc_unroll=4, sc_cpf=1), dict(sc_vpt=4, sc_unroll=4, sc_cpf=1, K=12),
+                                   dict(sc_vpt=4, sc_unroll=4, sc_occ=4), dict(sc_vpt=4, sc_unroll=4, sc_blk=512),
+                                   dict(sc_vpt=4, sc_unroll=4, sc_cpf=1, sc_occ=4, K=16),
+                                   dict(sc_vpt=4, sc_unroll=4, sc_cpf=1, sc_blk=512, grid_cap=3, K=8),
+                                   dict(sc_vpt=4, sc_unroll=4, sc_occ=2, sc_blk=512, K=16)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
     from substrafl_amd.engine import ScaffoldPlan, scaffold_weights
 
-    K, M = 11, 300_007
+    knobs = dict(knobs)
+    K, M = knobs.pop("K", 11), 300_007
     d = torch.randn((K, M + 1), device="cuda")
     cv = torch.randn((K, M + 1), device="cuda")
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
     default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_bsplit=0, sc_buf=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0,
-                   xcd=0, tpb=1)
+                   xcd=0, tpb=1, sc_cpf=0, sc_occ=0, sc_blk=256)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)

@@ -1,21 +1,19 @@
 #!/usr/bin/env python3
-"""Numerical drift and on-GPU cost of the north-star client-sharded mode.
+"""Numerical drift of the client-sharded (north-star) combines, computed by the product code
+(substrafl_amd.sharding.client_shard_fedavg with GpuShardOps) with G ranks as threads on one GPU
+(LoopbackGroup: the same per-rank kernels and the same exchange steps as over RCCL).
 
-Client sharding splits the K clients into G contiguous blocks, sums each block on its own GPU
-with the global weights fl32(n_k / n), and combines the G partial sums on the root (RCCL reduce,
-or a gather + rank-order sum).  That re-associates the reference's sequential client sum
-(fed_avg.py:222), so the result drifts from the reference.  This tool measures the drift in ulp
-against the single-pass kernel result -- bit-identical to the reference (tests/test_gpu_parity.py)
--- on N(0,1) data (SURVEY.md §8(e) setup: K = 64, M = 1M, n_k ~ U{100..10000}) and on
-cancellation-heavy data (G2-style: alternating +-1e4 plus N(0,1)), for G in {2, 4, 8}, and times
-the per-block partial kernels and the rank-order combine on one GPU.  The xGMI reduce itself
-needs several GPUs and is not timed here.
-
-Prints one JSON line per (data, G)."""
+For each combine (relay / ordered / rccl-style sum) and G in {2, 4, 8}, the root's result is
+compared with the single-pass kernel result -- bit-identical to the reference
+(tests/test_gpu_parity.py) -- in ulp, on N(0,1) data (SURVEY.md §8(e) setup: K = 64, M = 1M,
+n_k ~ U{100..10000}) and on cancellation-heavy data (alternating +-1e4 plus N(0,1)).  The
+loopback's reduce sums the partials in rank order (RCCL's order over xGMI is its own choice:
+same drift class).  Prints one JSON line per (data, combine, G)."""
 
 import argparse
 import json
 import sys
+import threading
 from pathlib import Path
 
 import numpy as np
@@ -36,11 +34,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--K", type=int, default=64)
     ap.add_argument("--M", type=int, default=1_000_000)
-    ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     import torch
 
     from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, LoopbackGroup, block_of, client_blocks,
+                                        client_shard_fedavg)
 
     K, M = args.K, args.M
     dev = torch.device("cuda", 0)
@@ -51,41 +50,45 @@ def main():
     data = {"normal": torch.randn((K, M), generator=g, device=dev)}
     sign = torch.tensor([1.0 if k % 2 == 0 else -1.0 for k in range(K)], device=dev)[:, None]
     data["cancellation"] = sign * 1e4 + torch.randn((K, M), generator=g, device=dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    pw = np.zeros(0, np.uint64)
     for name, x in data.items():
         ref = torch.empty(M, device=dev)
         FedAvgPlan("f32", x, w, M, ref).launch()
         ref_h = ref.cpu().numpy()
-        for G in (2, 4, 8):
-            per = -(-K // G)
-            blocks = [list(range(r * per, min(K, (r + 1) * per))) for r in range(G)]
-            parts = torch.empty((G, M), device=dev)
-            plans = [FedAvgPlan("f32", [x[k].data_ptr() for k in b], w[b], M, parts[r]) for r, b in enumerate(blocks)]
+        for combine in ("relay", "ordered", "rccl"):
+            for G in (2, 4, 8):
+                grp = LoopbackGroup(G)
+                res = [None] * G
+                err = [None] * G
 
-            def run():
-                for p in plans:
-                    p.launch()
-                tot = parts[0].clone()
-                for r in range(1, G):
-                    tot.add_(parts[r])  # rank-order combine on the root, fp32
-                return tot
+                def body(r):
+                    try:
+                        s = torch.cuda.Stream(device=dev)
+                        with torch.cuda.stream(s):
+                            k0, k1 = client_blocks(K, G)[block_of(r, G)]
+                            out = torch.empty(M, device=dev)
+                            sh = FedAvgShard("f32", x[k0:k1], w[k0:k1], k0, K, M, pw)
+                            if client_shard_fedavg(sh, out, grp.transport(r), GpuShardOps(), combine):
+                                s.synchronize()
+                                res[r] = out.cpu().numpy()
+                        s.synchronize()
+                    except BaseException as e:  # noqa: BLE001
+                        err[r] = e
 
-            tot = run()
-            torch.cuda.synchronize()
-            ev[0].record()
-            for _ in range(args.iters):
-                run()
-            ev[1].record()
-            torch.cuda.synchronize()
-            ms = ev[0].elapsed_time(ev[1]) / args.iters
-            d = ulp_distance(tot.cpu().numpy(), ref_h)
-            print(json.dumps({
-                "data": name, "K": K, "M": M, "G": G,
-                "median_ulp": float(np.median(d)), "p99_ulp": float(np.percentile(d, 99)), "max_ulp": int(d.max()),
-                "frac_gt_2ulp": round(float(np.mean(d > 2)), 4), "frac_exact": round(float(np.mean(d == 0)), 4),
-                "one_gpu_partials_plus_combine_ms": round(ms, 4),
-                "single_pass_equivalent_GBps": round((K * M * 4 + M * 4) / (ms / 1e3) / 1e9, 1),
-            }), flush=True)
+                th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+                for e in err:
+                    if e is not None:
+                        raise e
+                d = ulp_distance(res[0], ref_h)
+                print(json.dumps({
+                    "data": name, "combine": combine, "K": K, "M": M, "G": G,
+                    "median_ulp": float(np.median(d)), "p99_ulp": float(np.percentile(d, 99)), "max_ulp": int(d.max()),
+                    "frac_gt_2ulp": round(float(np.mean(d > 2)), 4), "frac_exact": round(float(np.mean(d == 0)), 4),
+                }), flush=True)
 
 
 if __name__ == "__main__":

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--kernel", default="fedavg_kernel")
     ap.add_argument("--bytes-alg", type=float, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--lib", default="", help="libfedagg.so the passes ran (its sha256 goes into the record)")
+    ap.add_argument("--collected", default="", help="free text: box / command / date of the passes")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     write = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -57,6 +59,12 @@ def main():
         "traffic_over_alg": (read_b + write_b) / a.bytes_alg,
         "correction": "FETCH_SIZE x2 (gfx950 wide-stream tally), KiB x1024",
     }
+    if a.lib:
+        import hashlib
+
+        res["lib_sha256"] = hashlib.sha256(Path(a.lib).read_bytes()).hexdigest()[:16]
+    if a.collected:
+        res["collected"] = a.collected
     Path(a.out).write_text(json.dumps(res, indent=1))
     print(json.dumps(res))
 

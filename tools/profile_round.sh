@@ -1,0 +1,42 @@
+#!/bin/bash
+# One profiling session per workload, on the GPU box (DESIGN.md §5 evidence):
+#   1. the bench line itself;
+#   2. rocprofv3 --kernel-trace --stats of the same bench command (kernel average duration);
+#   3. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) -> HBM bytes per launch (tools/pmc_traffic.py).
+# Usage: tools/profile_round.sh TAG WORKLOAD [WORKLOAD ...]   (outputs under gpurun_out/TAG_*)
+set -euo pipefail
+TAG=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+for WL in "$@"; do
+  case $WL in
+    c2) KERN=fedavg_kernel; ALG=900000000; STEPS=200 ;;
+    c3) KERN=fedavg_kernel; ALG=32500000000; STEPS=100 ;;
+    c4) KERN=scaffold_kernel; ALG=3700000000; STEPS=100 ;;
+    c5) KERN=fedavg_kernel; ALG=91000000000; STEPS=30 ;;
+    *) echo "unknown workload $WL"; exit 2 ;;
+  esac
+  echo "[$TAG] $WL: bench" >&2
+  timeout -k 10 400 python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 > "$OUT/${TAG}_bench_${WL}.json"
+  echo "[$TAG] $WL: kernel trace" >&2
+  rm -rf "$OUT/${TAG}_prof_${WL}"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof_${WL}" -o run -- \
+    python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 --no-cpu-baseline \
+    > "$OUT/${TAG}_profiled_bench_${WL}.json"
+  STATS=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_stats.csv' | head -1)
+  cp "$STATS" "$OUT/${TAG}_${WL}_kernel_stats.csv"
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "[$TAG] $WL: pmc $C" >&2
+    rm -rf "$OUT/${TAG}_pmc_${C}_${WL}"
+    timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/${TAG}_pmc_${C}_${WL}" -o run -- \
+      python3 "$ROOT/bench.py" --workload "$WL" --steps 10 --warmup 2 --no-cpu-baseline > /dev/null
+    cp "$(find "$OUT/${TAG}_pmc_${C}_${WL}" -name '*counter_collection.csv' | head -1)" "$OUT/${TAG}_${WL}_pmc_${C}.csv"
+  done
+  python3 "$ROOT/tools/pmc_traffic.py" --fetch "$OUT/${TAG}_${WL}_pmc_FETCH_SIZE.csv" \
+    --write "$OUT/${TAG}_${WL}_pmc_WRITE_SIZE.csv" --kernel $KERN --bytes-alg $ALG \
+    --lib "$ROOT/substrafl_amd/libfedagg.so" --collected "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, session $TAG" \
+    --out "$OUT/${TAG}_traffic_${WL}.json" > /dev/null
+done
+echo "[$TAG] done" >&2

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--M", type=int, default=25_000_000)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only-new", action="store_true", help="only the c-prefetch / occupancy / 512-thread variants")
     args = ap.parse_args()
     import torch
 
@@ -46,7 +47,14 @@ def main():
                  for v, u in ((8, 4), (8, 2), (4, 4), (4, 8), (2, 8))]
     variants += [dict(sc_split=0, sc_pipe=0, sc_buf=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
                  for v, u in ((4, 4), (4, 2), (8, 2), (8, 4))]
-    variants = [dict(dict(tpb=1, sc_bsplit=0, sc_buf=0), **v) for v in variants]
+    variants += [dict(sc_split=0, sc_pipe=0, sc_vpt=4, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0, sc_cpf=cpf,
+                      sc_occ=occ, sc_blk=blk)
+                 for cpf in (0, 1) for occ in (0, 4) for blk in (256, 512) if (cpf, occ, blk) != (0, 0, 256)
+                 if not (occ == 4 and blk == 512)]
+    if args.only_new:
+        variants = [v for v in variants if "sc_cpf" in v] + [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4,
+                                                                  nt_store=1, grid_cap=0, xcd=0)]
+    variants = [dict(dict(tpb=1, sc_bsplit=0, sc_buf=0, sc_cpf=0, sc_occ=0, sc_blk=256), **v) for v in variants]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {i: [] for i in range(len(variants))}
     for _ in range(args.rounds):
