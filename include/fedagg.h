@@ -298,7 +298,8 @@ int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes
  * same bytes of rows 1..K-1 are compared with it by value on the pack workers (+0 == -0,
  * NaN == NaN; byte-identical stretches skipped) and the number of mismatching elements is written
  * to *mismatches.  kind: FEDAGG_F32 or FEDAGG_F64 (every segment of that element type; the range
- * element-aligned).  Replaces K-1 PCIe copies plus the device check (fedagg_equal_count_*). */
+ * element-aligned).  Replaces K-1 PCIe copies plus the device check (fedagg_equal_count_*).
+ * d_dst may be NULL: compare only (rows already staged, e.g. while the inputs are still loading). */
 int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, const void* const* h_seg,
                                const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, int kind,
                                uint64_t* mismatches);

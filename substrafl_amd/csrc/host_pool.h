@@ -158,7 +158,7 @@ int stage_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, c
                    int check_esz = 0, uint64_t* mismatches = nullptr) {
   const uint64_t cb = ring.chunk_bytes;
   const int R = ring.size();
-  const int Ks = check_esz ? 1 : K;
+  const int Ks = !d_dst ? 0 : check_esz ? 1 : K;  // check_esz with no destination: compare only
   const uint64_t per_row = row ? (row + cb - 1) / cb : 0;
   const uint64_t units = per_row * (uint64_t)Ks;
   const bool two = two_queues && units > 1;

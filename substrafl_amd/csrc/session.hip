@@ -289,8 +289,10 @@ namespace {
 
 // shared argument checks and set-up of the staging entry points; returns the row length in bytes
 int stage_prepare(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg, const void* const* h_seg,
-                  const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, uint64_t* row_out) {
-  if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) || byte_hi < byte_lo)
+                  const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, uint64_t* row_out,
+                  bool dst_optional = false) {
+  if (!s || (!d_dst && !dst_optional) || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) ||
+      byte_hi < byte_lo)
     return FEDAGG_EINVAL;
   HIP_TRY(hipSetDevice(s->device));
   int rc = s->ensure_ring();
@@ -365,7 +367,7 @@ int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, 
     return FEDAGG_EINVAL;
   }
   uint64_t row = 0;
-  int rc = stage_prepare(s, d_dst, byte_hi - byte_lo, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row);
+  int rc = stage_prepare(s, d_dst, byte_hi - byte_lo, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row, true);
   if (rc) return rc;
   *mismatches = 0;
   return stage_run(s, d_dst, row, K, nseg, h_seg, seg_bytes, byte_lo, row, esz, mismatches);

@@ -369,8 +369,9 @@ class AggregationEngine:
     def _ingest_plan(self, state, strategy: str, K: int):
         """Layouts and buffers for staging rows shaped like ``state``'s (None: do not prestage)."""
         if strategy == "scaffold":
-            # the server control variates are not prestaged: the aggregation stages ONE copy and
-            # checks the others against it on the host (Session.stage_check)
+            # server control variates: ONE copy is staged (the first client loaded), every other
+            # client's copy is compared with it on the host as it arrives (Session.check) -- the
+            # check of scaffold.py:193-196 overlapped with the loading, K-1 PCIe copies saved
             lists = (("parameters_update", self._B_BUCKET), ("control_variate_update", self._B_CV))
         else:
             lists = (("parameters_update", self._B_BUCKET),)
@@ -398,20 +399,35 @@ class AggregationEngine:
             ld_bytes = layout.ld * dt.itemsize
             d = s.buffer(slot, K * ld_bytes)
             self._prestaged[slot] = [d, ld_bytes, {}]
-            plan.append((field, slot, layout, d, ld_bytes, row[0].dtype))
+            plan.append((field, slot, layout, d, ld_bytes, row[0].dtype, False))
+        if strategy == "scaffold" and self.c_check == "host" and c_row and all(
+                isinstance(a, np.ndarray) and a.dtype == targets[0] for a in c_row):
+            dt = targets[0]
+            layout = BucketLayout(list(range(len(c_row))), [a.shape for a in c_row], dt)
+            ld_bytes = layout.ld * dt.itemsize
+            d = s.buffer(self._B_C, K * ld_bytes)
+            self._prestaged[self._B_C] = [d, ld_bytes, {}]
+            self._c_ref, self._c_mism = None, 0
+            plan.append(("server_control_variate", self._B_C, layout, d, ld_bytes, dt, True))
         self._prestaged_session = s
         return plan
 
     def _ingest_row(self, plan, k: int, state) -> bool:
         s = self.session()
-        for field, slot, layout, d, ld_bytes, src in plan:
+        for field, slot, layout, d, ld_bytes, src, check in plan:
             row = list(getattr(state, field))
             if len(row) != len(layout.segments) or any(
                     a.dtype != src or a.shape != g.shape for a, g in zip(row, layout.segments)):
                 return False
-        for field, slot, layout, d, ld_bytes, src in plan:
+        for field, slot, layout, d, ld_bytes, src, check in plan:
             row = list(getattr(state, field))
-            self._stage_rows(s, [row], layout, d + k * ld_bytes)
+            if not check:
+                self._stage_rows(s, [row], layout, d + k * ld_bytes)
+            elif self._c_ref is None:  # the first client loaded: its c is the staged copy
+                self._stage_rows(s, [row], layout, d)
+                self._c_ref = row
+            else:  # value check against the staged copy (equality is an equivalence: +0 == -0, NaN == NaN)
+                self._c_mism += s.check([self._c_ref, row], src)
             self._prestaged[slot][2][k] = row  # holds the arrays: their ids stay unique
         return True
 
@@ -620,8 +636,11 @@ class AggregationEngine:
             else:
                 self._stage_rows(s, rows, lay, d)
         c_rows = [list(r) for r in server_control_variates]
+        c_ingested = host_c and self._take_prestaged(self._B_C, d_cc, lay_s.ld * isz, c_rows)
         if same_c:
             self._stage_rows(s, c_rows[:1], lay_s, d_cc)
+        elif c_ingested:  # one copy staged and the others checked while ingest() was loading them
+            host_mism = self._c_mism
         elif host_c:
             flats = [flat_of(r) for r in c_rows]
             if all(f is not None and f.size == lay_s.M for f in flats):
@@ -631,7 +650,7 @@ class AggregationEngine:
             self._stage_rows(s, c_rows, lay_s, d_cc)
         self._prestaged = {}
         tm["prestaged"] = pre == 2
-        tm["c_check"] = "identity" if same_c else ("host" if host_c else "device")
+        tm["c_check"] = "identity" if same_c else ("host-ingest" if c_ingested else "host" if host_c else "device")
         tm["stage_s"] = time.perf_counter() - t0
         t1 = time.perf_counter()
         cnt = s.buffer(self._B_CNT, 8)

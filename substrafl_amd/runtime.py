@@ -152,12 +152,17 @@ class Session:
                 if a.dtype != dtype:
                     raise ValueError("stage_check: every array must have the checked dtype")
         lo, hi = (0, sum(int(sizes[i]) for i in range(nseg))) if byte_range is None else byte_range
-        self._bump(d_dst)
+        if d_dst:
+            self._bump(d_dst)
         mism = ctypes.c_uint64(0)
         _native.check(self.lib.fedagg_session_stage_check(self._h, ctypes.c_void_p(d_dst), len(rows), nseg, ptrs,
                                                           sizes, int(lo), int(hi), kind, ctypes.byref(mism)),
                       "session_stage_check")
         return int(mism.value)
+
+    def check(self, rows: Sequence[Sequence[np.ndarray]], dtype) -> int:
+        """Value mismatches of rows[1:] against rows[0] on the pack workers (nothing staged)."""
+        return self.stage_check(0, rows, dtype)
 
     def event_record(self, ev: int) -> None:
         _native.check(self.lib.fedagg_session_event_record(self._h, int(ev)), "session_event_record")

@@ -916,9 +916,20 @@ def test_ingest_overlapped_staging(torch_gpu, dummy_algo_class, tmp_path):
     assert eng.last_ingest["prestaged_clients"] == K
     res = sc.avg_shared_states(sstates, _skip=True)
     assert eng.last_timing.get("prestaged") is True
+    # every file carries its own copy of c: one copy staged, the others checked while loading
+    assert eng.last_timing["c_check"] == "host-ingest"
     rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.4)
     _assert_same(res.server_control_variate, rc)
     _assert_same(res.avg_parameters_update, ra)
+    # a client whose c differs in one element fails the check
+    c_bad = [a.copy() for a in c]
+    c_bad[3][7] += 1.0
+    PickleSerializer.save(ScaffoldSharedState(parameters_update=pus[2], control_variate_update=cvs[2], n_samples=ns[2],
+                                              server_control_variate=c_bad), spaths[2])
+    sstates = sc.ingest_shared_states("avg_shared_states", spaths, PickleSerializer.load)
+    with pytest.raises(AssertionError):
+        sc.avg_shared_states(sstates, _skip=True)
+    assert eng.last_timing["c_check"] == "host-ingest"
 
 
 def test_fedavg_layout_edge_cases(torch_gpu, dummy_algo_class):
