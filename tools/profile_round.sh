@@ -22,7 +22,7 @@ for WL in "$@"; do
   timeout -k 10 400 python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 > "$OUT/${TAG}_bench_${WL}.json"
   echo "[$TAG] $WL: kernel trace" >&2
   rm -rf "$OUT/${TAG}_prof_${WL}"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof_${WL}" -o run -- \
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_${WL}" -o run -- \
     python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 --no-cpu-baseline \
     > "$OUT/${TAG}_profiled_bench_${WL}.json"
   STATS=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_stats.csv' | head -1)
@@ -30,7 +30,7 @@ for WL in "$@"; do
   for C in FETCH_SIZE WRITE_SIZE; do
     echo "[$TAG] $WL: pmc $C" >&2
     rm -rf "$OUT/${TAG}_pmc_${C}_${WL}"
-    timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/${TAG}_pmc_${C}_${WL}" -o run -- \
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/${TAG}_pmc_${C}_${WL}" -o run -- \
       python3 "$ROOT/bench.py" --workload "$WL" --steps 10 --warmup 2 --no-cpu-baseline > /dev/null
     cp "$(find "$OUT/${TAG}_pmc_${C}_${WL}" -name '*counter_collection.csv' | head -1)" "$OUT/${TAG}_${WL}_pmc_${C}.csv"
   done
