@@ -74,18 +74,21 @@ def _fedavg(G, K, combine, kind="f32", chunk_elems=4096):
 
     from substrafl_amd.engine import fedavg_weights
     from substrafl_amd.layout import BucketLayout
-    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, block_of, client_blocks, client_shard_fedavg)
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, block_of, client_blocks, client_shard_fedavg,
+                                        out_dtype)
 
     pus, ns = _data(K)
     if kind == "bf16":  # bf16-representable values: the reference runs on the exact upcast
         pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
-    layout = BucketLayout(range(len(SHAPES)), SHAPES, np.float32)
+    npdt = {"f32": np.float32, "bf16": np.float32, "f64": np.float64, "f16": np.float16}[kind]
+    pus = [[a.astype(npdt) for a in c] for c in pus]
+    layout = BucketLayout(range(len(SHAPES)), SHAPES, npdt)
     w = fedavg_weights(ns, kind)
 
     def rank_fn(r, tr):
         k0, k1 = client_blocks(K, G)[block_of(r, G)]
-        rows = _rows(torch, pus[k0:k1], layout, tdtype=torch.bfloat16 if kind == "bf16" else None)
-        out = torch.zeros(layout.ld, dtype=torch.float32, device="cuda")
+        rows = _rows(torch, pus[k0:k1], layout, dtype=npdt, tdtype=torch.bfloat16 if kind == "bf16" else None)
+        out = torch.zeros(layout.ld, dtype=out_dtype(torch, kind), device="cuda")
         sh = FedAvgShard(kind, rows, w[k0:k1], k0, K, layout.M, layout.pairwise_idx)
         if client_shard_fedavg(sh, out, tr, GpuShardOps(), combine, chunk_elems=chunk_elems):
             torch.cuda.current_stream().synchronize()
@@ -109,6 +112,15 @@ def test_relay_fedavg_bf16_bit_exact():
     got, ref = _fedavg(4, 9, "relay", kind="bf16")
     for g, r in zip(got, ref):
         assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+@pytest.mark.parametrize("kind,bits", [("f64", np.uint64), ("f16", np.uint16)])
+def test_relay_fedavg_other_kinds_bit_exact(kind, bits):
+    """fp64 and fp16 buckets: the accumulator travels between ranks in the product type (NumPy's
+    per-op rounding for fp16), the numel == 1 tree sums fp16 products in fp32."""
+    got, ref = _fedavg(3, 11, "relay", kind=kind)
+    for g, r in zip(got, ref):
+        assert g.dtype == r.dtype and np.array_equal(g.view(bits), r.view(bits))
 
 
 @pytest.mark.parametrize("combine", ["ordered", "rccl"])

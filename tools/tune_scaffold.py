@@ -51,8 +51,10 @@ def main():
                       sc_occ=occ, sc_blk=blk)
                  for cpf in (0, 1) for occ in (0, 4) for blk in (256, 512) if (cpf, occ, blk) != (0, 0, 256)
                  if not (occ == 4 and blk == 512)]
+    variants += [dict(sc_split=0, sc_pipe=0, sc_vpt=v, sc_unroll=u, nt_store=0, grid_cap=0, xcd=0)
+                 for v, u in ((4, 4), (4, 2), (8, 1))]
     if args.only_new:
-        variants = [v for v in variants if "sc_cpf" in v] + [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4,
+        variants = [v for v in variants if "sc_cpf" in v or v.get("nt_store") == 0] + [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4,
                                                                   nt_store=1, grid_cap=0, xcd=0)]
     variants = [dict(dict(tpb=1, sc_bsplit=0, sc_buf=0, sc_cpf=0, sc_occ=0, sc_blk=256), **v) for v in variants]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
