@@ -297,9 +297,6 @@ class GpuShardOps:
 # ======================================================================================
 # transports
 # ======================================================================================
-_WARMED: set = set()
-
-
 class DistTransport:
     """The exchange steps over a ``torch.distributed`` group: RCCL (backend "nccl") on device
     tensors in the product; gloo on CPU tensors in the CPU tests.  Ranks are group ranks."""
@@ -312,10 +309,10 @@ class DistTransport:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         # one group-wide collective before the first point-to-point call: NCCL's batched P2P must
-        # not be the first operation a communicator sees on only some of its ranks
-        if self.world > 1 and id(group) not in _WARMED:
+        # not be the first operation a communicator sees on only some of its ranks (a few tens of
+        # microseconds per transport; transports are built once per aggregation, not per step)
+        if self.world > 1:
             self.all_sum_int(0)
-            _WARMED.add(id(group))
 
     def _g(self, r: int) -> int:
         return r if self.group is None else self.dist.get_global_rank(self.group, r)

@@ -1,0 +1,111 @@
+"""Property tests of the client-sharded protocol (substrafl_amd.sharding) on CPU: G ranks as
+threads over LoopbackGroup with the NumPy per-rank ops (tests/shard_cpu_ops.py, test
+infrastructure) -- random client counts, rank counts, layer shapes (numel == 1 included) and
+relay chunk sizes.  The relay combine must reproduce the reference oracle bit for bit; the
+re-associating combines must agree to rounding and keep the numel == 1 tensors exact."""
+
+import threading
+
+import numpy as np
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from oracle import fedavg_reference_structure, scaffold_reference_structure
+from shard_cpu_ops import CpuShardOps
+from substrafl_amd.engine import fedavg_weights, scaffold_weights
+from substrafl_amd.layout import BucketLayout
+from substrafl_amd.sharding import (FedAvgShard, LoopbackGroup, ScaffoldShard, block_of, client_blocks,
+                                    client_shard_fedavg, client_shard_scaffold)
+
+
+def _rows(lists, layout, dtype):
+    rows = np.zeros((max(1, len(lists)), layout.ld), dtype)
+    for k, lay in enumerate(lists):
+        layout.pack_row(lay, rows[k])
+    return torch.from_numpy(rows)[: len(lists)]
+
+
+def _run(G, fn):
+    grp = LoopbackGroup(G)
+    res, err = [None] * G, [None] * G
+
+    def body(r):
+        try:
+            res[r] = fn(r, grp.transport(r))
+        except BaseException as e:  # noqa: BLE001
+            err[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+        assert not t.is_alive()
+    for e in err:
+        if e is not None:
+            raise e
+    assert all(x is None for x in res[1:])
+    return res[0]
+
+
+shape_st = st.lists(st.sampled_from([(1,), (1, 1), (7,), (33,), (5, 3), (200,), (2, 1, 3)]), min_size=1, max_size=5)
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.integers(1, 12), st.integers(1, 6), shape_st, st.sampled_from([512, 1024, 4096]),
+       st.sampled_from(["relay", "ordered", "rccl"]), st.integers(0, 2**31))
+def test_fedavg_client_shard_property(K, G, shapes, chunk, combine, seed):
+    rng = np.random.default_rng(seed)
+    pus = [[(rng.standard_normal(s) * 10.0 ** rng.integers(-2, 3)).astype(np.float32) for s in shapes] for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    layout = BucketLayout(range(len(shapes)), shapes, np.float32)
+    w = fedavg_weights(ns, "f32")
+
+    def rank(r, tr):
+        k0, k1 = client_blocks(K, G)[block_of(r, G)]
+        sh = FedAvgShard("f32", _rows(pus[k0:k1], layout, np.float32), w[k0:k1], k0, K, layout.M, layout.pairwise_idx)
+        out = torch.zeros(layout.ld, dtype=torch.float32)
+        if client_shard_fedavg(sh, out, tr, CpuShardOps(), combine, chunk_elems=chunk):
+            return out[: layout.M].numpy().copy()
+        return None
+
+    got = [a for _, a in layout.unpack(_run(G, rank))]
+    ref = fedavg_reference_structure(pus, ns)
+    for g, r in zip(got, ref):
+        if combine == "relay" or g.size == 1 or G == 1:
+            assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+        else:
+            np.testing.assert_allclose(g, r, rtol=1e-5, atol=1e-4)
+
+
+@settings(max_examples=25, deadline=None)
+@given(st.integers(1, 9), st.integers(1, 5), shape_st, st.sampled_from(["relay", "ordered", "rccl"]),
+       st.sampled_from([0.0, 0.5, 1.0, 2.0]), st.integers(0, 2**31))
+def test_scaffold_client_shard_property(K, G, shapes, combine, lr, seed):
+    rng = np.random.default_rng(seed)
+    mk = lambda: [rng.standard_normal(s).astype(np.float32) for s in shapes]  # noqa: E731
+    pus, cvs, c = [mk() for _ in range(K)], [mk() for _ in range(K)], mk()
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    layout = BucketLayout(range(len(shapes)), shapes, np.float32)
+    w = scaffold_weights(ns)
+
+    def rank(r, tr):
+        k0, k1 = client_blocks(K, G)[block_of(r, G)]
+        sh = ScaffoldShard("f32", _rows(pus[k0:k1], layout, np.float32), _rows(cvs[k0:k1], layout, np.float32),
+                           _rows([c], layout, np.float32)[0], w[k0:k1], k0, K, layout.M, lr, layout.pairwise_idx)
+        dout = torch.zeros(layout.ld, dtype=torch.float64)
+        cout = torch.zeros(layout.ld, dtype=torch.float64)
+        if client_shard_scaffold(sh, dout, cout, tr, CpuShardOps(), combine, chunk_elems=512):
+            return dout[: layout.M].numpy().copy(), cout[: layout.M].numpy().copy()
+        return None
+
+    d, cc = _run(G, rank)
+    lay64 = BucketLayout(range(len(shapes)), shapes, np.float64)
+    got = [a for _, a in lay64.unpack(cc)] + [a for _, a in lay64.unpack(d)]
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
+    for g, r in zip(got, rc + ra):
+        if combine == "relay" or g.size == 1 or G == 1:
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+        else:
+            np.testing.assert_allclose(g, r, rtol=1e-12, atol=1e-12)
