@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--grid-cap", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=-1)
     ap.add_argument("--traffic", default="", help="JSON with PMC-derived bytes per launch (profiles/)")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="run only the cpu_baseline leg (no GPU) and print its JSON")
+    ap.add_argument("--cpu-full-size", action="store_true",
+                    help="cpu_baseline over the workload's full K x M instead of a bounded sample (C3: ~40 GB host)")
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="tests only: run the launcher / rank / timing plumbing with no GPU (no measurement)")
     return ap.parse_args()
@@ -156,6 +160,10 @@ def read_traffic(args, sha):
 # ======================================================================================
 def main():
     args = parse()
+    if args.cpu_only:
+        print(json.dumps(cpu_baseline(WORKLOADS[args.workload], args.cpu_seconds, full=args.cpu_full_size)),
+              flush=True)
+        return None
     if args.engine == "multi-device":
         return multi_device_bench(args)
     world_env = os.environ.get("WORLD_SIZE")
@@ -354,7 +362,7 @@ def main():
     # ---- CPU baseline (rank 0, N == 1): the reference call structure timed on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(wl, args.cpu_seconds)
+        cpu = cpu_baseline(wl, args.cpu_seconds, full=args.cpu_full_size)
 
     sha = lib_sha256()
     traffic, tsrc = read_traffic(args, sha) if (world == 1 or args.scaling == "weak") and not client_shard \
@@ -606,19 +614,26 @@ def rehearse(args, world, rank):
         dist.destroy_process_group()
 
 
-def cpu_baseline(wl, budget_s):
+def cpu_baseline(wl, budget_s, full=False):
     """Time the oracle's reference-call-structure FedAvg/Scaffold (list of products, np.sum) on a
-    bounded host sample of the same workload shape.  NumPy's ufuncs are single-threaded here,
-    so the reference path uses one core whatever the machine has."""
+    bounded host sample of the same workload shape (``full``: the workload's whole K x M; C3 is
+    32 GB of client states, ~40 GB peak; C5 cannot be held by the reference on a box's host).
+    NumPy's ufuncs are single-threaded here, so the reference path uses one core whatever the
+    machine has."""
     from oracle import fedavg_reference_structure, scaffold_reference_structure
     from substrafl_amd.layout import synthetic_state_dict_shapes
 
     K = wl["K"]
-    M_s = min(wl["M"], 25_000_000 if K <= 16 else 4_000_000)
+    M_s = wl["M"] if full else min(wl["M"], 25_000_000 if K <= 16 else 4_000_000)
     shapes = synthetic_state_dict_shapes(M_s)
     rng = np.random.default_rng(1)
+    base = [rng.standard_normal(s, dtype=np.float32) for s in shapes] if full else None
+    counter = [0]
 
     def client():
+        if base is not None:  # full size: distinct clients as scaled copies (no K x M random draws)
+            counter[0] += 1
+            return [(a * np.float32(1 + 1e-3 * counter[0])).astype(np.float32) for a in base]
         return [rng.standard_normal(s, dtype=np.float32) for s in shapes]
 
     n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
@@ -637,7 +652,7 @@ def cpu_baseline(wl, budget_s):
         nbytes = 2 * K * M_s * 4 + M_s * 4 + 2 * M_s * 8
     times = []
     t_end = time.perf_counter() + budget_s
-    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 50):
+    while len(times) < (2 if full else 3) or (time.perf_counter() < t_end and len(times) < 50):
         t0 = time.perf_counter()
         fn()
         times.append(time.perf_counter() - t0)
@@ -653,7 +668,8 @@ def cpu_baseline(wl, budget_s):
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{K} clients x {M_s} fp32 params ({len(shapes)} layers), best of {len(times)} runs "
+        "sample": f"{'FULL SIZE: ' if full else ''}{K} clients x {M_s} fp32 params ({len(shapes)} layers), "
+                  f"best of {len(times)} runs "
                   f"({best * 1e3:.1f} ms); oracle/aggregation.py reference call structure; "
                   f"host has {os.cpu_count()} cpus, affinity {aff}, NumPy ufuncs single-threaded",
     }
