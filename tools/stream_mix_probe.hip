@@ -28,7 +28,7 @@ constexpr int SU = 4;
 
 // B buckets of K client rows each (row stride nvec vectors), plus C extra single streams read
 // last; W = output vectors written per input vector and bucket (0: none, 1: 16 B, 2: 32 B).
-template <int K, int B, int C, int W>
+template <int K, int B, int C, int W, bool INTER = false>
 __global__ void __launch_bounds__(BLOCK) pattern(const u32x4* __restrict__ x, const u32x4* __restrict__ c,
                                                  uint64_t nvec, u32x4* __restrict__ out) {
   const uint64_t tile = (uint64_t)VPT * BLOCK;
@@ -48,8 +48,10 @@ __global__ void __launch_bounds__(BLOCK) pattern(const u32x4* __restrict__ x, co
       for (int n = 0; n < VPT; ++n)
 #pragma unroll
         for (int b = 0; b < B; ++b)
-          r[b][u][n] = __builtin_nontemporal_load(x + ((uint64_t)b * K + k0 + u) * nvec + t * tile +
-                                                  (uint64_t)n * BLOCK + threadIdx.x);
+          r[b][u][n] = __builtin_nontemporal_load(
+              x + (INTER ? (t * (B * K) + (uint64_t)b * K + k0 + u) * tile   // tile-major: the B*K client
+                         : ((uint64_t)b * K + k0 + u) * nvec + t * tile) +  // tiles of one step adjacent
+              (uint64_t)n * BLOCK + threadIdx.x);
 #pragma unroll
     for (int b = 0; b < B; ++b)
 #pragma unroll
@@ -84,17 +86,18 @@ __global__ void __launch_bounds__(BLOCK) pattern(const u32x4* __restrict__ x, co
   }
 }
 
-template <int K, int B, int C, int W>
+template <int K, int B, int C, int W, bool INTER = false>
 static void run(const char* name, const u32x4* x, const u32x4* c, uint64_t nvec, u32x4* out) {
   const int grid = (int)(nvec / (VPT * BLOCK));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((pattern<K, B, C, W>), dim3(grid), dim3(BLOCK), 0, 0, x, c, nvec, out);
+  for (int i = 0; i < 3; ++i)
+    hipLaunchKernelGGL((pattern<K, B, C, W, INTER>), dim3(grid), dim3(BLOCK), 0, 0, x, c, nvec, out);
   std::vector<float> ms(15);
   for (auto& m : ms) {
     CK(hipEventRecord(a));
-    hipLaunchKernelGGL((pattern<K, B, C, W>), dim3(grid), dim3(BLOCK), 0, 0, x, c, nvec, out);
+    hipLaunchKernelGGL((pattern<K, B, C, W, INTER>), dim3(grid), dim3(BLOCK), 0, 0, x, c, nvec, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     CK(hipEventElapsedTime(&m, a, b));
@@ -124,5 +127,9 @@ int main(int argc, char** argv) {
   run<8, 1, 0, 1>("fedavg 8 clients: 8 streams, 16-B output", x, c, nvec, out);
   run<8, 1, 0, 0>("fedavg 8 clients, reads only", x, c, nvec, out);
   run<32, 1, 0, 1>("fedavg 32 clients, 16-B output", x, c, nvec, out);
+  // tile-major layout (the K client tiles of one workgroup step adjacent in memory: one stream)
+  run<16, 2, 1, 2, true>("tile-major scaffold 16 clients, 2 x 32-B outputs", x, c, nvec, out);
+  run<16, 2, 1, 0, true>("tile-major scaffold 16 clients, reads only", x, c, nvec, out);
+  run<8, 1, 0, 1, true>("tile-major fedavg 8 clients, 16-B output", x, c, nvec, out);
   return 0;
 }
