@@ -148,6 +148,29 @@ struct Ring {
   int size() const { return (int)slot.size(); }
 };
 
+// Value check of bytes [byte_lo, byte_lo + row) of rows 1..K-1 against row 0 (esz-byte elements),
+// in 1 MiB pieces of the row on the pool; returns the number of mismatching elements.  Touches
+// nothing but the pool and the caller's segments, so it may run beside a staging call.
+inline uint64_t check_rows(Pool& pool, const void* const* h_seg, const uint64_t* seg_bytes, int nseg, int K,
+                           uint64_t byte_lo, uint64_t row, int esz) {
+  const uint64_t piece = 1ull << 20;
+  const uint64_t npieces = (K >= 2 && row) ? (row + piece - 1) / piece : 0;
+  std::atomic<uint64_t> bad{0};
+  std::vector<Done> cdone(npieces ? npieces : 1);
+  for (uint64_t p = 0; p < npieces; ++p) {
+    const uint64_t a = byte_lo + p * piece, b = byte_lo + std::min(row, (p + 1) * piece);
+    Done* d = &cdone[p];
+    pool.submit([=, &bad] {
+      uint64_t n = 0;
+      for (int k = 1; k < K; ++k) n += count_mismatch_range(h_seg + (size_t)k * nseg, h_seg, seg_bytes, nseg, a, b, esz);
+      bad.fetch_add(n, std::memory_order_relaxed);
+      d->set();
+    });
+  }
+  for (uint64_t p = 0; p < npieces; ++p) cdone[p].wait();
+  return bad.load();
+}
+
 // K rows of nseg host segments -> d_dst + k * ld_bytes, bytes [byte_lo, byte_lo + row) of each
 // row.  check_esz > 0: only row 0 is staged, rows 1..K-1 are compared with it by value on the
 // host (mismatching elements added to *mismatches) -- the server-control-variate check of
@@ -158,7 +181,7 @@ int stage_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, c
                    int check_esz = 0, uint64_t* mismatches = nullptr) {
   const uint64_t cb = ring.chunk_bytes;
   const int R = ring.size();
-  const int Ks = !d_dst ? 0 : check_esz ? 1 : K;  // check_esz with no destination: compare only
+  const int Ks = check_esz ? 1 : K;
   const uint64_t per_row = row ? (row + cb - 1) / cb : 0;
   const uint64_t units = per_row * (uint64_t)Ks;
   const bool two = two_queues && units > 1;
@@ -201,24 +224,8 @@ int stage_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, c
   for (size_t i = 0; i < done.size(); ++i)  // packs still running read the caller's segments
     if (pending[i]) done[i].wait();
   if (rc || !check_esz || K < 2) return rc;
-  // value check of rows 1..K-1 against row 0, in 1 MiB pieces of the row, on the pool
-  const uint64_t piece = 1ull << 20;
-  const uint64_t npieces = row ? (row + piece - 1) / piece : 0;
-  std::atomic<uint64_t> bad{0};
-  std::vector<Done> cdone(npieces ? npieces : 1);
-  for (uint64_t p = 0; p < npieces; ++p) {
-    const uint64_t a = byte_lo + p * piece, b = byte_lo + std::min(row, (p + 1) * piece);
-    Done* d = &cdone[p];
-    pool.submit([=, &bad] {
-      uint64_t n = 0;
-      for (int k = 1; k < K; ++k) n += count_mismatch_range(h_seg + (size_t)k * nseg, h_seg, seg_bytes, nseg, a, b,
-                                                            check_esz);
-      bad.fetch_add(n, std::memory_order_relaxed);
-      d->set();
-    });
-  }
-  for (uint64_t p = 0; p < npieces; ++p) cdone[p].wait();
-  if (mismatches) *mismatches += bad.load();
+  const uint64_t bad = check_rows(pool, h_seg, seg_bytes, nseg, K, byte_lo, row, check_esz);
+  if (mismatches) *mismatches += bad;
   return 0;
 }
 

@@ -118,7 +118,9 @@ struct fedagg_session {
     ring.chunk_bytes = 0;
     ring_ev.clear();
   }
+  std::mutex pool_m;  // workers() may be reached from a compare-only check beside a stage call
   Pool& workers() {
+    std::lock_guard<std::mutex> g(pool_m);
     if (!pool || pool->size() != threads) {
       delete pool;
       pool = new Pool(threads);
@@ -289,10 +291,8 @@ namespace {
 
 // shared argument checks and set-up of the staging entry points; returns the row length in bytes
 int stage_prepare(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg, const void* const* h_seg,
-                  const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, uint64_t* row_out,
-                  bool dst_optional = false) {
-  if (!s || (!d_dst && !dst_optional) || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) ||
-      byte_hi < byte_lo)
+                  const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t byte_hi, uint64_t* row_out) {
+  if (!s || !d_dst || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) || byte_hi < byte_lo)
     return FEDAGG_EINVAL;
   HIP_TRY(hipSetDevice(s->device));
   int rc = s->ensure_ring();
@@ -366,10 +366,27 @@ int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, 
     fedagg_internal::set_error("fedagg_session_stage_check: byte range not element-aligned");
     return FEDAGG_EINVAL;
   }
-  uint64_t row = 0;
-  int rc = stage_prepare(s, d_dst, byte_hi - byte_lo, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row, true);
-  if (rc) return rc;
   *mismatches = 0;
+  if (!d_dst) {  // compare only: no HIP call, no ring -- safe beside a stage call on the same session
+    if (!s || K <= 0 || nseg < 0 || (nseg > 0 && (!h_seg || !seg_bytes)) || byte_hi < byte_lo) return FEDAGG_EINVAL;
+    uint64_t full = 0;
+    for (int i = 0; i < nseg; ++i) full += seg_bytes[i];
+    for (int k = 0; k < K; ++k)
+      for (int i = 0; i < nseg; ++i)
+        if (!h_seg[(size_t)k * nseg + i] && seg_bytes[i]) {
+          fedagg_internal::set_error("fedagg_session_stage_check: NULL host segment");
+          return FEDAGG_EINVAL;
+        }
+    if (byte_hi > full) {
+      fedagg_internal::set_error("fedagg_session_stage_check: byte range beyond the row");
+      return FEDAGG_EINVAL;
+    }
+    *mismatches = fedagg_host::check_rows(s->workers(), h_seg, seg_bytes, nseg, K, byte_lo, byte_hi - byte_lo, esz);
+    return FEDAGG_OK;
+  }
+  uint64_t row = 0;
+  int rc = stage_prepare(s, d_dst, byte_hi - byte_lo, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row);
+  if (rc) return rc;
   return stage_run(s, d_dst, row, K, nseg, h_seg, seg_bytes, byte_lo, row, esz, mismatches);
 }
 

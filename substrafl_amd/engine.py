@@ -346,6 +346,7 @@ class AggregationEngine:
             futures = [ex.submit(load, p) for p in paths]
             index = {f: k for k, f in enumerate(futures)}
             plan = None
+            checks = []  # Scaffold: value checks of the c copies, on the loader threads
             for f in as_completed(futures):
                 if f.exception() is not None:
                     plan = False  # stop staging; the error is raised below in path order
@@ -354,12 +355,16 @@ class AggregationEngine:
                 try:
                     if plan is None:
                         plan = self._ingest_plan(f.result(), strategy, K)
-                    if plan and self._ingest_row(plan, index[f], f.result()):
+                    if plan and self._ingest_row(plan, index[f], f.result(), lambda *a: checks.append(ex.submit(*a))):
                         staged += 1
                 except Exception:  # noqa: BLE001 - staging is best effort; aggregation re-validates
                     plan = False
                     self._prestaged = {}
             states = [f.result() for f in futures]
+            try:
+                self._c_mism = sum(c.result() for c in checks)
+            except Exception:  # noqa: BLE001 - the aggregation call checks again
+                self._prestaged.pop(self._B_C, None)
         s = getattr(self, "_prestaged_session", None)
         for slot, rec in self._prestaged.items():  # seal: the slots as this ingest left them
             rec.append(s.generation(slot) if s is not None else -1)
@@ -412,7 +417,7 @@ class AggregationEngine:
         self._prestaged_session = s
         return plan
 
-    def _ingest_row(self, plan, k: int, state) -> bool:
+    def _ingest_row(self, plan, k: int, state, submit=None) -> bool:
         s = self.session()
         for field, slot, layout, d, ld_bytes, src, check in plan:
             row = list(getattr(state, field))
@@ -426,7 +431,9 @@ class AggregationEngine:
             elif self._c_ref is None:  # the first client loaded: its c is the staged copy
                 self._stage_rows(s, [row], layout, d)
                 self._c_ref = row
-            else:  # value check against the staged copy (equality is an equivalence: +0 == -0, NaN == NaN)
+            elif submit is not None:  # value check against the staged copy, beside the staging
+                submit(s.check, [self._c_ref, row], src)  # (equality is an equivalence: +0 == -0, NaN == NaN)
+            else:
                 self._c_mism += s.check([self._c_ref, row], src)
             self._prestaged[slot][2][k] = row  # holds the arrays: their ids stay unique
         return True

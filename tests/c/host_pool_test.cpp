@@ -220,6 +220,36 @@ static int fetch_with_failure(Pool& pool, std::mt19937_64& rng) {
   return (dma.fail_at <= units) == (rc != 0) ? 0 : 1;
 }
 
+// check_rows (the compare-only Scaffold c check) from several threads while a staging pipeline
+// runs on the same pool -- the ingest path of engine.py does exactly this.
+static int concurrent_checks(Pool& pool, std::mt19937_64& rng) {
+  const int nseg = 3, K = 2;
+  std::vector<std::vector<float>> ref(nseg), x(nseg);
+  std::vector<uint64_t> len(nseg);
+  for (int i = 0; i < nseg; ++i) {
+    ref[i].resize(50000 + rng() % 400000);
+    for (auto& f : ref[i]) f = (float)(int)(rng() % 1000);
+    x[i] = ref[i];
+    len[i] = ref[i].size() * 4;
+  }
+  x[1][17] += 1.0f;
+  x[2][x[2].size() - 1] = -x[2][x[2].size() - 1] + 0.5f;
+  std::vector<const void*> segs;
+  for (int i = 0; i < nseg; ++i) segs.push_back(ref[i].data());
+  for (int i = 0; i < nseg; ++i) segs.push_back(x[i].data());
+  uint64_t row = 0;
+  for (auto l : len) row += l;
+  std::vector<uint64_t> got(4, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < 4; ++t)
+    th.emplace_back([&, t] { got[t] = fedagg_host::check_rows(pool, segs.data(), len.data(), nseg, K, 0, row, 4); });
+  const int bad = staging_round_trip(pool, rng, 0, false);
+  for (auto& t : th) t.join();
+  for (auto g : got)
+    if (g != 2) return 1;
+  return bad;
+}
+
 int main() {
   std::mt19937_64 rng(20241016);
   for (int t = 0; t < 4000; ++t)
@@ -253,6 +283,14 @@ int main() {
         return 1;
       }
     }
+  }
+  {
+    Pool pool(4);
+    for (int rep = 0; rep < 20; ++rep)
+      if (concurrent_checks(pool, rng)) {
+        fprintf(stderr, "concurrent check_rows failed (rep %d)\n", rep);
+        return 1;
+      }
   }
   printf("host_pool_test: ok\n");
   return 0;
