@@ -261,7 +261,8 @@ def main():
                 else:
                     FedAvgPlan(kind, clients, w_all, M, out, pw).launch(stream)
 
-            kplan = FedAvgPlan(kind, clients, w_all[k0:k1], M, out, None)  # this block's partial kernel
+            # this block's partial kernel (a rank with no clients, K < N, has none)
+            kplan = FedAvgPlan(kind, clients, w_all[k0:k1], M, out, None) if Kr else None
         else:
             plan = FedAvgPlan(kind, clients, w_all, M, out, pw)
             kplan = plan
@@ -269,7 +270,7 @@ def main():
             def step():
                 plan.launch(stream)
         bytes_job = K * M_glob * s_in + M_glob * 4
-        bytes_kernel = kplan.bytes_alg()
+        bytes_kernel = kplan.bytes_alg() if kplan else 0
     else:
         delta = synth_clients(torch, Kr, ld, M, kind, device, seed0)
         cv = synth_clients(torch, Kr, ld, M, kind, device, seed0 + 7919)
@@ -289,7 +290,7 @@ def main():
                 else:
                     ScaffoldPlan(kind, delta, cv, c, w_all, M, 1.0, dout, cout, pw).launch(stream)
 
-            kplan = ScaffoldPlan(kind, delta, cv, c, w_all[k0:k1], M, 1.0, dout, cout, None)
+            kplan = ScaffoldPlan(kind, delta, cv, c, w_all[k0:k1], M, 1.0, dout, cout, None) if Kr else None
         else:
             plan = ScaffoldPlan(kind, delta, cv, c, w_all, M, 1.0, dout, cout, pw)
             kplan = plan
@@ -297,7 +298,7 @@ def main():
             def step():
                 plan.launch(stream)
         bytes_job = 2 * K * M_glob * 4 + M_glob * 4 + 2 * M_glob * 8
-        bytes_kernel = kplan.bytes_alg()
+        bytes_kernel = kplan.bytes_alg() if kplan else 0
     if not client_shard and args.scaling == "weak":  # every rank reduces a full M-param slice
         bytes_job = bytes_kernel * world
 
@@ -325,14 +326,16 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_each)]
     for a, b in evs:
         a.record(stream)
-        kplan.launch(stream)
+        if kplan:
+            kplan.launch(stream)
         b.record(stream)
     torch.cuda.synchronize(device)
     each_ms = np.array([a.elapsed_time(b) for a, b in evs])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(max(5, min(args.steps, 50))):
-        kplan.launch(stream)
+        if kplan:
+            kplan.launch(stream)
     e1.record(stream)
     torch.cuda.synchronize(device)
     kern_ms = e0.elapsed_time(e1) / max(5, min(args.steps, 50))
@@ -368,7 +371,7 @@ def main():
     traffic, tsrc = read_traffic(args, sha) if (world == 1 or args.scaling == "weak") and not client_shard \
         else (None, None)
 
-    achieved = bytes_kernel / (kern_ms / 1e3) / 1e9
+    achieved = bytes_kernel / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     if rank == 0:
         kname = (f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>" if not scaffold else "scaffold_kernel<float>")
         line = {
