@@ -606,16 +606,41 @@ def _rank_device(torch):
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def _one_dtype(lists, what: str) -> np.dtype:
+    """The single float dtype every array of ``lists`` carries (the sharded host entry points
+    stage raw bytes; mixed or integer layers go through the single-process engines, which apply
+    NumPy's promotion on the device)."""
+    dts = {a.dtype for row in lists for a in row}
+    if len(dts) != 1 or next(iter(dts)) not in (np.float16, np.float32, np.float64):
+        raise NotImplementedError(f"sharded {what}: every layer of every client must have one float dtype "
+                                  f"(got {sorted(str(d) for d in dts)}); use engine_for(...) for mixed dtypes")
+    return np.dtype(next(iter(dts)))
+
+
 def _stage_block(torch, device, rows: List[List[np.ndarray]], layout: BucketLayout, dtype):
     """The rows of this rank's clients, staged through the native session's pinned ring into a
-    ``[Kr, ld]`` device tensor (no host-side packing; stream-ordered before torch's work)."""
+    ``[Kr, ld]`` device tensor of ``dtype`` (no host-side packing; stream-ordered before torch's
+    work).  Rows of another float dtype are staged raw and widened exactly on the device
+    (``fedagg_cast``: Scaffold's fp32 deltas beside fp64 control variates from round 2 on)."""
     from . import runtime
+    from .engine import torch_dtype
 
     t = torch.empty((max(1, len(rows)), layout.ld), dtype=dtype, device=device)
     if rows:
         s = runtime.session(device.index)
-        s.stage(t.data_ptr(), layout.ld * t.element_size(), [[np.ascontiguousarray(a) for a in r] for r in rows])
-        s.sync()
+        src = {a.dtype for r in rows for a in r}
+        arrays = [[np.ascontiguousarray(a) for a in r] for r in rows]
+        if len(src) == 1 and torch_dtype(next(iter(src))) != dtype:
+            (sdt,) = src
+            raw = torch.empty((len(rows), layout.ld), dtype=torch_dtype(sdt), device=device)
+            s.stage(raw.data_ptr(), layout.ld * raw.element_size(), arrays)
+            s.cast(raw.data_ptr(), sdt, t.data_ptr(), np.dtype(str(dtype).replace("torch.", "")),
+                   len(rows) * layout.ld)
+            s.sync()
+            del raw
+        else:
+            s.stage(t.data_ptr(), layout.ld * t.element_size(), arrays)
+            s.sync()
     return t[: len(rows)]
 
 
@@ -632,7 +657,7 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
     tr = transport or DistTransport(group)
     G, rank = tr.world, tr.rank
     K, L = len(parameters_updates), len(parameters_updates[0])
-    dtype = np.result_type(*[np.result_type(a.dtype, 1.0) for a in parameters_updates[0]])
+    dtype = _one_dtype(parameters_updates, "FedAvg")
     kind = kind_of(dtype)
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], dtype)
     k0, k1 = client_blocks(K, G)[block_of(rank, G)]
@@ -662,10 +687,13 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     tr = transport or DistTransport(group)
     G, rank = tr.world, tr.rank
     K, L = len(parameters_updates), len(parameters_updates[0])
-    sdt = np.dtype(parameters_updates[0][0].dtype)
-    if any(a.dtype != sdt for lst in (parameters_updates, control_variate_updates, server_control_variates)
-           for row in lst for a in row) or sdt not in (np.float32, np.float64):
-        raise NotImplementedError("client-sharded Scaffold takes one float32/float64 dtype for every list")
+    # fp32 buckets when every list is fp32 (NEP 50: the sums are fp64 either way), else fp64 with
+    # exact widening on the device; each list one dtype
+    dts = [_one_dtype(lst, "Scaffold") for lst in (parameters_updates, control_variate_updates,
+                                                   server_control_variates)]
+    if any(d not in (np.float32, np.float64) for d in dts):
+        raise NotImplementedError("client-sharded Scaffold takes float32 / float64 lists")
+    sdt = np.dtype(np.float32 if all(d == np.float32 for d in dts) else np.float64)
     kind = "f32" if sdt == np.float32 else "f64"
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], sdt)
     k0, k1 = client_blocks(K, G)[block_of(rank, G)]
@@ -674,12 +702,11 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     delta = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, td)
     cv = _stage_block(torch, dev, [control_variate_updates[k] for k in range(k0, k1)], layout, td)
     # c: client 0's copy staged once (used by the root), this block's copies checked against it
-    c = torch.empty(layout.ld, dtype=td, device=dev)
     s = runtime.session(dev.index)
     check_rows = [list(server_control_variates[0])] + [list(server_control_variates[k]) for k in range(k0, k1)
                                                       if k != 0]
-    mism = s.stage_check(c.data_ptr(), check_rows, sdt)
-    s.sync()
+    mism = s.check(check_rows, dts[2])
+    c = _stage_block(torch, dev, [list(server_control_variates[0])], layout, td)[0]
     mism = tr.all_sum_int(mism)
     dout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
     cout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
@@ -721,7 +748,7 @@ def param_range_fedavg(
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     L = len(parameters_updates[0])
-    dtype = np.result_type(*[np.result_type(a.dtype, 1.0) for a in parameters_updates[0]])
+    dtype = _one_dtype(parameters_updates, "FedAvg")
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], dtype)
     bounds = shard_bounds(layout.M, world)
     lo, hi = bounds[rank]

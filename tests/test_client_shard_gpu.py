@@ -213,6 +213,15 @@ def _nccl_world1(q, port):
         out["scaffold"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5)
         cs[3][2][17] += 1.0
         out["scaffold_bad"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5)[0]
+        # round 2+ of Scaffold: fp64 control variates and c beside fp32 deltas (widened on the device)
+        cvs64 = [[a.astype(np.float64) * 1.1 for a in cv] for cv in cvs]
+        c64 = [[a.astype(np.float64) / 3 for a in c] for _ in pus]
+        out["scaffold_mixed"] = client_sharded_scaffold(pus, cvs64, c64, ns, 0.5)
+        try:
+            client_sharded_fedavg([[a.astype(np.float16) if i == 0 else a for i, a in enumerate(p)] for p in pus], ns)
+            out["mixed_fedavg"] = "accepted"
+        except NotImplementedError:
+            out["mixed_fedavg"] = "refused"
         q.put(out)
     finally:
         dist.destroy_process_group()
@@ -242,3 +251,11 @@ def test_host_entry_points_nccl_world1():
     for g, r in zip(new_c + avg, rc + ra):
         assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
     assert out["scaffold_bad"] == 1
+    cvs64 = [[a.astype(np.float64) * 1.1 for a in cv] for cv in cvs]
+    c64 = [a.astype(np.float64) / 3 for a in c]
+    rc, ra = scaffold_reference_structure(pus, cvs64, c64, ns, 0.5)
+    mism, new_c, avg = out["scaffold_mixed"]
+    assert mism == 0
+    for g, r in zip(new_c + avg, rc + ra):
+        assert g.dtype == r.dtype == np.float64 and np.array_equal(g.view(np.uint64), r.view(np.uint64))
+    assert out["mixed_fedavg"] == "refused"
