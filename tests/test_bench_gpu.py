@@ -1,0 +1,67 @@
+"""bench.py's JSON contract on the GPU (small step counts): the fields the driver and the judge read,
+the parity spot check, the roofline block with its PMC-traffic provenance, and the other modes
+(client-shard on one rank, strong scaling with two ranks sharing the GPU, the one-process
+multi-device engine)."""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _bench(*args, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, env=env,
+                       timeout=timeout, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def test_default_line_fields():
+    line = _bench("--workload", "c2", "--steps", "5", "--warmup", "2", "--cpu-seconds", "1")
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in line
+    assert line["n_gpus"] == 1 and line["steps"] == 5 and line["unit"] == "GB/s" and line["value"] > 0
+    assert line["config"]["workload"] == "fedavg_fp32_8x25M"
+    roof = line["roofline"]
+    assert roof["bound"] == "hbm" and roof["peak"] == 8000.0 and 0 < roof["frac"] < 1
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
+    assert roof["traffic_source"] is None or "same_build" in roof["traffic_source"]
+    assert line["cpu_baseline"]["cores"] == 1 and line["cpu_baseline"]["kind"] == "port"
+    assert line["parity"]["mismatches"] == 0
+
+
+def test_scaffold_line():
+    line = _bench("--workload", "c4", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert line["dtype"] == "f32-in/f64-acc" and line["parity"]["mismatches"] == 0
+    assert line["roofline"]["kernel"] == "scaffold_kernel<float>"
+
+
+def test_client_shard_single_rank():
+    line = _bench("--workload", "c2", "--mode", "client-shard", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert line["parity"]["mismatches"] == 0 and line["config"]["clients_per_gpu"] == 8
+
+
+def test_strong_scaling_two_ranks_shared_gpu():
+    line = _bench("--workload", "c2", "--scaling", "strong", "--gpus", "2", "--steps", "3", "--warmup", "1",
+                  "--no-cpu-baseline")
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["global_params"] == 25_000_000
+    assert line["config"]["params_per_gpu"] < 25_000_000
+    assert line["config"]["bytes_alg_per_step_job"] == 8 * 25_000_000 * 4 + 25_000_000 * 4
+
+
+def test_multi_device_engine_line():
+    line = _bench("--engine", "multi-device", "--workload", "c2", "--gpus", "2", "--steps", "2", "--warmup", "1")
+    assert line["n_gpus"] == 2 and len(line["shards"]) == 2
+    assert all(s["kernel_ms"] > 0 for s in line["shards"])
