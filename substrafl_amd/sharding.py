@@ -351,6 +351,20 @@ class _Done:
         return None
 
 
+class _LoopbackRecv:
+    """A posted receive of the loopback transport: ``wait()`` takes the matching message (sent by
+    ``src`` to ``owner``) and copies it into ``dst`` on the waiting thread's current stream."""
+
+    def __init__(self, owner: "_LoopbackTransport", dst, src: int):
+        self.owner, self.dst, self.src, self.done = owner, dst, src, False
+
+    def wait(self):
+        if not self.done:
+            src_t, ev = self.owner._get((self.src, self.owner.rank))
+            self.dst.copy_(_take(src_t, ev))
+            self.done = True
+
+
 class LoopbackGroup:
     """G ranks as threads of ONE process (rehearsal of the multi-rank protocol on one GPU, and
     the drift tool): point-to-point messages and collectives through in-process mailboxes.
@@ -411,19 +425,7 @@ class _LoopbackTransport:
                 self._put((self.rank, peer), (t, _event(t)))
                 works.append(_Done())
             else:
-                outer = self
-
-                class _Recv:
-                    def __init__(self, dst, src):
-                        self.dst, self.src, self.done = dst, src, False
-
-                    def wait(self):
-                        if not self.done:
-                            src_t, ev = outer._get((self.src, outer.rank))
-                            self.dst.copy_(_take(src_t, ev))
-                            self.done = True
-
-                works.append(_Recv(t, peer))
+                works.append(_LoopbackRecv(self, t, peer))
         return works
 
     def _collect(self, t, root):
@@ -458,12 +460,15 @@ class _LoopbackTransport:
         key = self._seq
         self._seq += 1
         with self.g._cv:
-            if got is not None:
-                self.g._coll[(key, -1)] = int(sum(int(x.item()) for x in got))
+            if got is not None:  # [total, ranks still to read it]
+                self.g._coll[(key, -1)] = [int(sum(int(x.item()) for x in got)), self.world]
                 self.g._cv.notify_all()
             self.g._cv.wait_for(lambda: (key, -1) in self.g._coll)
-            total = self.g._coll[(key, -1)]
-        return int(total)
+            rec = self.g._coll[(key, -1)]
+            rec[1] -= 1
+            if rec[1] == 0:
+                del self.g._coll[(key, -1)]
+        return int(rec[0])
 
 
 # ======================================================================================

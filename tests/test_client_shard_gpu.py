@@ -259,3 +259,70 @@ def test_host_entry_points_nccl_world1():
     for g, r in zip(new_c + avg, rc + ra):
         assert g.dtype == r.dtype == np.float64 and np.array_equal(g.view(np.uint64), r.view(np.uint64))
     assert out["mixed_fedavg"] == "refused"
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_relay_random_sweep(seed):
+    """Random client counts (up to 300: blocks beyond one 128-client kernel-argument chunk
+    continue their own accumulator too), rank counts, layer sets, dtypes and relay chunk sizes:
+    the relay is bit-identical to the reference; Scaffold over > 64-client blocks likewise."""
+    import torch
+
+    from substrafl_amd.engine import fedavg_weights, scaffold_weights
+    from substrafl_amd.layout import BucketLayout
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, ScaffoldShard, block_of, client_blocks,
+                                        client_shard_fedavg, client_shard_scaffold, out_dtype)
+
+    rng = np.random.default_rng(1000 + seed)
+    G = int(rng.integers(1, 9))
+    K = int(rng.choice([1, 2, 5, 17, 70, 130, 300]))
+    pool = [(1,), (1, 1), (3,), (129,), (4096,), (31, 7), (2, 2, 2)]
+    shapes = [pool[i] for i in rng.integers(0, len(pool), int(rng.integers(1, 6)))]
+    kind = ["f32", "bf16", "f64", "f16"][seed % 4]
+    npdt = {"f32": np.float32, "bf16": np.float32, "f64": np.float64, "f16": np.float16}[kind]
+    pus = [[(rng.standard_normal(s) * 10.0 ** rng.integers(-2, 3)).astype(npdt) for s in shapes] for _ in range(K)]
+    if kind == "bf16":
+        pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    layout = BucketLayout(range(len(shapes)), shapes, npdt)
+    chunk = int(rng.choice([512, 2048, 1 << 20]))
+    w = fedavg_weights(ns, kind)
+
+    def rank_fn(r, tr):
+        k0, k1 = client_blocks(K, G)[block_of(r, G)]
+        rows = _rows(torch, pus[k0:k1], layout, dtype=npdt, tdtype=torch.bfloat16 if kind == "bf16" else None)
+        out = torch.zeros(layout.ld, dtype=out_dtype(torch, kind), device="cuda")
+        sh = FedAvgShard(kind, rows, w[k0:k1], k0, K, layout.M, layout.pairwise_idx)
+        if client_shard_fedavg(sh, out, tr, GpuShardOps(), "relay", chunk_elems=chunk):
+            torch.cuda.current_stream().synchronize()
+            return out[: layout.M].cpu().numpy().copy()
+        return None
+
+    got = [a for _, a in layout.unpack(_loopback(G, rank_fn)[0])]
+    bits = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+    for g, r in zip(got, fedavg_reference_structure(pus, ns)):
+        assert g.dtype == r.dtype and np.array_equal(g.view(bits[g.itemsize]), r.view(bits[r.itemsize]))
+
+    if kind in ("f32", "f64") and K <= 130:
+        cvs = [[rng.standard_normal(s).astype(npdt) for s in shapes] for _ in range(K)]
+        c = [rng.standard_normal(s).astype(npdt) for s in shapes]
+        lr = float(rng.choice([0.0, 0.5, 1.0, 1.7]))
+        ws = scaffold_weights(ns)
+
+        def srank(r, tr):
+            k0, k1 = client_blocks(K, G)[block_of(r, G)]
+            sh = ScaffoldShard(kind, _rows(torch, pus[k0:k1], layout, dtype=npdt),
+                               _rows(torch, cvs[k0:k1], layout, dtype=npdt), _rows(torch, [c], layout, dtype=npdt)[0],
+                               ws[k0:k1], k0, K, layout.M, lr, layout.pairwise_idx)
+            dout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+            cout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+            if client_shard_scaffold(sh, dout, cout, tr, GpuShardOps(), "relay", chunk_elems=chunk):
+                torch.cuda.current_stream().synchronize()
+                return dout[: layout.M].cpu().numpy().copy(), cout[: layout.M].cpu().numpy().copy()
+            return None
+
+        d, cc = _loopback(G, srank)[0]
+        lay64 = BucketLayout(range(len(shapes)), shapes, np.float64)
+        rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
+        for g, r in zip([a for _, a in lay64.unpack(cc)] + [a for _, a in lay64.unpack(d)], rc + ra):
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
