@@ -109,3 +109,35 @@ def test_scaffold_client_shard_property(K, G, shapes, combine, lr, seed):
             assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
         else:
             np.testing.assert_allclose(g, r, rtol=1e-12, atol=1e-12)
+
+
+def test_loopback_collectives():
+    """The in-process transport's collectives: reduce / gather onto rank 0 in rank order,
+    all_sum_int everywhere (repeatedly, so its bookkeeping is released), P2P in FIFO order."""
+    G = 4
+    grp = LoopbackGroup(G)
+    out = [None] * G
+
+    def body(r):
+        tr = grp.transport(r)
+        sums = [tr.all_sum_int(r + i) for i in range(3)]
+        t = torch.full((5,), float(r + 1))
+        tr.reduce_sum(t, 0)
+        g = tr.gather(torch.tensor([r]), 0)
+        recv = torch.zeros(2)
+        works = tr.exchange([("send", torch.tensor([float(r), 1.0 * r]), (r + 1) % G),
+                             ("recv", recv, (r - 1) % G)])
+        for w in works:
+            w.wait()
+        out[r] = (sums, t.tolist() if r == 0 else None, None if g is None else [int(x) for x in g], recv.tolist())
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    for r in range(G):
+        assert out[r][0] == [6, 10, 14]
+        assert out[r][3] == [float((r - 1) % G)] * 2
+    assert out[0][1] == [10.0] * 5 and out[0][2] == [0, 1, 2, 3]
+    assert not grp._coll  # every collective's entries consumed
