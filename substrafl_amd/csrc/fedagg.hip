@@ -78,6 +78,7 @@ int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per work
 int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
 int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
 int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
+int g_fa_blk = 256;     // FedAvg fp32/bf16 global-load tiles: threads per workgroup (256 or 512)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -500,37 +501,42 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 // VPT grid-strided vectors.
 // OCC (fedagg_tune "fa_occ"): minimum waves per SIMD the register allocation must allow
 // (amdgpu_waves_per_eu; 1 = no constraint beyond the launch bound).
-template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false>
-__global__ void __launch_bounds__(FA_BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
+// BLK (fedagg_tune "fa_blk"): threads per workgroup of the global-load tiles; 512 gives a
+// workgroup step the footprint of the 256-thread tile with twice the vectors per thread, at half
+// the registers per thread.
+template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
+          int BLK = FA_BLOCK>
+__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
                   const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
-  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
-  const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
+  static_assert(!BUF || BLK == FA_BLOCK, "buffer-descriptor tiles assume 256-thread workgroups");
+  const uint64_t stride = (uint64_t)gridDim.x * BLK;
+  const uint64_t gid = (uint64_t)blockIdx.x * BLK + threadIdx.x;
 
   if constexpr (TILE) {
     constexpr bool WIDE = E::L * sizeof(typename E::Out) == 32;
-    __shared__ u32x4 stage[WIDE ? FA_BLOCK / 64 : 1][128];
+    __shared__ u32x4 stage[WIDE ? BLK / 64 : 1][128];
     u32x4* lds_wave = stage[WIDE ? threadIdx.x / 64 : 0];
-    const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+    const uint64_t tile = (uint64_t)VPT * BLK;
     uint64_t t;
     for (uint64_t it = 0; block_tile(remap, tpb, it, &t) && t * tile < nvec; ++it) {
       const uint64_t base = t * tile + threadIdx.x;
       // wave-uniform: every lane of this wave has all VPT vectors in range
-      const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
-      if (base + (VPT - 1) * FA_BLOCK < nvec) {
+      const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * BLK < nvec;
+      if (base + (VPT - 1) * BLK < nvec) {
         uint64_t v[VPT];
 #pragma unroll
-        for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+        for (int n = 0; n < VPT; ++n) v[n] = base + n * BLK;
         P acc[VPT][L];
         fedavg_vectors<E, KC, NT, VPT, U, PIPE, BUF>(a, K, first, v, acc, out, t * tile * 16);
         if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
 #pragma unroll
         for (int n = 0; n < VPT; ++n) store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
       } else {
-        for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK) {
+        for (uint64_t v0 = base; v0 < nvec; v0 += BLK) {
           P acc[1][L];
           fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
           if (pw.n) patch_pairwise<E, KC, 1>(a, pw, K, &v0, acc);
@@ -1476,12 +1482,13 @@ inline unsigned grid_for(uint64_t work) {
   return (unsigned)g;
 }
 
-template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false>
+template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
+          int BLK = FA_BLOCK>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
-  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF>), dim3(grid),
-                     dim3(FA_BLOCK), 0,
-                     s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb);
+  if (BLK != FA_BLOCK) grid = (grid + BLK / FA_BLOCK - 1) / (BLK / FA_BLOCK);  // the caller sized it for 256
+  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF, BLK>), dim3(grid),
+                     dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb);
 }
 
 // Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
@@ -1543,6 +1550,12 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
       }
     }
     if constexpr (NTS && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
+      if (g_fa_blk > FA_BLOCK && !sh.buf && !sh.pipe) {  // 512-thread workgroups (experiment knob)
+        if (sh.vpt >= 16) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
+        if (sh.vpt >= 8 && sh.unroll <= 2) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true, 1, false, 512>(FA_ARGS);
+        if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 1, false, 512>(FA_ARGS);
+        return launch_fedavg_variant<E, true, NTS, 4, 4, false, true, 1, false, 512>(FA_ARGS);
+      }
       if (sh.buf && !sh.pipe) {  // buffer-descriptor loads (one lane offset for every client stream)
         if (sh.vpt >= 16) {
           if (sh.unroll <= 1) {
@@ -2081,6 +2094,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
   else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
+  else if (!strcmp(key, "fa_blk")) g_fa_blk = value >= 512 ? 512 : 256;
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

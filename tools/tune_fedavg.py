@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--occ", action="store_true",
                     help="register-capped occupancy variants (fa_occ 2-4) of the 8/16-KiB shapes beside the uncapped ones")
     ap.add_argument("--buf", action="store_true", help="buffer-descriptor client loads (buf 1) beside global loads")
+    ap.add_argument("--blk", action="store_true", help="512-thread workgroups (fa_blk 512) beside the auto shape")
     ap.add_argument("--gridstride", action="store_true",
                     help="grid-strided and tile shapes under grid caps (the read probe's walk), next to the auto shape")
     args = ap.parse_args()
@@ -82,8 +83,13 @@ def main():
                                   median_us=round(m * 1e3, 2), GBps=round(nbytes / (m / 1e3) / 1e9, 1))))
         return
 
-    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1, fa_occ=0, buf=0)
-    if args.buf:
+    base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1, fa_occ=0, buf=0,
+                fa_blk=256)
+    if args.blk:
+        variants = [dict(base, vpt=0, tile=1, nt_store=1)]
+        variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_blk=512)
+                     for v, u in ((16, 2), (8, 2), (8, 4), (4, 4))]
+    elif args.buf:
         variants = [dict(base, vpt=0, tile=1, nt_store=1, buf=b) for b in (0, 1)]
         variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_occ=o, buf=b)
                      for v, u, o, b in ((8, 4, 0, 0), (8, 4, 0, 1), (8, 4, 3, 1), (16, 2, 2, 0), (16, 2, 0, 1),
