@@ -68,7 +68,7 @@ const char* fedagg_last_error(void);
  *   "sc_cpf"        Scaffold 4x4 tile: load c with the last client group (0/1)
  *   "sc_occ"        Scaffold 4x4 tile: register-capped build, waves per SIMD (0 = uncapped)
  *   "sc_blk"        Scaffold 4x4 tile: threads per workgroup (256 / 512)
- *   "fa_blk"        FedAvg fp32/bf16 global-load tiles: threads per workgroup (256 / 512)
+ *   "fa_blk"        FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto / 256 / 512)
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);
 

@@ -78,7 +78,7 @@ int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per work
 int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
 int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
 int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
-int g_fa_blk = 256;     // FedAvg fp32/bf16 global-load tiles: threads per workgroup (256 or 512)
+int g_fa_blk = 0;       // FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto, 256, 512)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
 
@@ -1505,10 +1505,12 @@ struct Shape {
   bool pipe;
   int occ;  // > 1: the register-capped (amdgpu_waves_per_eu) build of the 8/16-KiB tile
   bool buf;  // buffer-descriptor client loads
+  int blk = FA_BLOCK;  // threads per workgroup (global-load tiles without pipelining)
 };
 template <typename E>
 inline Shape shape_for(int K, uint64_t nvec) {
-  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0, g_fa_occ, g_buf != 0};
+  const int blk = g_fa_blk ? g_fa_blk : FA_BLOCK;
+  if (g_vpt > 0) return {g_vpt, g_unroll, g_pipe != 0, g_fa_occ, g_buf != 0, blk};
   // fp64: the adds of a client group take long enough that the HBM idles unless the next
   // group's loads are already in flight (software-pipelined tiles: 8 x 25M fp64 6.0 vs 5.1 TB/s,
   // 64 x 62.5M 6.1 vs 4.9; profiles/r01_tune2_f64_*.log)
@@ -1519,14 +1521,17 @@ inline Shape shape_for(int K, uint64_t nvec) {
   if (K >= 32 && nvec >= (uint64_t)16 * FA_BLOCK * 2048) {
     // bf16: client pairs with buffer-descriptor loads (128 x 350M: 12.64 vs 12.96 ms with global
     // loads, 64 x 125M: -7.7 %; profiles/r01_buf2_*.log; slower for fp32, r01_buf_c{2,3}.log);
-    // fp32: client pairs built for 2 waves per SIMD (247 VGPRs, no spill; the uncapped build
-    // takes 257 registers and runs 1 wave; 64 x 125M: -1.4 %, profiles/r01_occ_c3.log)
-    if constexpr (std::is_same<E, BF16>::value) return Shape{16, 2, false, g_fa_occ, true};
-    if constexpr (std::is_same<E, F32>::value) return Shape{16, 2, false, g_fa_occ > 1 ? g_fa_occ : 2, false};
-    return Shape{16, 2, false, g_fa_occ, false};
+    // fp32: client pairs in 512-thread workgroups (253 VGPRs under the 512-thread launch bound,
+    // 2 waves per SIMD, no spill): 64 x 125M 4.68 vs 4.79 ms for the 256-thread build capped to 2
+    // waves, 0.3-1.4 % on five other K >= 32 shapes, never slower (profiles/r02_blk*.log); the
+    // 256-thread build uncapped takes 257 registers and runs 1 wave (-1.4 %, r01_occ_c3.log)
+    if constexpr (std::is_same<E, BF16>::value) return Shape{16, 2, false, g_fa_occ, true, blk};
+    if constexpr (std::is_same<E, F32>::value)
+      return Shape{16, 2, false, g_fa_occ > 1 ? g_fa_occ : 2, false, g_fa_blk ? g_fa_blk : 2 * FA_BLOCK};
+    return Shape{16, 2, false, g_fa_occ, false, blk};
   }
   if constexpr (std::is_same<E, F16>::value) return Shape{4, 4, false, 0, g_buf != 0};  // 8 x 25M: +5 % over 8 KiB
-  return Shape{8, 4, false, g_fa_occ, g_buf != 0};
+  return Shape{8, 4, false, g_fa_occ, g_buf != 0, blk};
 }
 
 template <typename E, bool NTS>
@@ -1550,7 +1555,7 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
       }
     }
     if constexpr (NTS && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
-      if (g_fa_blk > FA_BLOCK && !sh.buf && !sh.pipe) {  // 512-thread workgroups (experiment knob)
+      if (sh.blk > FA_BLOCK && !sh.buf && !sh.pipe) {  // 512-thread workgroups
         if (sh.vpt >= 16) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
         if (sh.vpt >= 8 && sh.unroll <= 2) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true, 1, false, 512>(FA_ARGS);
         if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true, 1, false, 512>(FA_ARGS);
@@ -2094,7 +2099,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
   else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
-  else if (!strcmp(key, "fa_blk")) g_fa_blk = value >= 512 ? 512 : 256;
+  else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 512 ? 512 : 256);
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

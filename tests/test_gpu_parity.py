@@ -608,7 +608,8 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda")
     ns = list(range(3, 3 + K))
     outs = []
-    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0)
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
+                   fa_blk=0)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
@@ -627,6 +628,7 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
                                    dict(vpt=16, unroll=2, fa_occ=2, buf=1), dict(vpt=16, unroll=1, buf=1),
                                    dict(vpt=16, unroll=1, fa_occ=2, buf=1, grid_cap=3),
                                    dict(vpt=16, unroll=2, fa_blk=512), dict(vpt=8, unroll=2, fa_blk=512),
+                                   dict(vpt=0, fa_blk=256), dict(vpt=0, fa_blk=512),
                                    dict(vpt=8, unroll=4, fa_blk=512, grid_cap=3), dict(vpt=4, unroll=4, fa_blk=512)])
 def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     """Register-capped (amdgpu_waves_per_eu) builds of the 8/16-KiB shapes: same bits as the
@@ -640,7 +642,7 @@ def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     x = torch.randn((K, M + 5), device="cuda").to(dt)
     ns = list(range(7, 7 + K))
     default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
-                   fa_blk=256)
+                   fa_blk=0)
     outs = []
     for kn in (default, dict(default, **knobs)):
         _native.tune(**kn)

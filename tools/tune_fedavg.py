@@ -84,7 +84,7 @@ def main():
         return
 
     base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1, fa_occ=0, buf=0,
-                fa_blk=256)
+                fa_blk=0)
     if args.blk:
         variants = [dict(base, vpt=0, tile=1, nt_store=1)]
         variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_blk=512)
