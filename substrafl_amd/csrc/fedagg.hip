@@ -78,9 +78,15 @@ int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per work
 int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
 int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
 int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
+int g_sc_sc1 = 0;       // Scaffold 4 x 4 tiles: write-through (sc1) output stores
+int g_st_sc1 = -1;      // FedAvg: write-through (sc1) output stores (-1: auto, below SC1_MAX_K clients)
 int g_fa_blk = 0;       // FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto, 256, 512)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
 constexpr int NT_STORE_MIN_K = 16;
+// Output stores as device-scope write-through (sc1) instead of non-temporal: 8 x 25M fp32 133.6
+// vs 140.0 us, fp16 71.5 vs 75.0, fp64 280 vs 298; from 32 clients the output is <= 3 % of the
+// bytes and it is neutral (64 x 125M fp32 +0.4 %, 128 x 350M bf16 -0.6 %; profiles/r02_sc1_*.log)
+constexpr int SC1_MAX_K = 32;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -181,16 +187,30 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
     return *reinterpret_cast<const u32x4*>(p);
 }
 
-template <bool NT>
+// Store policy SP: 0 plain, 1 non-temporal, 2 device-scope write-through (sc1) as a buffer store
+// based at the first active lane's address (callers' lanes store at ascending addresses within
+// one wave, so every lane offset is a small non-negative 32-bit number).
+template <int SP>
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
-  if constexpr (NT)
+  if constexpr (SP == 2) {
+    const uint64_t addr = reinterpret_cast<uint64_t>(p);
+    // readfirstlane returns int: widen through unsigned (a sign-extended low word would corrupt
+    // the high address bits)
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(addr >> 32));
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)addr);
+    const uint64_t base = ((uint64_t)hi << 32) | (uint64_t)lo;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(addr - base), 0, 16);
+  } else if constexpr (SP == 1) {
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-  else
+  } else {
     *reinterpret_cast<u32x4*>(p) = v;
+  }
 }
 
 // out[v*L .. v*L+L) for one 16-byte input vector (L Out elements: 16 or 32 bytes).
-template <typename E, bool NTS>
+template <typename E, int NTS>
 __device__ __forceinline__ void store_vec(typename E::Out* out, uint64_t v, const typename E::P* acc) {
   typename E::Out o[E::L];
 #pragma unroll
@@ -207,7 +227,7 @@ __device__ __forceinline__ void store_vec(typename E::Out* out, uint64_t v, cons
 // lane at a 32-B stride (half of each 64-B line per instruction: PMC WRITE_SIZE showed 1.36x
 // the written bytes).  Transposing through 2 KiB of LDS turns them into two fully coalesced
 // 1 KiB store instructions.  Requires all 64 lanes active (callers check wave-uniformly).
-template <bool NTS>
+template <int NTS>
 __device__ __forceinline__ void store32_coalesced(void* wave_dst, u32x4 lo, u32x4 hi, u32x4* lds_wave) {
   const int lane = threadIdx.x & 63;
   lds_wave[2 * lane] = lo;
@@ -223,7 +243,7 @@ __device__ __forceinline__ void store32_coalesced(void* wave_dst, u32x4 lo, u32x
   __builtin_amdgcn_wave_barrier();
 }
 
-template <typename E, bool NTS>
+template <typename E, int NTS>
 __device__ __forceinline__ void store_vec_wave(typename E::Out* out, uint64_t v, const typename E::P* acc,
                                                bool wave_full, u32x4* lds_wave) {
   constexpr int bytes = E::L * sizeof(typename E::Out);
@@ -504,7 +524,7 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 // BLK (fedagg_tune "fa_blk"): threads per workgroup of the global-load tiles; 512 gives a
 // workgroup step the footprint of the 256-thread tile with twice the vectors per thread, at half
 // the registers per thread.
-template <typename E, int KC, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
+template <typename E, int KC, bool NT, int NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
           int BLK = FA_BLOCK>
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
@@ -667,7 +687,7 @@ __device__ __forceinline__ void scaffold_accumulate(const u32x4 (&rd)[N][SU], co
 // + c and * lr, the fused numel==1 patch, and the fp64 stores.  PIPE: software-pipelined groups.
 // CPF: the server c vectors of the last chunk are loaded together with the last client group's
 // loads instead of after the client walk (one dependent HBM round trip less per tile).
-template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, bool PIPE = false, bool BUF = false,
+template <typename TIn, int KC, bool NT, int NTS, int N, int SU, bool PIPE = false, bool BUF = false,
           bool CPF = false>
 __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                  const int first, const int last, const TIn* __restrict__ c,
@@ -800,7 +820,7 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
 // thread streams all K delta vectors first (and stores the delta result), then all K control
 // variate vectors: half the concurrent streams and half the live accumulators of the fused
 // walk, so a wave can own twice the contiguous bytes per stream.
-template <typename TIn, int KC, bool NT, bool NTS, int N, int SU, int PH>
+template <typename TIn, int KC, bool NT, int NTS, int N, int SU, int PH>
 __device__ __forceinline__ void scaffold_phase(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                const int first, const int last, const TIn* __restrict__ c,
                                                const double lr, const uint64_t* v, double* __restrict__ out,
@@ -900,7 +920,7 @@ __device__ __forceinline__ void scaffold_phase(const ScArgs<TIn, KC>& a, const P
   }
 }
 
-template <typename TIn, int KC, bool NT, bool NTS, int N, int SU>
+template <typename TIn, int KC, bool NT, int NTS, int N, int SU>
 __device__ __forceinline__ void scaffold_vectors_split(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                        const int first, const int last, const TIn* __restrict__ c,
                                                        const double lr, const uint64_t* v, double* __restrict__ dout,
@@ -913,7 +933,7 @@ __device__ __forceinline__ void scaffold_vectors_split(const ScArgs<TIn, KC>& a,
 // OCC (fedagg_tune "sc_occ"): minimum waves per SIMD for the register allocation; BLK
 // ("sc_blk"): threads per workgroup (256, or 512: 32 KiB per stream per workgroup step at VPT 4);
 // CPF ("sc_cpf"): c loaded with the last client group.
-template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU, bool SPLIT, bool PIPE = false, bool BUF = false,
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, bool SPLIT, bool PIPE = false, bool BUF = false,
           bool CPF = false, int OCC = 1, int BLK = FA_BLOCK>
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     scaffold_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
@@ -973,7 +993,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
 // flight chip-wide at once (unlike sc_split, which walks them one after the other per thread).
 // Same per-element arithmetic and order as scaffold_kernel.  Vector path only (16-B aligned
 // operands, nvec = M / L); the grid is even.
-template <typename TIn, int KC, bool NT, bool NTS, int VPT, int SU>
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU>
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_bsplit_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                            const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
@@ -1482,7 +1502,7 @@ inline unsigned grid_for(uint64_t work) {
   return (unsigned)g;
 }
 
-template <typename E, bool NT, bool NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
+template <typename E, bool NT, int NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
           int BLK = FA_BLOCK>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
@@ -1534,17 +1554,32 @@ inline Shape shape_for(int K, uint64_t nvec) {
   return Shape{8, 4, false, g_fa_occ, g_buf != 0, blk};
 }
 
-template <typename E, bool NTS>
+template <typename E, int NTS>
 void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
                          int first, uint64_t nvec, uint64_t M, typename E::Out* out, Shape sh) {
 #define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
+  if constexpr (NTS == 2) {  // write-through (sc1) output stores: the auto shapes and their neighbours only
+    if (sh.pipe) {
+      if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
+      return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
+    }
+    if constexpr (std::is_same<E, F32>::value || std::is_same<E, BF16>::value) {
+      if (sh.vpt >= 16 && sh.blk > FA_BLOCK && !sh.buf)
+        return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
+      if (sh.vpt >= 16 && sh.buf) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, true>(FA_ARGS);
+      if (sh.vpt >= 16 && sh.occ > 1) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 2>(FA_ARGS);
+    }
+    if (sh.vpt >= 16) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true>(FA_ARGS);
+    if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
+    return launch_fedavg_variant<E, true, NTS, 4, 4, false, true>(FA_ARGS);
+  } else {
   if (!g_nt_load) return launch_fedavg_variant<E, false, NTS, 1, 8, false, false>(FA_ARGS);
   if (g_tile) {
     if (sh.pipe) {  // contiguous tiles with the next client group's loads issued before this group's adds
       if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
     }
-    if constexpr (NTS && std::is_same<E, F16>::value) {
+    if constexpr (NTS == 1 && std::is_same<E, F16>::value) {
       if (sh.buf && !sh.pipe) {  // fp16: buffer-descriptor loads, uncapped builds only
         if (sh.vpt >= 16) {
           if (sh.unroll <= 1) return launch_fedavg_variant<E, true, NTS, 16, 1, false, true, 1, true>(FA_ARGS);
@@ -1554,7 +1589,7 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
         if (sh.vpt >= 4 && sh.unroll >= 4) return launch_fedavg_variant<E, true, NTS, 4, 4, false, true, 1, true>(FA_ARGS);
       }
     }
-    if constexpr (NTS && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
+    if constexpr (NTS == 1 && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
       if (sh.blk > FA_BLOCK && !sh.buf && !sh.pipe) {  // 512-thread workgroups
         if (sh.vpt >= 16) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
         if (sh.vpt >= 8 && sh.unroll <= 2) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true, 1, false, 512>(FA_ARGS);
@@ -1609,16 +1644,19 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
   if (sh.unroll >= 16) return launch_fedavg_variant<E, true, NTS, 1, 16, false, false>(FA_ARGS);
   if (sh.unroll <= 4) return launch_fedavg_variant<E, true, NTS, 1, 4, false, false>(FA_ARGS);
   return launch_fedavg_variant<E, true, NTS, 1, 8, false, false>(FA_ARGS);
+  }
 #undef FA_ARGS
 }
 
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
-                   int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts, Shape sh) {
-  if (nts)
-    launch_fedavg_shape<E, true>(grid, s, a, pw, kc, first, nvec, M, out, sh);
+                   int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts, bool sc1, Shape sh) {
+  if (nts && sc1 && g_nt_load && g_tile)
+    launch_fedavg_shape<E, 2>(grid, s, a, pw, kc, first, nvec, M, out, sh);
+  else if (nts)
+    launch_fedavg_shape<E, 1>(grid, s, a, pw, kc, first, nvec, M, out, sh);
   else
-    launch_fedavg_shape<E, false>(grid, s, a, pw, kc, first, nvec, M, out, sh);
+    launch_fedavg_shape<E, 0>(grid, s, a, pw, kc, first, nvec, M, out, sh);
 }
 
 template <typename E>
@@ -1748,7 +1786,8 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const bool nts = g_nt_store < 0 ? K >= NT_STORE_MIN_K : g_nt_store != 0;
-    launch_fedavg<E>(grid, s, a, pw, kc, (k0 == 0 && seed) ? 1 : 0, nvec, M, out, nts, sh);
+    const bool sc1 = g_st_sc1 < 0 ? K < SC1_MAX_K : g_st_sc1 != 0;
+    launch_fedavg<E>(grid, s, a, pw, kc, (k0 == 0 && seed) ? 1 : 0, nvec, M, out, nts, sc1, sh);
     int rc = check_launch("fedavg_kernel");
     if (rc) return rc;
   }
@@ -1853,7 +1892,7 @@ int scaffold_finish_launch(double* ws, int Ktot, const TIn* c, const uint64_t* i
   return FEDAGG_OK;
 }
 
-template <typename TIn, bool NT, bool NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false, bool BUF = false,
+template <typename TIn, bool NT, int NTS, int VPT, int SU, bool SPLIT = false, bool PIPE = false, bool BUF = false,
           bool CPF = false, int OCC = 1, int BLK = FA_BLOCK>
 void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
                              const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr, uint64_t nvec,
@@ -1905,6 +1944,7 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
     }
     if (sv >= 4) {
       if (su <= 2) return launch_scaffold_variant<TIn, true, true, 4, 2, false, false, true>(SC_ARGS);
+      if (g_sc_sc1) return launch_scaffold_variant<TIn, true, 2, 4, 4, false, false, true>(SC_ARGS);
       return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, true>(SC_ARGS);
     }
   }
@@ -1942,6 +1982,7 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
         default: return launch_scaffold_variant<TIn, true, true, 4, 4, false, false, false, true, 2, 512>(SC_ARGS);
       }
     }
+    if (nts && g_sc_sc1) return launch_scaffold_variant<TIn, true, 2, 4, 4>(SC_ARGS);  // write-through stores
     if (nts) return launch_scaffold_variant<TIn, true, true, 4, 4>(SC_ARGS);
     return launch_scaffold_variant<TIn, true, false, 4, 4>(SC_ARGS);
   }
@@ -2099,6 +2140,8 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
   else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
+  else if (!strcmp(key, "sc_sc1")) g_sc_sc1 = value ? 1 : 0;
+  else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
   else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 512 ? 512 : 256);
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;

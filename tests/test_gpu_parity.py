@@ -629,6 +629,9 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
                                    dict(vpt=16, unroll=1, fa_occ=2, buf=1, grid_cap=3),
                                    dict(vpt=16, unroll=2, fa_blk=512), dict(vpt=8, unroll=2, fa_blk=512),
                                    dict(vpt=0, fa_blk=256), dict(vpt=0, fa_blk=512),
+                                   dict(vpt=0, st_sc1=1), dict(vpt=0, st_sc1=0), dict(vpt=8, unroll=4, st_sc1=1, grid_cap=3),
+                                   dict(vpt=16, unroll=2, fa_occ=2, st_sc1=1), dict(vpt=16, unroll=2, buf=1, st_sc1=1),
+                                   dict(vpt=16, unroll=2, fa_blk=512, st_sc1=1), dict(vpt=4, unroll=4, st_sc1=1),
                                    dict(vpt=8, unroll=4, fa_blk=512, grid_cap=3), dict(vpt=4, unroll=4, fa_blk=512)])
 def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     """Register-capped (amdgpu_waves_per_eu) builds of the 8/16-KiB shapes: same bits as the
@@ -642,7 +645,7 @@ def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     x = torch.randn((K, M + 5), device="cuda").to(dt)
     ns = list(range(7, 7 + K))
     default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
-                   fa_blk=0)
+                   fa_blk=0, st_sc1=-1)
     outs = []
     for kn in (default, dict(default, **knobs)):
         _native.tune(**kn)
@@ -676,6 +679,35 @@ def test_fp16_buffer_load_variants_bit_identical(torch_gpu, knobs):
         outs.append(out[:M].clone())
     _native.tune(**default)
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
+@pytest.mark.parametrize("kind", ["f16", "f64"])
+@pytest.mark.parametrize("knobs", [dict(st_sc1=1), dict(st_sc1=0), dict(st_sc1=1, vpt=8, unroll=4),
+                                   dict(st_sc1=1, vpt=16, unroll=2), dict(st_sc1=1, grid_cap=5)])
+def test_write_through_store_variants_bit_identical(torch_gpu, kind, knobs):
+    """Device-scope write-through output stores (fedagg_tune "st_sc1", buffer stores based at the
+    first active lane) for fp16 and fp64 (pipelined) tiles: same bits as the default stores,
+    ragged tail and numel==1 patches included."""
+    torch = torch_gpu
+    from substrafl_amd import _native
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    K, M = 9, 1_000_007
+    dt = torch.float16 if kind == "f16" else torch.float64
+    x = torch.randn((K, M + 7), device="cuda").to(dt)
+    ns = list(range(11, 11 + K))
+    default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
+                   fa_blk=0, st_sc1=-1)
+    outs = []
+    for kn in (default, dict(default, **knobs)):
+        _native.tune(**kn)
+        out = torch.empty(M + 7, device="cuda", dtype=dt)
+        FedAvgPlan(kind, x, fedavg_weights(ns, kind), M, out, [3, M - 2]).launch()
+        torch.cuda.synchronize()
+        outs.append(out[:M].clone())
+    _native.tune(**default)
+    iv = torch.int16 if kind == "f16" else torch.int64
+    assert torch.equal(outs[0].view(iv), outs[1].view(iv))
 
 
 def test_auto_shape_many_clients_bit_identical(torch_gpu):
@@ -756,7 +788,10 @@ def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
                                    dict(sc_vpt=4, sc_unroll=4, sc_occ=4), dict(sc_vpt=4, sc_unroll=4, sc_blk=512),
                                    dict(sc_vpt=4, sc_unroll=4, sc_cpf=1, sc_occ=4, K=16),
                                    dict(sc_vpt=4, sc_unroll=4, sc_cpf=1, sc_blk=512, grid_cap=3, K=8),
-                                   dict(sc_vpt=4, sc_unroll=4, sc_occ=2, sc_blk=512, K=16)])
+                                   dict(sc_vpt=4, sc_unroll=4, sc_occ=2, sc_blk=512, K=16),
+                                   dict(sc_vpt=4, sc_unroll=4, sc_sc1=1), dict(sc_sc1=1, K=16),
+                                   dict(sc_buf=1, sc_vpt=4, sc_unroll=4, sc_sc1=1, K=32),
+                                   dict(sc_sc1=1, grid_cap=3, K=8)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -769,7 +804,7 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
     default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_bsplit=0, sc_buf=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0,
-                   xcd=0, tpb=1, sc_cpf=0, sc_occ=0, sc_blk=256)
+                   xcd=0, tpb=1, sc_cpf=0, sc_occ=0, sc_blk=256, sc_sc1=0)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)

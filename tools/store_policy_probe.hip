@@ -1,0 +1,143 @@
+// Store cache-policy probe: the Scaffold C4 memory pattern of
+// tools/stream_mix_probe.hip (33 non-temporal read streams, two 32-B outputs per input vector)
+// and the FedAvg C2 pattern (8 streams, one 16-B output), with the output stores issued as
+// buffer stores under every combination of the gfx950 cache-policy bits (aux: 1 = sc0,
+// 2 = nt, 16 = sc1), against the __builtin_nontemporal_store form the kernels use.  Writes
+// are the part of the mix that costs (a marginal ~3.5 TB/s); this asks whether a policy other
+// than nt drains them more cheaply.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/store_policy_probe.hip -o tools/_store_policy_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));      \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int BLOCK = 256;
+constexpr int VPT = 4;
+constexpr int SU = 4;
+
+// B buckets of K client rows, C single streams read last, W output vectors per input vector and
+// bucket; AUX < 0: __builtin_nontemporal_store, else a buffer store with that cache policy.
+template <int K, int B, int C, int W, int AUX>
+__global__ void __launch_bounds__(BLOCK) pattern(const u32x4* __restrict__ x, const u32x4* __restrict__ c,
+                                                 uint64_t nvec, u32x4* __restrict__ out) {
+  const uint64_t tile = (uint64_t)VPT * BLOCK;
+  const uint64_t t = blockIdx.x;
+  if ((t + 1) * tile > nvec) return;
+  u32x4 acc[B][VPT];
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+#pragma unroll
+    for (int n = 0; n < VPT; ++n) acc[b][n] = u32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += SU) {
+    u32x4 r[B][SU][VPT];
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+#pragma unroll
+      for (int n = 0; n < VPT; ++n)
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+          r[b][u][n] = __builtin_nontemporal_load(x + ((uint64_t)b * K + k0 + u) * nvec + t * tile +
+                                                  (uint64_t)n * BLOCK + threadIdx.x);
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+      for (int u = 0; u < SU; ++u)
+#pragma unroll
+        for (int n = 0; n < VPT; ++n) acc[b][n] ^= r[b][u][n];
+  }
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+#pragma unroll
+    for (int n = 0; n < VPT; ++n)
+      acc[B - 1][n] ^= __builtin_nontemporal_load(c + (uint64_t)i * nvec + t * tile + (uint64_t)n * BLOCK + threadIdx.x);
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave0 = t * tile + (threadIdx.x - lane);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+#pragma unroll
+    for (int n = 0; n < VPT; ++n) {
+      const uint64_t o = ((uint64_t)b * nvec + wave0 + (uint64_t)n * BLOCK) * W;  // vectors
+#pragma unroll
+      for (int s = 0; s < W; ++s) {
+        if constexpr (AUX < 0) {
+          __builtin_nontemporal_store(acc[b][n] + s, out + o + s * 64 + lane);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(acc[b][n] + s, rs, (int)((o + s * 64 + lane) * 16), 0, AUX);
+        }
+      }
+    }
+}
+
+template <int K, int B, int C, int W, int AUX>
+static void run(const char* name, const u32x4* x, const u32x4* c, uint64_t nvec, u32x4* out) {
+  const int grid = (int)(nvec / (VPT * BLOCK));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((pattern<K, B, C, W, AUX>), dim3(grid), dim3(BLOCK), 0, 0, x, c, nvec, out);
+  std::vector<float> ms(15);
+  for (auto& m : ms) {
+    CK(hipEventRecord(a));
+    hipLaunchKernelGGL((pattern<K, B, C, W, AUX>), dim3(grid), dim3(BLOCK), 0, 0, x, c, nvec, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&m, a, b));
+  }
+  std::sort(ms.begin(), ms.end());
+  const double bytes = ((double)B * K + C + (double)B * W) * nvec * 16;
+  printf("{\"pattern\": \"%s\", \"aux\": %d, \"us\": %.2f, \"GBps\": %.1f}\n", name, AUX, ms[7] * 1e3,
+         bytes / (ms[7] * 1e-3) / 1e9);
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+}
+
+template <int AUX>
+static void both(const u32x4* x, const u32x4* c, uint64_t nvec, u32x4* out) {
+  run<16, 2, 1, 2, AUX>("scaffold 16 clients, 2 x 32-B outputs", x, c, nvec, out);
+  run<8, 1, 0, 1, AUX>("fedavg 8 clients, 16-B output", x, c, nvec, out);
+}
+
+int main(int argc, char** argv) {
+  const uint64_t M = argc > 1 ? strtoull(argv[1], nullptr, 10) : 25000000ull;  // fp32 elements per row
+  const uint64_t tile = (uint64_t)VPT * BLOCK;
+  const uint64_t nvec = (M / 4) / tile * tile;
+  if (2 * 2 * nvec * 16 >= 0x7FFFFFFFull) {
+    fprintf(stderr, "output exceeds the 32-bit buffer offset range\n");
+    return 2;
+  }
+  u32x4 *x, *c, *out;
+  CK(hipMalloc(&x, 2 * 16 * nvec * 16));
+  CK(hipMalloc(&c, nvec * 16));
+  CK(hipMalloc(&out, 2 * 2 * nvec * 16));
+  CK(hipMemset(x, 1, 2 * 16 * nvec * 16));
+  CK(hipMemset(c, 2, nvec * 16));
+  for (int rep = 0; rep < 2; ++rep) {
+    both<-1>(x, c, nvec, out);
+    both<0>(x, c, nvec, out);
+    both<2>(x, c, nvec, out);
+    both<1>(x, c, nvec, out);
+    both<16>(x, c, nvec, out);
+    both<17>(x, c, nvec, out);
+    both<3>(x, c, nvec, out);
+    both<18>(x, c, nvec, out);
+    both<19>(x, c, nvec, out);
+  }
+  CK(hipFree(x));
+  CK(hipFree(c));
+  CK(hipFree(out));
+  return 0;
+}

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--occ", action="store_true",
                     help="register-capped occupancy variants (fa_occ 2-4) of the 8/16-KiB shapes beside the uncapped ones")
     ap.add_argument("--buf", action="store_true", help="buffer-descriptor client loads (buf 1) beside global loads")
+    ap.add_argument("--sc1", action="store_true", help="write-through (sc1) output stores beside nt / plain")
     ap.add_argument("--blk", action="store_true", help="512-thread workgroups (fa_blk 512) beside the auto shape")
     ap.add_argument("--gridstride", action="store_true",
                     help="grid-strided and tile shapes under grid caps (the read probe's walk), next to the auto shape")
@@ -84,8 +85,11 @@ def main():
         return
 
     base = dict(grid_cap=0, vpt=1, nt_load=1, nt_store=0, unroll=8, pipe=0, tile=0, xcd=0, tpb=1, fa_occ=0, buf=0,
-                fa_blk=0)
-    if args.blk:
+                fa_blk=0, st_sc1=-1)
+    if args.sc1:
+        variants = [dict(base, vpt=0, tile=1, nt_store=n, st_sc1=c) for n, c in ((1, 0), (1, 1), (0, 0))]
+        variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, st_sc1=1) for v, u in ((8, 4), (4, 4), (16, 2))]
+    elif args.blk:
         variants = [dict(base, vpt=0, tile=1, nt_store=1)]
         variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_blk=512)
                      for v, u in ((16, 2), (8, 2), (8, 4), (4, 4))]
