@@ -1590,6 +1590,12 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
       }
     }
     if constexpr (NTS == 1 && (std::is_same<E, F32>::value || std::is_same<E, BF16>::value)) {
+      if constexpr (std::is_same<E, F32>::value) {
+        if (sh.blk > 2 * FA_BLOCK && !sh.buf && !sh.pipe) {  // 1024-thread workgroups (experiment)
+          if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true, 1, false, 1024>(FA_ARGS);
+          return launch_fedavg_variant<E, true, NTS, 4, 4, false, true, 1, false, 1024>(FA_ARGS);
+        }
+      }
       if (sh.blk > FA_BLOCK && !sh.buf && !sh.pipe) {  // 512-thread workgroups
         if (sh.vpt >= 16) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
         if (sh.vpt >= 8 && sh.unroll <= 2) return launch_fedavg_variant<E, true, NTS, 8, 2, false, true, 1, false, 512>(FA_ARGS);
@@ -2142,7 +2148,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
   else if (!strcmp(key, "sc_sc1")) g_sc_sc1 = value ? 1 : 0;
   else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
-  else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 512 ? 512 : 256);
+  else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 1024 ? 1024 : (value >= 512 ? 512 : 256));
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;
 }

@@ -628,7 +628,8 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
                                    dict(vpt=16, unroll=2, fa_occ=2, buf=1), dict(vpt=16, unroll=1, buf=1),
                                    dict(vpt=16, unroll=1, fa_occ=2, buf=1, grid_cap=3),
                                    dict(vpt=16, unroll=2, fa_blk=512), dict(vpt=8, unroll=2, fa_blk=512),
-                                   dict(vpt=0, fa_blk=256), dict(vpt=0, fa_blk=512),
+                                   dict(vpt=0, fa_blk=256), dict(vpt=0, fa_blk=512), dict(vpt=8, unroll=2, fa_blk=1024),
+                                   dict(vpt=4, unroll=4, fa_blk=1024, grid_cap=3),
                                    dict(vpt=0, st_sc1=1), dict(vpt=0, st_sc1=0), dict(vpt=8, unroll=4, st_sc1=1, grid_cap=3),
                                    dict(vpt=16, unroll=2, fa_occ=2, st_sc1=1), dict(vpt=16, unroll=2, buf=1, st_sc1=1),
                                    dict(vpt=16, unroll=2, fa_blk=512, st_sc1=1), dict(vpt=4, unroll=4, st_sc1=1),

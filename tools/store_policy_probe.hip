@@ -6,7 +6,7 @@
 // are the part of the mix that costs (a marginal ~3.5 TB/s); this asks whether a policy other
 // than nt drains them more cheaply.  `load` mode does the same for the client loads (buffer
 // loads per client row under each policy, against __builtin_nontemporal_load).
-// Usage: _store_policy_probe [M] [load]
+// Usage: _store_policy_probe [M] [load | c3]
 // Build: hipcc --offload-arch=gfx950 -O3 tools/store_policy_probe.hip -o tools/_store_policy_probe
 #include <hip/hip_runtime.h>
 
@@ -141,9 +141,36 @@ static void loads(const u32x4* x, const u32x4* c, uint64_t nvec, u32x4* out) {
   run<32, 1, 0, 0, 16, LAUX>("32 clients, reads only", x, c, nvec, out);
 }
 
+// C3's pattern: 64 client streams, one 16-B output (or none), M fp32 per row.
+static int c3_mode(uint64_t M) {
+  const uint64_t tile = (uint64_t)VPT * BLOCK;
+  const uint64_t nvec = (M / 4) / tile * tile;
+  if (nvec * 16 >= 0x7FFFFFFFull) {
+    fprintf(stderr, "output exceeds the 32-bit buffer offset range\n");
+    return 2;
+  }
+  u32x4 *x, *c, *out;
+  CK(hipMalloc(&x, 64 * nvec * 16));
+  CK(hipMalloc(&c, 16));
+  CK(hipMalloc(&out, nvec * 16));
+  CK(hipMemset(x, 1, 64 * nvec * 16));
+  for (int rep = 0; rep < 2; ++rep) {
+    run<64, 1, 0, 0, -1>("64 clients, reads only", x, c, nvec, out);
+    run<64, 1, 0, 1, -1>("64 clients, 16-B output (nt)", x, c, nvec, out);
+    run<64, 1, 0, 1, 16>("64 clients, 16-B output (sc1)", x, c, nvec, out);
+    run<32, 1, 0, 0, -1>("32 clients, reads only", x, c, nvec, out);
+    run<32, 1, 0, 1, -1>("32 clients, 16-B output (nt)", x, c, nvec, out);
+  }
+  CK(hipFree(x));
+  CK(hipFree(c));
+  CK(hipFree(out));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const bool load_mode = argc > 2 && argv[2][0] == 'l';
   const uint64_t M = argc > 1 ? strtoull(argv[1], nullptr, 10) : 25000000ull;  // fp32 elements per row
+  if (argc > 2 && argv[2][0] == 'c') return c3_mode(M);
   const uint64_t tile = (uint64_t)VPT * BLOCK;
   const uint64_t nvec = (M / 4) / tile * tile;
   if (2 * 2 * nvec * 16 >= 0x7FFFFFFFull) {

@@ -93,6 +93,8 @@ def main():
         variants = [dict(base, vpt=0, tile=1, nt_store=1)]
         variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_blk=512)
                      for v, u in ((16, 2), (8, 2), (8, 4), (4, 4))]
+        if args.kind == "f32":
+            variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_blk=1024) for v, u in ((8, 2), (4, 4))]
     elif args.buf:
         variants = [dict(base, vpt=0, tile=1, nt_store=1, buf=b) for b in (0, 1)]
         variants += [dict(base, vpt=v, unroll=u, tile=1, nt_store=1, fa_occ=o, buf=b)
