@@ -78,6 +78,7 @@ int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per work
 int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
 int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
 int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
+int g_sc_2l = 0;        // Scaffold: one launch per bucket (delta, then control variate + c)
 int g_sc_sc1 = 0;       // Scaffold 4 x 4 tiles: write-through (sc1) output stores
 int g_st_sc1 = -1;      // FedAvg: write-through (sc1) output stores (-1: auto, below SC1_MAX_K clients)
 int g_fa_blk = 0;       // FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto, 256, 512)
@@ -1047,6 +1048,54 @@ __global__ void __launch_bounds__(FA_BLOCK)
   }
 }
 
+// One-bucket launches (fedagg_tune "sc_2l"): the whole grid walks ONE of the two buckets --
+// PH 0: the K delta rows into dout (lr applied after the sum), PH 1: the K control-variate rows
+// plus c into cout -- and the host launches PH 0 then PH 1.  The two sums are independent, so the
+// bytes and the per-element arithmetic are those of scaffold_kernel; what changes is that only
+// K (or K + 1) client streams are in flight at a time instead of 2K + 1.
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int PH>
+__global__ void __launch_bounds__(FA_BLOCK)
+    scaffold_bucket_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
+                           const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
+                           double* __restrict__ out, const int remap, const int tpb) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
+  const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
+  __shared__ u32x4 stage[FA_BLOCK / 64][128];
+  u32x4* lds_wave = stage[threadIdx.x / 64];
+  const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+  uint64_t t;
+  for (uint64_t it = 0; block_tile(remap, tpb, it, &t) && t * tile < nvec; ++it) {
+    const uint64_t base = t * tile + threadIdx.x;
+    const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
+    if (base + (VPT - 1) * FA_BLOCK < nvec) {
+      uint64_t v[VPT];
+#pragma unroll
+      for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+      scaffold_phase<TIn, KC, NT, NTS, VPT, SU, PH>(a, pw, K, first, last, c, lr, v, out, wave_full, lds_wave);
+    } else {
+      for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
+        scaffold_phase<TIn, KC, NT, NTS, 1, SU, PH>(a, pw, K, first, last, c, lr, &v0, out, false, lds_wave);
+    }
+  }
+  for (uint64_t i = nvec * L + gid; i < M; i += stride) {  // scalar remainder
+    double acc = first ? 0.0 : out[i];
+    for (int k = 0; k < K; ++k) {
+      const double p = a.w[k] * (double)(PH == 0 ? a.d[k][i] : a.cv[k][i]);
+      acc = acc + p;
+    }
+    if (last) acc = PH == 0 ? lr * acc : acc + (double)c[i];
+    for (int p = 0; p < pw.n; ++p)
+      if (pw.idx[p] == i) {
+        double dv, cvv;
+        scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, i, &dv, &cvv);
+        acc = PH == 0 ? dv : cvv;
+      }
+    out[i] = acc;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Separate numel==1 path (K > one chunk, or more indices than fit the kernel arguments)
 // ------------------------------------------------------------------------------------
@@ -1936,6 +1985,51 @@ void launch_scaffold_bsplit(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDA
 #undef SC_ARGS
 }
 
+template <typename TIn, int NTS, int VPT, int SU>
+void launch_scaffold_2l_variant(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
+                                int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M,
+                                double* dout, double* cout) {
+  const unsigned grid = grid_for(nvec ? (nvec + VPT - 1) / VPT : M);
+  hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 0>), dim3(grid),
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, g_xcd, 1);
+  hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 1>), dim3(grid),
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, cout, g_xcd, 1);
+}
+
+// One-bucket launch pairs (sc_2l): 4 x 4, 8 x 4, 8 x 2 and 16 x 2 tiles with nt or write-through
+// (sc_sc1) stores; plain stores for the 4 x 4 tile only.
+template <typename TIn, int NTS>
+void launch_scaffold_2l_shape(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw, int kc,
+                              int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
+                              double* cout, const int sv, const int su) {
+#define SC2_ARGS s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
+  if constexpr (NTS == 0) {
+    return launch_scaffold_2l_variant<TIn, 0, 4, 4>(SC2_ARGS);
+  } else {
+    if (sv >= 16) {
+      if (su <= 1) return launch_scaffold_2l_variant<TIn, NTS, 16, 1>(SC2_ARGS);
+      return launch_scaffold_2l_variant<TIn, NTS, 16, 2>(SC2_ARGS);
+    }
+    if (sv >= 8 && su <= 2) return launch_scaffold_2l_variant<TIn, NTS, 8, 2>(SC2_ARGS);
+    if (sv >= 8) return launch_scaffold_2l_variant<TIn, NTS, 8, 4>(SC2_ARGS);
+    if (su >= 8) return launch_scaffold_2l_variant<TIn, NTS, 4, 8>(SC2_ARGS);
+    return launch_scaffold_2l_variant<TIn, NTS, 4, 4>(SC2_ARGS);
+  }
+#undef SC2_ARGS
+}
+
+template <typename TIn>
+void launch_scaffold_2l(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw, int kc,
+                        int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
+                        double* cout, const int sv, const int su) {
+  if (g_nt_store == 0)
+    launch_scaffold_2l_shape<TIn, 0>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+  else if (g_sc_sc1)
+    launch_scaffold_2l_shape<TIn, 2>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+  else
+    launch_scaffold_2l_shape<TIn, 1>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+}
+
 template <typename TIn>
 void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
                      int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
@@ -2060,7 +2154,10 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0 && seed, last = (k0 + kc) == K && finish;
-    if (bsplit)
+    if (g_sc_2l && g_nt_load)
+      launch_scaffold_2l<TIn>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout,
+                              g_sc_vpt > 0 ? g_sc_vpt : 8, g_sc_vpt > 0 ? g_sc_unroll : 4);
+    else if (bsplit)
       launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     else
       launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, buf);
@@ -2146,6 +2243,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
   else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
+  else if (!strcmp(key, "sc_2l")) g_sc_2l = value ? 1 : 0;
   else if (!strcmp(key, "sc_sc1")) g_sc_sc1 = value ? 1 : 0;
   else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
   else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 1024 ? 1024 : (value >= 512 ? 512 : 256));

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only-new", action="store_true", help="only the c-prefetch / occupancy / 512-thread variants")
+    ap.add_argument("--two-launch", action="store_true", help="one launch per bucket (sc_2l) shapes")
     ap.add_argument("--sc1", action="store_true", help="write-through (sc1) output stores on the 4 x 4 tiles")
     args = ap.parse_args()
     import torch
@@ -60,10 +61,15 @@ def main():
                     dict(sc_split=0, sc_pipe=0, sc_buf=1, sc_vpt=4, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0),
                     dict(sc_split=0, sc_pipe=0, sc_buf=1, sc_vpt=4, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0,
                          sc_sc1=1)]
+    elif args.two_launch:
+        variants = [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0)]
+        variants += [dict(sc_split=0, sc_pipe=0, sc_2l=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0,
+                          sc_sc1=s1) for v, u in ((4, 4), (8, 4), (8, 2), (16, 2), (4, 8), (16, 1))
+                     for s1 in (0, 1)]
     elif args.only_new:
         variants = [v for v in variants if "sc_cpf" in v or v.get("nt_store") == 0] + [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4,
                                                                   nt_store=1, grid_cap=0, xcd=0)]
-    variants = [dict(dict(tpb=1, sc_bsplit=0, sc_buf=0, sc_cpf=0, sc_occ=0, sc_blk=256, sc_sc1=0), **v) for v in variants]
+    variants = [dict(dict(tpb=1, sc_bsplit=0, sc_buf=0, sc_cpf=0, sc_occ=0, sc_blk=256, sc_sc1=0, sc_2l=0), **v) for v in variants]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {i: [] for i in range(len(variants))}
     for _ in range(args.rounds):
