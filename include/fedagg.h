@@ -71,7 +71,7 @@ const char* fedagg_last_error(void);
  *   "fa_blk"        FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto / 256 / 512)
  *   "st_sc1"        FedAvg output stores as write-through (sc1) stores (-1 auto: below 32 clients)
  *   "sc_sc1"        Scaffold 4 x 4 tiles: write-through (sc1) output stores
- *   "sc_2l"         Scaffold: one launch per bucket (delta, then control variate + c)
+ *   "sc_2l"         Scaffold: one bucket at a time (1: a launch per bucket, 2: one launch, bucket-ordered halves)
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);
 

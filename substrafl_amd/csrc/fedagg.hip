@@ -78,7 +78,7 @@ int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per work
 int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
 int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
 int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
-int g_sc_2l = 0;        // Scaffold: one launch per bucket (delta, then control variate + c)
+int g_sc_2l = -1;       // Scaffold: one bucket at a time (-1 auto: from SC_2L_MIN_K clients; 1 / 2 / 0)
 int g_sc_sc1 = 0;       // Scaffold 4 x 4 tiles: write-through (sc1) output stores
 int g_st_sc1 = -1;      // FedAvg: write-through (sc1) output stores (-1: auto, below SC1_MAX_K clients)
 int g_fa_blk = 0;       // FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto, 256, 512)
@@ -88,6 +88,11 @@ constexpr int NT_STORE_MIN_K = 16;
 // vs 140.0 us, fp16 71.5 vs 75.0, fp64 280 vs 298; from 32 clients the output is <= 3 % of the
 // bytes and it is neutral (64 x 125M fp32 +0.4 %, 128 x 350M bf16 -0.6 %; profiles/r02_sc1_*.log)
 constexpr int SC1_MAX_K = 32;
+// Scaffold one bucket at a time (two launches, K streams in flight instead of 2K + 1), 8 x 4
+// tiles: 16 x 25M fp32 571 vs 594 us for the fused 4 x 4 walk, 32 x 25M 1.032 vs 1.087 ms,
+// 64 x 25M 1.949 vs 2.013 ms; 8 x 100M ties (1.467 ms either way), so the fused walk stays
+// below 16 clients (profiles/r02_sc2l_*.log)
+constexpr int SC_2L_MIN_K = 16;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1048,51 +1053,70 @@ __global__ void __launch_bounds__(FA_BLOCK)
   }
 }
 
-// One-bucket launches (fedagg_tune "sc_2l"): the whole grid walks ONE of the two buckets --
-// PH 0: the K delta rows into dout (lr applied after the sum), PH 1: the K control-variate rows
-// plus c into cout -- and the host launches PH 0 then PH 1.  The two sums are independent, so the
-// bytes and the per-element arithmetic are those of scaffold_kernel; what changes is that only
-// K (or K + 1) client streams are in flight at a time instead of 2K + 1.
-template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int PH>
-__global__ void __launch_bounds__(FA_BLOCK)
-    scaffold_bucket_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
-                           const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
-                           double* __restrict__ out, const int remap, const int tpb) {
+// One-bucket launches (fedagg_tune "sc_2l"): the grid walks ONE of the two buckets at a time --
+// phase 0: the K delta rows into dout (lr applied after the sum), phase 1: the K control-variate
+// rows plus c into cout.  The two sums are independent, so the bytes and the per-element
+// arithmetic are those of scaffold_kernel; what changes is that only K (or K + 1) client streams
+// are in flight at a time instead of 2K + 1.  PH 0 / 1: one launch per phase (the host launches
+// 0 then 1); PH 2: one launch whose first half of workgroups runs phase 0 and second half phase
+// 1 (the dispatcher starts workgroups in index order, so the phases overlap only at the seam).
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int P>
+__device__ __forceinline__ void scaffold_bucket_walk(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
+                                                     const int first, const int last, const TIn* __restrict__ c,
+                                                     const double lr, const uint64_t nvec, const uint64_t M,
+                                                     double* __restrict__ out, const uint64_t lb,
+                                                     const uint64_t nblk, u32x4* lds_wave) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
-  const uint64_t stride = (uint64_t)gridDim.x * FA_BLOCK;
-  const uint64_t gid = (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x;
-  __shared__ u32x4 stage[FA_BLOCK / 64][128];
-  u32x4* lds_wave = stage[threadIdx.x / 64];
   const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
-  uint64_t t;
-  for (uint64_t it = 0; block_tile(remap, tpb, it, &t) && t * tile < nvec; ++it) {
+  for (uint64_t t = lb; t * tile < nvec; t += nblk) {
     const uint64_t base = t * tile + threadIdx.x;
     const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
     if (base + (VPT - 1) * FA_BLOCK < nvec) {
       uint64_t v[VPT];
 #pragma unroll
       for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
-      scaffold_phase<TIn, KC, NT, NTS, VPT, SU, PH>(a, pw, K, first, last, c, lr, v, out, wave_full, lds_wave);
+      scaffold_phase<TIn, KC, NT, NTS, VPT, SU, P>(a, pw, K, first, last, c, lr, v, out, wave_full, lds_wave);
     } else {
       for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
-        scaffold_phase<TIn, KC, NT, NTS, 1, SU, PH>(a, pw, K, first, last, c, lr, &v0, out, false, lds_wave);
+        scaffold_phase<TIn, KC, NT, NTS, 1, SU, P>(a, pw, K, first, last, c, lr, &v0, out, false, lds_wave);
     }
   }
-  for (uint64_t i = nvec * L + gid; i < M; i += stride) {  // scalar remainder
+  for (uint64_t i = nvec * L + lb * FA_BLOCK + threadIdx.x; i < M; i += nblk * FA_BLOCK) {  // scalar remainder
     double acc = first ? 0.0 : out[i];
     for (int k = 0; k < K; ++k) {
-      const double p = a.w[k] * (double)(PH == 0 ? a.d[k][i] : a.cv[k][i]);
+      const double p = a.w[k] * (double)(P == 0 ? a.d[k][i] : a.cv[k][i]);
       acc = acc + p;
     }
-    if (last) acc = PH == 0 ? lr * acc : acc + (double)c[i];
+    if (last) acc = P == 0 ? lr * acc : acc + (double)c[i];
     for (int p = 0; p < pw.n; ++p)
       if (pw.idx[p] == i) {
         double dv, cvv;
         scaffold_pairwise_elem<TIn, KC>(a, K, c, lr, i, &dv, &cvv);
-        acc = PH == 0 ? dv : cvv;
+        acc = P == 0 ? dv : cvv;
       }
     out[i] = acc;
+  }
+}
+
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int PH>
+__global__ void __launch_bounds__(FA_BLOCK)
+    scaffold_bucket_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
+                           const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
+                           double* __restrict__ dout, double* __restrict__ cout) {
+  __shared__ u32x4 stage[FA_BLOCK / 64][128];
+  u32x4* lds_wave = stage[threadIdx.x / 64];
+  if constexpr (PH == 2) {
+    const uint64_t half = gridDim.x / 2;
+    if (blockIdx.x < half)
+      scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, 0>(a, pw, K, first, last, c, lr, nvec, M, dout, blockIdx.x,
+                                                          half, lds_wave);
+    else
+      scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, 1>(a, pw, K, first, last, c, lr, nvec, M, cout,
+                                                          blockIdx.x - half, half, lds_wave);
+  } else {
+    scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, PH>(a, pw, K, first, last, c, lr, nvec, M, PH == 0 ? dout : cout,
+                                                         blockIdx.x, gridDim.x, lds_wave);
   }
 }
 
@@ -1990,10 +2014,15 @@ void launch_scaffold_2l_variant(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_S
                                 int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M,
                                 double* dout, double* cout) {
   const unsigned grid = grid_for(nvec ? (nvec + VPT - 1) / VPT : M);
+  if (g_sc_2l == 2) {  // one launch, phase-ordered halves
+    hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 2>), dim3(2 * grid),
+                       dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+    return;
+  }
   hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 0>), dim3(grid),
-                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, g_xcd, 1);
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
   hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 1>), dim3(grid),
-                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, cout, g_xcd, 1);
+                     dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
 }
 
 // One-bucket launch pairs (sc_2l): 4 x 4, 8 x 4, 8 x 2 and 16 x 2 tiles with nt or write-through
@@ -2135,6 +2164,7 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   // bucket-split pairs: vector path with nt loads/stores only (the tail is in-kernel)
   const bool bsplit = g_sc_bsplit && nvec && g_nt_load && g_nt_store != 0;
+  const bool two = g_nt_load && (g_sc_2l < 0 ? (K >= SC_2L_MIN_K && nvec && !bsplit && g_sc_vpt <= 0) : g_sc_2l != 0);
   if (bsplit) grid *= 2;
   else if (g_tpb > 1 && nvec)  // every tile exactly once: no grid cap with tpb
     grid = (unsigned)(((nvec + per_thread - 1) / per_thread + g_tpb - 1) / g_tpb);
@@ -2154,9 +2184,10 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0 && seed, last = (k0 + kc) == K && finish;
-    if (g_sc_2l && g_nt_load)
+    if (two)  // fp64 inputs: 4 x 8 tiles (16 x 25M: 1.338 vs 1.397 ms fused, 8 x 4: 1.577)
       launch_scaffold_2l<TIn>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout,
-                              g_sc_vpt > 0 ? g_sc_vpt : 8, g_sc_vpt > 0 ? g_sc_unroll : 4);
+                              g_sc_vpt > 0 ? g_sc_vpt : (sizeof(TIn) == 4 ? 8 : 4),
+                              g_sc_vpt > 0 ? g_sc_unroll : (sizeof(TIn) == 4 ? 4 : 8));
     else if (bsplit)
       launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     else
@@ -2243,7 +2274,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
   else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
-  else if (!strcmp(key, "sc_2l")) g_sc_2l = value ? 1 : 0;
+  else if (!strcmp(key, "sc_2l")) g_sc_2l = value < 0 ? -1 : (value == 0 ? 0 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_sc1")) g_sc_sc1 = value ? 1 : 0;
   else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
   else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 1024 ? 1024 : (value >= 512 ? 512 : 256));

@@ -796,7 +796,8 @@ def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
                                    dict(sc_2l=1), dict(sc_2l=1, sc_vpt=8, sc_unroll=4), dict(sc_2l=1, K=70),
                                    dict(sc_2l=1, sc_vpt=16, sc_unroll=2, K=16), dict(sc_2l=1, sc_vpt=8, sc_unroll=2, sc_sc1=1),
                                    dict(sc_2l=1, nt_store=0, K=5), dict(sc_2l=1, grid_cap=3, K=33),
-                                   dict(sc_2l=1, sc_vpt=4, sc_unroll=8), dict(sc_2l=1, sc_vpt=16, sc_unroll=1, K=12)])
+                                   dict(sc_2l=1, sc_vpt=4, sc_unroll=8), dict(sc_2l=1, sc_vpt=16, sc_unroll=1, K=12),
+                                   dict(sc_2l=2, sc_vpt=8, sc_unroll=4), dict(sc_2l=2, K=70, grid_cap=5)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -809,7 +810,7 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(5, 5 + K)))
     default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_bsplit=0, sc_buf=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0,
-                   xcd=0, tpb=1, sc_cpf=0, sc_occ=0, sc_blk=256, sc_sc1=0, sc_2l=0)
+                   xcd=0, tpb=1, sc_cpf=0, sc_occ=0, sc_blk=256, sc_sc1=0, sc_2l=-1)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)
@@ -866,7 +867,8 @@ def test_scaffold_auto_shape_many_clients_bit_identical(torch_gpu, K):
 
 
 @pytest.mark.parametrize("K", [9, 67])
-@pytest.mark.parametrize("knobs", [dict(sc_2l=1), dict(sc_2l=1, sc_vpt=8, sc_unroll=2, sc_sc1=1)])
+@pytest.mark.parametrize("knobs", [dict(sc_2l=1), dict(sc_2l=1, sc_vpt=8, sc_unroll=2, sc_sc1=1), dict(sc_2l=2),
+                                   dict(sc_2l=-1)])
 def test_scaffold_one_bucket_launches_fp64_bit_identical(torch_gpu, K, knobs):
     """fp64 inputs through the one-bucket launch pair (sc_2l): same bits as the fused walk, with a
     ragged tail, numel==1 elements and (K = 67) two client chunks."""
@@ -889,7 +891,7 @@ def test_scaffold_one_bucket_launches_fp64_bit_identical(torch_gpu, K, knobs):
                      do, co, [2, M - 1]).launch()
         torch.cuda.synchronize()
         outs.append((do[:M].clone(), co[:M].clone()))
-    _native.tune(**base)
+    _native.tune(**dict(base, sc_2l=-1))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a.view(torch.int64), b.view(torch.int64))
 

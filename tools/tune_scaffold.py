@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only-new", action="store_true", help="only the c-prefetch / occupancy / 512-thread variants")
     ap.add_argument("--two-launch", action="store_true", help="one launch per bucket (sc_2l) shapes")
+    ap.add_argument("--kind", default="f32", choices=["f32", "f64"], help="client bucket dtype")
     ap.add_argument("--sc1", action="store_true", help="write-through (sc1) output stores on the 4 x 4 tiles")
     args = ap.parse_args()
     import torch
@@ -28,14 +29,15 @@ def main():
     from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
 
     shapes = synthetic_state_dict_shapes(args.M)
-    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
-    d = torch.randn((args.K, lay.ld), device="cuda")
-    cv = torch.randn((args.K, lay.ld), device="cuda")
-    c = torch.randn(lay.ld, device="cuda")
+    ndt, tdt = (np.float32, torch.float32) if args.kind == "f32" else (np.float64, torch.float64)
+    lay = BucketLayout(range(len(shapes)), shapes, ndt)
+    d = torch.randn((args.K, lay.ld), device="cuda", dtype=tdt)
+    cv = torch.randn((args.K, lay.ld), device="cuda", dtype=tdt)
+    c = torch.randn(lay.ld, device="cuda", dtype=tdt)
     dout = torch.empty(lay.ld, dtype=torch.float64, device="cuda")
     cout = torch.empty(lay.ld, dtype=torch.float64, device="cuda")
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, args.K)]
-    plan = ScaffoldPlan("f32", d, cv, c, scaffold_weights(ns), args.M, 1.0, dout, cout, lay.pairwise_idx)
+    plan = ScaffoldPlan(args.kind, d, cv, c, scaffold_weights(ns), args.M, 1.0, dout, cout, lay.pairwise_idx)
     nbytes = plan.bytes_alg()
     variants = [dict(sc_split=0, sc_pipe=0, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
                 for v, u in ((0, 4), (2, 4), (2, 8), (1, 8), (4, 2), (4, 4), (8, 1), (8, 2))]  # sc_vpt 0: auto
@@ -62,10 +64,13 @@ def main():
                     dict(sc_split=0, sc_pipe=0, sc_buf=1, sc_vpt=4, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0,
                          sc_sc1=1)]
     elif args.two_launch:
-        variants = [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0)]
+        variants = [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0),
+                    dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4, nt_store=1, grid_cap=0, xcd=0, sc_2l=-1)]
         variants += [dict(sc_split=0, sc_pipe=0, sc_2l=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0,
                           sc_sc1=s1) for v, u in ((4, 4), (8, 4), (8, 2), (16, 2), (4, 8), (16, 1))
                      for s1 in (0, 1)]
+        variants += [dict(sc_split=0, sc_pipe=0, sc_2l=2, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
+                     for v, u in ((8, 4), (4, 8))]
     elif args.only_new:
         variants = [v for v in variants if "sc_cpf" in v or v.get("nt_store") == 0] + [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4,
                                                                   nt_store=1, grid_cap=0, xcd=0)]
