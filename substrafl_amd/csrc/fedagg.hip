@@ -91,7 +91,8 @@ constexpr int SC1_MAX_K = 32;
 // Scaffold one bucket at a time (two launches, K streams in flight instead of 2K + 1), 8 x 4
 // tiles: 16 x 25M fp32 571 vs 594 us for the fused 4 x 4 walk, 32 x 25M 1.032 vs 1.087 ms,
 // 64 x 25M 1.949 vs 2.013 ms; 8 x 100M ties (1.467 ms either way), so the fused walk stays
-// below 16 clients (profiles/r02_sc2l_*.log)
+// below 16 clients for fp32 inputs; fp64 inputs take the pipelined one-bucket tiles at any K
+// (profiles/r02_sc2l_*.log)
 constexpr int SC_2L_MIN_K = 16;
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -826,7 +827,42 @@ __device__ __forceinline__ void scaffold_vectors(const ScArgs<TIn, KC>& a, const
 // thread streams all K delta vectors first (and stores the delta result), then all K control
 // variate vectors: half the concurrent streams and half the live accumulators of the fused
 // walk, so a wave can own twice the contiguous bytes per stream.
-template <typename TIn, int KC, bool NT, int NTS, int N, int SU, int PH>
+template <typename TIn, int KC, bool NT, int N, int SU, int PH>
+__device__ __forceinline__ void scaffold_phase_load(const ScArgs<TIn, KC>& a, const int k, const uint64_t* v,
+                                                    u32x4 (&r)[N][SU]) {
+  constexpr int L = 16 / sizeof(TIn);
+#pragma unroll
+  for (int u = 0; u < SU; ++u)
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      if constexpr (PH == 0) r[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
+      else r[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+    }
+}
+
+template <typename TIn, int KC, int N, int SU>
+__device__ __forceinline__ void scaffold_phase_add(const ScArgs<TIn, KC>& a, const int k, const u32x4 (&r)[N][SU],
+                                                   double (&acc)[N][16 / sizeof(TIn)]) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const double w = a.w[k + u];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      double x[L];
+      unpack_d<TIn>(r[n][u], x);
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const double p = w * x[j];
+        acc[n][j] = acc[n][j] + p;
+      }
+    }
+  }
+}
+
+// PIPE: the next client group's loads are issued before this group's fp64 products and adds.
+template <typename TIn, int KC, bool NT, int NTS, int N, int SU, int PH, bool PIPE = false>
 __device__ __forceinline__ void scaffold_phase(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                const int first, const int last, const TIn* __restrict__ c,
                                                const double lr, const uint64_t* v, double* __restrict__ out,
@@ -839,28 +875,28 @@ __device__ __forceinline__ void scaffold_phase(const ScArgs<TIn, KC>& a, const P
 #pragma unroll
     for (int j = 0; j < L; ++j) acc[n][j] = first ? 0.0 : out[v[n] * L + j];
   int k = 0;
-  for (; k + SU <= K; k += SU) {
-    u32x4 r[N][SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u)
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        if constexpr (PH == 0) r[n][u] = ld16<NT>(a.d[k + u] + v[n] * L);
-        else r[n][u] = ld16<NT>(a.cv[k + u] + v[n] * L);
+  if constexpr (PIPE) {
+    if (K >= SU) {
+      u32x4 ra[N][SU], rb[N][SU];
+      scaffold_phase_load<TIn, KC, NT, N, SU, PH>(a, 0, v, ra);
+      for (;;) {
+        const bool mb = k + 2 * SU <= K;
+        if (mb) scaffold_phase_load<TIn, KC, NT, N, SU, PH>(a, k + SU, v, rb);
+        scaffold_phase_add<TIn, KC, N, SU>(a, k, ra, acc);
+        k += SU;
+        if (!mb) break;
+        const bool ma = k + 2 * SU <= K;
+        if (ma) scaffold_phase_load<TIn, KC, NT, N, SU, PH>(a, k + SU, v, ra);
+        scaffold_phase_add<TIn, KC, N, SU>(a, k, rb, acc);
+        k += SU;
+        if (!ma) break;
       }
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const double w = a.w[k + u];
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        double x[L];
-        unpack_d<TIn>(r[n][u], x);
-#pragma unroll
-        for (int j = 0; j < L; ++j) {
-          const double p = w * x[j];
-          acc[n][j] = acc[n][j] + p;
-        }
-      }
+    }
+  } else {
+    for (; k + SU <= K; k += SU) {
+      u32x4 r[N][SU];
+      scaffold_phase_load<TIn, KC, NT, N, SU, PH>(a, k, v, r);
+      scaffold_phase_add<TIn, KC, N, SU>(a, k, r, acc);
     }
   }
   for (; k < K; ++k) {
@@ -1060,7 +1096,7 @@ __global__ void __launch_bounds__(FA_BLOCK)
 // are in flight at a time instead of 2K + 1.  PH 0 / 1: one launch per phase (the host launches
 // 0 then 1); PH 2: one launch whose first half of workgroups runs phase 0 and second half phase
 // 1 (the dispatcher starts workgroups in index order, so the phases overlap only at the seam).
-template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int P>
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int P, bool PIPE>
 __device__ __forceinline__ void scaffold_bucket_walk(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                      const int first, const int last, const TIn* __restrict__ c,
                                                      const double lr, const uint64_t nvec, const uint64_t M,
@@ -1076,7 +1112,7 @@ __device__ __forceinline__ void scaffold_bucket_walk(const ScArgs<TIn, KC>& a, c
       uint64_t v[VPT];
 #pragma unroll
       for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
-      scaffold_phase<TIn, KC, NT, NTS, VPT, SU, P>(a, pw, K, first, last, c, lr, v, out, wave_full, lds_wave);
+      scaffold_phase<TIn, KC, NT, NTS, VPT, SU, P, PIPE>(a, pw, K, first, last, c, lr, v, out, wave_full, lds_wave);
     } else {
       for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
         scaffold_phase<TIn, KC, NT, NTS, 1, SU, P>(a, pw, K, first, last, c, lr, &v0, out, false, lds_wave);
@@ -1099,7 +1135,7 @@ __device__ __forceinline__ void scaffold_bucket_walk(const ScArgs<TIn, KC>& a, c
   }
 }
 
-template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int PH>
+template <typename TIn, int KC, bool NT, int NTS, int VPT, int SU, int PH, bool PIPE = false>
 __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_bucket_kernel(const ScArgs<TIn, KC> a, const PwArgs pw, const int K, const int first, const int last,
                            const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
@@ -1109,13 +1145,13 @@ __global__ void __launch_bounds__(FA_BLOCK)
   if constexpr (PH == 2) {
     const uint64_t half = gridDim.x / 2;
     if (blockIdx.x < half)
-      scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, 0>(a, pw, K, first, last, c, lr, nvec, M, dout, blockIdx.x,
+      scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, 0, PIPE>(a, pw, K, first, last, c, lr, nvec, M, dout, blockIdx.x,
                                                           half, lds_wave);
     else
-      scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, 1>(a, pw, K, first, last, c, lr, nvec, M, cout,
+      scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, 1, PIPE>(a, pw, K, first, last, c, lr, nvec, M, cout,
                                                           blockIdx.x - half, half, lds_wave);
   } else {
-    scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, PH>(a, pw, K, first, last, c, lr, nvec, M, PH == 0 ? dout : cout,
+    scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, PH, PIPE>(a, pw, K, first, last, c, lr, nvec, M, PH == 0 ? dout : cout,
                                                          blockIdx.x, gridDim.x, lds_wave);
   }
 }
@@ -2009,19 +2045,19 @@ void launch_scaffold_bsplit(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDA
 #undef SC_ARGS
 }
 
-template <typename TIn, int NTS, int VPT, int SU>
+template <typename TIn, int NTS, int VPT, int SU, bool PIPE = false>
 void launch_scaffold_2l_variant(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
                                 int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M,
                                 double* dout, double* cout) {
   const unsigned grid = grid_for(nvec ? (nvec + VPT - 1) / VPT : M);
   if (g_sc_2l == 2) {  // one launch, phase-ordered halves
-    hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 2>), dim3(2 * grid),
+    hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 2, PIPE>), dim3(2 * grid),
                        dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
     return;
   }
-  hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 0>), dim3(grid),
+  hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 0, PIPE>), dim3(grid),
                      dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
-  hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 1>), dim3(grid),
+  hipLaunchKernelGGL((scaffold_bucket_kernel<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, NTS, VPT, SU, 1, PIPE>), dim3(grid),
                      dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
 }
 
@@ -2030,11 +2066,16 @@ void launch_scaffold_2l_variant(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_S
 template <typename TIn, int NTS>
 void launch_scaffold_2l_shape(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw, int kc,
                               int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
-                              double* cout, const int sv, const int su) {
+                              double* cout, const int sv, const int su, const bool pipe) {
 #define SC2_ARGS s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
   if constexpr (NTS == 0) {
     return launch_scaffold_2l_variant<TIn, 0, 4, 4>(SC2_ARGS);
   } else {
+    if (pipe) {  // pipelined client groups
+      if (sv >= 8) return launch_scaffold_2l_variant<TIn, NTS, 8, 2, true>(SC2_ARGS);
+      if (su >= 4) return launch_scaffold_2l_variant<TIn, NTS, 4, 4, true>(SC2_ARGS);
+      return launch_scaffold_2l_variant<TIn, NTS, 4, 2, true>(SC2_ARGS);
+    }
     if (sv >= 16) {
       if (su <= 1) return launch_scaffold_2l_variant<TIn, NTS, 16, 1>(SC2_ARGS);
       return launch_scaffold_2l_variant<TIn, NTS, 16, 2>(SC2_ARGS);
@@ -2050,13 +2091,13 @@ void launch_scaffold_2l_shape(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCA
 template <typename TIn>
 void launch_scaffold_2l(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw, int kc,
                         int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
-                        double* cout, const int sv, const int su) {
+                        double* cout, const int sv, const int su, const bool pipe) {
   if (g_nt_store == 0)
-    launch_scaffold_2l_shape<TIn, 0>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+    launch_scaffold_2l_shape<TIn, 0>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, pipe);
   else if (g_sc_sc1)
-    launch_scaffold_2l_shape<TIn, 2>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+    launch_scaffold_2l_shape<TIn, 2>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, pipe);
   else
-    launch_scaffold_2l_shape<TIn, 1>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+    launch_scaffold_2l_shape<TIn, 1>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, pipe);
 }
 
 template <typename TIn>
@@ -2164,7 +2205,9 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   // bucket-split pairs: vector path with nt loads/stores only (the tail is in-kernel)
   const bool bsplit = g_sc_bsplit && nvec && g_nt_load && g_nt_store != 0;
-  const bool two = g_nt_load && (g_sc_2l < 0 ? (K >= SC_2L_MIN_K && nvec && !bsplit && g_sc_vpt <= 0) : g_sc_2l != 0);
+  const bool two = g_nt_load && (g_sc_2l < 0 ? ((K >= SC_2L_MIN_K || sizeof(TIn) == 8) && nvec && !bsplit &&
+                                                 g_sc_vpt <= 0)
+                                              : g_sc_2l != 0);
   if (bsplit) grid *= 2;
   else if (g_tpb > 1 && nvec)  // every tile exactly once: no grid cap with tpb
     grid = (unsigned)(((nvec + per_thread - 1) / per_thread + g_tpb - 1) / g_tpb);
@@ -2184,10 +2227,13 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0 && seed, last = (k0 + kc) == K && finish;
-    if (two)  // fp64 inputs: 4 x 8 tiles (16 x 25M: 1.338 vs 1.397 ms fused, 8 x 4: 1.577)
+    // fp64 inputs: software-pipelined 4 x 2 tiles (16 x 25M: 1.178 ms, against 1.409 fused, 1.340
+    // for the best unpipelined one-bucket tile; the fp32 one-bucket tiles lose 11-20 % pipelined)
+    if (two)
       launch_scaffold_2l<TIn>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout,
                               g_sc_vpt > 0 ? g_sc_vpt : (sizeof(TIn) == 4 ? 8 : 4),
-                              g_sc_vpt > 0 ? g_sc_unroll : (sizeof(TIn) == 4 ? 4 : 8));
+                              g_sc_vpt > 0 ? g_sc_unroll : (sizeof(TIn) == 4 ? 4 : 2),
+                              g_sc_vpt > 0 ? g_sc_pipe != 0 : sizeof(TIn) == 8);
     else if (bsplit)
       launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
     else

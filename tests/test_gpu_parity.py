@@ -797,7 +797,9 @@ def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
                                    dict(sc_2l=1, sc_vpt=16, sc_unroll=2, K=16), dict(sc_2l=1, sc_vpt=8, sc_unroll=2, sc_sc1=1),
                                    dict(sc_2l=1, nt_store=0, K=5), dict(sc_2l=1, grid_cap=3, K=33),
                                    dict(sc_2l=1, sc_vpt=4, sc_unroll=8), dict(sc_2l=1, sc_vpt=16, sc_unroll=1, K=12),
-                                   dict(sc_2l=2, sc_vpt=8, sc_unroll=4), dict(sc_2l=2, K=70, grid_cap=5)])
+                                   dict(sc_2l=2, sc_vpt=8, sc_unroll=4), dict(sc_2l=2, K=70, grid_cap=5),
+                                   dict(sc_2l=1, sc_pipe=1, sc_vpt=8, sc_unroll=2), dict(sc_2l=1, sc_pipe=1, K=70),
+                                   dict(sc_2l=1, sc_pipe=1, sc_vpt=4, sc_unroll=2, K=7)])
 def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     torch = torch_gpu
     from substrafl_amd import _native
@@ -868,7 +870,7 @@ def test_scaffold_auto_shape_many_clients_bit_identical(torch_gpu, K):
 
 @pytest.mark.parametrize("K", [9, 67])
 @pytest.mark.parametrize("knobs", [dict(sc_2l=1), dict(sc_2l=1, sc_vpt=8, sc_unroll=2, sc_sc1=1), dict(sc_2l=2),
-                                   dict(sc_2l=-1)])
+                                   dict(sc_2l=-1), dict(sc_2l=1, sc_pipe=1, sc_vpt=4, sc_unroll=4)])
 def test_scaffold_one_bucket_launches_fp64_bit_identical(torch_gpu, K, knobs):
     """fp64 inputs through the one-bucket launch pair (sc_2l): same bits as the fused walk, with a
     ragged tail, numel==1 elements and (K = 67) two client chunks."""
@@ -881,7 +883,7 @@ def test_scaffold_one_bucket_launches_fp64_bit_identical(torch_gpu, K, knobs):
     cv = torch.randn((K, M + 1), device="cuda", dtype=torch.float64)
     c = torch.randn(M + 1, device="cuda", dtype=torch.float64)
     w = scaffold_weights(list(range(4, 4 + K)))
-    base = dict(sc_2l=0, sc_vpt=0, sc_unroll=4, sc_sc1=0)
+    base = dict(sc_2l=0, sc_vpt=0, sc_unroll=4, sc_sc1=0, sc_pipe=0)
     outs = []
     for kn in (base, dict(base, **knobs)):
         _native.tune(**kn)

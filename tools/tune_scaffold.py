@@ -71,6 +71,8 @@ def main():
                      for s1 in (0, 1)]
         variants += [dict(sc_split=0, sc_pipe=0, sc_2l=2, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
                      for v, u in ((8, 4), (4, 8))]
+        variants += [dict(sc_split=0, sc_pipe=1, sc_2l=1, sc_vpt=v, sc_unroll=u, nt_store=1, grid_cap=0, xcd=0)
+                     for v, u in ((8, 2), (4, 4), (4, 2))]
     elif args.only_new:
         variants = [v for v in variants if "sc_cpf" in v or v.get("nt_store") == 0] + [dict(sc_split=0, sc_pipe=0, sc_vpt=0, sc_unroll=4,
                                                                   nt_store=1, grid_cap=0, xcd=0)]
