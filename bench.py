@@ -373,7 +373,12 @@ def main():
 
     achieved = bytes_kernel / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     if rank == 0:
-        kname = (f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>" if not scaffold else "scaffold_kernel<float>")
+        if not scaffold:
+            kname = f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>"
+        elif lib.fedagg_scaffold_launches(max(1, Kr), 4, M, 1) == 2:  # the library's own launch plan
+            kname = "scaffold_bucket_kernel<float> x2 (delta bucket, then control variate + c)"
+        else:
+            kname = "scaffold_kernel<float>"
         line = {
             "metric": METRIC,
             "value": round(value, 2),

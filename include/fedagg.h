@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 5
+#define FEDAGG_ABI_VERSION 6
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -127,6 +127,11 @@ int fedagg_scaffold_f32(const float* const* d_delta, const float* const* d_cv, c
 int fedagg_scaffold_f64(const double* const* d_delta, const double* const* d_cv, const double* d_c,
                         const double* h_w, int K, uint64_t M, const uint64_t* h_idx, int P, void* d_ws, double lr,
                         double* d_delta_out, double* d_c_out, void* stream);
+/* Kernel launches per chunk of <= 64 clients that fedagg_scaffold_* makes under the current
+ * tuning: 1 (scaffold_kernel, both buckets in one walk) or 2 (scaffold_bucket_kernel, the delta
+ * bucket then the control-variate bucket); in_elem_bytes 4 or 8, aligned = every operand 16-B
+ * aligned.  For profilers and benchmarks that attribute kernel time; < 0 on bad arguments. */
+int fedagg_scaffold_launches(int K, int in_elem_bytes, uint64_t M, int aligned);
 
 /* ---------------------------------------------------------------------------
  * Scaffold server-control-variate check, scaffold.py:193-196

@@ -34,6 +34,7 @@ SIGNATURES = {
     "fedagg_fedavg_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
     "fedagg_fedavg_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
     "fedagg_fedavg_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_scaffold_launches": (c_int, [c_int, c_int, c_u64, c_int]),
     "fedagg_scaffold_f32": (
         c_int,
         [P(c_void), P(c_void), c_void, P(c_dbl), c_int, c_u64, P(c_u64), c_int, c_void, c_dbl, c_void, c_void, c_void],
@@ -101,7 +102,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

@@ -2045,6 +2045,13 @@ void launch_scaffold_bsplit(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDA
 #undef SC_ARGS
 }
 
+// Does a Scaffold call walk one bucket per launch (scaffold_bucket_kernel x 2) or both at once?
+inline bool scaffold_one_bucket(int K, size_t in_bytes, uint64_t nvec) {
+  const bool bsplit = g_sc_bsplit && nvec && g_nt_load && g_nt_store != 0;
+  return g_nt_load && (g_sc_2l < 0 ? ((K >= SC_2L_MIN_K || in_bytes == 8) && nvec && !bsplit && g_sc_vpt <= 0)
+                                   : g_sc_2l != 0);
+}
+
 template <typename TIn, int NTS, int VPT, int SU, bool PIPE = false>
 void launch_scaffold_2l_variant(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw,
                                 int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M,
@@ -2205,9 +2212,7 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
   unsigned grid = grid_for(nvec ? (nvec + per_thread - 1) / per_thread : M);
   // bucket-split pairs: vector path with nt loads/stores only (the tail is in-kernel)
   const bool bsplit = g_sc_bsplit && nvec && g_nt_load && g_nt_store != 0;
-  const bool two = g_nt_load && (g_sc_2l < 0 ? ((K >= SC_2L_MIN_K || sizeof(TIn) == 8) && nvec && !bsplit &&
-                                                 g_sc_vpt <= 0)
-                                              : g_sc_2l != 0);
+  const bool two = scaffold_one_bucket(K, sizeof(TIn), nvec);
   if (bsplit) grid *= 2;
   else if (g_tpb > 1 && nvec)  // every tile exactly once: no grid cap with tpb
     grid = (unsigned)(((nvec + per_thread - 1) / per_thread + g_tpb - 1) / g_tpb);
@@ -2291,6 +2296,14 @@ void set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
 extern "C" {
 
 int fedagg_abi_version(void) { return FEDAGG_ABI_VERSION; }
+
+int fedagg_scaffold_launches(int K, int in_elem_bytes, uint64_t M, int aligned) {
+  if (K <= 0 || (in_elem_bytes != 4 && in_elem_bytes != 8))
+    return fail(FEDAGG_EINVAL, "scaffold_launches: bad K or element bytes (K=%lld; element bytes must be 4 or 8)",
+                (long long)K);
+  const uint64_t nvec = aligned ? M / (16 / (uint64_t)in_elem_bytes) : 0;
+  return scaffold_one_bucket(K, (size_t)in_elem_bytes, nvec) ? 2 : 1;
+}
 const char* fedagg_last_error(void) { return g_err; }
 
 int fedagg_tune(const char* key, long long value) {

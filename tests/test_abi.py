@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_invalid_arguments():
     lib = _native.load()
-    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 5
+    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 6
     w = (ctypes.c_float * 1)(1.0)
     ptrs = _native.ptr_array([0])
     assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, 0, None, None, None) == -1  # K == 0
@@ -46,6 +46,17 @@ def test_abi_version_and_invalid_arguments():
     assert lib.fedagg_pairwise_ws_bytes(8, 3, 4) == 2 * 64 * 9 * 8
     assert lib.fedagg_tune(b"no_such_knob", 1) == -1
     assert lib.fedagg_tune(b"grid_cap", 4096) == 0
+    assert lib.fedagg_tune(b"grid_cap", 0) == 0
+    # Scaffold launch plan under the default tuning (no HIP call): one bucket per launch from 16
+    # fp32 clients and for fp64 inputs, the fused walk below 16 fp32 clients or unaligned operands
+    assert lib.fedagg_scaffold_launches(16, 4, 25_000_000, 1) == 2
+    assert lib.fedagg_scaffold_launches(8, 4, 25_000_000, 1) == 1
+    assert lib.fedagg_scaffold_launches(8, 8, 25_000_000, 1) == 2
+    assert lib.fedagg_scaffold_launches(16, 4, 25_000_000, 0) == 1
+    assert lib.fedagg_scaffold_launches(16, 2, 25_000_000, 1) == -1
+    assert lib.fedagg_tune(b"sc_2l", 0) == 0
+    assert lib.fedagg_scaffold_launches(16, 4, 25_000_000, 1) == 1
+    assert lib.fedagg_tune(b"sc_2l", -1) == 0
     # kind-generic flat ops: operand kinds are checked before any HIP call
     numel = (ctypes.c_uint64 * 1)(4)
     kinds = (ctypes.c_int * 2)(_native.FEDAGG_F32, _native.FEDAGG_F64)

@@ -15,7 +15,10 @@ import json
 from pathlib import Path
 
 
-def per_dispatch(path, counter, kernel):
+def per_dispatch(path, counter, kernel, group=1):
+    """Counter total per dispatch of ``kernel`` (substring of the name); with ``group`` > 1,
+    totals of consecutive groups of that many dispatches (one call = several launches, e.g.
+    Scaffold's two one-bucket launches)."""
     vals = {}
     with open(path) as f:
         for row in csv.DictReader(f):
@@ -24,9 +27,14 @@ def per_dispatch(path, counter, kernel):
                 continue
             if row.get("Counter_Name") != counter:
                 continue
-            d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            d = int(row.get("Dispatch_Id") or row.get("Correlation_Id"))
             vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+    seq = [vals[d] for d in sorted(vals)]
+    if group > 1:
+        if len(seq) % group:
+            raise SystemExit(f"{len(seq)} dispatches of {kernel} do not split into groups of {group}")
+        seq = [sum(seq[i:i + group]) for i in range(0, len(seq), group)]
+    return seq
 
 
 def main():
@@ -35,12 +43,13 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--kernel", default="fedavg_kernel")
     ap.add_argument("--bytes-alg", type=float, required=True)
+    ap.add_argument("--group", type=int, default=1, help="launches per call (summed per call)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--lib", default="", help="libfedagg.so the passes ran (its sha256 goes into the record)")
     ap.add_argument("--collected", default="", help="free text: box / command / date of the passes")
     a = ap.parse_args()
-    fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
-    write = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
+    fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel, a.group)
+    write = per_dispatch(a.write, "WRITE_SIZE", a.kernel, a.group)
     if not fetch or not write:
         raise SystemExit(f"no rows for {a.kernel}: fetch={len(fetch)} write={len(write)}")
     f_kib = sorted(fetch)[len(fetch) // 2]
@@ -49,6 +58,7 @@ def main():
     write_b = w_kib * 1024
     res = {
         "kernel": a.kernel,
+        "launches_per_call": a.group,
         "dispatches": {"fetch": len(fetch), "write": len(write)},
         "FETCH_SIZE_KiB_median": f_kib,
         "WRITE_SIZE_KiB_median": w_kib,

@@ -12,10 +12,13 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for WL in "$@"; do
   case $WL in
-    c2) KERN=fedavg_kernel; ALG=900000000; STEPS=200 ;;
-    c3) KERN=fedavg_kernel; ALG=32500000000; STEPS=100 ;;
-    c4) KERN=scaffold_kernel; ALG=3700000000; STEPS=100 ;;
-    c5) KERN=fedavg_kernel; ALG=91000000000; STEPS=30 ;;
+    c2) KERN=fedavg_kernel; ALG=900000000; STEPS=200; GROUP=1 ;;
+    c3) KERN=fedavg_kernel; ALG=32500000000; STEPS=100; GROUP=1 ;;
+    c4) KERN=scaffold; ALG=3700000000; STEPS=100
+        # launches per Scaffold call under the library's defaults (1 fused walk, or 2 one-bucket launches)
+        GROUP=$(python3 -c "import sys; sys.path.insert(0, '$ROOT'); from substrafl_amd import _native; \
+print(_native.load().fedagg_scaffold_launches(16, 4, 25000000, 1))") ;;
+    c5) KERN=fedavg_kernel; ALG=91000000000; STEPS=30; GROUP=1 ;;
     *) echo "unknown workload $WL"; exit 2 ;;
   esac
   echo "[$TAG] $WL: bench" >&2
@@ -35,7 +38,7 @@ for WL in "$@"; do
     cp "$(find "$OUT/${TAG}_pmc_${C}_${WL}" -name '*counter_collection.csv' | head -1)" "$OUT/${TAG}_${WL}_pmc_${C}.csv"
   done
   python3 "$ROOT/tools/pmc_traffic.py" --fetch "$OUT/${TAG}_${WL}_pmc_FETCH_SIZE.csv" \
-    --write "$OUT/${TAG}_${WL}_pmc_WRITE_SIZE.csv" --kernel $KERN --bytes-alg $ALG \
+    --write "$OUT/${TAG}_${WL}_pmc_WRITE_SIZE.csv" --kernel $KERN --group $GROUP --bytes-alg $ALG \
     --lib "$ROOT/substrafl_amd/libfedagg.so" --collected "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, session $TAG" \
     --out "$OUT/${TAG}_traffic_${WL}.json" > /dev/null
 done
