@@ -15,9 +15,12 @@ environment, and a WORLD_SIZE that differs from --gpus is an error.  Modes:
   parameter range of all K clients -- no data-path collective.  ``--scaling weak`` (default): each
   rank owns a full M-param slice of an N*M-param model; ``--scaling strong``: the workload's own M
   is split over the N ranks (C3 at 64 x 125M over 8 GPUs = 15.6M params per GPU).
-* ``--mode client-shard --combine relay|rccl|ordered`` (the north-star mode): the K clients are
+* ``--mode client-shard --combine relay|rccl|ordered`` (the north-star mode): the clients are
   split over the ranks, partial sums stay in HBM and are combined over RCCL/xGMI on the root
-  (``relay`` bit-exact; see substrafl_amd/sharding.py).  Needs one GPU per rank.
+  (``relay`` bit-exact; see substrafl_amd/sharding.py).  ``--scaling weak``: every rank holds the
+  workload's K clients (N*K clients of M params in all -- the "buckets overflow one GPU" case);
+  ``--scaling strong``: the workload's K clients are split over the N ranks.  Needs one GPU per
+  rank.
 * ``--engine multi-device``: the drop-in's own multi-GPU path, ONE process driving N GPUs
   (MultiDeviceEngine: host buckets staged over each GPU's PCIe link, per-shard kernel time from
   HIP events on the session streams) -- an end-to-end line, not the device-resident metric.
@@ -213,6 +216,8 @@ def main():
 
     wl = WORKLOADS[args.workload]
     K, M_glob, kind = wl["K"], wl["M"], wl["kind"]
+    if client_shard and args.scaling == "weak":
+        K *= world  # every rank holds the workload's K clients
     scaffold = wl["strategy"] == "scaffold"
     n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
     s_in = 2 if kind == "bf16" else 4
@@ -222,7 +227,7 @@ def main():
         M = M_glob
         k0, k1 = client_blocks(K, world)[block_of(rank, world)]
         parallelism = f"client-shard x{world} ({args.combine})" if world > 1 else "single-gpu"
-        scaling = "strong"
+        scaling = args.scaling
     elif args.scaling == "strong":
         lo, hi = shard_bounds(M_glob, world)[rank]
         M = hi - lo
