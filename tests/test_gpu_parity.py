@@ -1273,7 +1273,7 @@ def test_random_sweep_fedavg(torch_gpu, dummy_algo_class, seed):
     _assert_same(got, fedavg_reference_structure(pus, ns))
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(40))
 def test_random_sweep_scaffold(torch_gpu, dummy_algo_class, seed):
     from substrafl_amd.schemas import ScaffoldSharedState
     from substrafl_amd.strategies import Scaffold
