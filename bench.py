@@ -15,9 +15,11 @@ environment, and a WORLD_SIZE that differs from --gpus is an error.  Modes:
   parameter range of all K clients -- no data-path collective.  ``--scaling weak`` (default): each
   rank owns a full M-param slice of an N*M-param model; ``--scaling strong``: the workload's own M
   is split over the N ranks (C3 at 64 x 125M over 8 GPUs = 15.6M params per GPU).
-* ``--mode client-shard --combine relay|rccl|ordered`` (the north-star mode): the clients are
-  split over the ranks, partial sums stay in HBM and are combined over RCCL/xGMI on the root
-  (``relay`` bit-exact; see substrafl_amd/sharding.py).  ``--scaling weak``: every rank holds the
+* ``--mode client-shard --combine relay|rccl|ordered|striped`` (the north-star mode): the clients
+  are split over the ranks, partial sums stay in HBM and are combined over RCCL/xGMI on the root
+  (``relay`` and ``striped`` bit-exact; ``striped``: the relay over up to four parameter stripes
+  whose chains hop over disjoint xGMI links, one communicator each; see
+  substrafl_amd/sharding.py).  ``--scaling weak``: every rank holds the
   workload's K clients (N*K clients of M params in all -- the "buckets overflow one GPU" case);
   ``--scaling strong``: the workload's K clients are split over the N ranks.  Needs one GPU per
   rank.
@@ -64,7 +66,7 @@ def parse():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--mode", default="param-range", choices=["param-range", "client-shard"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered"])
+    ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered", "striped"])
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -189,7 +191,9 @@ def main():
     from substrafl_amd.engine import FedAvgPlan, ScaffoldPlan, fedavg_weights, scaffold_weights
     from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
     from substrafl_amd.sharding import (DistTransport, FedAvgShard, GpuShardOps, ScaffoldShard, block_of,
-                                        client_blocks, client_shard_fedavg, client_shard_scaffold, shard_bounds)
+                                        client_blocks, client_shard_fedavg, client_shard_fedavg_striped,
+                                        client_shard_scaffold, client_shard_scaffold_striped, shard_bounds,
+                                        stripe_layout)
 
     ndev = torch.cuda.device_count()
     if ndev == 0:
@@ -245,6 +249,32 @@ def main():
     ld = layout.ld
     pw = layout.pairwise_idx
     seed0 = 20241016 + k0 + (1_000_003 * rank if not client_shard else 0)
+    # striped relay: this rank's block per parameter stripe, one communicator per stripe
+    striped = client_shard and args.combine == "striped" and world > 1
+    stripes = stripe_layout(M, K, world, rank) if striped else []
+    if striped:
+        strs = [DistTransport()] + [DistTransport(dist.new_group()) for _ in range(len(stripes) - 1)]
+        bounds = [(lo, hi, a) for lo, hi, a, *_ in stripes]
+        pw64 = pw.astype(np.int64)
+
+        def local_pw(lo, hi):
+            return (pw64[(pw64 >= lo) & (pw64 < hi)] - lo).astype(np.uint64)
+
+        def stripe_rows(si, lo, hi, k0s, k1s, salt=0):  # client k's stripe si: Philox seed per (k, stripe)
+            n = hi - lo
+            return synth_clients(torch, k1s - k0s, max(64, -(-n // 64) * 64), n, kind, device,
+                                 20241016 + 7919 * salt + 104729 * si + k0s)
+
+    class _Plans:  # the stripes' block kernels, back to back
+        def __init__(self, plans):
+            self.plans = plans
+
+        def launch(self, st):
+            for p in self.plans:
+                p.launch(st)
+
+        def bytes_alg(self):
+            return sum(p.bytes_alg() for p in self.plans)
 
     def barrier():
         if world > 1:
@@ -255,7 +285,20 @@ def main():
         clients = synth_clients(torch, Kr, ld, M, kind, device, seed0)
         out = torch.empty(ld, dtype=torch.float32, device=device)
         w_all = fedavg_weights(n_samples, kind)
-        if client_shard:
+        if striped:
+            del clients
+            parts = [FedAvgShard(kind, stripe_rows(si, lo, hi, k0s, k1s), w_all[k0s:k1s], k0s, K, hi - lo,
+                                 local_pw(lo, hi)) for si, (lo, hi, a, b, k0s, k1s) in enumerate(stripes)]
+            clients = parts  # spot check
+            ops = GpuShardOps()
+            ws = torch.zeros((max(1, pw.size), K), dtype=torch.float32, device=device)
+
+            def step():
+                client_shard_fedavg_striped(parts, bounds, out, strs, ops, pw, ws=ws)
+
+            kplan = _Plans([FedAvgPlan(kind, sh.rows, sh.w, sh.M, out[lo:], None)
+                            for sh, (lo, hi, a) in zip(parts, bounds) if sh.Kr and sh.M])
+        elif client_shard:
             sh = FedAvgShard(kind, clients, w_all[k0:k1], k0, K, M, pw)
             ops, tr = GpuShardOps(), DistTransport() if world > 1 else None
             ws = torch.zeros((max(1, pw.size), K), dtype=torch.float32, device=device)
@@ -285,7 +328,20 @@ def main():
         dout = torch.empty(ld, dtype=torch.float64, device=device)
         cout = torch.empty(ld, dtype=torch.float64, device=device)
         w_all = scaffold_weights(n_samples)
-        if client_shard:
+        if striped:
+            del delta, cv
+            parts = [ScaffoldShard(kind, stripe_rows(si, lo, hi, k0s, k1s), stripe_rows(si, lo, hi, k0s, k1s, salt=1),
+                                   c[lo:hi], w_all[k0s:k1s], k0s, K, hi - lo, 1.0, local_pw(lo, hi))
+                     for si, (lo, hi, a, b, k0s, k1s) in enumerate(stripes)]
+            delta, cv = parts, parts  # spot check
+            ops = GpuShardOps()
+
+            def step():
+                client_shard_scaffold_striped(parts, bounds, dout, cout, strs, ops, pw, c=c)
+
+            kplan = _Plans([ScaffoldPlan(kind, sh.delta, sh.cv, sh.c, sh.w, sh.M, 1.0, dout[lo:], cout[lo:], None)
+                            for sh, (lo, hi, a) in zip(parts, bounds) if sh.Kr and sh.M])
+        elif client_shard:
             sh = ScaffoldShard(kind, delta, cv, c, w_all[k0:k1], k0, K, M, 1.0, pw)
             ops, tr = GpuShardOps(), DistTransport() if world > 1 else None
 
@@ -365,6 +421,8 @@ def main():
 
     # ---- read-stream ceiling on the same box (same 16-B nt load path) ----
     src = clients if not scaffold else delta
+    if isinstance(src, list):  # striped: this rank's largest stripe block
+        src = max((p.rows if not scaffold else p.delta for p in src), key=lambda t: t.numel())
     read_ceiling = read_probe(torch, lib, src, stream, device, _native)
 
     # ---- CPU baseline (rank 0, N == 1): the reference call structure timed on host cores ----
@@ -436,7 +494,9 @@ def main():
             line["combine"] = {"mode": args.combine, "step_ms": round(ms_per_step, 5),
                                "block_kernel_ms": round(kern_ms_max, 5),
                                "exchange_and_final_ms": round(max(0.0, ms_per_step - kern_ms_max), 5),
-                               "bit_exact_by_construction": args.combine == "relay"}
+                               "bit_exact_by_construction": args.combine in ("relay", "striped")}
+            if striped:
+                line["combine"]["stripes"] = [{"params": hi - lo, "hop": a} for lo, hi, a in bounds]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -454,7 +514,37 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
     tidx = torch.from_numpy(idx).to(device)
     Kr = k1 - k0
 
+    def cols_striped(parts, field):
+        """Striped relay: every rank holds a different block per stripe; gather each stripe's
+        sampled columns from its holders and assemble [K, S] on the root."""
+        from substrafl_amd.sharding import client_blocks, stripe_layout, stripe_rank
+
+        lay = stripe_layout(M, K, world, rank)
+        per = -(-K // world)
+        sel = [np.nonzero((idx >= lo) & (idx < hi))[0] for lo, hi, *_ in lay]
+        ni = max(1, max(len(x) for x in sel))
+        pad = torch.zeros((len(lay), per, ni), dtype=torch.float64, device=device)
+        for si, ((lo, hi, a, b, k0s, k1s), part) in enumerate(zip(lay, parts)):
+            rows = getattr(part, field)
+            if k1s > k0s and len(sel[si]):
+                loc = torch.from_numpy(idx[sel[si]] - lo).to(device)
+                pad[si, : k1s - k0s, : len(sel[si])] = rows[:, loc].to(torch.float64)
+        got = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad, gather_list=got, dst=0)
+        if rank != 0:
+            return None
+        xs = np.zeros((K, idx.size))
+        blocks = client_blocks(K, world)
+        for si, (lo, hi, a, *_rest) in enumerate(lay):
+            for b, (k0b, k1b) in enumerate(blocks):
+                if k1b > k0b and len(sel[si]):
+                    src = got[stripe_rank(b, world, a)][si, : k1b - k0b, : len(sel[si])].cpu().numpy()
+                    xs[k0b:k1b, sel[si]] = src
+        return xs
+
     def cols(x):  # [Kr, S] sampled columns of this rank's rows, gathered on the root in block order
+        if isinstance(x, tuple):
+            return cols_striped(*x)
         xs = x[:, tidx].to(torch.float64) if Kr else torch.zeros((0, idx.size), dtype=torch.float64, device=device)
         if not (client_shard and world > 1):
             return xs.cpu().numpy()
@@ -471,8 +561,12 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
         return np.concatenate([got[chain_rank(b, world)][: blocks[b][1] - blocks[b][0]].cpu().numpy()
                                for b in range(world)], axis=0)
 
+    def src(name, field):
+        v = env[name]
+        return (v, field) if isinstance(v, list) else v
+
     if not scaffold:
-        xs = cols(env["clients"])
+        xs = cols(src("clients", "rows"))
         if rank != 0 or xs is None:
             return None
         got = env["out"][tidx].cpu().numpy()
@@ -486,7 +580,7 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
             ia, ib = acc.view(np.int32).astype(np.int64), got.view(np.int32).astype(np.int64)
             res["max_ulp"] = int(np.max(np.abs(ia - ib)))
         return res
-    xd, xc = cols(env["delta"]), cols(env["cv"])
+    xd, xc = cols(src("delta", "delta")), cols(src("cv", "cv"))
     if rank != 0 or xd is None:
         return None
     cc = env["c"][tidx].double().cpu().numpy()

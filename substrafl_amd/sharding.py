@@ -25,6 +25,12 @@ Two layouts:
   ``combine="ordered"``: the partials are gathered on the root and added in block order by the
   bucket kernel (weight 1.0 per partial; Scaffold: lr and + c in the same launch).
   Deterministic, same drift class as ``rccl``.
+  ``striped`` (:func:`client_shard_fedavg_striped`, **bit-exact**): the relay, but the bucket is
+  cut into S parameter stripes and stripe s places block b on rank ``a_s * (b + 1) mod G`` for a
+  different unit ``a_s`` of Z_G per stripe.  Every element still passes through blocks 0..G-1
+  in order (the same rounding sequence), every stripe still ends on the root, but stripe s's
+  hops all go ``a_s`` ranks ahead: on a fully connected xGMI node the S stripes' accumulators
+  travel over S disjoint sets of G links at once instead of all over the same G - 1.
 
   The numel == 1 tensors follow NumPy's pairwise order over ALL K products,
   which no block can compute alone: every rank writes its products into its columns of a
@@ -51,7 +57,7 @@ from .layout import BucketLayout
 
 SHARD_ALIGN = 512  # elements (2 KiB of fp32): every shard starts on a 256-B boundary
 RELAY_CHUNK_ELEMS = 2 << 20  # pipelined relay: >= 2M elements (8 MB fp32) per P2P message
-COMBINES = ("relay", "rccl", "ordered")
+COMBINES = ("relay", "rccl", "ordered")  # client_shard_fedavg / _scaffold; "striped": *_striped below
 
 
 def shard_bounds(M: int, world: int, align: int = SHARD_ALIGN) -> List[Tuple[int, int]]:
@@ -605,6 +611,194 @@ def client_shard_scaffold(sh: ScaffoldShard, dout, cout, transport, ops, combine
 
 
 # ======================================================================================
+# striped relay: S parameter stripes, each a relay over its own chain order
+# ======================================================================================
+def _units(G: int) -> List[int]:
+    """The units of Z_G (chain multipliers), alternating 1, G-1, 3, G-3, ... (for G = 8: 1 7 3 5)."""
+    import math
+
+    lo = [a for a in range(1, G) if math.gcd(a, G) == 1] or [1]
+    out, i, j = [], 0, len(lo) - 1
+    while i <= j:
+        out.append(lo[i])
+        if j != i:
+            out.append(lo[j])
+        i, j = i + 1, j - 1
+    return out
+
+
+def stripe_multipliers(G: int, stripes: Optional[int] = None) -> List[int]:
+    """One chain multiplier per stripe (default: as many as Z_G has units, at most 4)."""
+    u = _units(G)
+    n = min(len(u), 4) if stripes is None else max(1, min(int(stripes), len(u)))
+    return u[:n]
+
+
+def stripe_rank(block: int, world: int, a: int) -> int:
+    """Rank holding client block ``block`` in a stripe with multiplier ``a``: ``a * (block + 1) mod
+    G`` (a = 1 is :func:`chain_rank`); the last block is on the root for every unit ``a``."""
+    return (a * (block + 1)) % world
+
+
+def stripe_block(rank: int, world: int, a: int) -> int:
+    """Inverse of :func:`stripe_rank`: the block ``rank`` holds in that stripe."""
+    inv = pow(a, -1, world) if world > 1 else 0
+    return (inv * rank - 1) % world
+
+
+def stripe_layout(M: int, K: int, world: int, rank: int, stripes: Optional[int] = None):
+    """This rank's part of a striped client-sharded reduction: per stripe ``(lo, hi, a, block,
+    k0, k1)`` -- element range, chain multiplier, the client block it holds there and that block's
+    clients."""
+    mult = stripe_multipliers(world, stripes)
+    blocks = client_blocks(K, world)
+    out = []
+    for (lo, hi), a in zip(shard_bounds(M, len(mult)), mult):
+        b = stripe_block(rank, world, a)
+        out.append((lo, hi, a, b) + tuple(blocks[b]))
+    return out
+
+
+def _stripe_neighbours(rank: int, world: int, a: int) -> Tuple[Optional[int], Optional[int]]:
+    b = stripe_block(rank, world, a)
+    prev = stripe_rank(b - 1, world, a) if b > 0 else None
+    nxt = stripe_rank(b + 1, world, a) if b < world - 1 else None
+    return prev, nxt
+
+
+def _run_stripes(jobs: Sequence[Callable[[], None]], device) -> None:
+    """Run the stripes' relays concurrently: one host thread each, each on its own HIP stream
+    (ordered after the caller's stream, and the caller's stream after all of them), so the
+    stripes' P2P traffic (one communicator per stripe) and kernels overlap."""
+    import torch
+
+    if len(jobs) == 1:
+        jobs[0]()
+        return
+    cuda = device is not None and device.type == "cuda"
+    main = torch.cuda.current_stream(device) if cuda else None
+    streams = [torch.cuda.Stream(device) for _ in jobs] if cuda else [None] * len(jobs)
+    err: List[Optional[BaseException]] = [None] * len(jobs)
+
+    def body(i):
+        try:
+            if cuda:
+                torch.cuda.set_device(device)
+                with torch.cuda.stream(streams[i]):
+                    jobs[i]()
+            else:
+                jobs[i]()
+        except BaseException as e:  # noqa: BLE001 -- re-raised on the caller's thread
+            err[i] = e
+
+    if cuda:
+        for st in streams:
+            st.wait_stream(main)
+    th = [threading.Thread(target=body, args=(i,), name=f"stripe-{i}") for i in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if cuda:
+        for st in streams:
+            main.wait_stream(st)
+    for e in err:
+        if e is not None:
+            raise e
+
+
+def client_shard_fedavg_striped(parts: Sequence[FedAvgShard], bounds: Sequence[Tuple[int, int, int]], out,
+                                transports: Sequence, ops, pairwise_idx, ws=None,
+                                chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
+    """Striped relay FedAvg (bit-exact, see the module docstring).  Per stripe s: ``bounds[s] =
+    (lo, hi, a)``, ``parts[s]`` this rank's block for that stripe (``rows`` ``[Kb, hi - lo]``, the
+    block's global weights, ``kbase``, ``K``, ``M = hi - lo``, ``pairwise_idx`` relative to
+    ``lo``), ``transports[s]`` a transport of its own (one communicator per stripe).  The result
+    lands in ``out[:M]`` on the root (rank 0), which this returns True on; ``pairwise_idx``: the
+    global numel == 1 indices (sorted)."""
+    import torch
+
+    tr0 = transports[0]
+    rank, G = tr0.rank, tr0.world
+    kind, K = parts[0].kind, parts[0].K
+    jobs = []
+    for sh, (lo, hi, a), tr in zip(parts, bounds, transports):
+        o = out[lo:hi]
+        if G == 1:
+            jobs.append(lambda sh=sh, o=o: ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, o))
+            continue
+        prev, nxt = _stripe_neighbours(rank, G, a)
+        jobs.append(lambda sh=sh, o=o, tr=tr, prev=prev, nxt=nxt: _relay(
+            tr, relay_chunks(sh.M, chunk_elems), lambda x, y: [o[x:y]],
+            lambda x, y, seed, last: ops.fedavg_chain(sh.kind, sh.rows, sh.w, x, y, seed, o), prev, nxt))
+    _run_stripes(jobs, out.device)
+    P = int(np.asarray(pairwise_idx).size)
+    if P:
+        pw = np.asarray(pairwise_idx, np.int64)
+        if ws is None:
+            ws = torch.zeros((P, K), dtype=ws_dtype(torch, kind), device=out.device)
+        else:
+            ws.zero_()
+        for sh, (lo, hi, a) in zip(parts, bounds):
+            p0, p1 = int(np.searchsorted(pw, lo)), int(np.searchsorted(pw, hi))
+            if p1 > p0:
+                ops.fedavg_products(sh, ws[p0:p1])
+        if G > 1:
+            tr0.reduce_sum(ws, 0)
+        if rank == 0:
+            ops.fedavg_finish(kind, ws, K, pw.astype(np.uint64), out)
+    return rank == 0
+
+
+def client_shard_scaffold_striped(parts: Sequence[ScaffoldShard], bounds: Sequence[Tuple[int, int, int]], dout,
+                                  cout, transports: Sequence, ops, pairwise_idx, c=None, ws=None,
+                                  chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
+    """Striped relay Scaffold (scaffold.py:262-263, 293; bit-exact): per stripe as
+    :func:`client_shard_fedavg_striped`, ``parts[s].c`` the stripe's slice of the server control
+    variate (read by the root, which holds every stripe's last block and applies ``+ c`` and
+    ``lr`` inside its last kernel); ``c``: the whole ``c`` (root, numel == 1 elements only)."""
+    import torch
+
+    tr0 = transports[0]
+    rank, G = tr0.rank, tr0.world
+    K, lr = parts[0].K, parts[0].lr
+    jobs = []
+    for sh, (lo, hi, a), tr in zip(parts, bounds, transports):
+        d, co = dout[lo:hi], cout[lo:hi]
+        if G == 1:
+            jobs.append(lambda sh=sh, d=d, co=co: ops.scaffold_chain(sh, 0, sh.M, True, True, d, co))
+            continue
+        prev, nxt = _stripe_neighbours(rank, G, a)
+        jobs.append(lambda sh=sh, d=d, co=co, tr=tr, prev=prev, nxt=nxt: _relay(
+            tr, relay_chunks(sh.M, chunk_elems), lambda x, y: [d[x:y], co[x:y]],
+            lambda x, y, seed, last: ops.scaffold_chain(sh, x, y, seed, last, d, co), prev, nxt))
+    _run_stripes(jobs, dout.device)
+    P = int(np.asarray(pairwise_idx).size)
+    if P:
+        pw = np.asarray(pairwise_idx, np.int64)
+        n = P * (2 * K + 1)
+        if ws is None:
+            ws = torch.zeros(n, dtype=torch.float64, device=dout.device)
+        else:
+            ws.zero_()
+        wd, wc = ws[: P * K].view(P, K), ws[P * K:].view(P, K + 1)
+        for sh, (lo, hi, a) in zip(parts, bounds):
+            p0, p1 = int(np.searchsorted(pw, lo)), int(np.searchsorted(pw, hi))
+            if p1 > p0 and sh.Kr:
+                tmp = torch.zeros((p1 - p0) * (2 * K + 1), dtype=torch.float64, device=dout.device)
+                ops.scaffold_products(sh, tmp)
+                wd[p0:p1] += tmp[: (p1 - p0) * K].view(p1 - p0, K)
+                wc[p0:p1] += tmp[(p1 - p0) * K:].view(p1 - p0, K + 1)
+        if G > 1:
+            tr0.reduce_sum(ws, 0)
+        if rank == 0:
+            glob = ScaffoldShard(parts[0].kind, None, None, c, np.zeros(0), 0, K, int(dout.shape[0]), lr,
+                                 pw.astype(np.uint64))
+            ops.scaffold_finish(glob, ws, dout, cout)
+    return rank == 0
+
+
+# ======================================================================================
 # host entry points (every rank reads the same K host shared states, stages its block)
 # ======================================================================================
 def _rank_device(torch):
@@ -622,51 +816,101 @@ def _one_dtype(lists, what: str) -> np.dtype:
     return np.dtype(next(iter(dts)))
 
 
-def _stage_block(torch, device, rows: List[List[np.ndarray]], layout: BucketLayout, dtype):
+def _stage_block(torch, device, rows: List[List[np.ndarray]], layout: BucketLayout, dtype,
+                 lo: int = 0, hi: Optional[int] = None):
     """The rows of this rank's clients, staged through the native session's pinned ring into a
     ``[Kr, ld]`` device tensor of ``dtype`` (no host-side packing; stream-ordered before torch's
     work).  Rows of another float dtype are staged raw and widened exactly on the device
-    (``fedagg_cast``: Scaffold's fp32 deltas beside fp64 control variates from round 2 on)."""
+    (``fedagg_cast``: Scaffold's fp32 deltas beside fp64 control variates from round 2 on).
+    ``lo``/``hi``: only elements ``[lo, hi)`` of every row (a parameter stripe), into a
+    ``[Kr, hi - lo]`` view of 64-element-padded rows."""
     from . import runtime
     from .engine import torch_dtype
 
-    t = torch.empty((max(1, len(rows)), layout.ld), dtype=dtype, device=device)
-    if rows:
+    full = hi is None
+    hi = layout.M if full else hi
+    n = hi - lo
+    ld = layout.ld if full else max(64, -(-n // 64) * 64)
+    t = torch.empty((max(1, len(rows)), ld), dtype=dtype, device=device)
+    if rows and n > 0:
         s = runtime.session(device.index)
         src = {a.dtype for r in rows for a in r}
         arrays = [[np.ascontiguousarray(a) for a in r] for r in rows]
-        if len(src) == 1 and torch_dtype(next(iter(src))) != dtype:
-            (sdt,) = src
-            raw = torch.empty((len(rows), layout.ld), dtype=torch_dtype(sdt), device=device)
-            s.stage(raw.data_ptr(), layout.ld * raw.element_size(), arrays)
-            s.cast(raw.data_ptr(), sdt, t.data_ptr(), np.dtype(str(dtype).replace("torch.", "")),
-                   len(rows) * layout.ld)
+        sdt = next(iter(src))
+        rng = None if full else (lo * np.dtype(sdt).itemsize, hi * np.dtype(sdt).itemsize)
+        if len(src) == 1 and torch_dtype(sdt) != dtype:
+            raw = torch.empty((len(rows), ld), dtype=torch_dtype(sdt), device=device)
+            s.stage(raw.data_ptr(), ld * raw.element_size(), arrays, byte_range=rng)
+            s.cast(raw.data_ptr(), sdt, t.data_ptr(), np.dtype(str(dtype).replace("torch.", "")), len(rows) * ld)
             s.sync()
             del raw
         else:
-            s.stage(t.data_ptr(), layout.ld * t.element_size(), arrays)
+            s.stage(t.data_ptr(), ld * t.element_size(), arrays, byte_range=rng)
             s.sync()
-    return t[: len(rows)]
+    return t[: len(rows)] if full else t[: len(rows), :n]
+
+
+_STRIPE_GROUPS: Dict[tuple, list] = {}
+
+
+def _stripe_transports(transport, group, stripes: Optional[int], transports):
+    """One transport per stripe of the striped relay: given, or one new process group each (every
+    rank creates them in the same order)."""
+    import torch.distributed as dist
+
+    if transports is not None:
+        return list(transports)
+    tr = transport or DistTransport(group)
+    S = len(stripe_multipliers(tr.world, stripes))
+    if tr.world == 1:
+        return [tr] * S
+    key = (None if group is None else tuple(dist.get_process_group_ranks(group)), S)
+    if key not in _STRIPE_GROUPS:  # communicators are set up once per process, not per aggregation
+        ranks = None if group is None else list(key[0])
+        _STRIPE_GROUPS[key] = [dist.new_group(ranks=ranks) for _ in range(S - 1)]
+    return [tr] + [DistTransport(g) for g in _STRIPE_GROUPS[key]]
 
 
 def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int], group=None,
-                          combine: str = "relay", transport=None):
+                          combine: str = "relay", transport=None, stripes: Optional[int] = None, transports=None):
     """FedAvg (fed_avg.py:217-222) with the clients sharded over the process group: rank r stages
     only its block's buckets (to its own GPU), the chain / reduce runs over RCCL and the root
     (rank 0) returns the averaged layers; other ranks return None.  Layers must share one float
-    dtype.  ``combine="relay"`` is bit-identical to the reference."""
+    dtype.  ``combine="relay"`` and ``"striped"`` are bit-identical to the reference
+    (``striped``: ``stripes`` parameter stripes, one process group each, see the module
+    docstring)."""
     import torch
 
     from .engine import fedavg_weights, kind_of, torch_dtype
 
-    tr = transport or DistTransport(group)
+    if combine == "striped":
+        trs = _stripe_transports(transport, group, stripes, transports)
+        tr = trs[0]
+    else:
+        tr = transport or DistTransport(group)
     G, rank = tr.world, tr.rank
     K, L = len(parameters_updates), len(parameters_updates[0])
     dtype = _one_dtype(parameters_updates, "FedAvg")
     kind = kind_of(dtype)
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], dtype)
-    k0, k1 = client_blocks(K, G)[block_of(rank, G)]
     dev = _rank_device(torch)
+    if combine == "striped":
+        w_all = fedavg_weights(n_samples, kind)
+        pw = layout.pairwise_idx.astype(np.int64)
+        lay = stripe_layout(layout.M, K, G, rank, len(trs))
+        parts = []
+        for lo, hi, a, b, k0, k1 in lay:
+            rows = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout,
+                                torch_dtype(kind), lo, hi)
+            parts.append(FedAvgShard(kind, rows, w_all[k0:k1], k0, K, hi - lo,
+                                     (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)))
+        out = torch.empty(layout.ld, dtype=out_dtype(torch, kind), device=dev)
+        if not client_shard_fedavg_striped(parts, [(lo, hi, a) for lo, hi, a, *_ in lay], out, trs, GpuShardOps(),
+                                           pw):
+            return None
+        flat = out[: layout.M].cpu().numpy()
+        return [a for _, a in layout.unpack(np.array(flat, copy=True))]
+    k0, k1 = client_blocks(K, G)[block_of(rank, G)]
     rows = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, torch_dtype(kind))
     w = fedavg_weights(n_samples, kind)[k0:k1]
     out = torch.empty(layout.ld, dtype=out_dtype(torch, kind), device=dev)
@@ -678,7 +922,8 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
 
 
 def client_sharded_scaffold(parameters_updates, control_variate_updates, server_control_variates, n_samples,
-                            aggregation_lr, group=None, combine: str = "relay", transport=None):
+                            aggregation_lr, group=None, combine: str = "relay", transport=None,
+                            stripes: Optional[int] = None, transports=None):
     """Scaffold (scaffold.py:193-196, 297-337) with the clients sharded over the process group.
     Every rank checks its block's server control variates against client 0's on the host while
     staging (one device copy of ``c``, needed by the root only).  Returns
@@ -689,7 +934,11 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     from . import runtime
     from .engine import scaffold_weights, torch_dtype
 
-    tr = transport or DistTransport(group)
+    if combine == "striped":
+        trs = _stripe_transports(transport, group, stripes, transports)
+        tr = trs[0]
+    else:
+        tr = transport or DistTransport(group)
     G, rank = tr.world, tr.rank
     K, L = len(parameters_updates), len(parameters_updates[0])
     # fp32 buckets when every list is fp32 (NEP 50: the sums are fp64 either way), else fp64 with
@@ -701,9 +950,13 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     sdt = np.dtype(np.float32 if all(d == np.float32 for d in dts) else np.float64)
     kind = "f32" if sdt == np.float32 else "f64"
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], sdt)
-    k0, k1 = client_blocks(K, G)[block_of(rank, G)]
     dev = _rank_device(torch)
     td = torch_dtype(kind)
+    if combine == "striped":
+        return _client_sharded_scaffold_striped(torch, runtime, trs, layout, kind, td, dts[2], dev, parameters_updates,
+                                                control_variate_updates, server_control_variates,
+                                                scaffold_weights(n_samples), float(aggregation_lr))
+    k0, k1 = client_blocks(K, G)[block_of(rank, G)]
     delta = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, td)
     cv = _stage_block(torch, dev, [control_variate_updates[k] for k in range(k0, k1)], layout, td)
     # c: client 0's copy staged once (used by the root), this block's copies checked against it
@@ -718,6 +971,39 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     sh = ScaffoldShard(kind, delta, cv, c, scaffold_weights(n_samples)[k0:k1], k0, K, layout.M,
                        float(aggregation_lr), layout.pairwise_idx)
     if not client_shard_scaffold(sh, dout, cout, tr, GpuShardOps(), combine):
+        return None
+    d = dout[: layout.M].cpu().numpy().copy()
+    cc = cout[: layout.M].cpu().numpy().copy()
+    return mism, [a for _, a in layout.unpack(cc)], [a for _, a in layout.unpack(d)]
+
+
+def _client_sharded_scaffold_striped(torch, runtime, trs, layout, kind, td, c_dtype, dev, pus, cvs, cs, w_all, lr):
+    """client_sharded_scaffold's striped form: per stripe this rank stages its block's delta and
+    control-variate slices, checks the block's server control variates against client 0's on the
+    host over the stripe's bytes, and the root stages c once."""
+    tr = trs[0]
+    G, rank = tr.world, tr.rank
+    K = len(pus)
+    pw = layout.pairwise_idx.astype(np.int64)
+    lay = stripe_layout(layout.M, K, G, rank, len(trs))
+    s = runtime.session(dev.index)
+    isz = np.dtype(c_dtype).itemsize
+    c = _stage_block(torch, dev, [list(cs[0])], layout, td)[0] if rank == 0 else None
+    mism = 0
+    parts = []
+    for lo, hi, a, b, k0, k1 in lay:
+        delta = _stage_block(torch, dev, [pus[k] for k in range(k0, k1)], layout, td, lo, hi)
+        cv = _stage_block(torch, dev, [cvs[k] for k in range(k0, k1)], layout, td, lo, hi)
+        check_rows = [list(cs[0])] + [list(cs[k]) for k in range(k0, k1) if k != 0]
+        if len(check_rows) > 1 and hi > lo:
+            mism += s.stage_check(0, check_rows, c_dtype, byte_range=(lo * isz, hi * isz))
+        parts.append(ScaffoldShard(kind, delta, cv, c[lo:hi] if c is not None else None, w_all[k0:k1], k0, K, hi - lo,
+                                   lr, (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)))
+    mism = tr.all_sum_int(mism)
+    dout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
+    cout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
+    if not client_shard_scaffold_striped(parts, [(lo, hi, a) for lo, hi, a, *_ in lay], dout, cout, trs,
+                                         GpuShardOps(), pw, c=c):
         return None
     d = dout[: layout.M].cpu().numpy().copy()
     cc = cout[: layout.M].cpu().numpy().copy()

@@ -141,3 +141,84 @@ def test_loopback_collectives():
         assert out[r][3] == [float((r - 1) % G)] * 2
     assert out[0][1] == [10.0] * 5 and out[0][2] == [0, 1, 2, 3]
     assert not grp._coll  # every collective's entries consumed
+
+
+def _run_striped(G, S, fn):
+    """G ranks as threads; every rank gets one transport per stripe (one loopback group each)."""
+    groups = [LoopbackGroup(G) for _ in range(S)]
+    return _run(G, lambda r, _tr: fn(r, [g.transport(r) for g in groups]))
+
+
+@settings(max_examples=30, deadline=None)
+@given(st.integers(1, 12), st.integers(1, 8), st.integers(1, 4), shape_st, st.sampled_from([512, 1024]),
+       st.booleans(), st.integers(0, 2**31))
+def test_striped_relay_property(K, G, stripes, shapes, chunk, scaffold, seed):
+    """The striped relay (S parameter stripes, stripe s's chain a_s ranks per hop) reproduces the
+    reference bit for bit for FedAvg and Scaffold, empty stripes and empty blocks included."""
+    from substrafl_amd.sharding import (client_shard_fedavg_striped, client_shard_scaffold_striped, stripe_layout,
+                                        stripe_multipliers)
+
+    shapes = shapes + [(700,)]  # at least two 512-element stripes' worth
+    rng = np.random.default_rng(seed)
+    pus = [[(rng.standard_normal(s) * 10.0 ** rng.integers(-2, 3)).astype(np.float32) for s in shapes] for _ in range(K)]
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    layout = BucketLayout(range(len(shapes)), shapes, np.float32)
+    pw = layout.pairwise_idx.astype(np.int64)
+    S = len(stripe_multipliers(G, stripes))
+
+    def rank(r, trs):
+        lay = stripe_layout(layout.M, K, G, r, stripes)
+        bounds = [(lo, hi, a) for lo, hi, a, *_ in lay]
+        ct = _rows([c], layout, np.float32)[0]
+        parts = []
+        for lo, hi, a, b, k0, k1 in lay:
+            loc = (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)
+            d = _rows(pus[k0:k1], layout, np.float32)[:, lo:hi].contiguous()
+            if not scaffold:
+                parts.append(FedAvgShard("f32", d, fedavg_weights(ns, "f32")[k0:k1], k0, K, hi - lo, loc))
+            else:
+                v = _rows(cvs[k0:k1], layout, np.float32)[:, lo:hi].contiguous()
+                parts.append(ScaffoldShard("f32", d, v, ct[lo:hi], scaffold_weights(ns)[k0:k1], k0, K, hi - lo, 0.6,
+                                           loc))
+        if not scaffold:
+            out = torch.zeros(layout.ld, dtype=torch.float32)
+            if client_shard_fedavg_striped(parts, bounds, out, trs, CpuShardOps(), pw, chunk_elems=chunk):
+                return out[: layout.M].numpy().copy()
+            return None
+        dout = torch.zeros(layout.ld, dtype=torch.float64)
+        cout = torch.zeros(layout.ld, dtype=torch.float64)
+        if client_shard_scaffold_striped(parts, bounds, dout, cout, trs, CpuShardOps(), pw, c=ct, chunk_elems=chunk):
+            return dout[: layout.M].numpy().copy(), cout[: layout.M].numpy().copy()
+        return None
+
+    res = _run_striped(G, S, rank)
+    if not scaffold:
+        for g, r in zip([a for _, a in layout.unpack(res)], fedavg_reference_structure(pus, ns)):
+            assert np.array_equal(g.view(np.uint32), r.view(np.uint32))
+        return
+    lay64 = BucketLayout(range(len(shapes)), shapes, np.float64)
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.6)
+    got = [a for _, a in lay64.unpack(res[1])] + [a for _, a in lay64.unpack(res[0])]
+    for g, r in zip(got, rc + ra):
+        assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+
+
+def test_stripe_chains_cover_disjoint_links():
+    """G = 8: four stripes whose chain hops are 1, 7, 3 and 5 ranks long -- 4 x 7 distinct directed
+    links, every chain ends on the root, and every rank holds exactly one block per stripe."""
+    from substrafl_amd.sharding import stripe_block, stripe_multipliers, stripe_rank
+
+    G = 8
+    mult = stripe_multipliers(G)
+    assert mult == [1, 7, 3, 5]
+    links = set()
+    for a in mult:
+        order = [stripe_rank(b, G, a) for b in range(G)]
+        assert sorted(order) == list(range(G)) and order[-1] == 0
+        assert all(stripe_block(stripe_rank(b, G, a), G, a) == b for b in range(G))
+        hops = {(order[b], order[b + 1]) for b in range(G - 1)}
+        assert not hops & links
+        links |= hops
+    assert len(links) == 4 * (G - 1)

@@ -205,12 +205,13 @@ def _nccl_world1(q, port):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         pus, ns = _data(6, seed=3)
-        out = {"fedavg": {m: client_sharded_fedavg(pus, ns, combine=m) for m in ("relay", "ordered", "rccl")}}
+        out = {"fedavg": {m: client_sharded_fedavg(pus, ns, combine=m) for m in ("relay", "ordered", "rccl", "striped")}}
         rng = np.random.default_rng(2)
         cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
         c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
         cs = [[a.copy() for a in c] for _ in pus]  # separately unpickled copies: checked on the host
         out["scaffold"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5)
+        out["scaffold_striped"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5, combine="striped")
         cs[3][2][17] += 1.0
         out["scaffold_bad"] = client_sharded_scaffold(pus, cvs, cs, ns, 0.5)[0]
         # round 2+ of Scaffold: fp64 control variates and c beside fp32 deltas (widened on the device)
@@ -246,10 +247,11 @@ def test_host_entry_points_nccl_world1():
     cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
     c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
     rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.5)
-    mism, new_c, avg = out["scaffold"]
-    assert mism == 0
-    for g, r in zip(new_c + avg, rc + ra):
-        assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+    for key in ("scaffold", "scaffold_striped"):
+        mism, new_c, avg = out[key]
+        assert mism == 0
+        for g, r in zip(new_c + avg, rc + ra):
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), key
     assert out["scaffold_bad"] == 1
     cvs64 = [[a.astype(np.float64) * 1.1 for a in cv] for cv in cvs]
     c64 = [a.astype(np.float64) / 3 for a in c]
@@ -326,3 +328,83 @@ def test_relay_random_sweep(seed):
         rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
         for g, r in zip([a for _, a in lay64.unpack(cc)] + [a for _, a in lay64.unpack(d)], rc + ra):
             assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
+
+
+# ---- striped relay: S parameter stripes, each a relay over its own chain order ----
+def _striped(G, K, strategy="fedavg", kind="f32", stripes=None, chunk_elems=1024, shapes=SHAPES, seed=4, lr=0.9):
+    import torch
+
+    from substrafl_amd.engine import fedavg_weights, scaffold_weights
+    from substrafl_amd.layout import BucketLayout
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, LoopbackGroup, ScaffoldShard,
+                                        client_shard_fedavg_striped, client_shard_scaffold_striped, out_dtype,
+                                        stripe_layout, stripe_multipliers)
+
+    npdt = {"f32": np.float32, "f64": np.float64, "f16": np.float16}[kind]
+    pus, ns = _data(K, seed=seed, shapes=shapes)
+    pus = [[a.astype(npdt) for a in c] for c in pus]
+    layout = BucketLayout(range(len(shapes)), shapes, npdt)
+    S = len(stripe_multipliers(G, stripes))
+    groups = [LoopbackGroup(G) for _ in range(S)]
+    rng = np.random.default_rng(seed + 1)
+    cvs = [[rng.standard_normal(a.shape).astype(npdt) for a in pu] for pu in pus]
+    c = [rng.standard_normal(a.shape).astype(npdt) for a in pus[0]]
+    pw = layout.pairwise_idx.astype(np.int64)
+
+    def rank_fn(r, _tr):
+        trs = [g.transport(r) for g in groups]
+        lay = stripe_layout(layout.M, K, G, r, stripes)
+        bounds = [(lo, hi, a) for lo, hi, a, *_ in lay]
+        full_c = _rows(torch, [c], layout, dtype=npdt)[0]
+        parts = []
+        for lo, hi, a, b, k0, k1 in lay:
+            loc = (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)
+            d = _rows(torch, pus[k0:k1], layout, dtype=npdt)[:, lo:hi].contiguous()
+            if strategy == "fedavg":
+                parts.append(FedAvgShard(kind, d, fedavg_weights(ns, kind)[k0:k1], k0, K, hi - lo, loc))
+            else:
+                v = _rows(torch, cvs[k0:k1], layout, dtype=npdt)[:, lo:hi].contiguous()
+                parts.append(ScaffoldShard(kind, d, v, full_c[lo:hi], scaffold_weights(ns)[k0:k1], k0, K, hi - lo, lr,
+                                           loc))
+        if strategy == "fedavg":
+            out = torch.zeros(layout.ld, dtype=out_dtype(torch, kind), device="cuda")
+            if client_shard_fedavg_striped(parts, bounds, out, trs, GpuShardOps(), pw, chunk_elems=chunk_elems):
+                torch.cuda.current_stream().synchronize()
+                return out[: layout.M].cpu().numpy().copy()
+            return None
+        dout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+        cout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+        if client_shard_scaffold_striped(parts, bounds, dout, cout, trs, GpuShardOps(), pw, c=full_c,
+                                         chunk_elems=chunk_elems):
+            torch.cuda.current_stream().synchronize()
+            return dout[: layout.M].cpu().numpy().copy(), cout[: layout.M].cpu().numpy().copy()
+        return None
+
+    res = _loopback(G, rank_fn)
+    assert all(x is None for x in res[1:])
+    if strategy == "fedavg":
+        return [a for _, a in layout.unpack(res[0])], fedavg_reference_structure(pus, ns)
+    lay64 = BucketLayout(range(len(shapes)), shapes, np.float64)
+    d, cc = res[0]
+    rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
+    return [a for _, a in lay64.unpack(cc)] + [a for _, a in lay64.unpack(d)], rc + ra
+
+
+@pytest.mark.parametrize("G,K,kind,stripes", [(8, 20, "f32", None), (4, 9, "f32", 2), (3, 2, "f64", None),
+                                              (2, 5, "f16", None), (8, 7, "f32", 3), (1, 4, "f32", None)])
+def test_striped_relay_fedavg_bit_exact(G, K, kind, stripes):
+    """Every stripe's chain visits the blocks in client order, so each element keeps the
+    reference's rounding sequence; K < G leaves empty blocks in every stripe."""
+    shapes = SHAPES + [(5000,), (1,)]
+    got, ref = _striped(G, K, kind=kind, stripes=stripes, shapes=shapes)
+    bits = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+    for g, r in zip(got, ref):
+        assert g.dtype == r.dtype and np.array_equal(g.view(bits[g.itemsize]), r.view(bits[r.itemsize]))
+
+
+@pytest.mark.parametrize("G,K,kind", [(8, 17, "f32"), (4, 3, "f64"), (2, 6, "f32")])
+def test_striped_relay_scaffold_bit_exact(G, K, kind):
+    shapes = SHAPES + [(5000,), (1,)]
+    got, ref = _striped(G, K, strategy="scaffold", kind=kind, shapes=shapes)
+    for g, r in zip(got, ref):
+        assert g.dtype == np.float64 and np.array_equal(g.view(np.uint64), r.view(np.uint64))

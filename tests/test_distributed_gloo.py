@@ -60,6 +60,8 @@ def _client_shard_cpu(rank, world, mode, K, strategy, chunk_elems):
     """This rank's block of the client-sharded FedAvg / Scaffold over gloo with the NumPy ops."""
     pus, ns = _data(K=K)
     layout = BucketLayout(range(len(pus[0])), [a.shape for a in pus[0]], np.float32)
+    if mode == "striped":
+        return _client_shard_striped_cpu(rank, world, K, strategy, chunk_elems, pus, ns, layout)
     k0, k1 = client_blocks(K, world)[block_of(rank, world)]
     tr = DistTransport()
     if strategy == "fedavg":
@@ -79,6 +81,44 @@ def _client_shard_cpu(rank, world, mode, K, strategy, chunk_elems):
     cout = torch.zeros(layout.ld, dtype=torch.float64)
     root = client_shard_scaffold(sh, dout, cout, tr, CpuShardOps(), combine=mode, chunk_elems=chunk_elems)
     if not root:
+        return None
+    lay64 = BucketLayout(range(len(pus[0])), [a.shape for a in pus[0]], np.float64)
+    return ([a for _, a in lay64.unpack(cout[: layout.M].numpy().copy())]
+            + [a for _, a in lay64.unpack(dout[: layout.M].numpy().copy())])
+
+
+def _client_shard_striped_cpu(rank, world, K, strategy, chunk_elems, pus, ns, layout):
+    """The striped relay over gloo: one process group per stripe, the stripes' relays on their own
+    threads of every rank (the product's thread / communicator structure), NumPy per-rank ops."""
+    from substrafl_amd.sharding import (client_shard_fedavg_striped, client_shard_scaffold_striped, stripe_layout,
+                                        stripe_multipliers)
+
+    S = len(stripe_multipliers(world))
+    trs = [DistTransport()] + [DistTransport(dist.new_group()) for _ in range(S - 1)]
+    lay = stripe_layout(layout.M, K, world, rank)
+    bounds = [(lo, hi, a) for lo, hi, a, *_ in lay]
+    pw = layout.pairwise_idx.astype(np.int64)
+    rng = np.random.default_rng(5)
+    cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+    c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+    ct = torch.from_numpy(_flat_rows([c], layout, np.float32)[0])
+    parts = []
+    for lo, hi, a, b, k0, k1 in lay:
+        loc = (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)
+        d = torch.from_numpy(_flat_rows(pus[k0:k1], layout, np.float32)[:, lo:hi].copy())
+        if strategy == "fedavg":
+            parts.append(FedAvgShard("f32", d, fedavg_weights(ns, "f32")[k0:k1], k0, K, hi - lo, loc))
+        else:
+            v = torch.from_numpy(_flat_rows(cvs[k0:k1], layout, np.float32)[:, lo:hi].copy())
+            parts.append(ScaffoldShard("f32", d, v, ct[lo:hi], scaffold_weights(ns)[k0:k1], k0, K, hi - lo, 0.7, loc))
+    if strategy == "fedavg":
+        out = torch.zeros(layout.ld, dtype=torch.float32)
+        root = client_shard_fedavg_striped(parts, bounds, out, trs, CpuShardOps(), pw, chunk_elems=chunk_elems)
+        return [a for _, a in layout.unpack(out[: layout.M].numpy().copy())] if root else None
+    dout = torch.zeros(layout.ld, dtype=torch.float64)
+    cout = torch.zeros(layout.ld, dtype=torch.float64)
+    if not client_shard_scaffold_striped(parts, bounds, dout, cout, trs, CpuShardOps(), pw, c=ct,
+                                         chunk_elems=chunk_elems):
         return None
     lay64 = BucketLayout(range(len(pus[0])), [a.shape for a in pus[0]], np.float64)
     return ([a for _, a in lay64.unpack(cout[: layout.M].numpy().copy())]
@@ -169,6 +209,27 @@ def test_client_sharded_relay_bit_exact(world, K):
     assert all(out[r] is None for r in range(1, world))
     for g, r in zip(out[0], ref):
         assert g.shape == r.shape and np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+@pytest.mark.parametrize("world,K,strategy", [(2, 5, "fedavg"), (4, 9, "fedavg"), (3, 2, "fedavg"),
+                                              (4, 6, "scaffold"), (2, 3, "scaffold")])
+def test_client_sharded_striped_bit_exact(world, K, strategy):
+    """The striped relay over real gloo process groups (one per stripe, driven from one thread per
+    stripe): bit-identical to the reference, empty blocks included."""
+    pus, ns = _data(K=K)
+    out = _run("striped", world=world, K=K, strategy=strategy)
+    assert all(out[r] is None for r in range(1, world))
+    if strategy == "fedavg":
+        ref = fedavg_reference_structure(pus, ns)
+        bits = np.uint32
+    else:
+        rng = np.random.default_rng(5)
+        cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+        c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+        rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.7)
+        ref, bits = rc + ra, np.uint64
+    for g, r in zip(out[0], ref):
+        assert g.shape == r.shape and np.array_equal(g.view(bits), r.view(bits))
 
 
 @pytest.mark.parametrize("mode", ["ordered", "rccl"])
