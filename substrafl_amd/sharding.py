@@ -335,6 +335,11 @@ class DistTransport:
     def reduce_sum(self, t, root: int) -> None:
         self.dist.reduce(t, dst=self._g(root), op=self.dist.ReduceOp.SUM, group=self.group)
 
+    def reduce_sum_async(self, t, root: int):
+        """As reduce_sum, returning the work: ``wait()`` orders the current stream after it, so
+        the next chunk's kernel overlaps this chunk's reduction."""
+        return self.dist.reduce(t, dst=self._g(root), op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
+
     def gather(self, t, root: int) -> Optional[list]:
         import torch
 
@@ -455,6 +460,10 @@ class _LoopbackTransport:
                 acc.add_(x)
             t.copy_(acc)
 
+    def reduce_sum_async(self, t, root: int):
+        self.reduce_sum(t, root)
+        return _Done()
+
     def gather(self, t, root: int):
         got = self._collect(t, root)
         return None if got is None else [x.clone() for x in got]
@@ -522,6 +531,15 @@ def _relay(transport, chunks, tensors: Callable[[int, int], list], run: Callable
         w.wait()
 
 
+def _reduce_async(transport, t, root):
+    """transport.reduce_sum_async when the transport has it (else the blocking form)."""
+    fn = getattr(transport, "reduce_sum_async", None)
+    if fn is not None:
+        return fn(t, root)
+    transport.reduce_sum(t, root)
+    return _Done()
+
+
 def client_shard_fedavg(sh: FedAvgShard, out, transport, ops, combine: str = "relay", ws=None,
                         chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
     """Client-sharded FedAvg (fed_avg.py:217-222) over ``transport``'s ranks: every rank passes
@@ -547,10 +565,15 @@ def client_shard_fedavg(sh: FedAvgShard, out, transport, ops, combine: str = "re
         _relay(transport, relay_chunks(sh.M, chunk_elems), lambda a, b_: [out[a:b_]],
                lambda a, b_, seed, last: ops.fedavg_chain(sh.kind, sh.rows, sh.w, a, b_, seed, out), prev, nxt)
     else:
-        ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, out)  # this block's partial from +0.0
-        if combine == "rccl":
-            transport.reduce_sum(out[: sh.M], root)
+        if combine == "rccl":  # chunk j's reduction overlaps chunk j + 1's partial
+            works = []
+            for a, b_ in relay_chunks(sh.M, chunk_elems):
+                ops.fedavg_chain(sh.kind, sh.rows, sh.w, a, b_, True, out)  # this block's partial from +0.0
+                works.append(_reduce_async(transport, out[a:b_], root))
+            for w in works:
+                w.wait()
         else:
+            ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, out)  # this block's partial from +0.0
             parts = transport.gather(out[: sh.M].contiguous(), root)
             if rank == root:
                 stack = torch.stack([parts[chain_rank(i, G)] for i in range(G)])  # block order
@@ -589,14 +612,18 @@ def client_shard_scaffold(sh: ScaffoldShard, dout, cout, transport, ops, combine
         _relay(transport, relay_chunks(sh.M, chunk_elems), lambda a, b_: [dout[a:b_], cout[a:b_]],
                lambda a, b_, seed, last: ops.scaffold_chain(sh, a, b_, seed, last, dout, cout), prev, nxt)
     else:
-        ops.scaffold_chain(sh, 0, sh.M, True, False, dout, cout)  # plain fp64 partial sums
-        if combine == "rccl":
-            transport.reduce_sum(dout[: sh.M], root)
-            transport.reduce_sum(cout[: sh.M], root)
+        if combine == "rccl":  # chunk j's reductions overlap chunk j + 1's partial sums
+            works = []
+            for a, b_ in relay_chunks(sh.M, chunk_elems):
+                ops.scaffold_chain(sh, a, b_, True, False, dout, cout)  # plain fp64 partial sums
+                works += [_reduce_async(transport, dout[a:b_], root), _reduce_async(transport, cout[a:b_], root)]
+            for w in works:
+                w.wait()
             if rank == root:  # final step: lr * (0 + 1.0 * sum), 0 + 1.0 * sum + c
                 ops.scaffold_combine(sh, dout[: sh.M].unsqueeze(0).clone(), cout[: sh.M].unsqueeze(0).clone(),
                                      dout, cout)
         else:
+            ops.scaffold_chain(sh, 0, sh.M, True, False, dout, cout)  # plain fp64 partial sums
             dp = transport.gather(dout[: sh.M].contiguous(), root)
             cp = transport.gather(cout[: sh.M].contiguous(), root)
             if rank == root:
