@@ -891,9 +891,10 @@ def _stripe_transports(transport, group, stripes: Optional[int], transports):
     S = len(stripe_multipliers(tr.world, stripes))
     if tr.world == 1:
         return [tr] * S
-    key = (None if group is None else tuple(dist.get_process_group_ranks(group)), S)
+    # keyed by the default group too: a re-initialised process group gets fresh communicators
+    key = (id(dist.group.WORLD), None if group is None else tuple(dist.get_process_group_ranks(group)), S)
     if key not in _STRIPE_GROUPS:  # communicators are set up once per process, not per aggregation
-        ranks = None if group is None else list(key[0])
+        ranks = None if group is None else list(key[1])
         _STRIPE_GROUPS[key] = [dist.new_group(ranks=ranks) for _ in range(S - 1)]
     return [tr] + [DistTransport(g) for g in _STRIPE_GROUPS[key]]
 
