@@ -600,25 +600,29 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
 
 
 def read_probe(torch, lib, src, stream, device, _native) -> float:
-    """Best single-stream 16-B non-temporal read rate over the client buckets (2K..64K grids)."""
-    probe_n = min(src.numel(), 2_000_000_000)
+    """Best single-stream 16-B non-temporal read rate over the client buckets (up to 40 GB of
+    them): the grid-strided probe at 2K..64K workgroups and the full grid, and the tile-walk probe
+    (one workgroup per 4/8/16 x 256 contiguous vectors; tools/hbm_ceiling_probe.hip found it the
+    fastest pattern, 7.1-7.2 TB/s over 32 GiB)."""
+    probe_n = min(src.numel(), 40_000_000_000 // src.element_size())
     if probe_n < 4096:
         return 0.0
     nbytes_probe = probe_n * src.element_size()
     floats = nbytes_probe // 4 // 4 * 4
     full = int(min(floats // 4 // 256, 1 << 20))
     sink = torch.empty(max(1, full), dtype=torch.float32, device=device)
+    ptr, sp, s = src.data_ptr(), sink.data_ptr(), stream.cuda_stream
+    probes = [lambda g=g: lib.fedagg_read_probe_f32(ptr, floats, sp, g, s)
+              for g in sorted({min(g, full) for g in (2048, 4096, 8192, 16384, 65536)} | {full}) if g > 0]
+    probes += [lambda v=v: lib.fedagg_read_probe_tile_f32(ptr, floats, sp, v, s) for v in (4, 8, 16)]
     best = 0.0
-    for pgrid in sorted({min(g, full) for g in (2048, 4096, 8192, 16384, 65536)} | {full}):
-        if pgrid <= 0:
-            continue
+    for probe in probes:
         for _ in range(3):
-            _native.check(lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid,
-                                                    stream.cuda_stream), "probe")
+            _native.check(probe(), "probe")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(10):
-            lib.fedagg_read_probe_f32(src.data_ptr(), floats, sink.data_ptr(), pgrid, stream.cuda_stream)
+            probe()
         e1.record(stream)
         torch.cuda.synchronize(device)
         best = max(best, floats * 4 / (e0.elapsed_time(e1) / 10 / 1e3) / 1e9)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 6
+#define FEDAGG_ABI_VERSION 7
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -264,6 +264,10 @@ int fedagg_scale_cast(const void* d_in, int in_kind, double w, void* d_out, int 
  * ceiling the roofline fraction is also quoted against.
  * -------------------------------------------------------------------------*/
 int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid, void* stream);
+/* The same, in the bucket kernels' tile walk: one workgroup per tile of vpt x 256 contiguous 16-B
+ * vectors (vpt 4, 8 or 16), every load of a thread in flight at once; d_sink needs one float
+ * (written only on an impossible value).  The read ceiling is the best of both probes. */
+int fedagg_read_probe_tile_f32(const float* d_x, uint64_t M, float* d_sink, int vpt, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Host runtime ("session"): one GPU, one HIP stream, grow-only HBM buffers, a pinned

@@ -46,6 +46,7 @@ SIGNATURES = {
     "fedagg_equal_count_f32": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_equal_count_f64": (c_int, [P(c_void), c_int, c_u64, c_void, c_void]),
     "fedagg_read_probe_f32": (c_int, [c_void, c_u64, c_void, c_int, c_void]),
+    "fedagg_read_probe_tile_f32": (c_int, [c_void, c_u64, c_void, c_int, c_void]),
     "fedagg_cast": (c_int, [c_void, c_int, c_void, c_int, c_u64, c_void]),
     "fedagg_flat_gather_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_void]),
     "fedagg_flat_scatter_f32": (c_int, [P(c_void), P(c_u64), c_int, c_void, c_void]),
@@ -102,7 +103,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

@@ -1599,6 +1599,27 @@ __global__ void __launch_bounds__(FA_BLOCK) read_probe_kernel(const float* __res
   if (threadIdx.x == 0) sink[blockIdx.x] = t;
 }
 
+// The bucket kernels' own walk with one stream: one workgroup per tile of VPT x 256 contiguous
+// 16-B vectors, all VPT nt loads issued before use (tools/hbm_ceiling_probe.hip: the fastest
+// read pattern found, 7.1-7.2 TB/s over 32 GiB).  The sink is written only on an impossible fold
+// value, so it needs one float and adds no traffic.
+template <int VPT>
+__global__ void __launch_bounds__(FA_BLOCK) read_probe_tile_kernel(const u32x4* __restrict__ x, uint64_t nvec,
+                                                                   float* __restrict__ sink) {
+  const uint64_t base = (uint64_t)blockIdx.x * VPT * FA_BLOCK + threadIdx.x;
+  unsigned f = 0;
+  if (base + (uint64_t)(VPT - 1) * FA_BLOCK < nvec) {
+    u32x4 r[VPT];
+#pragma unroll
+    for (int n = 0; n < VPT; ++n) r[n] = __builtin_nontemporal_load(x + base + (uint64_t)n * FA_BLOCK);
+#pragma unroll
+    for (int n = 0; n < VPT; ++n) f ^= r[n].x ^ r[n].y ^ r[n].z ^ r[n].w;
+  } else {
+    for (uint64_t v = base; v < nvec; v += FA_BLOCK) f ^= x[v].x ^ x[v].y ^ x[v].z ^ x[v].w;
+  }
+  if (f == 0x9e3779b9u) sink[0] = __uint_as_float(f);
+}
+
 // ------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------
@@ -2528,6 +2549,18 @@ int fedagg_read_probe_f32(const float* d_x, uint64_t M, float* d_sink, int grid,
   if (!d_x || !d_sink || grid <= 0 || !aligned16(d_x)) return fail(FEDAGG_EINVAL, "read_probe: invalid argument");
   hipLaunchKernelGGL(read_probe_kernel, dim3(grid), dim3(FA_BLOCK), 0, (hipStream_t)stream, d_x, M / 4, d_sink);
   return check_launch("read_probe_kernel");
+}
+
+int fedagg_read_probe_tile_f32(const float* d_x, uint64_t M, float* d_sink, int vpt, void* stream) {
+  if (!d_x || !d_sink || !aligned16(d_x) || M < 4 || (vpt != 4 && vpt != 8 && vpt != 16))
+    return fail(FEDAGG_EINVAL, "read_probe_tile: invalid argument");
+  const uint64_t nvec = M / 4, tile = (uint64_t)vpt * FA_BLOCK, grid = (nvec + tile - 1) / tile;
+  if (grid > 0x7fffffffull) return fail(FEDAGG_EINVAL, "read_probe_tile: buffer too large");
+  hipStream_t s = (hipStream_t)stream;
+  if (vpt == 4) hipLaunchKernelGGL(read_probe_tile_kernel<4>, dim3(grid), dim3(FA_BLOCK), 0, s, (const u32x4*)d_x, nvec, d_sink);
+  if (vpt == 8) hipLaunchKernelGGL(read_probe_tile_kernel<8>, dim3(grid), dim3(FA_BLOCK), 0, s, (const u32x4*)d_x, nvec, d_sink);
+  if (vpt == 16) hipLaunchKernelGGL(read_probe_tile_kernel<16>, dim3(grid), dim3(FA_BLOCK), 0, s, (const u32x4*)d_x, nvec, d_sink);
+  return check_launch("read_probe_tile_kernel");
 }
 
 }  // extern "C"

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_invalid_arguments():
     lib = _native.load()
-    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 6
+    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 7
     w = (ctypes.c_float * 1)(1.0)
     ptrs = _native.ptr_array([0])
     assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, 0, None, None, None) == -1  # K == 0
@@ -44,6 +44,10 @@ def test_abi_version_and_invalid_arguments():
     assert lib.fedagg_fedavg_f32(ptrs, w, 1, 16, idx, 1, None, 64, None) == -1  # index out of range
     assert b"out of range" in lib.fedagg_last_error()
     assert lib.fedagg_pairwise_ws_bytes(8, 3, 4) == 2 * 64 * 9 * 8
+    # read-ceiling probes: arguments are checked before any launch
+    assert lib.fedagg_read_probe_tile_f32(None, 4096, None, 4, None) == -1
+    assert lib.fedagg_read_probe_tile_f32(256, 4096, 256, 5, None) == -1  # vpt must be 4, 8 or 16
+    assert b"read_probe_tile" in lib.fedagg_last_error()
     assert lib.fedagg_tune(b"no_such_knob", 1) == -1
     assert lib.fedagg_tune(b"grid_cap", 4096) == 0
     assert lib.fedagg_tune(b"grid_cap", 0) == 0
