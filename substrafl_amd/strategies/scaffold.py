@@ -5,7 +5,8 @@ aggregation hot path.  NumPy 2 (NEP 50) makes the reference compute everything i
 client weights are a float64 array (scaffold.py:319-320) -- and return fp64 arrays; the HIP
 kernel does the same, adds the server control variate ``c`` last (scaffold.py:262-263) and
 applies ``aggregation_lr`` after the sum (scaffold.py:293).  The check that every client sent
-the same ``c`` (scaffold.py:193-196) runs on the GPU too.
+the same ``c`` (scaffold.py:193-196) runs on the host while one copy of ``c`` is staged (the
+engine's ``c_check="device"`` keeps the GPU ``equal_count`` kernel as an option).
 """
 
 from typing import List, Optional
@@ -42,7 +43,7 @@ class Scaffold(Strategy):
 
     def _check_shared_states(self, shared_states: List[ScaffoldSharedState]) -> None:
         """Host-decidable half of scaffold.py:168-202 (types, list lengths, shapes of ``c``);
-        the element-wise ``c`` equality runs on the GPU (``equal_count`` kernel)."""
+        the element-wise ``c`` equality is counted by the engine while it stages ``c``."""
         assert shared_states, "shared_states should contain at least one element"
         assert isinstance(shared_states, (list, tuple)), "shared_states should be a list"
         first = shared_states[0]

@@ -1,8 +1,8 @@
 #!/bin/bash
 # One profiling session per workload, on the GPU box (DESIGN.md §5 evidence):
-#   1. the bench line itself;
-#   2. rocprofv3 --kernel-trace --stats of the same bench command (kernel average duration);
-#   3. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) -> HBM bytes per launch (tools/pmc_traffic.py).
+#   1. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) -> HBM bytes per launch (tools/pmc_traffic.py);
+#   2. the bench line itself, whose roofline.traffic is that file (same build, same session);
+#   3. rocprofv3 --kernel-trace --stats of the same bench command (kernel average duration).
 # Usage: tools/profile_round.sh TAG WORKLOAD [WORKLOAD ...]   (outputs under gpurun_out/TAG_*)
 set -euo pipefail
 TAG=$1; shift
@@ -21,15 +21,6 @@ print(_native.load().fedagg_scaffold_launches(16, 4, 25000000, 1))") ;;
     c5) KERN=fedavg_kernel; ALG=91000000000; STEPS=30; GROUP=1 ;;
     *) echo "unknown workload $WL"; exit 2 ;;
   esac
-  echo "[$TAG] $WL: bench" >&2
-  timeout -k 10 400 python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 > "$OUT/${TAG}_bench_${WL}.json"
-  echo "[$TAG] $WL: kernel trace" >&2
-  rm -rf "$OUT/${TAG}_prof_${WL}"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_${WL}" -o run -- \
-    python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 --no-cpu-baseline \
-    > "$OUT/${TAG}_profiled_bench_${WL}.json"
-  STATS=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_stats.csv' | head -1)
-  cp "$STATS" "$OUT/${TAG}_${WL}_kernel_stats.csv"
   for C in FETCH_SIZE WRITE_SIZE; do
     echo "[$TAG] $WL: pmc $C" >&2
     rm -rf "$OUT/${TAG}_pmc_${C}_${WL}"
@@ -41,5 +32,16 @@ print(_native.load().fedagg_scaffold_launches(16, 4, 25000000, 1))") ;;
     --write "$OUT/${TAG}_${WL}_pmc_WRITE_SIZE.csv" --kernel $KERN --group $GROUP --bytes-alg $ALG \
     --lib "$ROOT/substrafl_amd/libfedagg.so" --collected "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, session $TAG" \
     --out "$OUT/${TAG}_traffic_${WL}.json" > /dev/null
+  # the bench line of this session carries the traffic just measured on this very build
+  echo "[$TAG] $WL: bench" >&2
+  timeout -k 10 400 python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 \
+    --traffic "$OUT/${TAG}_traffic_${WL}.json" > "$OUT/${TAG}_bench_${WL}.json"
+  echo "[$TAG] $WL: kernel trace" >&2
+  rm -rf "$OUT/${TAG}_prof_${WL}"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_${WL}" -o run -- \
+    python3 "$ROOT/bench.py" --workload "$WL" --steps $STEPS --warmup 10 --no-cpu-baseline \
+    --traffic "$OUT/${TAG}_traffic_${WL}.json" > "$OUT/${TAG}_profiled_bench_${WL}.json"
+  STATS=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_stats.csv' | head -1)
+  cp "$STATS" "$OUT/${TAG}_${WL}_kernel_stats.csv"
 done
 echo "[$TAG] done" >&2
