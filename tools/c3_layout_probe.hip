@@ -20,9 +20,7 @@
   } while (0)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int K = 64;
-
-template <bool INTER, bool WRITE, int VPT, int BLK, int U>
+template <int K, bool INTER, bool WRITE, int VPT, int BLK, int U>
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(BLK >= 512 ? 2 : 1)))
 fa(const f32x4* __restrict__ x, const float* __restrict__ w, uint64_t nvec, f32x4* __restrict__ out) {
 #pragma clang fp contract(off)
@@ -58,19 +56,19 @@ fa(const f32x4* __restrict__ x, const float* __restrict__ w, uint64_t nvec, f32x
   }
 }
 
-template <bool INTER, bool WRITE, int VPT, int BLK, int U>
+template <int K, bool INTER, bool WRITE, int VPT, int BLK, int U>
 void run(const char* name, const f32x4* x, const float* w, uint64_t nvec, f32x4* out) {
   const unsigned grid = (unsigned)(nvec / ((uint64_t)VPT * BLK));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((fa<INTER, WRITE, VPT, BLK, U>), dim3(grid), dim3(BLK), 0, 0, x, w, nvec, out);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((fa<K, INTER, WRITE, VPT, BLK, U>), dim3(grid), dim3(BLK), 0, 0, x, w, nvec, out);
   CK(hipDeviceSynchronize());
   float best = 1e30f, tot = 0.f;
   const int reps = 10;
   for (int i = 0; i < reps; ++i) {
     CK(hipEventRecord(a));
-    hipLaunchKernelGGL((fa<INTER, WRITE, VPT, BLK, U>), dim3(grid), dim3(BLK), 0, 0, x, w, nvec, out);
+    hipLaunchKernelGGL((fa<K, INTER, WRITE, VPT, BLK, U>), dim3(grid), dim3(BLK), 0, 0, x, w, nvec, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -80,14 +78,15 @@ void run(const char* name, const f32x4* x, const float* w, uint64_t nvec, f32x4*
   }
   CK(hipGetLastError());
   const double bytes = (double)grid * VPT * BLK * 16.0 * (K + (WRITE ? 1 : 0));
-  printf("{\"pattern\": \"%s\", \"vpt\": %d, \"block\": %d, \"u\": %d, \"write\": %d, \"us_best\": %.1f, \"us_mean\": %.1f, "
+  printf("{\"K\": %d, \"pattern\": \"%s\", \"vpt\": %d, \"block\": %d, \"u\": %d, \"write\": %d, \"us_best\": %.1f, \"us_mean\": %.1f, "
          "\"GBps_best\": %.1f}\n",
-         name, VPT, BLK, U, (int)WRITE, best * 1e3, tot / reps * 1e3, bytes / (best * 1e-3) / 1e9);
+         K, name, VPT, BLK, U, (int)WRITE, best * 1e3, tot / reps * 1e3, bytes / (best * 1e-3) / 1e9);
   fflush(stdout);
 }
 
-int main() {
-  const uint64_t M = 125000000ull / (16 * 512 * 4) * (16 * 512 * 4);  // whole tiles of every shape
+template <int K>
+void sweep(uint64_t m_req, bool full) {
+  const uint64_t M = m_req / (16 * 512 * 4) * (16 * 512 * 4);  // whole tiles of every shape
   const uint64_t nvec = M / 4;
   f32x4 *x, *out;
   float* w;
@@ -99,17 +98,26 @@ int main() {
   for (int k = 0; k < K; ++k) hw[k] = 1.0f / K;
   CK(hipMemcpy(w, hw, sizeof hw, hipMemcpyHostToDevice));
   for (int rep = 0; rep < 2; ++rep) {
-    run<false, true, 16, 512, 2>("rows", x, w, nvec, out);
-    run<true, true, 16, 512, 2>("interleaved", x, w, nvec, out);
-    run<false, false, 16, 512, 2>("rows", x, w, nvec, out);
-    run<true, false, 16, 512, 2>("interleaved", x, w, nvec, out);
-    run<false, true, 8, 256, 4>("rows", x, w, nvec, out);
-    run<true, true, 8, 256, 4>("interleaved", x, w, nvec, out);
-    run<false, true, 4, 256, 4>("rows", x, w, nvec, out);
-    run<true, true, 4, 256, 4>("interleaved", x, w, nvec, out);
+    run<K, false, true, 16, 512, 2>("rows", x, w, nvec, out);
+    run<K, true, true, 16, 512, 2>("interleaved", x, w, nvec, out);
+    run<K, false, false, 16, 512, 2>("rows", x, w, nvec, out);
+    if (!full) continue;
+    run<K, true, false, 16, 512, 2>("interleaved", x, w, nvec, out);
+    run<K, false, true, 8, 256, 4>("rows", x, w, nvec, out);
+    run<K, true, true, 8, 256, 4>("interleaved", x, w, nvec, out);
+    run<K, false, true, 4, 256, 4>("rows", x, w, nvec, out);
+    run<K, true, true, 4, 256, 4>("interleaved", x, w, nvec, out);
   }
   CK(hipFree(x));
   CK(hipFree(out));
   CK(hipFree(w));
+}
+
+// no argument: the C3 shape (64 x 125M, every tile); "c5": 64 x 125M and 128 x 175M fp32 (the C5
+// footprint, 89.6 GB, with C5's 128 client streams) side by side
+int main(int argc, char** argv) {
+  const bool c5 = argc > 1 && argv[1][0] == 'c' && argv[1][1] == '5';
+  sweep<64>(125000000ull, !c5);
+  if (c5) sweep<128>(175000000ull, false);
   return 0;
 }
