@@ -21,7 +21,7 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int K, bool INTER, bool WRITE, int VPT, int BLK, int U>
-__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(BLK >= 512 ? 2 : 1)))
+__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(BLK >= 512 && VPT * U <= 32 ? 2 : 1)))
 fa(const f32x4* __restrict__ x, const float* __restrict__ w, uint64_t nvec, f32x4* __restrict__ out) {
 #pragma clang fp contract(off)
   constexpr uint64_t T = (uint64_t)VPT * BLK;
@@ -113,10 +113,43 @@ void sweep(uint64_t m_req, bool full) {
   CK(hipFree(w));
 }
 
+// 128 x 175M fp32 rows (C5's streams and footprint): bytes per stream per workgroup step
+template <int K>
+void tiles(uint64_t m_req) {
+  const uint64_t M = m_req / (32 * 1024 * 4) * (32 * 1024 * 4);
+  const uint64_t nvec = M / 4;
+  f32x4 *x, *out;
+  float* w;
+  CK(hipMalloc(&x, (uint64_t)K * M * 4));
+  CK(hipMalloc(&out, M * 4));
+  CK(hipMalloc(&w, K * 4));
+  CK(hipMemset(x, 0, (uint64_t)K * M * 4));
+  float hw[K];
+  for (int k = 0; k < K; ++k) hw[k] = 1.0f / K;
+  CK(hipMemcpy(w, hw, sizeof hw, hipMemcpyHostToDevice));
+  for (int rep = 0; rep < 2; ++rep) {
+    run<K, false, true, 16, 512, 2>("rows 128K/stream", x, w, nvec, out);
+    run<K, false, true, 32, 512, 1>("rows 256K/stream", x, w, nvec, out);
+    run<K, false, true, 16, 1024, 1>("rows 256K/stream", x, w, nvec, out);
+    run<K, false, true, 8, 1024, 2>("rows 128K/stream", x, w, nvec, out);
+    run<K, false, true, 32, 256, 1>("rows 128K/stream", x, w, nvec, out);
+    run<K, false, true, 8, 256, 4>("rows 32K/stream", x, w, nvec, out);
+    run<K, false, true, 4, 256, 8>("rows 16K/stream", x, w, nvec, out);
+  }
+  CK(hipFree(x));
+  CK(hipFree(out));
+  CK(hipFree(w));
+}
+
 // no argument: the C3 shape (64 x 125M, every tile); "c5": 64 x 125M and 128 x 175M fp32 (the C5
-// footprint, 89.6 GB, with C5's 128 client streams) side by side
+// footprint, 89.6 GB, with C5's 128 client streams) side by side; "tiles": tile shapes at 128 x 175M
 int main(int argc, char** argv) {
-  const bool c5 = argc > 1 && argv[1][0] == 'c' && argv[1][1] == '5';
+  const char* mode = argc > 1 ? argv[1] : "";
+  if (mode[0] == 't') {
+    tiles<128>(175000000ull);
+    return 0;
+  }
+  const bool c5 = mode[0] == 'c' && mode[1] == '5';
   sweep<64>(125000000ull, !c5);
   if (c5) sweep<128>(175000000ull, false);
   return 0;
