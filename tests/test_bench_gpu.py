@@ -37,6 +37,8 @@ def test_default_line_fields():
     assert roof["bound"] == "hbm" and roof["peak"] == 8000.0 and 0 < roof["frac"] < 1
     assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
     assert roof["traffic_source"] is None or "same_build" in roof["traffic_source"]
+    # best of the grid-strided and tile-walk read probes over the same buffer
+    assert roof["read_stream_ceiling_GBps"] > 1000 and 0.5 < roof["frac_of_read_ceiling"] < 1.1
     assert line["cpu_baseline"]["cores"] == 1 and line["cpu_baseline"]["kind"] == "port"
     assert line["parity"]["mismatches"] == 0
 
