@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered", "striped"])
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
+    ap.add_argument("--layout", default="rows", choices=["rows", "tiles", "auto"],
+                    help="client buckets in HBM: [K, ld] rows, tile-interleaved (fedagg_fedavg_tiled_*; "
+                         "FedAvg fp32/bf16), or tiles where the library recommends them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--grid-cap", type=int, default=0)
@@ -137,6 +140,25 @@ def synth_clients(torch, K, ld, M, kind, device, seed0):
             buf[k, :M].normal_(generator=g)
         buf[k, M:].zero_()
     return buf[:K]
+
+
+def synth_tiled(torch, K, M, kind, device, seed0):
+    """The same client buckets as synth_clients (client k: Philox seed seed0 + k), laid out
+    tile-interleaved (engine.tiled_client_view): tile t of client k is tile t * K + k."""
+    from substrafl_amd.engine import tiled_client_view, tiled_elems
+
+    dt = torch.bfloat16 if kind == "bf16" else torch.float32
+    buf = torch.zeros(tiled_elems(kind, K, M), dtype=dt, device=device)
+    g = torch.Generator(device=device)
+    row = None
+    for k in range(K):
+        view = tiled_client_view(buf, kind, K, k)
+        if row is None:
+            row = torch.zeros(view.numel(), dtype=torch.float32, device=device)
+        g.manual_seed(seed0 + k)
+        row[:M].normal_(generator=g)
+        view.copy_(row.view(view.shape))
+    return buf
 
 
 def lib_sha256() -> str:
@@ -281,11 +303,25 @@ def main():
             dist.barrier()
 
     stream = torch.cuda.current_stream(device)
+    from substrafl_amd.engine import TiledFedAvgPlan, tiled_recommended
+
+    tiled = (not scaffold and not client_shard and kind in ("f32", "bf16")
+             and (args.layout == "tiles" or (args.layout == "auto" and tiled_recommended(kind, K, M))))
+    if args.layout == "tiles" and not tiled:
+        print("bench.py: --layout tiles takes the FedAvg fp32/bf16 workloads in param-range mode", file=sys.stderr)
+        sys.exit(2)
     if not scaffold:
-        clients = synth_clients(torch, Kr, ld, M, kind, device, seed0)
+        clients = synth_tiled(torch, K, M, kind, device, seed0) if tiled else \
+            synth_clients(torch, Kr, ld, M, kind, device, seed0)
         out = torch.empty(ld, dtype=torch.float32, device=device)
         w_all = fedavg_weights(n_samples, kind)
-        if striped:
+        if tiled:
+            plan = TiledFedAvgPlan(kind, clients, K, w_all, M, out, pw)
+            kplan = plan
+
+            def step():
+                plan.launch(stream)
+        elif striped:
             del clients
             parts = [FedAvgShard(kind, stripe_rows(si, lo, hi, k0s, k1s), w_all[k0s:k1s], k0s, K, hi - lo,
                                  local_pw(lo, hi)) for si, (lo, hi, a, b, k0s, k1s) in enumerate(stripes)]
@@ -465,6 +501,7 @@ def main():
                 "global_params": M_glob if (client_shard or args.scaling == "strong") else M * world,
                 "layers": len(shapes),
                 "parallelism": parallelism,
+                "layout": "tile-interleaved" if tiled else "rows",
                 "bytes_alg_per_step_job": bytes_job,
                 "bytes_alg_per_launch_rank0": bytes_kernel,
             },
@@ -545,6 +582,11 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
     def cols(x):  # [Kr, S] sampled columns of this rank's rows, gathered on the root in block order
         if isinstance(x, tuple):
             return cols_striped(*x)
+        if env.get("tiled"):  # tile-interleaved buffer: gather each client's sampled elements
+            from substrafl_amd.engine import tiled_index
+
+            pos = tiled_index(kind, K, np.arange(K)[:, None], idx[None, :])
+            return x[torch.from_numpy(pos.reshape(-1)).to(device)].view(K, -1).to(torch.float64).cpu().numpy()
         xs = x[:, tidx].to(torch.float64) if Kr else torch.zeros((0, idx.size), dtype=torch.float64, device=device)
         if not (client_shard and world > 1):
             return xs.cpu().numpy()

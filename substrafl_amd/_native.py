@@ -32,6 +32,12 @@ SIGNATURES = {
     "fedagg_pairwise_ws_bytes": (c_size, [c_int, c_int, c_int]),
     "fedagg_fedavg_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
     "fedagg_fedavg_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
+    "fedagg_fedavg_tile_vectors_f32": (c_u64, [c_int, c_u64]),
+    "fedagg_fedavg_tile_vectors_bf16": (c_u64, [c_int, c_u64]),
+    "fedagg_fedavg_tiled_f32": (c_int, [c_void, P(ctypes.c_float), c_int, c_u64, c_u64, P(c_u64), c_int, c_void, c_void,
+                                        c_void]),
+    "fedagg_fedavg_tiled_bf16": (c_int, [c_void, P(ctypes.c_float), c_int, c_u64, c_u64, P(c_u64), c_int, c_void,
+                                         c_void, c_void]),
     "fedagg_fedavg_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
     "fedagg_fedavg_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
     "fedagg_scaffold_launches": (c_int, [c_int, c_int, c_u64, c_int]),
@@ -103,10 +109,12 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
+FEDAGG_TILE_VECTORS_F32 = 8192
+FEDAGG_TILE_VECTORS_BF16 = 4096
 FEDAGG_MAX_PAIRWISE = 64
 FEDAGG_FLAT_MAX_LISTS = 4
 FEDAGG_SESSION_BUFFERS = 16

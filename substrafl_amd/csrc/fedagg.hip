@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "fedagg.h"
 
@@ -350,7 +351,24 @@ __device__ T pw_sum(const G& get, int64_t n) {
   }
 }
 
-// Fused numel==1 patch: +0.0 + pairwise over the K products of element e.
+// Tile-interleaved client buckets (fedagg_fedavg_tiled_*): the K clients' tiles of TV 16-B
+// vectors alternate in HBM -- tile t of client k at vector (t * K + k) * TV -- so a workgroup
+// reads ONE contiguous K x TV region per step instead of K regions a row apart.  With the
+// per-client base base_k = base + k * TV, client k's vector v is at (v / TV) * pitch + v % TV of
+// base_k, pitch = K * TV.  TV = 0: the [K, ld] row layout (identity).
+template <int TV>
+__device__ __forceinline__ uint64_t in_vec(uint64_t v, uint64_t pitch) {
+  if constexpr (TV == 0) return v;
+  else return (v / TV) * pitch + v % TV;
+}
+template <int TV, int L>
+__device__ __forceinline__ uint64_t in_elem(uint64_t e, uint64_t pitch) {
+  if constexpr (TV == 0) return e;
+  else return in_vec<TV>(e / L, pitch) * L + e % L;
+}
+
+// Fused numel==1 patch: +0.0 + pairwise over the K products of element e (e: the element's
+// index in the client's bucket storage, see in_elem).
 template <typename E, int KC>
 __device__ __forceinline__ typename E::P fedavg_pairwise_elem(const FaArgs<E, KC>& a, int K, uint64_t e) {
 #pragma clang fp contract(off)
@@ -438,12 +456,13 @@ __device__ __forceinline__ void fedavg_load_group(const FaArgs<E, KC>& a, int k,
   }
 }
 
-// acc[n][:] = sum over the K clients (in order) for the N 16-byte vectors v[n].
+// acc[n][:] = sum over the K clients (in order) for the N 16-byte vectors v[n] (output
+// indices; vin[n]: where those vectors sit in the client buckets, == v[n] in the row layout).
 // PIPE: the loads of client group g+1 are issued before the adds of group g (two register
 // buffers), so a wave keeps 2*U*N loads in flight across the add chain.
 template <typename E, int KC, bool NT, int N, int U, bool PIPE, bool BUF = false>
 __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int K, const int first,
-                                               const uint64_t* v, typename E::P (*acc)[E::L],
+                                               const uint64_t* v, const uint64_t* vin, typename E::P (*acc)[E::L],
                                                const typename E::Out* out, const uint64_t tb = 0) {
 #pragma clang fp contract(off)
   using P = typename E::P;
@@ -461,15 +480,15 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
   if constexpr (PIPE) {
     if (K >= U) {
       u32x4 ra[N][U], rb[N][U];
-      fedavg_load_group<E, KC, NT, N, U>(a, 0, v, ra);
+      fedavg_load_group<E, KC, NT, N, U>(a, 0, vin, ra);
       for (;;) {
         const bool mb = k + 2 * U <= K;
-        if (mb) fedavg_load_group<E, KC, NT, N, U>(a, k + U, v, rb);
+        if (mb) fedavg_load_group<E, KC, NT, N, U>(a, k + U, vin, rb);
         fedavg_accumulate<E, N, U>(ra, a.w + k, acc);
         k += U;
         if (!mb) break;
         const bool ma = k + 2 * U <= K;
-        if (ma) fedavg_load_group<E, KC, NT, N, U>(a, k + U, v, ra);
+        if (ma) fedavg_load_group<E, KC, NT, N, U>(a, k + U, vin, ra);
         fedavg_accumulate<E, N, U>(rb, a.w + k, acc);
         k += U;
         if (!ma) break;
@@ -478,7 +497,7 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
   } else {
     for (; k + U <= K; k += U) {
       u32x4 raw[N][U];
-      fedavg_load_group<E, KC, NT, N, U, BUF>(a, k, v, raw, tb);
+      fedavg_load_group<E, KC, NT, N, U, BUF>(a, k, vin, raw, tb);
       fedavg_accumulate<E, N, U>(raw, a.w + k, acc);
     }
   }
@@ -488,7 +507,7 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
     for (int n = 0; n < N; ++n) {
       P xs[L];
       if constexpr (BUF) E::unpack(ld16_buf<NT>(tile_rsrc(a.x[k], tb), n), xs);
-      else E::unpack(ld16<NT>(a.x[k] + v[n] * L), xs);
+      else E::unpack(ld16<NT>(a.x[k] + vin[n] * L), xs);
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const P p = xs[j] * w;
@@ -500,9 +519,10 @@ __device__ __forceinline__ void fedavg_vectors(const FaArgs<E, KC>& a, const int
 
 // numel==1 patch for the N vectors v[] of this thread: one call site of the pairwise tree
 // (the owner vector is found first) keeps the unrolled kernel body small.
-template <typename E, int KC, int N>
+template <typename E, int KC, int N, int TV = 0>
 __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwArgs& pw, const int K,
-                                               const uint64_t* v, typename E::P (*acc)[E::L]) {
+                                               const uint64_t* v, typename E::P (*acc)[E::L],
+                                               const uint64_t pitch = 0) {
   constexpr int L = E::L;
   for (int p = 0; p < pw.n; ++p) {
     const uint64_t e = pw.idx[p];
@@ -511,7 +531,7 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
     for (int n = 0; n < N; ++n)
       if (e / L == v[n]) owner = n;
     if (owner >= 0) {
-      const typename E::P val = fedavg_pairwise_elem<E, KC>(a, K, e);
+      const typename E::P val = fedavg_pairwise_elem<E, KC>(a, K, in_elem<TV, L>(e, pitch));
       const int j = (int)(e % L);
 #pragma unroll
       for (int n = 0; n < N; ++n)
@@ -531,15 +551,19 @@ __device__ __forceinline__ void patch_pairwise(const FaArgs<E, KC>& a, const PwA
 // BLK (fedagg_tune "fa_blk"): threads per workgroup of the global-load tiles; 512 gives a
 // workgroup step the footprint of the 256-thread tile with twice the vectors per thread, at half
 // the registers per thread.
+// TV (fedagg_fedavg_tiled_*): the client buckets are tile-interleaved with tiles of TV = VPT*BLK
+// vectors and `pitch` = K * TV (in_vec above); 0: the [K, ld] row layout.
 template <typename E, int KC, bool NT, int NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
-          int BLK = FA_BLOCK>
+          int BLK = FA_BLOCK, int TV = 0>
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
-                  const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb) {
+                  const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb,
+                  const uint64_t pitch) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
   static_assert(!BUF || BLK == FA_BLOCK, "buffer-descriptor tiles assume 256-thread workgroups");
+  static_assert(TV == 0 || (TILE && !PIPE && TV == VPT * BLK), "tile-interleaved buckets: one tile per workgroup step");
   const uint64_t stride = (uint64_t)gridDim.x * BLK;
   const uint64_t gid = (uint64_t)blockIdx.x * BLK + threadIdx.x;
 
@@ -554,19 +578,23 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
       // wave-uniform: every lane of this wave has all VPT vectors in range
       const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * BLK < nvec;
       if (base + (VPT - 1) * BLK < nvec) {
-        uint64_t v[VPT];
+        uint64_t v[VPT], vin[VPT];
 #pragma unroll
-        for (int n = 0; n < VPT; ++n) v[n] = base + n * BLK;
+        for (int n = 0; n < VPT; ++n) {
+          v[n] = base + n * BLK;
+          vin[n] = TV ? t * pitch + n * BLK + threadIdx.x : v[n];
+        }
         P acc[VPT][L];
-        fedavg_vectors<E, KC, NT, VPT, U, PIPE, BUF>(a, K, first, v, acc, out, t * tile * 16);
-        if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE, BUF>(a, K, first, v, vin, acc, out, (TV ? t * pitch : t * tile) * 16);
+        if (pw.n) patch_pairwise<E, KC, VPT, TV>(a, pw, K, v, acc, pitch);
 #pragma unroll
         for (int n = 0; n < VPT; ++n) store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
       } else {
         for (uint64_t v0 = base; v0 < nvec; v0 += BLK) {
           P acc[1][L];
-          fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
-          if (pw.n) patch_pairwise<E, KC, 1>(a, pw, K, &v0, acc);
+          const uint64_t vi0 = in_vec<TV>(v0, pitch);
+          fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, &vi0, acc, out);
+          if (pw.n) patch_pairwise<E, KC, 1, TV>(a, pw, K, &v0, acc, pitch);
           store_vec<E, NTS>(out, v0, acc[0]);
         }
       }
@@ -579,7 +607,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
 #pragma unroll
         for (int n = 0; n < VPT; ++n) v[n] = v0 + n * stride;
         P acc[VPT][L];
-        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, acc, out);
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, v, acc, out);
         if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
 #pragma unroll
         for (int n = 0; n < VPT; ++n) store_vec<E, NTS>(out, v[n], acc[n]);
@@ -587,7 +615,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     }
     for (; v0 < nvec; v0 += stride) {
       P acc[1][L];
-      fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, acc, out);
+      fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, &v0, acc, out);
       if (pw.n) patch_pairwise<E, KC, 1>(a, pw, K, &v0, acc);
       store_vec<E, NTS>(out, v0, acc[0]);
     }
@@ -596,12 +624,13 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
   // Scalar remainder (M % L elements, or everything when a pointer is not 16-B aligned).
   for (uint64_t i = nvec * L + gid; i < M; i += stride) {
     P acc = first ? P(0.0f) : E::in_out(out[i]);
+    const uint64_t ii = in_elem<TV, L>(i, pitch);
     for (int k = 0; k < K; ++k) {
-      const P p = E::cvt(a.x[k][i]) * a.w[k];
+      const P p = E::cvt(a.x[k][ii]) * a.w[k];
       acc = acc + p;
     }
     for (int p = 0; p < pw.n; ++p)
-      if (pw.idx[p] == i) acc = fedavg_pairwise_elem<E, KC>(a, K, i);
+      if (pw.idx[p] == i) acc = fedavg_pairwise_elem<E, KC>(a, K, ii);
     out[i] = E::out(acc);
   }
 }
@@ -1633,12 +1662,12 @@ inline unsigned grid_for(uint64_t work) {
 }
 
 template <typename E, bool NT, int NTS, int VPT, int U, bool PIPE, bool TILE, int OCC = 1, bool BUF = false,
-          int BLK = FA_BLOCK>
+          int BLK = FA_BLOCK, bool INTER = false>
 void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw,
-                           int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out) {
+                           int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out, uint64_t pitch = 0) {
   if (BLK != FA_BLOCK) grid = (grid + BLK / FA_BLOCK - 1) / (BLK / FA_BLOCK);  // the caller sized it for 256
-  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF, BLK>), dim3(grid),
-                     dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb);
+  hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF, BLK, INTER ? VPT * BLK : 0>),
+                     dim3(grid), dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb, pitch);
 }
 
 // Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
@@ -1795,9 +1824,11 @@ void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>&
     launch_fedavg_shape<E, 0>(grid, s, a, pw, kc, first, nvec, M, out, sh);
 }
 
+// idx_in (tile-interleaved buckets): where each numel==1 element sits in the client buckets
+// (NULL: at its output index, the row layout).
 template <typename E>
 int fedavg_pairwise_launch(const typename E::In* const* x, const typename E::P* w, int K, const uint64_t* idx, int P,
-                           void* ws, typename E::Out* out, hipStream_t s) {
+                           void* ws, typename E::Out* out, hipStream_t s, const uint64_t* idx_in = nullptr) {
   if (P == 0) return FEDAGG_OK;
   if (K <= 0 || P < 0 || !x || !w || !idx || !ws || !out)
     return fail(FEDAGG_EINVAL, "fedavg_pairwise: invalid argument (K=%lld)", K);
@@ -1805,9 +1836,12 @@ int fedavg_pairwise_launch(const typename E::In* const* x, const typename E::P* 
   W* wsT = static_cast<W*>(ws);
   for (int p0 = 0; p0 < P; p0 += FEDAGG_MAX_PAIRWISE) {
     const int pc = (P - p0) < FEDAGG_MAX_PAIRWISE ? (P - p0) : FEDAGG_MAX_PAIRWISE;
-    IdxArgs ix;
+    IdxArgs ix, ixin;
     memset(&ix, 0, sizeof(ix));
     for (int p = 0; p < pc; ++p) ix.idx[p] = idx[p0 + p];
+    ixin = ix;
+    if (idx_in)
+      for (int p = 0; p < pc; ++p) ixin.idx[p] = idx_in[p0 + p];
     for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
       const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
       FaArgs<E, FEDAGG_KCHUNK> a;
@@ -1817,7 +1851,7 @@ int fedavg_pairwise_launch(const typename E::In* const* x, const typename E::P* 
         a.w[k] = w[k0 + k];
       }
       const unsigned g = (unsigned)((pc * kc + FA_BLOCK - 1) / FA_BLOCK);
-      hipLaunchKernelGGL((pairwise_gather_kernel<E, FEDAGG_KCHUNK>), dim3(g), dim3(FA_BLOCK), 0, s, a, kc, k0, ix,
+      hipLaunchKernelGGL((pairwise_gather_kernel<E, FEDAGG_KCHUNK>), dim3(g), dim3(FA_BLOCK), 0, s, a, kc, k0, ixin,
                          pc, (int64_t)K, wsT);
       int rc = check_launch("pairwise_gather_kernel");
       if (rc) return rc;
@@ -1928,6 +1962,79 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
     if (rc) return rc;
   }
   if (P > 0 && !fuse) return fedavg_pairwise_launch<E>(x, w, K, idx, P, ws, out, s);
+  return FEDAGG_OK;
+}
+
+// Tile-interleaved buckets (fedagg_fedavg_tiled_*): the tiled kernels walk the same tiles as the
+// auto shapes from 32 clients over large buckets (16 vectors x 512 threads for fp32, 16 x 256
+// with buffer loads for bf16).  The layout is recommended (fedagg_fedavg_tile_vectors_*) where
+// the row-layout auto shape is that very tile; the tiled entry points take any K and M.
+template <typename E>
+constexpr uint64_t tiled_tile() {
+  return std::is_same<E, F32>::value ? FEDAGG_TILE_VECTORS_F32 : std::is_same<E, BF16>::value ? FEDAGG_TILE_VECTORS_BF16 : 0;
+}
+
+template <typename E>
+uint64_t tiled_tile_vectors(int K, uint64_t M) {
+  if (K <= 0 || !g_nt_load || !g_tile || g_vpt > 0 || g_tpb > 1) return 0;
+  const Shape sh = shape_for<E>(K, M / E::L);
+  if (sh.vpt != 16 || sh.unroll != 2 || sh.pipe) return 0;
+  if constexpr (std::is_same<E, F32>::value) return sh.blk == 2 * FA_BLOCK && !sh.buf ? tiled_tile<E>() : 0;
+  if constexpr (std::is_same<E, BF16>::value) return sh.buf && sh.occ <= 1 ? tiled_tile<E>() : 0;
+  return 0;
+}
+
+template <typename E>
+int fedavg_tiled_launch(const typename E::In* base, const typename E::P* w, int K, uint64_t M, uint64_t tv,
+                        const uint64_t* idx, int P, void* ws, typename E::Out* out, hipStream_t s) {
+  if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg_tiled: K must be > 0 (got %lld)", K);
+  if (!base || !w || !out) return fail(FEDAGG_EINVAL, "fedavg_tiled: NULL argument");
+  if (!aligned16(base) || !aligned16(out)) return fail(FEDAGG_EINVAL, "fedavg_tiled: buffers must be 16-B aligned");
+  if (tv != tiled_tile<E>())
+    return fail(FEDAGG_EINVAL, "fedavg_tiled: the tile must be %lld vectors (FEDAGG_TILE_VECTORS_*)",
+                (long long)tiled_tile<E>());
+  if (P < 0 || (P > 0 && !idx)) return fail(FEDAGG_EINVAL, "fedavg_tiled: bad pairwise index list (P=%lld)", P);
+  for (int p = 0; p < P; ++p)
+    if (idx[p] >= M) return fail(FEDAGG_EINVAL, "fedavg_tiled: pairwise index %lld out of range", (long long)idx[p]);
+  const bool fuse = g_fuse_pw && P <= FEDAGG_FUSED_PAIRWISE && K <= FEDAGG_KCHUNK;
+  if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg_tiled: workspace needed for %lld pairwise segments", P);
+  constexpr int L = E::L;
+  const uint64_t nvec = M / L, pitch = (uint64_t)K * tv;
+  const unsigned grid = grid_for((nvec + 15) / 16);
+  std::vector<const typename E::In*> x(K);
+  for (int k = 0; k < K; ++k) x[k] = base + (uint64_t)k * tv * L;
+  for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
+    const int kc = (K - k0) < FEDAGG_KCHUNK ? (K - k0) : FEDAGG_KCHUNK;
+    FaArgs<E, FEDAGG_KCHUNK> a;
+    memset(&a, 0, sizeof(a));
+    for (int k = 0; k < kc; ++k) {
+      a.x[k] = x[k0 + k];
+      a.w[k] = w[k0 + k];
+    }
+    PwArgs pw;
+    memset(&pw, 0, sizeof(pw));
+    if (fuse) {
+      pw.n = P;
+      for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
+    }
+    const int first = k0 == 0 ? 1 : 0;
+    if constexpr (std::is_same<E, F32>::value)
+      launch_fedavg_variant<E, true, 1, 16, 2, false, true, 1, false, 2 * FA_BLOCK, true>(grid, s, a, pw, kc, first,
+                                                                                          nvec, M, out, pitch);
+    else
+      launch_fedavg_variant<E, true, 1, 16, 2, false, true, 1, true, FA_BLOCK, true>(grid, s, a, pw, kc, first, nvec,
+                                                                                    M, out, pitch);
+    int rc = check_launch("fedavg_kernel (tiled)");
+    if (rc) return rc;
+  }
+  if (P > 0 && !fuse) {
+    std::vector<uint64_t> in(P);
+    for (int p = 0; p < P; ++p) {
+      const uint64_t v = idx[p] / L;
+      in[p] = ((v / tv) * pitch + v % tv) * L + idx[p] % L;
+    }
+    return fedavg_pairwise_launch<E>(x.data(), w, K, idx, P, ws, out, s, in.data());
+  }
   return FEDAGG_OK;
 }
 
@@ -2377,6 +2484,16 @@ int fedagg_fedavg_f32(const float* const* d_clients, const float* h_w, int K, ui
 int fedagg_fedavg_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, const uint64_t* h_idx,
                        int P, void* d_ws, float* d_out, void* stream) {
   return fedavg_launch<BF16>(d_clients, h_w, K, M, h_idx, P, d_ws, d_out, (hipStream_t)stream);
+}
+uint64_t fedagg_fedavg_tile_vectors_f32(int K, uint64_t M) { return tiled_tile_vectors<F32>(K, M); }
+uint64_t fedagg_fedavg_tile_vectors_bf16(int K, uint64_t M) { return tiled_tile_vectors<BF16>(K, M); }
+int fedagg_fedavg_tiled_f32(const float* d_base, const float* h_w, int K, uint64_t M, uint64_t tile_vectors,
+                            const uint64_t* h_idx, int P, void* d_ws, float* d_out, void* stream) {
+  return fedavg_tiled_launch<F32>(d_base, h_w, K, M, tile_vectors, h_idx, P, d_ws, d_out, (hipStream_t)stream);
+}
+int fedagg_fedavg_tiled_bf16(const uint16_t* d_base, const float* h_w, int K, uint64_t M, uint64_t tile_vectors,
+                             const uint64_t* h_idx, int P, void* d_ws, float* d_out, void* stream) {
+  return fedavg_tiled_launch<BF16>(d_base, h_w, K, M, tile_vectors, h_idx, P, d_ws, d_out, (hipStream_t)stream);
 }
 int fedagg_fedavg_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, const uint64_t* h_idx,
                       int P, void* d_ws, double* d_out, void* stream) {

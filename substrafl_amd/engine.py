@@ -161,6 +161,68 @@ class FedAvgPlan:
         return self.K * self.M * s_in + self.M * s_out
 
 
+TILED_KINDS = ("f32", "bf16")
+_ELEMS_PER_VEC = {"f32": 4, "bf16": 8}
+
+
+def tile_vectors(kind: str) -> int:
+    """16-B vectors per client tile of the tile-interleaved layout (FEDAGG_TILE_VECTORS_*)."""
+    return {"f32": _native.FEDAGG_TILE_VECTORS_F32, "bf16": _native.FEDAGG_TILE_VECTORS_BF16}[kind]
+
+
+def tiled_recommended(kind: str, K: int, M: int) -> bool:
+    """Whether the library recommends the tile-interleaved layout for K clients of M elements
+    (its row-layout kernel for that shape walks the same tile; fedagg_fedavg_tile_vectors_*)."""
+    if kind not in TILED_KINDS:
+        return False
+    return bool(getattr(_native.load(), f"fedagg_fedavg_tile_vectors_{kind}")(int(K), int(M)))
+
+
+def tiled_elems(kind: str, K: int, M: int) -> int:
+    """Elements of a tile-interleaved buffer of K clients of M elements (last tile padded)."""
+    L, T = _ELEMS_PER_VEC[kind], tile_vectors(kind)
+    nvec = -(-int(M) // L)
+    return -(-nvec // T) * int(K) * T * L
+
+
+def tiled_index(kind: str, K: int, k, e):
+    """Element offset, in the tile-interleaved buffer, of element ``e`` of client ``k`` (NumPy
+    broadcasting): vector v = e // L of client k sits at ((v // T) * K + k) * T + v % T."""
+    L, T = _ELEMS_PER_VEC[kind], tile_vectors(kind)
+    e = np.asarray(e, dtype=np.int64)
+    v = e // L
+    return (((v // T) * int(K) + np.asarray(k, dtype=np.int64)) * T + v % T) * L + e % L
+
+
+def tiled_client_view(buf, kind: str, K: int, k: int):
+    """Client ``k``'s tiles of a tile-interleaved torch buffer: a strided ``[tiles, T * L]`` view
+    (its first M elements in row-major order are the client's bucket)."""
+    L, T = _ELEMS_PER_VEC[kind], tile_vectors(kind)
+    return buf.view(-1, int(K), T * L)[:, int(k), :]
+
+
+class TiledFedAvgPlan(FedAvgPlan):
+    """FedAvg over tile-interleaved client buckets (``fedagg_fedavg_tiled_{f32,bf16}``): ``base``
+    is one device buffer (tensor or pointer) of :func:`tiled_elems` elements in which tile t of
+    client k is tile ``t * K + k``; a workgroup then reads one contiguous K-tile region per step.
+    Same kernel arithmetic and results as :class:`FedAvgPlan` over the row layout."""
+
+    def __init__(self, kind: str, base, K: int, weights: np.ndarray, M: int, out, pairwise_idx=None, ws=None):
+        if kind not in TILED_KINDS:
+            raise ValueError(f"tile-interleaved buckets take {TILED_KINDS}")
+        T = tile_vectors(kind)
+        # the per-client tile-0 pointers size the pairwise workspace and validate K like the rows plan
+        super().__init__(kind, [_ptr(base) + k * T * 16 for k in range(int(K))], weights, M, out, pairwise_idx, ws)
+        self._keep = (base,) + tuple(self._keep)
+        self._base, self._tv = _ptr(base), T
+        self._tiled = getattr(self.lib, f"fedagg_fedavg_tiled_{kind}")
+
+    def launch(self, stream=None) -> None:
+        rc = self._tiled(self._base, self._w, self.K, self.M, self._tv, self._idx, self.P, self._ws, self._out,
+                         _stream_handle(stream))
+        _native.check(rc, "fedavg_tiled")
+
+
 class ScaffoldPlan:
     """Scaffold two-bucket reduction over device-resident buckets (fp32 or fp64 inputs, fp64 out)."""
 

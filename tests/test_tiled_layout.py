@@ -1,0 +1,154 @@
+"""Tile-interleaved client buckets (``fedagg_fedavg_tiled_{f32,bf16}``, engine.TiledFedAvgPlan):
+tile t of client k at tile ``t * K + k``, same kernel arithmetic as the row layout, so the
+results are bit-identical to the oracle (fed_avg.py:217-222) -- partial last tiles, element
+remainders, numel == 1 layers (fused patch and the separate pairwise path) and more clients than
+one launch takes (K > 128) included."""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import fedavg_reference_structure
+
+
+def _bits(a):
+    a = np.asarray(a)
+    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize])
+
+
+# ---------------------------------------------------------------------------------------------
+# layout arithmetic and argument checks (CPU)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["f32", "bf16"])
+@pytest.mark.parametrize("K,M", [(1, 5), (3, 70_001), (7, 300_000)])
+def test_tiled_index_is_a_bijection_into_the_buffer(kind, K, M):
+    from substrafl_amd import engine
+
+    n = engine.tiled_elems(kind, K, M)
+    e = np.arange(M)
+    pos = np.concatenate([engine.tiled_index(kind, K, k, e) for k in range(K)])
+    assert pos.min() >= 0 and pos.max() < n
+    assert np.unique(pos).size == pos.size
+    # a client's elements keep their order inside a tile
+    T, L = engine.tile_vectors(kind), {"f32": 4, "bf16": 8}[kind]
+    p0 = engine.tiled_index(kind, K, 0, e)
+    inside = (e[1:] // (T * L)) == (e[:-1] // (T * L))
+    assert np.all(np.diff(p0)[inside] == 1)
+
+
+def test_tiled_entry_rejects_a_foreign_tile():
+    from substrafl_amd import _native
+
+    lib = _native.load()
+    w = (ctypes.c_float * 1)(1.0)
+    idx = (ctypes.c_uint64 * 1)(0)
+    assert lib.fedagg_fedavg_tiled_f32(256, w, 1, 1024, 4096, idx, 0, None, 256, None) == -1
+    assert b"tile must be" in lib.fedagg_last_error()
+    assert lib.fedagg_fedavg_tiled_bf16(256, w, 1, 1024, 8192, idx, 0, None, 256, None) == -1
+    assert lib.fedagg_fedavg_tiled_f32(None, w, 1, 1024, 8192, idx, 0, None, 256, None) == -1
+    # recommended exactly where the row layout's kernel walks the same tile (>= 32 clients, large buckets)
+    assert lib.fedagg_fedavg_tile_vectors_f32(64, 125_000_000) == _native.FEDAGG_TILE_VECTORS_F32
+    assert lib.fedagg_fedavg_tile_vectors_bf16(128, 350_000_000) == _native.FEDAGG_TILE_VECTORS_BF16
+    assert lib.fedagg_fedavg_tile_vectors_f32(8, 25_000_000) == 0
+    assert lib.fedagg_fedavg_tile_vectors_f32(64, 1_000_000) == 0
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU parity
+# ---------------------------------------------------------------------------------------------
+def _case(rng, K, M, P, bf16):
+    """K clients of M elements as layers, P of them numel == 1 (scattered), values N(0,1) x 10^U."""
+    cuts = np.sort(rng.choice(np.arange(1, M - 1), size=P, replace=False)) if P else np.array([], int)
+    shapes, pos = [], 0
+    for c in cuts:
+        if c > pos:
+            shapes.append((int(c - pos),))
+        shapes.append((1,))
+        pos = c + 1
+    if M > pos:
+        shapes.append((int(M - pos),))
+    pus = []
+    for _ in range(K):
+        layers = [(rng.standard_normal(s) * 10.0 ** rng.integers(-3, 3)).astype(np.float32) for s in shapes]
+        if bf16:
+            layers = [(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in layers]
+        pus.append(layers)
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    return shapes, pus, ns
+
+
+def _tiled_device(torch, kind, pus, M):
+    from substrafl_amd import engine
+
+    K = len(pus)
+    dt = torch.bfloat16 if kind == "bf16" else torch.float32
+    buf = torch.zeros(engine.tiled_elems(kind, K, M), dtype=dt, device="cuda")
+    T, L = engine.tile_vectors(kind), {"f32": 4, "bf16": 8}[kind]
+    tiles = buf.numel() // (K * T * L)
+    for k, layers in enumerate(pus):
+        row = torch.zeros(tiles * T * L, dtype=torch.float32)
+        row[:M] = torch.from_numpy(np.concatenate([a.ravel() for a in layers]))
+        engine.tiled_client_view(buf, kind, K, k).copy_(row.view(tiles, T * L).to(dt).cuda())
+    return buf
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["f32", "bf16"])
+@pytest.mark.parametrize("K,tiles,P", [(1, 1, 0), (3, 2, 1), (9, 3, 5), (40, 2, 16), (20, 2, 17), (130, 1, 3)])
+def test_tiled_fedavg_bit_exact(kind, K, tiles, P):
+    import torch
+
+    from substrafl_amd import engine
+    from substrafl_amd.layout import BucketLayout
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    rng = np.random.default_rng(K * 31 + tiles + P)
+    T, L = engine.tile_vectors(kind), {"f32": 4, "bf16": 8}[kind]
+    M = (tiles - 1) * T * L + int(rng.integers(1, T * L))  # a partial last tile, any remainder mod L
+    shapes, pus, ns = _case(rng, K, M, P, kind == "bf16")
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    assert lay.M == M and lay.pairwise_idx.size == P
+    buf = _tiled_device(torch, kind, pus, M)
+    out = torch.full((lay.ld,), np.nan, dtype=torch.float32, device="cuda")
+    w = engine.fedavg_weights(ns, kind)
+    engine.TiledFedAvgPlan(kind, buf, K, w, M, out, lay.pairwise_idx).launch()
+    torch.cuda.synchronize()
+    got = out[:M].cpu().numpy()
+    ref = np.concatenate([r.ravel() for r in fedavg_reference_structure(pus, ns)])
+    assert np.array_equal(_bits(got), _bits(ref))
+
+
+@pytest.mark.gpu
+def test_tiled_matches_rows_at_the_recommended_shape():
+    """At a recommended shape (32 fp32 clients, >= 2048 tiles) the tiled kernel and the row
+    layout's kernel give the same bits (the row kernel is pinned to the oracle elsewhere)."""
+    import torch
+
+    from substrafl_amd import engine
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+
+    K, M = 32, 34_000_000
+    assert engine.tiled_recommended("f32", K, M)
+    shapes = synthetic_state_dict_shapes(M)
+    lay = BucketLayout(list(range(len(shapes))), shapes, np.float32)
+    g = torch.Generator(device="cuda")
+    rows = torch.empty((K, lay.ld), dtype=torch.float32, device="cuda")
+    for k in range(K):
+        g.manual_seed(7 + k)
+        rows[k].normal_(generator=g)
+    T, L = engine.tile_vectors("f32"), 4
+    buf = torch.zeros(engine.tiled_elems("f32", K, lay.M), dtype=torch.float32, device="cuda")
+    tiles = buf.numel() // (K * T * L)
+    for k in range(K):
+        row = torch.zeros(tiles * T * L, dtype=torch.float32, device="cuda")
+        row[: lay.M] = rows[k, : lay.M]
+        engine.tiled_client_view(buf, "f32", K, k).copy_(row.view(tiles, T * L))
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    w = engine.fedavg_weights(ns, "f32")
+    a = torch.empty(lay.ld, dtype=torch.float32, device="cuda")
+    b = torch.empty(lay.ld, dtype=torch.float32, device="cuda")
+    engine.FedAvgPlan("f32", rows, w, lay.M, a, lay.pairwise_idx).launch()
+    engine.TiledFedAvgPlan("f32", buf, K, w, lay.M, b, lay.pairwise_idx).launch()
+    torch.cuda.synchronize()
+    assert torch.equal(a[: lay.M].view(torch.int32), b[: lay.M].view(torch.int32))
