@@ -68,9 +68,10 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered", "striped"])
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
-    ap.add_argument("--layout", default="rows", choices=["rows", "tiles", "auto"],
+    ap.add_argument("--layout", default="auto", choices=["rows", "tiles", "auto"],
                     help="client buckets in HBM: [K, ld] rows, tile-interleaved (fedagg_fedavg_tiled_*; "
-                         "FedAvg fp32/bf16), or tiles where the library recommends them")
+                         "FedAvg fp32/bf16), or (default) tiles where the library recommends them -- the "
+                         "layout the drop-in host path stages (AggregationEngine.tiled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--grid-cap", type=int, default=0)

@@ -323,6 +323,13 @@ int fedagg_session_stage(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int 
 int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
                                const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
                                uint64_t byte_hi);
+/* K rows of host segments in the tile-interleaved layout of fedagg_fedavg_tiled_*: tile t of row k
+ * (row bytes [t * tile_bytes, (t + 1) * tile_bytes)) lands at d_dst + (t * K + k) * tile_bytes;
+ * the K rows' tiles are gathered into each pinned chunk on the workers, so every H2D copy is one
+ * contiguous run of blocks.  tile_bytes: FEDAGG_TILE_VECTORS_* x 16 (a multiple of 16, at most the
+ * session's chunk_bytes); d_dst holds ceil(row / tile_bytes) * K * tile_bytes bytes. */
+int fedagg_session_stage_tiled(fedagg_session* s, void* d_dst, uint64_t tile_bytes, int K, int nseg,
+                               const void* const* h_seg, const uint64_t* seg_bytes);
 /* Scaffold's server-control-variate check on the host, during staging (scaffold.py:193-196,
  * np.testing.assert_array_equal(c_0, c_k)): K clients' c rows (nseg host segments each, as
  * fedagg_session_stage); ONE copy -- bytes [byte_lo, byte_hi) of row 0 -- is staged to d_dst, the

@@ -96,6 +96,7 @@ SIGNATURES = {
     "fedagg_session_warm": (c_int, [c_void, P(c_u64), c_int]),
     "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
     "fedagg_session_stage_range": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64]),
+    "fedagg_session_stage_tiled": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
     "fedagg_session_stage_check": (c_int, [c_void, c_void, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64, c_int,
                                            P(c_u64)]),
     "fedagg_session_event_record": (c_int, [c_void, c_int]),

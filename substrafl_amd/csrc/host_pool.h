@@ -171,6 +171,53 @@ inline uint64_t check_rows(Pool& pool, const void* const* h_seg, const uint64_t*
   return bad.load();
 }
 
+// The staging ring: `units` pieces, unit u packed by a worker into ring slot u % R
+// (pack(u, slot) on the pool) and copied to the device by the calling thread (dest(u, &d, &n):
+// n bytes of the slot to device address d; alternate units over two queues with two_queues).
+// In-order window: R-1 packs run ahead of the copy being enqueued; a slot is refilled only after
+// the copy that read it completed, while the next copy is already in flight, so the link never
+// waits on the enqueueing thread.  On an error the packs already submitted are waited for (they
+// read the caller's segments and write the ring) before the code is returned.
+template <class Eng, class Pack, class Dest>
+int ring_stage(Eng& eng, Pool& pool, Ring& ring, uint64_t units, bool two_queues, Pack pack, Dest dest) {
+  const int R = ring.size();
+  const bool two = two_queues && units > 1;
+  std::vector<Done> done(units ? std::min<uint64_t>(units, (uint64_t)R) : 1);
+  std::vector<bool> pending(done.size(), false);
+  int rc = 0;
+  uint64_t next_submit = 0;
+  auto submit = [&](uint64_t u) {
+    const int slot = (int)(u % R);
+    if (ring.used[slot]) eng.wait(slot);  // the copy of unit u - R is done
+    ring.used[slot] = false;
+    Done& d = done[slot];
+    d.done = false;
+    pending[slot] = true;
+    char* dst = static_cast<char*>(ring.slot[slot]);
+    pool.submit([=, &d] {
+      pack(u, dst);
+      d.set();
+    });
+  };
+  for (; next_submit < units && next_submit + 1 < (uint64_t)R; ++next_submit) submit(next_submit);
+  for (uint64_t u = 0; u < units && !rc; ++u) {
+    const int slot = (int)(u % R);
+    done[slot].wait();
+    pending[slot] = false;
+    char* d = nullptr;
+    uint64_t n = 0;
+    dest(u, &d, &n);
+    const int q = (two && (u & 1)) ? 1 : 0;
+    rc = eng.h2d(q, d, ring.slot[slot], n);
+    if (!rc) rc = eng.mark(slot, q);
+    if (!rc) ring.used[slot] = true;
+    if (!rc && next_submit < units) submit(next_submit++);
+  }
+  for (size_t i = 0; i < done.size(); ++i)  // packs still running read the caller's segments
+    if (pending[i]) done[i].wait();
+  return rc;
+}
+
 // K rows of nseg host segments -> d_dst + k * ld_bytes, bytes [byte_lo, byte_lo + row) of each
 // row.  check_esz > 0: only row 0 is staged, rows 1..K-1 are compared with it by value on the
 // host (mismatching elements added to *mismatches) -- the server-control-variate check of
@@ -180,53 +227,49 @@ int stage_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, c
                    int K, uint64_t byte_lo, uint64_t row, char* d_dst, uint64_t ld_bytes, bool two_queues,
                    int check_esz = 0, uint64_t* mismatches = nullptr) {
   const uint64_t cb = ring.chunk_bytes;
-  const int R = ring.size();
   const int Ks = check_esz ? 1 : K;
-  const uint64_t per_row = row ? (row + cb - 1) / cb : 0;
-  const uint64_t units = per_row * (uint64_t)Ks;
-  const bool two = two_queues && units > 1;
-  std::vector<Done> done(units ? std::min<uint64_t>(units, (uint64_t)R) : 1);
-  std::vector<bool> pending(done.size(), false);
-  int rc = 0;
-  // In-order window: unit u lives in slot u % R.  R-1 packs run ahead of the copy being
-  // enqueued; a slot is refilled only after the copy that read it completed, while the next
-  // copy is already in flight, so the link never waits on the enqueueing thread.
-  uint64_t next_submit = 0;
-  auto submit = [&](uint64_t u) {
-    const int slot = (int)(u % R);
-    if (ring.used[slot]) eng.wait(slot);  // the copy of unit u - R is done
-    ring.used[slot] = false;
-    Done& d = done[slot];
-    d.done = false;
-    pending[slot] = true;
-    const int k = (int)(u / per_row);
-    const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
-    const void* const* segs = h_seg + (size_t)k * nseg;
-    char* dst = static_cast<char*>(ring.slot[slot]);
-    pool.submit([=, &d] {
-      gather_range(segs, seg_bytes, nseg, byte_lo + a, byte_lo + b, dst);
-      d.set();
-    });
-  };
-  for (; next_submit < units && next_submit + 1 < (uint64_t)R; ++next_submit) submit(next_submit);
-  for (uint64_t u = 0; u < units && !rc; ++u) {
-    const int slot = (int)(u % R);
-    done[slot].wait();
-    pending[slot] = false;
-    const int k = (int)(u / per_row);
-    const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
-    const int q = (two && (u & 1)) ? 1 : 0;
-    rc = eng.h2d(q, d_dst + (uint64_t)k * ld_bytes + a, ring.slot[slot], b - a);
-    if (!rc) rc = eng.mark(slot, q);
-    if (!rc) ring.used[slot] = true;
-    if (!rc && next_submit < units) submit(next_submit++);
-  }
-  for (size_t i = 0; i < done.size(); ++i)  // packs still running read the caller's segments
-    if (pending[i]) done[i].wait();
+  const uint64_t per_row = row ? (row + cb - 1) / cb : 0;  // unit u: chunk u % per_row of row u / per_row
+  const int rc = ring_stage(
+      eng, pool, ring, per_row * (uint64_t)Ks, two_queues,
+      [=](uint64_t u, char* dst) {
+        const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
+        gather_range(h_seg + (size_t)(u / per_row) * nseg, seg_bytes, nseg, byte_lo + a, byte_lo + b, dst);
+      },
+      [=](uint64_t u, char** d, uint64_t* n) {
+        const uint64_t a = (u % per_row) * cb;
+        *d = d_dst + (u / per_row) * ld_bytes + a;
+        *n = std::min(row, a + cb) - a;
+      });
   if (rc || !check_esz || K < 2) return rc;
   const uint64_t bad = check_rows(pool, h_seg, seg_bytes, nseg, K, byte_lo, row, check_esz);
   if (mismatches) *mismatches += bad;
   return 0;
+}
+
+// K rows of nseg host segments (row bytes each) -> the tile-interleaved layout of
+// fedagg_fedavg_tiled_*: tile t of row k (bytes [t * tb, (t + 1) * tb)) at d_dst + (t * K + k) * tb.
+// The destination is one run of (tile, row) blocks, so a unit is a run of whole blocks gathered
+// from the K rows into one pinned slot and ONE contiguous copy; the pad of a row's last, partial
+// tile is not written on the host (the kernels never read it).  tb <= the ring's chunk_bytes.
+template <class Eng>
+int stage_tiled_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, const uint64_t* seg_bytes,
+                         int nseg, int K, uint64_t row, uint64_t tb, char* d_dst, bool two_queues) {
+  if (!tb || tb > ring.chunk_bytes) return -1;
+  const uint64_t tiles = row ? (row + tb - 1) / tb : 0;
+  const uint64_t blocks = tiles * (uint64_t)K, bpu = ring.chunk_bytes / tb;
+  return ring_stage(
+      eng, pool, ring, (blocks + bpu - 1) / bpu, two_queues,
+      [=](uint64_t u, char* dst) {
+        const uint64_t j1 = std::min(blocks, (u + 1) * bpu);
+        for (uint64_t j = u * bpu; j < j1; ++j) {
+          const uint64_t t = j / (uint64_t)K, a = t * tb, b = std::min(row, a + tb);
+          gather_range(h_seg + (size_t)(j % (uint64_t)K) * nseg, seg_bytes, nseg, a, b, dst + (j - u * bpu) * tb);
+        }
+      },
+      [=](uint64_t u, char** d, uint64_t* n) {
+        *d = d_dst + u * bpu * tb;
+        *n = (std::min(blocks, (u + 1) * bpu) - u * bpu) * tb;
+      });
 }
 
 // bytes from d_src into host h_dst through the ring: D2H in super-chunks of G adjacent slots

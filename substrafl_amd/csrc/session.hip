@@ -318,8 +318,12 @@ int stage_prepare(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int 
   return FEDAGG_OK;
 }
 
-int stage_run(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg, const void* const* h_seg,
-              const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t row, int check_esz, uint64_t* mismatches) {
+// run(engine, two_queues) between the joins of the two copy queues
+}  // namespace
+}  // extern "C"
+namespace {
+template <class Run>
+int stage_run_with(fedagg_session* s, Run run) {
   const double t0 = now_s();
   const bool two = s->copy_streams > 1;
   if (two) {  // the second queue starts after everything already enqueued on the session stream
@@ -327,8 +331,7 @@ int stage_run(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg
     HIP_TRY(hipStreamWaitEvent(s->xstream, s->join_ev, 0));
   }
   HipEngine eng{s};
-  int rc = fedagg_host::stage_pipeline(eng, s->workers(), s->ring, h_seg, seg_bytes, nseg, K, byte_lo, row,
-                                       static_cast<char*>(d_dst), ld_bytes, two, check_esz, mismatches);
+  int rc = run(eng, two);
   if (two) {  // work enqueued on the session stream after this call sees every staged byte
     hipError_t e = hipEventRecord(s->join_ev, s->xstream);
     if (e == hipSuccess) e = hipStreamWaitEvent(s->stream, s->join_ev, 0);
@@ -338,7 +341,17 @@ int stage_run(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg
   return rc;
 }
 
+int stage_run(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg, const void* const* h_seg,
+              const uint64_t* seg_bytes, uint64_t byte_lo, uint64_t row, int check_esz, uint64_t* mismatches) {
+  return stage_run_with(s, [&](HipEngine& eng, bool two) {
+    return fedagg_host::stage_pipeline(eng, s->workers(), s->ring, h_seg, seg_bytes, nseg, K, byte_lo, row,
+                                       static_cast<char*>(d_dst), ld_bytes, two, check_esz, mismatches);
+  });
+}
+
 }  // namespace
+
+extern "C" {
 
 int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes, int K, int nseg,
                                const void* const* h_seg, const uint64_t* seg_bytes, uint64_t byte_lo,
@@ -347,6 +360,23 @@ int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes
   int rc = stage_prepare(s, d_dst, ld_bytes, K, nseg, h_seg, seg_bytes, byte_lo, byte_hi, &row);
   if (rc) return rc;
   return stage_run(s, d_dst, ld_bytes, K, nseg, h_seg, seg_bytes, byte_lo, row, 0, nullptr);
+}
+
+int fedagg_session_stage_tiled(fedagg_session* s, void* d_dst, uint64_t tile_bytes, int K, int nseg,
+                               const void* const* h_seg, const uint64_t* seg_bytes) {
+  if (nseg < 0 || (nseg > 0 && !seg_bytes)) return FEDAGG_EINVAL;
+  uint64_t full = 0, row = 0;
+  for (int i = 0; i < nseg; ++i) full += seg_bytes[i];
+  int rc = stage_prepare(s, d_dst, full, K, nseg, h_seg, seg_bytes, 0, full, &row);
+  if (rc) return rc;
+  if (!tile_bytes || tile_bytes % 16 || tile_bytes > s->chunk_bytes) {
+    fedagg_internal::set_error("fedagg_session_stage_tiled: tile_bytes must be a multiple of 16 and <= chunk_bytes");
+    return FEDAGG_EINVAL;
+  }
+  return stage_run_with(s, [&](HipEngine& eng, bool two) {
+    return fedagg_host::stage_tiled_pipeline(eng, s->workers(), s->ring, h_seg, seg_bytes, nseg, K, row, tile_bytes,
+                                             static_cast<char*>(d_dst), two);
+  });
 }
 
 int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, const void* const* h_seg,

@@ -346,6 +346,11 @@ class AggregationEngine:
         # in parameter ranges (multi_device.MultiDeviceEngine with this one device); default:
         # 85 % of the device's free HBM at call time
         self.max_bucket_bytes = max_bucket_bytes
+        # HBM layout of FedAvg buckets staged by a call (not by ingest, whose clients arrive one by
+        # one and keep the row layout): "auto" = tile-interleaved where fedagg_fedavg_tile_vectors_*
+        # recommends it (from 32 fp32 clients over large buckets), True / False to force
+        env = os.environ.get("FEDAGG_TILED", "auto")
+        self.tiled: Union[str, bool] = {"0": False, "1": True}.get(env, "auto")
         self._ooc = None
         self.last_timing: Dict[str, float] = {}
         # rows already on the device from ingest(): slot -> (d_bucket, ld_bytes, {k: row arrays},
@@ -513,6 +518,20 @@ class AggregationEngine:
                 return False
         return True
 
+    def _tiled_rows(self, rows, R: np.dtype, kind: str, K: int, M: int):
+        """The rows as stageable segments when this call stages them tile-interleaved (``tiled``:
+        "auto" where the library recommends the layout, True wherever a tiled kernel exists for
+        the dtype, False never), else None."""
+        mode = self.tiled
+        if mode is False or kind not in TILED_KINDS or (mode == "auto" and not tiled_recommended(kind, K, M)):
+            return None
+        if not all(a.dtype == R for row in rows for a in row):
+            return None  # dtype conversions stage raw rows and cast on the device
+        flats = [flat_of(row) for row in rows]
+        if all(f is not None and f.size == M for f in flats):
+            return [[f] for f in flats]  # flat wire format: one segment per client
+        return [[np.ascontiguousarray(a) for a in row] for row in rows]
+
     def session(self):
         s = runtime.session(self._index())
         if self._pack_threads:
@@ -614,17 +633,27 @@ class AggregationEngine:
                     w[k] = 1  # x * 1 is exact: the client's product was formed in its own dtype
             d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * R.itemsize)
             t0 = time.perf_counter()
+            tiled = None
             if prescale is None and len(groups) == 1 and self._take_prestaged(
                     self._B_BUCKET, d_bucket, layout.ld * R.itemsize, rows):
                 tm["prestaged"] = True
             else:
-                self._stage_rows(s, rows, layout, d_bucket, prescale)
+                tiled = self._tiled_rows(rows, R, kind, K, layout.M) if prescale is None else None
+                if tiled is not None:  # tile-interleaved buckets (TiledFedAvgPlan), one gather per pinned chunk
+                    d_bucket = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M) * R.itemsize)
+                    s.stage_tiled(d_bucket, tile_vectors(kind) * 16, tiled)
+                else:
+                    self._stage_rows(s, rows, layout, d_bucket, prescale)
             tm["stage_s"] = tm.get("stage_s", 0.0) + time.perf_counter() - t0
+            tm["layout"] = "tiles" if tiled is not None else "rows"
             d_out = s.buffer(self._B_OUT, layout.ld * R.itemsize)
             ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, layout.pairwise_idx.size, 8))
-            ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
             t1 = time.perf_counter()
-            FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
+            if tiled is not None:
+                TiledFedAvgPlan(kind, d_bucket, K, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
+            else:
+                ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
+                FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
             out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}")
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
             tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1

@@ -139,6 +139,15 @@ class Session:
             _native.check(self.lib.fedagg_session_stage_range(self._h, ctypes.c_void_p(d_dst), int(ld_bytes), K,
                                                               nseg, ptrs, sizes, lo, hi), "session_stage_range")
 
+    def stage_tiled(self, d_dst: int, tile_bytes: int, rows: Sequence[Sequence[np.ndarray]]) -> None:
+        """rows[k] = client k's host arrays (bucket order) into the tile-interleaved layout of
+        ``engine.TiledFedAvgPlan``: tile t of row k at ``d_dst + (t * K + k) * tile_bytes``
+        (``fedagg_session_stage_tiled``)."""
+        nseg, ptrs, sizes, keep = _segments(rows)
+        self._bump(d_dst)
+        _native.check(self.lib.fedagg_session_stage_tiled(self._h, ctypes.c_void_p(d_dst), int(tile_bytes), len(rows),
+                                                          nseg, ptrs, sizes), "session_stage_tiled")
+
     def stage_check(self, d_dst: int, rows: Sequence[Sequence[np.ndarray]], dtype,
                     byte_range: Optional[tuple] = None) -> int:
         """Stage ``rows[0]`` (bytes ``byte_range`` of it, default all) to ``d_dst`` and compare the

@@ -200,6 +200,49 @@ static int staging_round_trip(Pool& pool, std::mt19937_64& rng, uint64_t fail_at
   return memcmp(back.data(), dev.data(), dev.size()) ? 1 : 0;
 }
 
+// The tile-interleaved staging (fedagg_session_stage_tiled): K rows of random segments -> tile t
+// of row k at block t * K + k; every row byte lands where the layout puts it; with fail_at, the
+// fail_at-th copy fails and the call returns the error after its packs drained.
+static int tiled_round_trip(Pool& pool, std::mt19937_64& rng, uint64_t fail_at) {
+  const int K = 1 + (int)(rng() % 7), nseg = 1 + (int)(rng() % 4), R = pool.size() + 2 + (int)(rng() % 3);
+  const uint64_t tb = 16 * (1 + rng() % 8), cb = tb * (1 + rng() % 5);
+  std::vector<uint64_t> len(nseg);
+  uint64_t row = 0;
+  for (auto& l : len) row += (l = 4 * (rng() % 150));
+  std::vector<std::vector<std::vector<char>>> data(K, std::vector<std::vector<char>>(nseg));
+  std::vector<const void*> segs((size_t)K * nseg);
+  for (int k = 0; k < K; ++k)
+    for (int i = 0; i < nseg; ++i) {
+      data[k][i].resize(len[i]);
+      for (auto& c : data[k][i]) c = (char)rng();
+      segs[(size_t)k * nseg + i] = data[k][i].data();
+    }
+  std::vector<char> ring_mem((size_t)R * cb);
+  Ring ring;
+  ring.chunk_bytes = cb;
+  for (int i = 0; i < R; ++i) ring.slot.push_back(ring_mem.data() + (size_t)i * cb);
+  ring.used.assign(R, false);
+  const uint64_t tiles = (row + tb - 1) / tb;
+  std::vector<char> dev((size_t)(tiles * K * tb) + 1, 0);
+  FakeDma dma(R);
+  dma.fail_at = fail_at;
+  const int rc = fedagg_host::stage_tiled_pipeline(dma, pool, ring, segs.data(), len.data(), nseg, K, row, tb,
+                                                   dev.data(), true);
+  dma.drain();
+  if (fail_at) {
+    const uint64_t bpu = cb / tb, units = (tiles * K + bpu - 1) / bpu;
+    return (fail_at <= units) == (rc != 0) ? 0 : 1;
+  }
+  if (rc) return 1;
+  for (int k = 0; k < K; ++k) {
+    std::vector<char> flat;
+    for (int i = 0; i < nseg; ++i) flat.insert(flat.end(), data[k][i].begin(), data[k][i].end());
+    for (uint64_t b = 0; b < row; ++b)
+      if (dev[(size_t)(((b / tb) * K + k) * tb + b % tb)] != flat[b]) return 1;
+  }
+  return dev.back() == 0 ? 0 : 1;  // nothing written past the layout
+}
+
 static int fetch_with_failure(Pool& pool, std::mt19937_64& rng) {
   const int R = pool.size() + 2;
   const uint64_t cb = 256;
@@ -276,6 +319,10 @@ int main() {
       if (staging_round_trip(pool, rng, fail_at, check)) {
         fprintf(stderr, "stage/fetch pipeline failed (threads %d, rep %d, fail_at %llu)\n", threads, rep,
                 (unsigned long long)fail_at);
+        return 1;
+      }
+      if (tiled_round_trip(pool, rng, rep % 4 == 3 ? 1 + rng() % 10 : 0)) {
+        fprintf(stderr, "tiled stage pipeline failed (threads %d, rep %d)\n", threads, rep);
         return 1;
       }
       if (fetch_with_failure(pool, rng)) {

@@ -152,3 +152,46 @@ def test_tiled_matches_rows_at_the_recommended_shape():
     engine.TiledFedAvgPlan("f32", buf, K, w, lay.M, b, lay.pairwise_idx).launch()
     torch.cuda.synchronize()
     assert torch.equal(a[: lay.M].view(torch.int32), b[: lay.M].view(torch.int32))
+
+
+# ---------------------------------------------------------------------------------------------
+# the drop-in host path staging tile-interleaved buckets (fedagg_session_stage_tiled)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 5, 40, 130])
+@pytest.mark.parametrize("wire", [False, True])
+def test_engine_stages_tiled_bit_exact(K, wire):
+    from substrafl_amd.engine import AggregationEngine
+    from substrafl_amd.wire import pack
+
+    rng = np.random.default_rng(K + 1000 * wire)
+    M = 2 * 32768 + 12345
+    shapes, pus, ns = _case(rng, K, M, 3, False)
+    eng = AggregationEngine(device=0)
+    eng.tiled = True  # the layout is recommended from 32 clients over >= 2048 tiles; forced here
+    got = eng.fedavg([pack(p) for p in pus] if wire else pus, ns)
+    assert eng.last_timing["layout"] == "tiles"
+    ref = fedavg_reference_structure(pus, ns)
+    for g, r in zip(got, ref):
+        assert g.shape == r.shape and np.array_equal(_bits(g), _bits(r))
+
+
+@pytest.mark.gpu
+def test_engine_layout_choice():
+    """auto: rows below the recommended shape; fp64 / fp16 and mixed layers always rows."""
+    from substrafl_amd.engine import AggregationEngine
+
+    rng = np.random.default_rng(3)
+    shapes, pus, ns = _case(rng, 4, 5000, 1, False)
+    eng = AggregationEngine(device=0)
+    assert eng.tiled == "auto"
+    got = eng.fedavg(pus, ns)
+    assert eng.last_timing["layout"] == "rows"
+    for g, r in zip(got, fedavg_reference_structure(pus, ns)):
+        assert np.array_equal(_bits(g), _bits(r))
+    eng.tiled = True
+    p64 = [[a.astype(np.float64) for a in p] for p in pus]
+    got = eng.fedavg(p64, ns)
+    assert eng.last_timing["layout"] == "rows"
+    for g, r in zip(got, fedavg_reference_structure(p64, ns)):
+        assert np.array_equal(_bits(g), _bits(r))
