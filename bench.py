@@ -143,17 +143,18 @@ def synth_clients(torch, K, ld, M, kind, device, seed0):
     return buf[:K]
 
 
-def synth_tiled(torch, K, M, kind, device, seed0):
+def synth_tiled(torch, K, M, kind, device, seed0, tv):
     """The same client buckets as synth_clients (client k: Philox seed seed0 + k), laid out
-    tile-interleaved (engine.tiled_client_view): tile t of client k is tile t * K + k."""
+    tile-interleaved with tiles of tv vectors (engine.tiled_client_view): tile t of client k is
+    tile t * K + k."""
     from substrafl_amd.engine import tiled_client_view, tiled_elems
 
     dt = torch.bfloat16 if kind == "bf16" else torch.float32
-    buf = torch.zeros(tiled_elems(kind, K, M), dtype=dt, device=device)
+    buf = torch.zeros(tiled_elems(kind, K, M, tv), dtype=dt, device=device)
     g = torch.Generator(device=device)
     row = None
     for k in range(K):
-        view = tiled_client_view(buf, kind, K, k)
+        view = tiled_client_view(buf, kind, K, k, tv)
         if row is None:
             row = torch.zeros(view.numel(), dtype=torch.float32, device=device)
         g.manual_seed(seed0 + k)
@@ -304,20 +305,21 @@ def main():
             dist.barrier()
 
     stream = torch.cuda.current_stream(device)
-    from substrafl_amd.engine import TiledFedAvgPlan, tiled_recommended
+    from substrafl_amd.engine import TiledFedAvgPlan, tiled_recommended, tiled_tile
 
     tiled = (not scaffold and not client_shard and kind in ("f32", "bf16")
              and (args.layout == "tiles" or (args.layout == "auto" and tiled_recommended(kind, K, M))))
+    tv = tiled_tile(kind, K, M) if tiled else 0
     if args.layout == "tiles" and not tiled:
         print("bench.py: --layout tiles takes the FedAvg fp32/bf16 workloads in param-range mode", file=sys.stderr)
         sys.exit(2)
     if not scaffold:
-        clients = synth_tiled(torch, K, M, kind, device, seed0) if tiled else \
+        clients = synth_tiled(torch, K, M, kind, device, seed0, tv) if tiled else \
             synth_clients(torch, Kr, ld, M, kind, device, seed0)
         out = torch.empty(ld, dtype=torch.float32, device=device)
         w_all = fedavg_weights(n_samples, kind)
         if tiled:
-            plan = TiledFedAvgPlan(kind, clients, K, w_all, M, out, pw)
+            plan = TiledFedAvgPlan(kind, clients, K, w_all, M, out, pw, tv=tv)
             kplan = plan
 
             def step():
@@ -502,7 +504,7 @@ def main():
                 "global_params": M_glob if (client_shard or args.scaling == "strong") else M * world,
                 "layers": len(shapes),
                 "parallelism": parallelism,
-                "layout": "tile-interleaved" if tiled else "rows",
+                "layout": f"tile-interleaved ({tv} vectors per client tile)" if tiled else "rows",
                 "bytes_alg_per_step_job": bytes_job,
                 "bytes_alg_per_launch_rank0": bytes_kernel,
             },
@@ -586,7 +588,7 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
         if env.get("tiled"):  # tile-interleaved buffer: gather each client's sampled elements
             from substrafl_amd.engine import tiled_index
 
-            pos = tiled_index(kind, K, np.arange(K)[:, None], idx[None, :])
+            pos = tiled_index(kind, K, np.arange(K)[:, None], idx[None, :], env["tv"])
             return x[torch.from_numpy(pos.reshape(-1)).to(device)].view(K, -1).to(torch.float64).cpu().numpy()
         xs = x[:, tidx].to(torch.float64) if Kr else torch.zeros((0, idx.size), dtype=torch.float64, device=device)
         if not (client_shard and world > 1):

@@ -72,6 +72,7 @@ const char* fedagg_last_error(void);
  *   "st_sc1"        FedAvg output stores as write-through (sc1) stores (-1 auto: below 32 clients)
  *   "sc_sc1"        Scaffold 4 x 4 tiles: write-through (sc1) output stores
  *   "sc_2l"         Scaffold: one bucket at a time (1: a launch per bucket, 2: one launch, bucket-ordered halves)
+ *   "tiled_few"     recommend tile-interleaved buckets below 32 fp32 clients too (0/1)
  * Returns FEDAGG_EINVAL for an unknown key. */
 int fedagg_tune(const char* key, long long value);
 
@@ -107,11 +108,13 @@ int fedagg_fedavg_bf16(const uint16_t* const* d_clients, const float* h_w, int K
  * T vectors, the last one padded -- makes a workgroup step read one contiguous K x T region
  * (64 x 125M fp32: 1.7 %, 128 x 175M: 3 % faster in tools/c3_layout_probe.hip).  Element i of
  * client k: vector v = i / L (L = 4 fp32, 8 bf16), at ((v / T) * K + k) * T + v % T, lane i % L.
- * T is fixed per element type (FEDAGG_TILE_VECTORS_*: the tile of the kernel the row layout
- * uses from 32 clients over large buckets); any K and M are accepted.  The layout is recommended
+ * T is one of the tiles the tiled kernels walk (FEDAGG_TILE_VECTORS_*: the tiles of the row
+ * layout's kernels from 32 clients over large buckets, and below 32 fp32 clients); any K and M
+ * are accepted.  The layout is recommended
  * where fedagg_fedavg_tile_vectors_*(K, M) returns T (0: keep the row layout, whose kernel for
  * that shape walks another tile).  Buffer: ceil(ceil(M / L) / T) * K * T * 16 bytes. */
 #define FEDAGG_TILE_VECTORS_F32 8192  /* 16 vectors x 512 threads: 128 KiB of fp32 per client */
+#define FEDAGG_TILE_VECTORS_F32_FEW 2048 /* 8 x 256 (the row layout's tile below 32 clients): 32 KiB */
 #define FEDAGG_TILE_VECTORS_BF16 4096 /* 16 vectors x 256 threads: 64 KiB of bf16 per client  */
 uint64_t fedagg_fedavg_tile_vectors_f32(int K, uint64_t M);
 uint64_t fedagg_fedavg_tile_vectors_bf16(int K, uint64_t M);

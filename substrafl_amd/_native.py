@@ -115,6 +115,7 @@ FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
 FEDAGG_TILE_VECTORS_F32 = 8192
+FEDAGG_TILE_VECTORS_F32_FEW = 2048
 FEDAGG_TILE_VECTORS_BF16 = 4096
 FEDAGG_MAX_PAIRWISE = 64
 FEDAGG_FLAT_MAX_LISTS = 4

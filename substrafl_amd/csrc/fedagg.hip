@@ -81,6 +81,8 @@ int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per
 int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
 int g_sc_2l = -1;       // Scaffold: one bucket at a time (-1 auto: from SC_2L_MIN_K clients; 1 / 2 / 0)
 int g_sc_sc1 = 0;       // Scaffold 4 x 4 tiles: write-through (sc1) output stores
+int g_tiled_few = 0;    // recommend the tile-interleaved layout below 32 fp32 clients too (fedagg_tune "tiled_few";
+                        // 8 x 25M: 134.5 vs 134.4 us on rows, profiles/r02_layout_c2_*.json -- no gain)
 int g_st_sc1 = -1;      // FedAvg: write-through (sc1) output stores (-1: auto, below SC1_MAX_K clients)
 int g_fa_blk = 0;       // FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto, 256, 512)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
@@ -1966,21 +1968,36 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
 }
 
 // Tile-interleaved buckets (fedagg_fedavg_tiled_*): the tiled kernels walk the same tiles as the
-// auto shapes from 32 clients over large buckets (16 vectors x 512 threads for fp32, 16 x 256
-// with buffer loads for bf16).  The layout is recommended (fedagg_fedavg_tile_vectors_*) where
-// the row-layout auto shape is that very tile; the tiled entry points take any K and M.
+// row-layout auto shapes -- fp32: 16 vectors x 512 threads from 32 clients over large buckets
+// (FEDAGG_TILE_VECTORS_F32), 8 x 256 with write-through stores below 32 clients
+// (FEDAGG_TILE_VECTORS_F32_FEW); bf16: 16 x 256 with buffer loads.  The layout is recommended
+// (fedagg_fedavg_tile_vectors_*) where the row-layout auto shape is that very tile; the tiled
+// entry points take any K and M with one of those tiles.
 template <typename E>
-constexpr uint64_t tiled_tile() {
-  return std::is_same<E, F32>::value ? FEDAGG_TILE_VECTORS_F32 : std::is_same<E, BF16>::value ? FEDAGG_TILE_VECTORS_BF16 : 0;
+bool tiled_tile_ok(uint64_t tv) {
+  if constexpr (std::is_same<E, F32>::value) return tv == FEDAGG_TILE_VECTORS_F32 || tv == FEDAGG_TILE_VECTORS_F32_FEW;
+  if constexpr (std::is_same<E, BF16>::value) return tv == FEDAGG_TILE_VECTORS_BF16;
+  return false;
 }
 
 template <typename E>
 uint64_t tiled_tile_vectors(int K, uint64_t M) {
   if (K <= 0 || !g_nt_load || !g_tile || g_vpt > 0 || g_tpb > 1) return 0;
-  const Shape sh = shape_for<E>(K, M / E::L);
-  if (sh.vpt != 16 || sh.unroll != 2 || sh.pipe) return 0;
-  if constexpr (std::is_same<E, F32>::value) return sh.blk == 2 * FA_BLOCK && !sh.buf ? tiled_tile<E>() : 0;
-  if constexpr (std::is_same<E, BF16>::value) return sh.buf && sh.occ <= 1 ? tiled_tile<E>() : 0;
+  const uint64_t nvec = M / E::L;
+  const Shape sh = shape_for<E>(K, nvec);
+  if (sh.pipe) return 0;
+  if constexpr (std::is_same<E, F32>::value) {
+    if (sh.vpt == 16 && sh.unroll == 2 && sh.blk == 2 * FA_BLOCK && !sh.buf) return FEDAGG_TILE_VECTORS_F32;
+    // the few-client tile with its write-through stores, over >= 1024 workgroup tiles
+    const bool sc1 = g_st_sc1 < 0 ? K < SC1_MAX_K : g_st_sc1 != 0;
+    const bool nts = g_nt_store < 0 ? K >= NT_STORE_MIN_K : g_nt_store != 0;
+    if (g_tiled_few && sh.vpt == 8 && sh.unroll == 4 && sh.blk == FA_BLOCK && !sh.buf && sh.occ <= 1 && sc1 && nts &&
+        nvec >= (uint64_t)FEDAGG_TILE_VECTORS_F32_FEW * 1024)
+      return FEDAGG_TILE_VECTORS_F32_FEW;
+    return 0;
+  }
+  if constexpr (std::is_same<E, BF16>::value)
+    return sh.vpt == 16 && sh.unroll == 2 && sh.buf && sh.occ <= 1 ? FEDAGG_TILE_VECTORS_BF16 : 0;
   return 0;
 }
 
@@ -1990,9 +2007,9 @@ int fedavg_tiled_launch(const typename E::In* base, const typename E::P* w, int 
   if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg_tiled: K must be > 0 (got %lld)", K);
   if (!base || !w || !out) return fail(FEDAGG_EINVAL, "fedavg_tiled: NULL argument");
   if (!aligned16(base) || !aligned16(out)) return fail(FEDAGG_EINVAL, "fedavg_tiled: buffers must be 16-B aligned");
-  if (tv != tiled_tile<E>())
-    return fail(FEDAGG_EINVAL, "fedavg_tiled: the tile must be %lld vectors (FEDAGG_TILE_VECTORS_*)",
-                (long long)tiled_tile<E>());
+  if (!tiled_tile_ok<E>(tv))
+    return fail(FEDAGG_EINVAL, "fedavg_tiled: the tile must be one of FEDAGG_TILE_VECTORS_* (got %lld vectors)",
+                (long long)tv);
   if (P < 0 || (P > 0 && !idx)) return fail(FEDAGG_EINVAL, "fedavg_tiled: bad pairwise index list (P=%lld)", P);
   for (int p = 0; p < P; ++p)
     if (idx[p] >= M) return fail(FEDAGG_EINVAL, "fedavg_tiled: pairwise index %lld out of range", (long long)idx[p]);
@@ -2000,7 +2017,8 @@ int fedavg_tiled_launch(const typename E::In* base, const typename E::P* w, int 
   if (P > 0 && !fuse && !ws) return fail(FEDAGG_EINVAL, "fedavg_tiled: workspace needed for %lld pairwise segments", P);
   constexpr int L = E::L;
   const uint64_t nvec = M / L, pitch = (uint64_t)K * tv;
-  const unsigned grid = grid_for((nvec + 15) / 16);
+  const uint64_t vpt = tv == FEDAGG_TILE_VECTORS_F32_FEW ? 8 : 16;
+  const unsigned grid = grid_for((nvec + vpt - 1) / vpt);
   std::vector<const typename E::In*> x(K);
   for (int k = 0; k < K; ++k) x[k] = base + (uint64_t)k * tv * L;
   for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK) {
@@ -2018,10 +2036,14 @@ int fedavg_tiled_launch(const typename E::In* base, const typename E::P* w, int 
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
     const int first = k0 == 0 ? 1 : 0;
-    if constexpr (std::is_same<E, F32>::value)
-      launch_fedavg_variant<E, true, 1, 16, 2, false, true, 1, false, 2 * FA_BLOCK, true>(grid, s, a, pw, kc, first,
-                                                                                          nvec, M, out, pitch);
-    else
+    if constexpr (std::is_same<E, F32>::value) {
+      if (tv == FEDAGG_TILE_VECTORS_F32_FEW)  // 8 x 256 tile, write-through (sc1) stores
+        launch_fedavg_variant<E, true, 2, 8, 4, false, true, 1, false, FA_BLOCK, true>(grid, s, a, pw, kc, first, nvec,
+                                                                                      M, out, pitch);
+      else
+        launch_fedavg_variant<E, true, 1, 16, 2, false, true, 1, false, 2 * FA_BLOCK, true>(grid, s, a, pw, kc, first,
+                                                                                            nvec, M, out, pitch);
+    } else
       launch_fedavg_variant<E, true, 1, 16, 2, false, true, 1, true, FA_BLOCK, true>(grid, s, a, pw, kc, first, nvec,
                                                                                     M, out, pitch);
     int rc = check_launch("fedavg_kernel (tiled)");
@@ -2464,6 +2486,7 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "sc_2l")) g_sc_2l = value < 0 ? -1 : (value == 0 ? 0 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_sc1")) g_sc_sc1 = value ? 1 : 0;
   else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
+  else if (!strcmp(key, "tiled_few")) g_tiled_few = value ? 1 : 0;
   else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 1024 ? 1024 : (value >= 512 ? 512 : 256));
   else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
   return FEDAGG_OK;

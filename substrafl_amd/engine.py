@@ -165,52 +165,62 @@ TILED_KINDS = ("f32", "bf16")
 _ELEMS_PER_VEC = {"f32": 4, "bf16": 8}
 
 
-def tile_vectors(kind: str) -> int:
-    """16-B vectors per client tile of the tile-interleaved layout (FEDAGG_TILE_VECTORS_*)."""
-    return {"f32": _native.FEDAGG_TILE_VECTORS_F32, "bf16": _native.FEDAGG_TILE_VECTORS_BF16}[kind]
-
-
 def tiled_recommended(kind: str, K: int, M: int) -> bool:
     """Whether the library recommends the tile-interleaved layout for K clients of M elements
-    (its row-layout kernel for that shape walks the same tile; fedagg_fedavg_tile_vectors_*)."""
+    (its row-layout kernel for that shape walks one of the tiled kernels' tiles;
+    fedagg_fedavg_tile_vectors_*)."""
     if kind not in TILED_KINDS:
         return False
     return bool(getattr(_native.load(), f"fedagg_fedavg_tile_vectors_{kind}")(int(K), int(M)))
 
 
-def tiled_elems(kind: str, K: int, M: int) -> int:
-    """Elements of a tile-interleaved buffer of K clients of M elements (last tile padded)."""
-    L, T = _ELEMS_PER_VEC[kind], tile_vectors(kind)
+def tiled_tile(kind: str, K: int, M: int) -> int:
+    """16-B vectors per client tile of the tile-interleaved layout for K clients of M elements:
+    the recommended tile, else the tile of the kernel the row layout would use for K clients
+    (FEDAGG_TILE_VECTORS_*)."""
+    rec = int(getattr(_native.load(), f"fedagg_fedavg_tile_vectors_{kind}")(int(K), int(M)))
+    if rec:
+        return rec
+    if kind == "bf16":
+        return _native.FEDAGG_TILE_VECTORS_BF16
+    return _native.FEDAGG_TILE_VECTORS_F32 if K >= 32 else _native.FEDAGG_TILE_VECTORS_F32_FEW
+
+
+def tiled_elems(kind: str, K: int, M: int, tv: int) -> int:
+    """Elements of a tile-interleaved buffer of K clients of M elements, tiles of ``tv`` 16-B
+    vectors (the last tile of every client padded)."""
+    L = _ELEMS_PER_VEC[kind]
     nvec = -(-int(M) // L)
-    return -(-nvec // T) * int(K) * T * L
+    return -(-nvec // int(tv)) * int(K) * int(tv) * L
 
 
-def tiled_index(kind: str, K: int, k, e):
+def tiled_index(kind: str, K: int, k, e, tv: int):
     """Element offset, in the tile-interleaved buffer, of element ``e`` of client ``k`` (NumPy
-    broadcasting): vector v = e // L of client k sits at ((v // T) * K + k) * T + v % T."""
-    L, T = _ELEMS_PER_VEC[kind], tile_vectors(kind)
+    broadcasting): vector v = e // L of client k sits at ((v // tv) * K + k) * tv + v % tv."""
+    L, T = _ELEMS_PER_VEC[kind], int(tv)
     e = np.asarray(e, dtype=np.int64)
     v = e // L
     return (((v // T) * int(K) + np.asarray(k, dtype=np.int64)) * T + v % T) * L + e % L
 
 
-def tiled_client_view(buf, kind: str, K: int, k: int):
-    """Client ``k``'s tiles of a tile-interleaved torch buffer: a strided ``[tiles, T * L]`` view
+def tiled_client_view(buf, kind: str, K: int, k: int, tv: int):
+    """Client ``k``'s tiles of a tile-interleaved torch buffer: a strided ``[tiles, tv * L]`` view
     (its first M elements in row-major order are the client's bucket)."""
-    L, T = _ELEMS_PER_VEC[kind], tile_vectors(kind)
-    return buf.view(-1, int(K), T * L)[:, int(k), :]
+    return buf.view(-1, int(K), int(tv) * _ELEMS_PER_VEC[kind])[:, int(k), :]
 
 
 class TiledFedAvgPlan(FedAvgPlan):
     """FedAvg over tile-interleaved client buckets (``fedagg_fedavg_tiled_{f32,bf16}``): ``base``
     is one device buffer (tensor or pointer) of :func:`tiled_elems` elements in which tile t of
     client k is tile ``t * K + k``; a workgroup then reads one contiguous K-tile region per step.
-    Same kernel arithmetic and results as :class:`FedAvgPlan` over the row layout."""
+    ``tv``: the tile (default :func:`tiled_tile`).  Same kernel arithmetic and results as
+    :class:`FedAvgPlan` over the row layout."""
 
-    def __init__(self, kind: str, base, K: int, weights: np.ndarray, M: int, out, pairwise_idx=None, ws=None):
+    def __init__(self, kind: str, base, K: int, weights: np.ndarray, M: int, out, pairwise_idx=None, ws=None,
+                 tv: Optional[int] = None):
         if kind not in TILED_KINDS:
             raise ValueError(f"tile-interleaved buckets take {TILED_KINDS}")
-        T = tile_vectors(kind)
+        T = int(tv) if tv is not None else tiled_tile(kind, K, M)
         # the per-client tile-0 pointers size the pairwise workspace and validate K like the rows plan
         super().__init__(kind, [_ptr(base) + k * T * 16 for k in range(int(K))], weights, M, out, pairwise_idx, ws)
         self._keep = (base,) + tuple(self._keep)
@@ -640,8 +650,9 @@ class AggregationEngine:
             else:
                 tiled = self._tiled_rows(rows, R, kind, K, layout.M) if prescale is None else None
                 if tiled is not None:  # tile-interleaved buckets (TiledFedAvgPlan), one gather per pinned chunk
-                    d_bucket = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M) * R.itemsize)
-                    s.stage_tiled(d_bucket, tile_vectors(kind) * 16, tiled)
+                    tv = tiled_tile(kind, K, layout.M)
+                    d_bucket = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, tv) * R.itemsize)
+                    s.stage_tiled(d_bucket, tv * 16, tiled)
                 else:
                     self._stage_rows(s, rows, layout, d_bucket, prescale)
             tm["stage_s"] = tm.get("stage_s", 0.0) + time.perf_counter() - t0
@@ -650,7 +661,7 @@ class AggregationEngine:
             ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, layout.pairwise_idx.size, 8))
             t1 = time.perf_counter()
             if tiled is not None:
-                TiledFedAvgPlan(kind, d_bucket, K, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
+                TiledFedAvgPlan(kind, d_bucket, K, w, layout.M, d_out, layout.pairwise_idx, ws, tv).launch(s.stream)
             else:
                 ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
                 FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)

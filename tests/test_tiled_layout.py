@@ -20,20 +20,24 @@ def _bits(a):
 # ---------------------------------------------------------------------------------------------
 # layout arithmetic and argument checks (CPU)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("kind", ["f32", "bf16"])
+TILES = [("f32", 8192), ("f32", 2048), ("bf16", 4096)]
+L_OF = {"f32": 4, "bf16": 8}
+
+
+@pytest.mark.parametrize("kind,tv", TILES)
 @pytest.mark.parametrize("K,M", [(1, 5), (3, 70_001), (7, 300_000)])
-def test_tiled_index_is_a_bijection_into_the_buffer(kind, K, M):
+def test_tiled_index_is_a_bijection_into_the_buffer(kind, tv, K, M):
     from substrafl_amd import engine
 
-    n = engine.tiled_elems(kind, K, M)
+    n = engine.tiled_elems(kind, K, M, tv)
     e = np.arange(M)
-    pos = np.concatenate([engine.tiled_index(kind, K, k, e) for k in range(K)])
+    pos = np.concatenate([engine.tiled_index(kind, K, k, e, tv) for k in range(K)])
     assert pos.min() >= 0 and pos.max() < n
     assert np.unique(pos).size == pos.size
     # a client's elements keep their order inside a tile
-    T, L = engine.tile_vectors(kind), {"f32": 4, "bf16": 8}[kind]
-    p0 = engine.tiled_index(kind, K, 0, e)
-    inside = (e[1:] // (T * L)) == (e[:-1] // (T * L))
+    L = L_OF[kind]
+    p0 = engine.tiled_index(kind, K, 0, e, tv)
+    inside = (e[1:] // (tv * L)) == (e[:-1] // (tv * L))
     assert np.all(np.diff(p0)[inside] == 1)
 
 
@@ -45,13 +49,21 @@ def test_tiled_entry_rejects_a_foreign_tile():
     idx = (ctypes.c_uint64 * 1)(0)
     assert lib.fedagg_fedavg_tiled_f32(256, w, 1, 1024, 4096, idx, 0, None, 256, None) == -1
     assert b"tile must be" in lib.fedagg_last_error()
+    assert lib.fedagg_fedavg_tiled_f32(256, w, 1, 1024, 1024, idx, 0, None, 256, None) == -1
     assert lib.fedagg_fedavg_tiled_bf16(256, w, 1, 1024, 8192, idx, 0, None, 256, None) == -1
     assert lib.fedagg_fedavg_tiled_f32(None, w, 1, 1024, 8192, idx, 0, None, 256, None) == -1
     # recommended exactly where the row layout's kernel walks the same tile (>= 32 clients, large buckets)
     assert lib.fedagg_fedavg_tile_vectors_f32(64, 125_000_000) == _native.FEDAGG_TILE_VECTORS_F32
     assert lib.fedagg_fedavg_tile_vectors_bf16(128, 350_000_000) == _native.FEDAGG_TILE_VECTORS_BF16
+    assert lib.fedagg_fedavg_tile_vectors_f32(64, 1_000_000) == 0  # another tile for 64 small buckets
+    # below 32 clients the layout measured no faster (C2): recommended only with the tiled_few knob
     assert lib.fedagg_fedavg_tile_vectors_f32(8, 25_000_000) == 0
-    assert lib.fedagg_fedavg_tile_vectors_f32(64, 1_000_000) == 0
+    assert lib.fedagg_tune(b"tiled_few", 1) == 0
+    try:
+        assert lib.fedagg_fedavg_tile_vectors_f32(8, 25_000_000) == _native.FEDAGG_TILE_VECTORS_F32_FEW
+        assert lib.fedagg_fedavg_tile_vectors_f32(8, 1_000_000) == 0  # too few tiles
+    finally:
+        assert lib.fedagg_tune(b"tiled_few", 0) == 0
 
 
 # ---------------------------------------------------------------------------------------------
@@ -59,7 +71,8 @@ def test_tiled_entry_rejects_a_foreign_tile():
 # ---------------------------------------------------------------------------------------------
 def _case(rng, K, M, P, bf16):
     """K clients of M elements as layers, P of them numel == 1 (scattered), values N(0,1) x 10^U."""
-    cuts = np.sort(rng.choice(np.arange(1, M - 1), size=P, replace=False)) if P else np.array([], int)
+    # numel == 1 layers at cuts >= 3 apart: every other layer has >= 2 elements
+    cuts = np.sort(rng.choice(np.arange(2, M - 3, 3), size=P, replace=False)) if P else np.array([], int)
     shapes, pos = [], 0
     for c in cuts:
         if c > pos:
@@ -78,41 +91,41 @@ def _case(rng, K, M, P, bf16):
     return shapes, pus, ns
 
 
-def _tiled_device(torch, kind, pus, M):
+def _tiled_device(torch, kind, pus, M, tv):
     from substrafl_amd import engine
 
     K = len(pus)
     dt = torch.bfloat16 if kind == "bf16" else torch.float32
-    buf = torch.zeros(engine.tiled_elems(kind, K, M), dtype=dt, device="cuda")
-    T, L = engine.tile_vectors(kind), {"f32": 4, "bf16": 8}[kind]
-    tiles = buf.numel() // (K * T * L)
+    buf = torch.zeros(engine.tiled_elems(kind, K, M, tv), dtype=dt, device="cuda")
+    L = L_OF[kind]
+    tiles = buf.numel() // (K * tv * L)
     for k, layers in enumerate(pus):
-        row = torch.zeros(tiles * T * L, dtype=torch.float32)
+        row = torch.zeros(tiles * tv * L, dtype=torch.float32)
         row[:M] = torch.from_numpy(np.concatenate([a.ravel() for a in layers]))
-        engine.tiled_client_view(buf, kind, K, k).copy_(row.view(tiles, T * L).to(dt).cuda())
+        engine.tiled_client_view(buf, kind, K, k, tv).copy_(row.view(tiles, tv * L).to(dt).cuda())
     return buf
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["f32", "bf16"])
+@pytest.mark.parametrize("kind,tv", TILES)
 @pytest.mark.parametrize("K,tiles,P", [(1, 1, 0), (3, 2, 1), (9, 3, 5), (40, 2, 16), (20, 2, 17), (130, 1, 3)])
-def test_tiled_fedavg_bit_exact(kind, K, tiles, P):
+def test_tiled_fedavg_bit_exact(kind, tv, K, tiles, P):
     import torch
 
     from substrafl_amd import engine
     from substrafl_amd.layout import BucketLayout
 
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
-    rng = np.random.default_rng(K * 31 + tiles + P)
-    T, L = engine.tile_vectors(kind), {"f32": 4, "bf16": 8}[kind]
-    M = (tiles - 1) * T * L + int(rng.integers(1, T * L))  # a partial last tile, any remainder mod L
+    rng = np.random.default_rng(K * 31 + tiles + P + tv)
+    L = L_OF[kind]
+    M = (tiles - 1) * tv * L + int(rng.integers(1, tv * L))  # a partial last tile, any remainder mod L
     shapes, pus, ns = _case(rng, K, M, P, kind == "bf16")
     lay = BucketLayout(range(len(shapes)), shapes, np.float32)
     assert lay.M == M and lay.pairwise_idx.size == P
-    buf = _tiled_device(torch, kind, pus, M)
+    buf = _tiled_device(torch, kind, pus, M, tv)
     out = torch.full((lay.ld,), np.nan, dtype=torch.float32, device="cuda")
     w = engine.fedavg_weights(ns, kind)
-    engine.TiledFedAvgPlan(kind, buf, K, w, M, out, lay.pairwise_idx).launch()
+    engine.TiledFedAvgPlan(kind, buf, K, w, M, out, lay.pairwise_idx, tv=tv).launch()
     torch.cuda.synchronize()
     got = out[:M].cpu().numpy()
     ref = np.concatenate([r.ravel() for r in fedavg_reference_structure(pus, ns)])
@@ -137,19 +150,20 @@ def test_tiled_matches_rows_at_the_recommended_shape():
     for k in range(K):
         g.manual_seed(7 + k)
         rows[k].normal_(generator=g)
-    T, L = engine.tile_vectors("f32"), 4
-    buf = torch.zeros(engine.tiled_elems("f32", K, lay.M), dtype=torch.float32, device="cuda")
+    T, L = engine.tiled_tile("f32", K, lay.M), 4
+    assert T == 8192
+    buf = torch.zeros(engine.tiled_elems("f32", K, lay.M, T), dtype=torch.float32, device="cuda")
     tiles = buf.numel() // (K * T * L)
     for k in range(K):
         row = torch.zeros(tiles * T * L, dtype=torch.float32, device="cuda")
         row[: lay.M] = rows[k, : lay.M]
-        engine.tiled_client_view(buf, "f32", K, k).copy_(row.view(tiles, T * L))
+        engine.tiled_client_view(buf, "f32", K, k, T).copy_(row.view(tiles, T * L))
     ns = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
     w = engine.fedavg_weights(ns, "f32")
     a = torch.empty(lay.ld, dtype=torch.float32, device="cuda")
     b = torch.empty(lay.ld, dtype=torch.float32, device="cuda")
     engine.FedAvgPlan("f32", rows, w, lay.M, a, lay.pairwise_idx).launch()
-    engine.TiledFedAvgPlan("f32", buf, K, w, lay.M, b, lay.pairwise_idx).launch()
+    engine.TiledFedAvgPlan("f32", buf, K, w, lay.M, b, lay.pairwise_idx, tv=T).launch()
     torch.cuda.synchronize()
     assert torch.equal(a[: lay.M].view(torch.int32), b[: lay.M].view(torch.int32))
 
