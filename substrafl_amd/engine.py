@@ -317,6 +317,17 @@ def _row_pointers(clients) -> List[int]:
 # ======================================================================================
 # host entry (drop-in path)
 # ======================================================================================
+def direct_rows(rows: List[List[np.ndarray]], dt: np.dtype, M: int) -> Optional[List[List[np.ndarray]]]:
+    """Rows as stageable segments when every array already has dtype ``dt`` (flat wire-format
+    rows as one segment each), else None."""
+    if not all(a.dtype == dt for row in rows for a in row):
+        return None
+    flats = [flat_of(row) for row in rows]
+    if all(f is not None and f.size == M for f in flats):
+        return [[f] for f in flats]
+    return [[np.ascontiguousarray(a) for a in row] for row in rows]
+
+
 def serialized(method):
     """Run an engine call under the locks of the engine's devices (``runtime.device_lock``), taken
     in device order, so concurrent callers never share a session's buffers mid-call."""
@@ -531,16 +542,12 @@ class AggregationEngine:
     def _tiled_rows(self, rows, R: np.dtype, kind: str, K: int, M: int):
         """The rows as stageable segments when this call stages them tile-interleaved (``tiled``:
         "auto" where the library recommends the layout, True wherever a tiled kernel exists for
-        the dtype, False never), else None."""
+        the dtype, False never), else None (also when a dtype conversion is needed: those stage
+        raw rows and cast on the device)."""
         mode = self.tiled
         if mode is False or kind not in TILED_KINDS or (mode == "auto" and not tiled_recommended(kind, K, M)):
             return None
-        if not all(a.dtype == R for row in rows for a in row):
-            return None  # dtype conversions stage raw rows and cast on the device
-        flats = [flat_of(row) for row in rows]
-        if all(f is not None and f.size == M for f in flats):
-            return [[f] for f in flats]  # flat wire format: one segment per client
-        return [[np.ascontiguousarray(a) for a in row] for row in rows]
+        return direct_rows(rows, R, M)
 
     def session(self):
         s = runtime.session(self._index())

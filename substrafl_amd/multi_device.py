@@ -34,11 +34,10 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native, runtime
-from .engine import (AggregationEngine, FedAvgPlan, ScaffoldPlan, equal_count, fedavg_weights, kind_of,
-                     scaffold_weights, serialized)
+from .engine import (AggregationEngine, FedAvgPlan, ScaffoldPlan, direct_rows, equal_count, fedavg_weights,
+                     kind_of, scaffold_weights, serialized)
 from .layout import ROW_ALIGN_BYTES, BucketLayout
 from .sharding import SHARD_ALIGN, shard_bounds
-from .wire import flat_of
 
 HBM_HEADROOM = 0.85  # fraction of a device's free HBM one sub-range may use when no cap is given
 
@@ -169,17 +168,6 @@ class MultiDeviceEngine:
             if e is not None:
                 raise e
 
-    @staticmethod
-    def _rows_direct(rows: List[List[np.ndarray]], dt: np.dtype, M: int) -> Optional[List[List[np.ndarray]]]:
-        """Rows as stageable segments when every array already has dtype ``dt`` (flat wire-format
-        rows as one segment), else None."""
-        if not all(a.dtype == dt for row in rows for a in row):
-            return None
-        flats = [flat_of(row) for row in rows]
-        if all(f is not None and f.size == M for f in flats):
-            return [[f] for f in flats]
-        return [[np.ascontiguousarray(a) for a in row] for row in rows]
-
     # ----------------------------------------------------------------------------------
     @serialized
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
@@ -196,7 +184,7 @@ class MultiDeviceEngine:
             return self._single().fedavg(parameters_updates, n_samples, wire)  # dtype groups / casts
         layout = BucketLayout(list(range(L)), [a.shape for a in parameters_updates[0]], R)
         M, isz = layout.M, R.itemsize
-        rows = self._rows_direct(parameters_updates, R, M)
+        rows = direct_rows(parameters_updates, R, M)
         kind = kind_of(R)
         w = fedavg_weights(n_samples, kind)
         pw_all = layout.pairwise_idx.astype(np.int64)
@@ -260,11 +248,11 @@ class MultiDeviceEngine:
         isz = sdt.itemsize
         layout = BucketLayout(list(range(L)), shapes[0], sdt)
         M = layout.M
-        rows_d = self._rows_direct(parameters_updates, sdt, M)
-        rows_c = self._rows_direct(control_variate_updates, sdt, M)
+        rows_d = direct_rows(parameters_updates, sdt, M)
+        rows_c = direct_rows(control_variate_updates, sdt, M)
         same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
                      for row in server_control_variates[1:])
-        rows_s = self._rows_direct(server_control_variates[:1] if same_c else server_control_variates, sdt, M)
+        rows_s = direct_rows(server_control_variates[:1] if same_c else server_control_variates, sdt, M)
         # identical c objects: one staged copy, no check; otherwise one staged copy and the check of
         # the others on the host while staging (Session.stage_check; see engine.scaffold)
         host_c = not same_c and self._single().c_check == "host"
