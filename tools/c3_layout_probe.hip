@@ -142,11 +142,18 @@ void tiles(uint64_t m_req) {
 }
 
 // no argument: the C3 shape (64 x 125M, every tile); "c5": 64 x 125M and 128 x 175M fp32 (the C5
-// footprint, 89.6 GB, with C5's 128 client streams) side by side; "tiles": tile shapes at 128 x 175M
+// footprint, 89.6 GB, with C5's 128 client streams) side by side; "tiles": tile shapes at 128 x 175M;
+// "kscan": 8, 16 and 32 clients
 int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "";
   if (mode[0] == 't') {
     tiles<128>(175000000ull);
+    return 0;
+  }
+  if (mode[0] == 'k') {  // "kscan": rows vs interleaved at 8, 16 and 32 clients (~16 GB each)
+    sweep<8>(500000000ull, false);
+    sweep<16>(250000000ull, false);
+    sweep<32>(125000000ull, false);
     return 0;
   }
   const bool c5 = mode[0] == 'c' && mode[1] == '5';
