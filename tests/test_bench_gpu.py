@@ -67,3 +67,13 @@ def test_multi_device_engine_line():
     line = _bench("--engine", "multi-device", "--workload", "c2", "--gpus", "2", "--steps", "2", "--warmup", "1")
     assert line["n_gpus"] == 2 and len(line["shards"]) == 2
     assert all(s["kernel_ms"] > 0 for s in line["shards"])
+
+
+def test_tiled_layout_line():
+    """--layout tiles (c2: the few-client tile) and the default auto (c2: rows, below the
+    recommended shape): both parity-clean, the layout named in the config."""
+    tiles = _bench("--workload", "c2", "--layout", "tiles", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert tiles["parity"]["mismatches"] == 0
+    assert tiles["config"]["layout"].startswith("tile-interleaved (2048")
+    auto = _bench("--workload", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert auto["config"]["layout"] == "rows"
