@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered", "striped"])
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
+    ap.add_argument("--tile", type=int, default=0, help="tiles layout: 16-B vectors per client tile "
+                    "(0: the library's choice; FEDAGG_TILE_VECTORS_*)")
     ap.add_argument("--layout", default="auto", choices=["rows", "tiles", "auto"],
                     help="client buckets in HBM: [K, ld] rows, tile-interleaved (fedagg_fedavg_tiled_*; "
                          "FedAvg fp32/bf16), or (default) tiles where the library recommends them -- the "
@@ -75,6 +77,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--grid-cap", type=int, default=0)
+    ap.add_argument("--tune", default="", help="library launch knobs for experiments, key=value[,key=value] "
+                    "(fedagg_tune; the default run sets none)")
     ap.add_argument("--nontemporal", type=int, default=-1)
     ap.add_argument("--traffic", default="", help="JSON with PMC-derived bytes per launch (profiles/)")
     ap.add_argument("--cpu-only", action="store_true",
@@ -241,6 +245,8 @@ def main():
         _native.tune(grid_cap=args.grid_cap)
     if args.nontemporal >= 0:
         _native.tune(nt_load=args.nontemporal)
+    if args.tune:
+        _native.tune(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
 
     wl = WORKLOADS[args.workload]
     K, M_glob, kind = wl["K"], wl["M"], wl["kind"]
@@ -309,7 +315,7 @@ def main():
 
     tiled = (not scaffold and not client_shard and kind in ("f32", "bf16")
              and (args.layout == "tiles" or (args.layout == "auto" and tiled_recommended(kind, K, M))))
-    tv = tiled_tile(kind, K, M) if tiled else 0
+    tv = (args.tile or tiled_tile(kind, K, M)) if tiled else 0
     if args.layout == "tiles" and not tiled:
         print("bench.py: --layout tiles takes the FedAvg fp32/bf16 workloads in param-range mode", file=sys.stderr)
         sys.exit(2)
