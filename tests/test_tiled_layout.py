@@ -209,3 +209,29 @@ def test_engine_layout_choice():
     assert eng.last_timing["layout"] == "rows"
     for g, r in zip(got, fedavg_reference_structure(p64, ns)):
         assert np.array_equal(_bits(g), _bits(r))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(24))
+def test_tiled_random_sweep(seed):
+    """Random client counts (1-300), bucket lengths (1-3 tiles, any remainder), numel == 1 counts
+    (0-24) and tiles, against the oracle."""
+    import torch
+
+    from substrafl_amd import engine
+    from substrafl_amd.layout import BucketLayout
+
+    rng = np.random.default_rng(4242 + seed)
+    kind, tv = TILES[seed % len(TILES)]
+    K = int(rng.integers(1, 301))
+    L = L_OF[kind]
+    M = int(rng.integers(64, 3 * tv * L))
+    P = int(rng.integers(0, min(25, M // 3 - 2)))
+    shapes, pus, ns = _case(rng, K, M, P, kind == "bf16")
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    buf = _tiled_device(torch, kind, pus, M, tv)
+    out = torch.empty(lay.ld, dtype=torch.float32, device="cuda")
+    engine.TiledFedAvgPlan(kind, buf, K, engine.fedavg_weights(ns, kind), M, out, lay.pairwise_idx, tv=tv).launch()
+    torch.cuda.synchronize()
+    ref = np.concatenate([r.ravel() for r in fedavg_reference_structure(pus, ns)])
+    assert np.array_equal(_bits(out[:M].cpu().numpy()), _bits(ref))
