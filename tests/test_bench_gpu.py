@@ -77,3 +77,11 @@ def test_tiled_layout_line():
     assert tiles["config"]["layout"].startswith("tile-interleaved (2048")
     auto = _bench("--workload", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
     assert auto["config"]["layout"] == "rows"
+
+
+def test_default_workload_line():
+    """The driver's own command shape on the default workload (C3, tile-interleaved buckets)."""
+    line = _bench("--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert line["config"]["workload"] == "fedavg_fp32_64x125M"
+    assert line["config"]["layout"].startswith("tile-interleaved (8192")
+    assert line["parity"]["mismatches"] == 0 and 0.5 < line["roofline"]["frac"] < 1
