@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 8
+#define FEDAGG_ABI_VERSION 9
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -333,6 +333,11 @@ int fedagg_session_stage_range(fedagg_session* s, void* d_dst, uint64_t ld_bytes
  * session's chunk_bytes); d_dst holds ceil(row / tile_bytes) * K * tile_bytes bytes. */
 int fedagg_session_stage_tiled(fedagg_session* s, void* d_dst, uint64_t tile_bytes, int K, int nseg,
                                const void* const* h_seg, const uint64_t* seg_bytes);
+/* ONE row (client k of K; nseg host segments) into the same tile-interleaved layout: its tile t
+ * lands at d_dst + (t * K + k) * tile_bytes, one strided 2-D H2D copy per pinned chunk -- the
+ * per-client staging of an ingest, where the clients arrive one by one (engine.ingest). */
+int fedagg_session_stage_tiled_row(fedagg_session* s, void* d_dst, uint64_t tile_bytes, int K, int k, int nseg,
+                                   const void* const* h_seg, const uint64_t* seg_bytes);
 /* Scaffold's server-control-variate check on the host, during staging (scaffold.py:193-196,
  * np.testing.assert_array_equal(c_0, c_k)): K clients' c rows (nseg host segments each, as
  * fedagg_session_stage); ONE copy -- bytes [byte_lo, byte_hi) of row 0 -- is staged to d_dst, the

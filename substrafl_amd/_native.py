@@ -97,6 +97,7 @@ SIGNATURES = {
     "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
     "fedagg_session_stage_range": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64]),
     "fedagg_session_stage_tiled": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
+    "fedagg_session_stage_tiled_row": (c_int, [c_void, c_void, c_u64, c_int, c_int, c_int, P(c_void), P(c_u64)]),
     "fedagg_session_stage_check": (c_int, [c_void, c_void, c_int, c_int, P(c_void), P(c_u64), c_u64, c_u64, c_int,
                                            P(c_u64)]),
     "fedagg_session_event_record": (c_int, [c_void, c_int]),
@@ -110,7 +111,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

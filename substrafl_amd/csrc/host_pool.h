@@ -172,14 +172,15 @@ inline uint64_t check_rows(Pool& pool, const void* const* h_seg, const uint64_t*
 }
 
 // The staging ring: `units` pieces, unit u packed by a worker into ring slot u % R
-// (pack(u, slot) on the pool) and copied to the device by the calling thread (dest(u, &d, &n):
-// n bytes of the slot to device address d; alternate units over two queues with two_queues).
+// (pack(u, slot) on the pool) and copied to the device by the calling thread (copy(u, slot, q):
+// enqueue the unit's copies from the slot on queue q, alternating over two queues with two_queues;
+// returns 0 or an error code).
 // In-order window: R-1 packs run ahead of the copy being enqueued; a slot is refilled only after
 // the copy that read it completed, while the next copy is already in flight, so the link never
 // waits on the enqueueing thread.  On an error the packs already submitted are waited for (they
 // read the caller's segments and write the ring) before the code is returned.
-template <class Eng, class Pack, class Dest>
-int ring_stage(Eng& eng, Pool& pool, Ring& ring, uint64_t units, bool two_queues, Pack pack, Dest dest) {
+template <class Eng, class Pack, class Copy>
+int ring_stage(Eng& eng, Pool& pool, Ring& ring, uint64_t units, bool two_queues, Pack pack, Copy copy) {
   const int R = ring.size();
   const bool two = two_queues && units > 1;
   std::vector<Done> done(units ? std::min<uint64_t>(units, (uint64_t)R) : 1);
@@ -204,11 +205,8 @@ int ring_stage(Eng& eng, Pool& pool, Ring& ring, uint64_t units, bool two_queues
     const int slot = (int)(u % R);
     done[slot].wait();
     pending[slot] = false;
-    char* d = nullptr;
-    uint64_t n = 0;
-    dest(u, &d, &n);
     const int q = (two && (u & 1)) ? 1 : 0;
-    rc = eng.h2d(q, d, ring.slot[slot], n);
+    rc = copy(u, static_cast<const char*>(ring.slot[slot]), q);
     if (!rc) rc = eng.mark(slot, q);
     if (!rc) ring.used[slot] = true;
     if (!rc && next_submit < units) submit(next_submit++);
@@ -235,10 +233,9 @@ int stage_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, c
         const uint64_t a = (u % per_row) * cb, b = std::min(row, a + cb);
         gather_range(h_seg + (size_t)(u / per_row) * nseg, seg_bytes, nseg, byte_lo + a, byte_lo + b, dst);
       },
-      [=](uint64_t u, char** d, uint64_t* n) {
+      [&, per_row, cb](uint64_t u, const char* slot, int q) {
         const uint64_t a = (u % per_row) * cb;
-        *d = d_dst + (u / per_row) * ld_bytes + a;
-        *n = std::min(row, a + cb) - a;
+        return eng.h2d(q, d_dst + (u / per_row) * ld_bytes + a, slot, std::min(row, a + cb) - a);
       });
   if (rc || !check_esz || K < 2) return rc;
   const uint64_t bad = check_rows(pool, h_seg, seg_bytes, nseg, K, byte_lo, row, check_esz);
@@ -266,9 +263,29 @@ int stage_tiled_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_
           gather_range(h_seg + (size_t)(j % (uint64_t)K) * nseg, seg_bytes, nseg, a, b, dst + (j - u * bpu) * tb);
         }
       },
-      [=](uint64_t u, char** d, uint64_t* n) {
-        *d = d_dst + u * bpu * tb;
-        *n = (std::min(blocks, (u + 1) * bpu) - u * bpu) * tb;
+      [&, blocks, bpu](uint64_t u, const char* slot, int q) {
+        return eng.h2d(q, d_dst + u * bpu * tb, slot, (std::min(blocks, (u + 1) * bpu) - u * bpu) * tb);
+      });
+}
+
+// ONE row (client k of K) into the tile-interleaved layout, as its bytes arrive (engine.ingest):
+// each unit is a run of whole tiles of the row, packed contiguous into a pinned slot and copied
+// with ONE 2-D copy whose rows are the tiles (width tb, source pitch tb, destination pitch K * tb,
+// first destination d_dst + (t0 * K + k) * tb).  Eng::h2d_2d(q, d, dpitch, h, spitch, width, height).
+template <class Eng>
+int stage_row_tiled_pipeline(Eng& eng, Pool& pool, Ring& ring, const void* const* h_seg, const uint64_t* seg_bytes,
+                             int nseg, uint64_t row, uint64_t tb, int K, int k, char* d_dst, bool two_queues) {
+  if (!tb || tb > ring.chunk_bytes || K <= 0 || k < 0 || k >= K) return -1;
+  const uint64_t tiles = row ? (row + tb - 1) / tb : 0, tpu = ring.chunk_bytes / tb;
+  return ring_stage(
+      eng, pool, ring, (tiles + tpu - 1) / tpu, two_queues,
+      [=](uint64_t u, char* dst) {
+        const uint64_t a = u * tpu * tb;
+        gather_range(h_seg, seg_bytes, nseg, a, std::min(row, a + tpu * tb), dst);
+      },
+      [&, tiles, tpu](uint64_t u, const char* slot, int q) {
+        const uint64_t t0 = u * tpu, n = std::min(tiles, t0 + tpu) - t0;
+        return eng.h2d_2d(q, d_dst + (t0 * (uint64_t)K + (uint64_t)k) * tb, (uint64_t)K * tb, slot, tb, tb, n);
       });
 }
 

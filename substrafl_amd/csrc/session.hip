@@ -145,6 +145,12 @@ struct HipEngine {
     hipError_t e = hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, q ? s->xstream : s->stream);
     return e == hipSuccess ? FEDAGG_OK : hip_fail("hipMemcpyAsync(H2D)", e);
   }
+  int h2d_2d(int q, void* d, uint64_t dpitch, const void* h, uint64_t spitch, uint64_t width, uint64_t height) {
+    if (injected()) return hip_fail("hipMemcpy2DAsync(H2D) [injected by the fail_copy_after knob]", hipErrorUnknown);
+    hipError_t e = hipMemcpy2DAsync(d, dpitch, h, spitch, width, height, hipMemcpyHostToDevice,
+                                    q ? s->xstream : s->stream);
+    return e == hipSuccess ? FEDAGG_OK : hip_fail("hipMemcpy2DAsync(H2D)", e);
+  }
   int d2h(void* h, const void* d, uint64_t n) {
     if (injected()) return hip_fail("hipMemcpyAsync(D2H) [injected by the fail_copy_after knob]", hipErrorUnknown);
     hipError_t e = hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s->stream);
@@ -376,6 +382,27 @@ int fedagg_session_stage_tiled(fedagg_session* s, void* d_dst, uint64_t tile_byt
   return stage_run_with(s, [&](HipEngine& eng, bool two) {
     return fedagg_host::stage_tiled_pipeline(eng, s->workers(), s->ring, h_seg, seg_bytes, nseg, K, row, tile_bytes,
                                              static_cast<char*>(d_dst), two);
+  });
+}
+
+int fedagg_session_stage_tiled_row(fedagg_session* s, void* d_dst, uint64_t tile_bytes, int K, int k, int nseg,
+                                   const void* const* h_seg, const uint64_t* seg_bytes) {
+  if (nseg < 0 || (nseg > 0 && !seg_bytes)) return FEDAGG_EINVAL;
+  if (K <= 0 || k < 0 || k >= K) {
+    fedagg_internal::set_error("fedagg_session_stage_tiled_row: need 0 <= k < K");
+    return FEDAGG_EINVAL;
+  }
+  uint64_t full = 0, row = 0;
+  for (int i = 0; i < nseg; ++i) full += seg_bytes[i];
+  int rc = stage_prepare(s, d_dst, full, 1, nseg, h_seg, seg_bytes, 0, full, &row);
+  if (rc) return rc;
+  if (!tile_bytes || tile_bytes % 16 || tile_bytes > s->chunk_bytes) {
+    fedagg_internal::set_error("fedagg_session_stage_tiled_row: tile_bytes must be a multiple of 16 and <= chunk_bytes");
+    return FEDAGG_EINVAL;
+  }
+  return stage_run_with(s, [&](HipEngine& eng, bool two) {
+    return fedagg_host::stage_row_tiled_pipeline(eng, s->workers(), s->ring, h_seg, seg_bytes, nseg, row, tile_bytes,
+                                                 K, k, static_cast<char*>(d_dst), two);
   });
 }
 

@@ -367,9 +367,9 @@ class AggregationEngine:
         # in parameter ranges (multi_device.MultiDeviceEngine with this one device); default:
         # 85 % of the device's free HBM at call time
         self.max_bucket_bytes = max_bucket_bytes
-        # HBM layout of FedAvg buckets staged by a call (not by ingest, whose clients arrive one by
-        # one and keep the row layout): "auto" = tile-interleaved where fedagg_fedavg_tile_vectors_*
-        # recommends it (from 32 fp32 clients over large buckets), True / False to force
+        # HBM layout of FedAvg buckets (staged by a call, or client by client by ingest): "auto" =
+        # tile-interleaved where fedagg_fedavg_tile_vectors_* recommends it (from 32 fp32 clients
+        # over large buckets), True / False to force
         env = os.environ.get("FEDAGG_TILED", "auto")
         self.tiled: Union[str, bool] = {"0": False, "1": True}.get(env, "auto")
         self._ooc = None
@@ -487,10 +487,20 @@ class AggregationEngine:
                 return None
         plan = []
         s = self.session()
+        self._ingest_K = K
         for (field, slot), row, dt in zip(lists, rows, targets):
             layout = BucketLayout(list(range(len(row))), [a.shape for a in row], dt)
             ld_bytes = layout.ld * dt.itemsize
-            d = s.buffer(slot, K * ld_bytes)
+            kind = kind_of(dt)
+            if strategy != "scaffold" and row[0].dtype == dt and self.tiled is not False and kind in TILED_KINDS and (
+                    self.tiled is True or tiled_recommended(kind, K, layout.M)):
+                # tile-interleaved, as fedavg() would stage them: each client's tiles land at
+                # their K-strided places (Session.stage_tiled_row); ld_bytes -tv marks the layout
+                tv = tiled_tile(kind, K, layout.M)
+                d = s.buffer(slot, tiled_elems(kind, K, layout.M, tv) * dt.itemsize)
+                ld_bytes = -tv
+            else:
+                d = s.buffer(slot, K * ld_bytes)
             self._prestaged[slot] = [d, ld_bytes, {}]
             plan.append((field, slot, layout, d, ld_bytes, row[0].dtype, False))
         if strategy == "scaffold" and self.c_check == "host" and c_row and all(
@@ -514,7 +524,9 @@ class AggregationEngine:
                 return False
         for field, slot, layout, d, ld_bytes, src, check in plan:
             row = list(getattr(state, field))
-            if not check:
+            if not check and ld_bytes < 0:
+                s.stage_tiled_row(d, -ld_bytes * 16, self._ingest_K, k, direct_rows([row], layout.dtype, layout.M)[0])
+            elif not check:
                 self._stage_rows(s, [row], layout, d + k * ld_bytes)
             elif self._c_ref is None:  # the first client loaded: its c is the staged copy
                 self._stage_rows(s, [row], layout, d)
@@ -650,24 +662,34 @@ class AggregationEngine:
                     w[k] = 1  # x * 1 is exact: the client's product was formed in its own dtype
             d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * R.itemsize)
             t0 = time.perf_counter()
-            tiled = None
-            if prescale is None and len(groups) == 1 and self._take_prestaged(
-                    self._B_BUCKET, d_bucket, layout.ld * R.itemsize, rows):
+            tv = None  # tile-interleaved buckets (TiledFedAvgPlan) when set
+            staged = False
+            if prescale is None and len(groups) == 1:
+                rec = self._prestaged.get(self._B_BUCKET)
+                if rec is not None and rec[1] < 0 and kind in TILED_KINDS:  # ingest staged them tiled
+                    d_t = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, -rec[1]) * R.itemsize)
+                    if self._take_prestaged(self._B_BUCKET, d_t, rec[1], rows):
+                        staged, d_bucket, tv = True, d_t, -rec[1]
+                else:
+                    staged = self._take_prestaged(self._B_BUCKET, d_bucket, layout.ld * R.itemsize, rows)
+            if staged:
                 tm["prestaged"] = True
             else:
+                self._prestaged.pop(self._B_BUCKET, None)
                 tiled = self._tiled_rows(rows, R, kind, K, layout.M) if prescale is None else None
-                if tiled is not None:  # tile-interleaved buckets (TiledFedAvgPlan), one gather per pinned chunk
+                if tiled is not None:  # tile-interleaved buckets, one gather per pinned chunk
                     tv = tiled_tile(kind, K, layout.M)
                     d_bucket = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, tv) * R.itemsize)
                     s.stage_tiled(d_bucket, tv * 16, tiled)
                 else:
+                    d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * R.itemsize)  # current after a regrow
                     self._stage_rows(s, rows, layout, d_bucket, prescale)
             tm["stage_s"] = tm.get("stage_s", 0.0) + time.perf_counter() - t0
-            tm["layout"] = "tiles" if tiled is not None else "rows"
+            tm["layout"] = "tiles" if tv is not None else "rows"
             d_out = s.buffer(self._B_OUT, layout.ld * R.itemsize)
             ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, layout.pairwise_idx.size, 8))
             t1 = time.perf_counter()
-            if tiled is not None:
+            if tv is not None:
                 TiledFedAvgPlan(kind, d_bucket, K, w, layout.M, d_out, layout.pairwise_idx, ws, tv).launch(s.stream)
             else:
                 ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]

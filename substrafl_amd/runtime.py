@@ -148,6 +148,15 @@ class Session:
         _native.check(self.lib.fedagg_session_stage_tiled(self._h, ctypes.c_void_p(d_dst), int(tile_bytes), len(rows),
                                                           nseg, ptrs, sizes), "session_stage_tiled")
 
+    def stage_tiled_row(self, d_dst: int, tile_bytes: int, K: int, k: int, row: Sequence[np.ndarray]) -> None:
+        """Client ``k``'s host arrays (bucket order) alone into the tile-interleaved layout of K
+        clients: its tile t at ``d_dst + (t * K + k) * tile_bytes``
+        (``fedagg_session_stage_tiled_row``; the other clients' tiles are left as they are)."""
+        nseg, ptrs, sizes, keep = _segments([row])
+        self._bump(d_dst)
+        _native.check(self.lib.fedagg_session_stage_tiled_row(self._h, ctypes.c_void_p(d_dst), int(tile_bytes), int(K),
+                                                              int(k), nseg, ptrs, sizes), "session_stage_tiled_row")
+
     def stage_check(self, d_dst: int, rows: Sequence[Sequence[np.ndarray]], dtype,
                     byte_range: Optional[tuple] = None) -> int:
         """Stage ``rows[0]`` (bytes ``byte_range`` of it, default all) to ``d_dst`` and compare the

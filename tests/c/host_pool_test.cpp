@@ -126,6 +126,13 @@ struct FakeDma {
     return 0;
   }
   int h2d(int, void* d, const void* s, uint64_t n) { return copy(d, s, n); }
+  int h2d_2d(int, void* d, uint64_t dpitch, const void* s, uint64_t spitch, uint64_t w, uint64_t h) {
+    for (uint64_t i = 0; i < h; ++i) {
+      const int rc = copy(static_cast<char*>(d) + i * dpitch, static_cast<const char*>(s) + i * spitch, w);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   int d2h(void* h, const void* d, uint64_t n) { return copy(h, d, n); }
   int mark(int slot, int) {
     std::lock_guard<std::mutex> g(m);
@@ -226,12 +233,21 @@ static int tiled_round_trip(Pool& pool, std::mt19937_64& rng, uint64_t fail_at) 
   std::vector<char> dev((size_t)(tiles * K * tb) + 1, 0);
   FakeDma dma(R);
   dma.fail_at = fail_at;
-  const int rc = fedagg_host::stage_tiled_pipeline(dma, pool, ring, segs.data(), len.data(), nseg, K, row, tb,
-                                                   dev.data(), true);
+  const bool per_row = rng() % 2 == 0;  // all rows at once, or one row at a time (engine.ingest)
+  int rc = 0;
+  if (per_row) {
+    for (int k = 0; k < K && !rc; ++k)
+      rc = fedagg_host::stage_row_tiled_pipeline(dma, pool, ring, segs.data() + (size_t)k * nseg, len.data(), nseg, row,
+                                                 tb, K, k, dev.data(), true);
+  } else {
+    rc = fedagg_host::stage_tiled_pipeline(dma, pool, ring, segs.data(), len.data(), nseg, K, row, tb, dev.data(),
+                                           true);
+  }
   dma.drain();
   if (fail_at) {
-    const uint64_t bpu = cb / tb, units = (tiles * K + bpu - 1) / bpu;
-    return (fail_at <= units) == (rc != 0) ? 0 : 1;
+    const uint64_t bpu = cb / tb;  // per_row: one 2-D copy per unit, one fake copy per tile
+    const uint64_t copies = per_row ? tiles * K : (tiles * K + bpu - 1) / bpu;
+    return (fail_at <= copies) == (rc != 0) ? 0 : 1;
   }
   if (rc) return 1;
   for (int k = 0; k < K; ++k) {
