@@ -726,7 +726,7 @@ def multi_device_bench(args):
         lo, hi = eng.last_timing["ranges"][g][0][0], eng.last_timing["ranges"][g][-1][1]
         kms = float(np.median([s.get("kernel_ms", float("nan")) for s in st]))
         b = K * (hi - lo) * 4 + (hi - lo) * 4
-        per_shard.append({"device": devices[g], "params": hi - lo,
+        per_shard.append({"device": devices[g], "params": hi - lo, "layout": st[-1].get("layout"),
                           "stage_s": round(float(np.median([s["stage_s"] for s in st])), 5),
                           "kernel_fetch_s": round(float(np.median([s["kernel_fetch_s"] for s in st])), 5),
                           "kernel_ms": round(kms, 4),

@@ -34,8 +34,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native, runtime
-from .engine import (AggregationEngine, FedAvgPlan, ScaffoldPlan, direct_rows, equal_count, fedavg_weights,
-                     kind_of, scaffold_weights, serialized)
+from .engine import (TILED_KINDS, AggregationEngine, FedAvgPlan, ScaffoldPlan, TiledFedAvgPlan, direct_rows,
+                     equal_count, fedavg_weights, kind_of, scaffold_weights, serialized, tiled_elems,
+                     tiled_recommended, tiled_tile)
 from .layout import ROW_ALIGN_BYTES, BucketLayout
 from .sharding import SHARD_ALIGN, shard_bounds
 
@@ -53,6 +54,20 @@ def _split(lo: int, hi: int, max_elems: int) -> List[Tuple[int, int]]:
         return []
     step = max(SHARD_ALIGN, (max_elems // SHARD_ALIGN) * SHARD_ALIGN)
     return [(a, min(hi, a + step)) for a in range(lo, hi, step)]
+
+
+def _range_rows(rows: List[List[np.ndarray]], lo: int, hi: int) -> List[List[np.ndarray]]:
+    """Elements ``[lo, hi)`` of every row (contiguous arrays in bucket order) as flat views."""
+    out = []
+    for row in rows:
+        segs, a0 = [], 0
+        for a in row:
+            a1 = a0 + a.size
+            if a1 > lo and a0 < hi:
+                segs.append(a.reshape(-1)[max(lo, a0) - a0:min(hi, a1) - a0])
+            a0 = a1
+        out.append(segs)
+    return out
 
 
 class MultiDeviceEngine:
@@ -76,6 +91,11 @@ class MultiDeviceEngine:
         # measurement switch (bench.py --engine multi-device): time each shard's kernel with HIP
         # events on its session stream (adds one event pair per sub-range)
         self.kernel_events = False
+        # FedAvg sub-ranges in the tile-interleaved layout: off unless FEDAGG_TILED=1 ("auto" =
+        # where the library recommends it for the sub-range's K x n).  Off by default: at C3 on
+        # one GPU it staged 0.61-0.82 s per call against 0.61-0.64 s on rows, with the kernel no
+        # faster right after the staging (profiles/r02i_md_bench_c3*.jsonl)
+        self.tiled = {"1": True, "auto": "auto"}.get(os.environ.get("FEDAGG_TILED", "0"), False)
 
     def lock_devices(self) -> List[int]:
         return list(self.devices)
@@ -199,16 +219,25 @@ class MultiDeviceEngine:
                 n = hi - lo
                 ld = _ld(n, isz)
                 t0 = time.perf_counter()
-                d_bucket = s.buffer(self._B_BUCKET, K * ld * isz)
-                s.stage(d_bucket, ld * isz, rows, byte_range=(lo * isz, hi * isz))
+                tv = None
+                if kind in TILED_KINDS and self.tiled is not False and (
+                        self.tiled is True or tiled_recommended(kind, K, n)):
+                    tv = tiled_tile(kind, K, n)
+                    d_bucket = s.buffer(self._B_BUCKET, tiled_elems(kind, K, n, tv) * isz)
+                    s.stage_tiled(d_bucket, tv * 16, _range_rows(rows, lo, hi))
+                else:
+                    d_bucket = s.buffer(self._B_BUCKET, K * ld * isz)
+                    s.stage(d_bucket, ld * isz, rows, byte_range=(lo * isz, hi * isz))
                 t1 = time.perf_counter()
                 d_out = s.buffer(self._B_OUT, ld * isz)
                 ws = s.buffer(self._B_WS, ws_bytes)
                 pw = (pw_all[(pw_all >= lo) & (pw_all < hi)] - lo).astype(np.uint64)
-                ptrs = [d_bucket + k * ld * isz for k in range(K)]
                 if self.kernel_events:
                     s.event_record(0)
-                FedAvgPlan(kind, ptrs, w, n, d_out, pw, ws).launch(s.stream)
+                if tv is not None:
+                    TiledFedAvgPlan(kind, d_bucket, K, w, n, d_out, pw, ws, tv).launch(s.stream)
+                else:
+                    FedAvgPlan(kind, [d_bucket + k * ld * isz for k in range(K)], w, n, d_out, pw, ws).launch(s.stream)
                 if self.kernel_events:
                     s.event_record(1)
                 s.fetch(d_out, out[lo:hi])
@@ -217,6 +246,7 @@ class MultiDeviceEngine:
                 tm["stage_s"] = tm.get("stage_s", 0.0) + t1 - t0
                 tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
                 tm["ranges"] = tm.get("ranges", 0) + 1
+                tm["layout"] = "tiles" if tv is not None else "rows"
 
         self._run(work)
         self.last_timing = {"shards": timing, "total_s": time.perf_counter() - t_start,

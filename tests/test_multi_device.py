@@ -93,15 +93,21 @@ SHAPES = [(300, 257), (1,), (4099,), (7, 1, 3), (1, 1), (65_537,), (1,)]
 @pytest.mark.gpu
 @pytest.mark.parametrize("devices,cap", [((0, 0), None), ((0, 0, 0), 64 * 1024), ((0,) * 5, 9_000)])
 @pytest.mark.parametrize("K", [1, 3, 8, 130])
-def test_fedavg_sharded_bit_exact(gpu, devices, cap, K):
+@pytest.mark.parametrize("tiled", [False, True])
+def test_fedavg_sharded_bit_exact(gpu, devices, cap, K, tiled):
+    """Parameter-range shards on rows or on tile-interleaved buckets (each sub-range staged as its
+    own K x n tiled bucket), bit-identical to fed_avg.py:217-222 either way."""
     from substrafl_amd.multi_device import MultiDeviceEngine
 
     rng = np.random.default_rng(100 + K + len(devices))
     pus = _updates(rng, K, SHAPES)
     ns = [int(v) for v in rng.integers(1, 5000, K)]
     eng = MultiDeviceEngine(devices, max_shard_bytes=cap)
+    eng.tiled = tiled
     got = eng.fedavg(pus, ns)
     _assert_same(got, fedavg_reference_structure(pus, ns))
+    want = "tiles" if tiled else "rows"
+    assert all(t.get("layout") in (None, want) for t in eng.last_timing["shards"])
     if cap:  # out-of-core: some shard streamed more than one sub-range
         assert max(len(r) for r in eng.last_timing["ranges"]) > 1
 
