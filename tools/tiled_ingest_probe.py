@@ -19,9 +19,11 @@ rows = [[base * np.float32(1 + 0.01 * k)] for k in range(K)]
 tv = tiled_tile("f32", K, M)
 ld = (M + 127) // 128 * 128
 s = Session(0)
+if len(sys.argv) > 1:  # pinned-chunk size in MiB (session knob chunk_bytes)
+    s.set("chunk_bytes", int(sys.argv[1]) << 20)
 d_rows = s.buffer(0, K * ld * 4)
 d_t = s.buffer(1, tiled_elems("f32", K, M, tv) * 4)
-res = {"K": K, "M": M, "tv": tv}
+res = {"K": K, "M": M, "tv": tv, "chunk_MiB": int(sys.argv[1]) if len(sys.argv) > 1 else "default"}
 for rep in range(3):
     for name in ("rows", "tiles"):
         s.sync()
