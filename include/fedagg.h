@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 9
+#define FEDAGG_ABI_VERSION 10
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -189,6 +189,13 @@ int fedagg_fedavg_chain_f64(const double* const* d_clients, const double* h_w, i
                             double* d_out, void* stream);
 int fedagg_fedavg_chain_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, uint64_t M, int seed,
                             uint16_t* d_out, void* stream);
+/* The same over a tile-interleaved block (the layout of fedagg_fedavg_tiled_*: tile t of client k
+ * at 16-B vector (t * K + k) * tile_vectors of d_base): a rank's client block in the client-sharded
+ * schedules, where each block holds >= 32 clients (the weak form holds C3's 64 per rank). */
+int fedagg_fedavg_chain_tiled_f32(const float* d_base, const float* h_w, int K, uint64_t M, uint64_t tile_vectors,
+                                  int seed, float* d_out, void* stream);
+int fedagg_fedavg_chain_tiled_bf16(const uint16_t* d_base, const float* h_w, int K, uint64_t M, uint64_t tile_vectors,
+                                   int seed, float* d_out, void* stream);
 /* d_ws[p * stride + kbase + k] = fl(x_k[h_idx[p]] * h_w[k]) in the pairwise-sum type (fp32 for
  * f32/bf16/f16 -- NumPy's HALF_pairwise_sum adds in fp32 -- fp64 for f64). */
 int fedagg_pairwise_products_f32(const float* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,

@@ -67,6 +67,8 @@ SIGNATURES = {
     "fedagg_fedavg_chain_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_tiled_f32": (c_int, [c_void, P(ctypes.c_float), c_int, c_u64, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_tiled_bf16": (c_int, [c_void, P(ctypes.c_float), c_int, c_u64, c_u64, c_int, c_void, c_void]),
     "fedagg_pairwise_products_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_i64, c_int,
                                              c_void, c_void]),
     "fedagg_pairwise_products_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, P(c_u64), c_int, c_i64, c_int,
@@ -111,7 +113,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

@@ -2003,7 +2003,7 @@ uint64_t tiled_tile_vectors(int K, uint64_t M) {
 
 template <typename E>
 int fedavg_tiled_launch(const typename E::In* base, const typename E::P* w, int K, uint64_t M, uint64_t tv,
-                        const uint64_t* idx, int P, void* ws, typename E::Out* out, hipStream_t s) {
+                        const uint64_t* idx, int P, void* ws, typename E::Out* out, hipStream_t s, bool seed = true) {
   if (K <= 0) return fail(FEDAGG_EINVAL, "fedavg_tiled: K must be > 0 (got %lld)", K);
   if (!base || !w || !out) return fail(FEDAGG_EINVAL, "fedavg_tiled: NULL argument");
   if (!aligned16(base) || !aligned16(out)) return fail(FEDAGG_EINVAL, "fedavg_tiled: buffers must be 16-B aligned");
@@ -2035,7 +2035,7 @@ int fedavg_tiled_launch(const typename E::In* base, const typename E::P* w, int 
       pw.n = P;
       for (int p = 0; p < P; ++p) pw.idx[p] = idx[p];
     }
-    const int first = k0 == 0 ? 1 : 0;
+    const int first = (k0 == 0 && seed) ? 1 : 0;
     if constexpr (std::is_same<E, F32>::value) {
       if (tv == FEDAGG_TILE_VECTORS_F32_FEW)  // 8 x 256 tile, write-through (sc1) stores
         launch_fedavg_variant<E, true, 2, 8, 4, false, true, 1, false, FA_BLOCK, true>(grid, s, a, pw, kc, first, nvec,
@@ -2623,6 +2623,17 @@ int fedagg_fedavg_chain_f16(const uint16_t* const* d_clients, const uint16_t* h_
   if (!h_w || K <= 0) return fail(FEDAGG_EINVAL, "fedavg_chain_f16: invalid weights (K=%lld)", K);
   return fedavg_launch<F16>(d_clients, reinterpret_cast<const _Float16*>(h_w), K, M, nullptr, 0, nullptr, d_out,
                             (hipStream_t)stream, seed != 0);
+}
+
+int fedagg_fedavg_chain_tiled_f32(const float* d_base, const float* h_w, int K, uint64_t M, uint64_t tile_vectors,
+                                  int seed, float* d_out, void* stream) {
+  return fedavg_tiled_launch<F32>(d_base, h_w, K, M, tile_vectors, nullptr, 0, nullptr, d_out, (hipStream_t)stream,
+                                  seed != 0);
+}
+int fedagg_fedavg_chain_tiled_bf16(const uint16_t* d_base, const float* h_w, int K, uint64_t M, uint64_t tile_vectors,
+                                   int seed, float* d_out, void* stream) {
+  return fedavg_tiled_launch<BF16>(d_base, h_w, K, M, tile_vectors, nullptr, 0, nullptr, d_out, (hipStream_t)stream,
+                                   seed != 0);
 }
 
 int fedagg_pairwise_products_f32(const float* const* d_clients, const float* h_w, int K, const uint64_t* h_idx,

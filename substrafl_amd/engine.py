@@ -508,7 +508,7 @@ class AggregationEngine:
             dt = targets[0]
             layout = BucketLayout(list(range(len(c_row))), [a.shape for a in c_row], dt)
             ld_bytes = layout.ld * dt.itemsize
-            d = s.buffer(self._B_C, K * ld_bytes)
+            d = s.buffer(self._B_C, ld_bytes)  # ONE copy staged, the others checked on the host
             self._prestaged[self._B_C] = [d, ld_bytes, {}]
             self._c_ref, self._c_mism = None, 0
             plan.append(("server_control_variate", self._B_C, layout, d, ld_bytes, dt, True))
@@ -739,8 +739,19 @@ class AggregationEngine:
         lay_s = BucketLayout(lid, [a.shape for a in server_control_variates[0]], sdt)
         same = [g.shape for g in lay_d.segments] == [g.shape for g in lay_c.segments] == \
             [g.shape for g in lay_s.segments]
+        # every client holding the very same c arrays (simulation mode: the server's broadcast):
+        # assert_array_equal holds by identity, so one copy is staged and the check is skipped
+        same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
+                     for row in server_control_variates[1:])
+        # otherwise (task process: K separately unpickled copies) the check runs on the host while
+        # the bytes are staged: ONE copy crosses PCIe, the others are compared with it on the pack
+        # workers (Session.stage_check); the device check over K staged copies stays as a knob
+        # (c_check="device") and for c lists of another dtype than the buckets
+        host_c = (not same_c and self.c_check == "host"
+                  and all(a.dtype == sdt for row in server_control_variates for a in row))
+        Kc = 1 if (same_c or host_c) else K  # rows of c in HBM: one copy unless the device checks all K
         if same and all(a.dtype == sdt for lst in lists for client in lst for a in client):
-            ooc = self._out_of_core(3 * K * lay_d.ld * sdt.itemsize + 2 * lay_d.ld * 8,
+            ooc = self._out_of_core((2 * K + Kc) * lay_d.ld * sdt.itemsize + 2 * lay_d.ld * 8,
                                     (self._B_BUCKET, self._B_CV, self._B_C, self._B_OUT, self._B_COUT, self._B_WS,
                                      self._B_CNT))
             if ooc is not None:
@@ -753,17 +764,7 @@ class AggregationEngine:
         t0 = time.perf_counter()
         d_d = s.buffer(self._B_BUCKET, K * lay_d.ld * isz)
         d_cv = s.buffer(self._B_CV, K * lay_c.ld * isz)
-        d_cc = s.buffer(self._B_C, K * lay_s.ld * isz)
-        # every client holding the very same c arrays (simulation mode: the server's broadcast):
-        # assert_array_equal holds by identity, so one copy is staged and the check is skipped
-        same_c = all(len(row) == len(server_control_variates[0]) and all(a is b for a, b in zip(row, server_control_variates[0]))
-                     for row in server_control_variates[1:])
-        # otherwise (task process: K separately unpickled copies) the check runs on the host while
-        # the bytes are staged: ONE copy crosses PCIe, the others are compared with it on the pack
-        # workers (Session.stage_check); the device check over K staged copies stays as a knob
-        # (c_check="device") and for c lists of another dtype than the buckets
-        host_c = (not same_c and self.c_check == "host"
-                  and all(a.dtype == sdt for row in server_control_variates for a in row))
+        d_cc = s.buffer(self._B_C, Kc * lay_s.ld * isz)
         pre = 0
         host_mism = 0
         for rows, lay, d, slot in ((parameters_updates, lay_d, d_d, self._B_BUCKET),

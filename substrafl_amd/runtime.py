@@ -98,13 +98,15 @@ class Session:
 
     def buffer(self, slot: int, nbytes: int) -> int:
         slot = int(slot)
-        self._held[slot] = max(self._held.get(slot, 0), max(16, int(nbytes)))
+        need = max(16, int(nbytes))
+        grew = need > self._held.get(slot, 0)  # the native slot reallocates: contents undefined
+        self._held[slot] = max(self._held.get(slot, 0), need)
         p = ctypes.c_void_p()
-        _native.check(self.lib.fedagg_session_buffer(self._h, slot, max(16, int(nbytes)), ctypes.byref(p)),
-                      "session_buffer")
-        if self._ptr.get(slot) != int(p.value):
+        _native.check(self.lib.fedagg_session_buffer(self._h, slot, need, ctypes.byref(p)), "session_buffer")
+        if grew or self._ptr.get(slot) != int(p.value):
+            # bumped on every regrowth, even when hipMalloc hands back the same address
             self._ptr[slot] = int(p.value)
-            self._bump(int(p.value))
+            self._gen[slot] = self._gen.get(slot, 0) + 1
         return int(p.value)
 
     # ----------------------------------------------------------------------------------

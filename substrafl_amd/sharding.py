@@ -8,29 +8,27 @@ Two layouts:
   one GPU.  No arithmetic crosses GPUs; results are bit-identical to the single-GPU path and to
   the reference.  The optional final gather to every rank is a plain all-gather of the result
   slices (RCCL over xGMI), not a reduction.
-* **Client sharding (the north-star mode).**  The K clients are cut into G contiguous blocks,
-  block ``b``'s buckets live in the HBM of rank ``chain_rank(b)`` (the last block on the root,
-  rank 0), and the reference's sequential client sum (fed_avg.py:221-222; scaffold.py:262-263,
-  293) is completed across the ranks in one of three ways, all device-resident (partial sums
-  stay in HBM, the exchange is RCCL over xGMI, the final step runs on the root's GPU):
+* **Client sharding (the north-star mode).**  The K clients are cut into G contiguous blocks
+  whose buckets live in different GPUs' HBM, and the reference's sequential client sum
+  (fed_avg.py:221-222; scaffold.py:262-263, 293) is completed across the ranks, device-resident
+  (partial sums stay in HBM, the exchange is RCCL over xGMI, the result lands on the root):
 
-  ``combine="relay"`` (default, **bit-exact**): block b CONTINUES the accumulator of blocks
-  0..b-1, received chunk by chunk from the previous rank (P2P send/recv), so every element sees
-  exactly the reference's rounding sequence; the chunks are pipelined, so all G ranks stream
-  at once.  The root holds the last block and applies the final step (Scaffold: + c, then
-  ``aggregation_lr``) inside its last kernel.
+  ``combine="relay"`` (default, **bit-exact**): rank ``(b + 1) % G`` holds block b for every
+  element; the bucket is cut into chunks whose accumulators travel down the chain of blocks
+  0..G-1 (each rank CONTINUES the accumulator it receives), so every element sees exactly the
+  reference's rounding sequence.  The last block is on the root, which applies Scaffold's final
+  step (+ c, then ``aggregation_lr``) inside its last kernel.
+  ``combine="striped"`` (**bit-exact**): the same chains, over pieces scheduled so that every
+  rank runs one block of one piece per ring at every step and sends on several xGMI links at
+  once (:mod:`lockstep`); a stripe's final chunk goes from its last rank to the root.
+  Both run as a :mod:`lockstep` schedule: ONE host thread, ONE communicator, exchange group t on
+  every rank pairing only with group t on its peers -- deadlock-free by construction.
   ``combine="rccl"``: every block sums from +0.0, the partials are summed by ``dist.reduce``
   (RCCL's order) and the root applies the final scale.  Re-associates the client sum: a few ulp
   off the reference (DESIGN.md §6 drift table).
   ``combine="ordered"``: the partials are gathered on the root and added in block order by the
   bucket kernel (weight 1.0 per partial; Scaffold: lr and + c in the same launch).
   Deterministic, same drift class as ``rccl``.
-  ``striped`` (:func:`client_shard_fedavg_striped`, **bit-exact**): the relay, but the bucket is
-  cut into S parameter stripes and stripe s places block b on rank ``a_s * (b + 1) mod G`` for a
-  different unit ``a_s`` of Z_G per stripe.  Every element still passes through blocks 0..G-1
-  in order (the same rounding sequence), every stripe still ends on the root, but stripe s's
-  hops all go ``a_s`` ranks ahead: on a fully connected xGMI node the S stripes' accumulators
-  travel over S disjoint sets of G links at once instead of all over the same G - 1.
 
   The numel == 1 tensors follow NumPy's pairwise order over ALL K products,
   which no block can compute alone: every rank writes its products into its columns of a
@@ -53,11 +51,13 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import lockstep
 from .layout import BucketLayout
+from .lockstep import SLOTS, chain_rank, ring_multipliers, striped_pieces
 
 SHARD_ALIGN = 512  # elements (2 KiB of fp32): every shard starts on a 256-B boundary
 RELAY_CHUNK_ELEMS = 2 << 20  # pipelined relay: >= 2M elements (8 MB fp32) per P2P message
-COMBINES = ("relay", "rccl", "ordered")  # client_shard_fedavg / _scaffold; "striped": *_striped below
+COMBINES = ("relay", "rccl", "ordered", "striped")
 
 
 def shard_bounds(M: int, world: int, align: int = SHARD_ALIGN) -> List[Tuple[int, int]]:
@@ -86,13 +86,8 @@ def client_blocks(K: int, world: int) -> List[Tuple[int, int]]:
     return [(min(K, b * per), min(K, (b + 1) * per)) for b in range(world)]
 
 
-def chain_rank(block: int, world: int) -> int:
-    """Rank holding client block ``block``: block b on rank (b + 1) % G, so the LAST block (whose
-    kernel finishes the chain) sits on the root, rank 0."""
-    return (block + 1) % world
-
-
 def block_of(rank: int, world: int) -> int:
+    """The block a rank holds in the plain relay (inverse of :func:`lockstep.chain_rank`)."""
     return (rank - 1) % world
 
 
@@ -102,6 +97,18 @@ def relay_chunks(M: int, chunk_elems: int = RELAY_CHUNK_ELEMS) -> List[Tuple[int
     if M <= 0:
         return [(0, 0)]
     return [(a, min(M, a + step)) for a in range(0, M, step)]
+
+
+def relay_plan(M: int, world: int, rank: int, chunk_elems: int = RELAY_CHUNK_ELEMS) -> lockstep.RankPlan:
+    """This rank's part of the plain relay (its one block's buffer is indexed by global element)."""
+    return lockstep.rank_plan(lockstep.relay_pieces(M, world, chunk_elems), world, rank, cols="global")
+
+
+def striped_plan(M: int, world: int, rank: int, rings: Optional[int] = None,
+                 rounds: Sequence[float] = lockstep.DEFAULT_ROUNDS) -> lockstep.RankPlan:
+    """This rank's part of the striped relay: per client block, the element ranges it holds
+    (``plan.blocks[b]``: ``(lo, hi, col)``, packed into a ``[Kb, plan.block_len[b]]`` buffer)."""
+    return lockstep.rank_plan(striped_pieces(M, world, rings, rounds), world, rank, cols="packed")
 
 
 # ======================================================================================
@@ -131,7 +138,7 @@ class FedAvgShard:
 @dataclass
 class ScaffoldShard:
     """This rank's part of a client-sharded Scaffold (fp32 or fp64 buckets, fp64 sums).  ``c``
-    (the server control variate, ``[ld]``) is read on the root only."""
+    (the server control variate, ``[ld]``) is read where a block's final step runs."""
 
     kind: str
     delta: object
@@ -147,6 +154,68 @@ class ScaffoldShard:
     @property
     def Kr(self) -> int:
         return int(self.delta.shape[0]) if self.delta is not None else 0
+
+
+class TiledView:
+    """One run's operand in the tile-interleaved layout (``engine.tiled_*``: tile t of client k at
+    tile ``t * K + k`` of ``base``): K clients x n elements, tiles of ``tv`` 16-B vectors."""
+
+    def __init__(self, kind: str, base, K: int, n: int, tv: int):
+        self.kind, self.base, self.K, self.n, self.tv = kind, base, int(K), int(n), int(tv)
+        self.shape = (self.K, self.n)
+
+
+class TiledBlock:
+    """A rank's buffer for one client block of a lockstep schedule in the tile-interleaved layout:
+    ONE tiled bucket per run of the plan (the run is the unit of a launch), so each workgroup step
+    of the chain kernel reads one contiguous Kb x tile region instead of Kb streams a row apart.
+    ``block[:, col:col + n]`` is the :class:`TiledView` of the run starting at ``col``."""
+
+    def __init__(self, kind: str, K: int, width: int, tv: int, buckets: Dict[int, Tuple[object, int]]):
+        self.kind, self.K, self.tv = kind, int(K), int(tv)
+        self.buckets = dict(buckets)  # col -> (flat device tensor, n)
+        self.shape = (self.K, int(width))
+
+    def __getitem__(self, idx):
+        _, sl = idx
+        t, n = self.buckets[sl.start]
+        if sl.stop - sl.start != n:
+            raise IndexError("a tiled block is sliced by whole runs")
+        return TiledView(self.kind, t, self.K, n, self.tv)
+
+    def locate(self, col: int) -> Tuple[object, int]:
+        """(bucket tensor, element offset in its run) of block column ``col``."""
+        for c0, (t, n) in self.buckets.items():
+            if c0 <= col < c0 + n:
+                return t, col - c0
+        raise IndexError(col)
+
+    @staticmethod
+    def run_extents(plan: lockstep.RankPlan, block: int) -> List[Tuple[int, int]]:
+        """(col, n) of every run of ``block`` in ``plan`` (the buckets a tiled block holds)."""
+        return sorted({(r.col, r.n) for runs in plan.runs for r in runs if r.block == block})
+
+    @classmethod
+    def empty(cls, torch, kind: str, K: int, width: int, tv: int, extents, device):
+        from .engine import tiled_elems, torch_dtype
+
+        return cls(kind, K, width, tv, {c: (torch.zeros(tiled_elems(kind, K, n, tv), dtype=torch_dtype(kind),
+                                                        device=device), n) for c, n in extents})
+
+    @classmethod
+    def from_rows(cls, torch, kind: str, rows, tv: int, extents):
+        """Re-tile a ``[Kb, width]`` rows buffer run by run on the device (one strided copy each)."""
+        from .engine import _ELEMS_PER_VEC
+
+        K, width = int(rows.shape[0]), int(rows.shape[1])
+        blk = cls.empty(torch, kind, K, width, tv, extents, rows.device)
+        TL = int(tv) * _ELEMS_PER_VEC[kind]
+        for c, (t, n) in blk.buckets.items():
+            tiles = -(-n // TL)
+            src = torch.zeros((K, tiles * TL), dtype=rows.dtype, device=rows.device)
+            src[:, :n] = rows[:, c: c + n]
+            t.view(tiles, K, TL).copy_(src.view(K, tiles, TL).permute(1, 0, 2))
+        return blk
 
 
 def out_dtype(torch, kind: str):
@@ -170,7 +239,8 @@ def _stream():
 class GpuShardOps:
     """libfedagg entry points (``include/fedagg.h``, client-sharded building blocks) on this
     rank's GPU, enqueued on torch's current stream (so torch.distributed's RCCL calls order
-    against them)."""
+    against them).  Operands are tensor views: ``rows`` ``[Kb, n]`` (row stride free),
+    accumulators ``[n]``."""
 
     def __init__(self):
         from . import _native
@@ -192,29 +262,55 @@ class GpuShardOps:
         base, step, esz = t.data_ptr(), t.stride(0) * t.element_size(), t.element_size()
         return [base + k * step + a * esz for k in range(t.shape[0])]
 
-    def fedavg_chain(self, kind, rows, w, a: int, b: int, seed: bool, out) -> None:
-        """out[a:b] = (seed ? +0 : out[a:b]) + the clients of ``rows`` in order."""
-        if b <= a:
+    def fedavg_run(self, kind, rows, w, seed: bool, acc) -> None:
+        """acc = (seed ? +0 : acc) + the clients of ``rows`` (``[Kb, n]``) in order."""
+        n = int(acc.shape[0])
+        if n == 0:
             return
         if rows.shape[0] == 0:  # an empty block passes the accumulator on (or starts it at +0)
             if seed:
-                out[a:b].zero_()
+                acc.zero_()
+            return
+        if isinstance(rows, TiledView):
+            fn = getattr(self.lib, f"fedagg_fedavg_chain_tiled_{kind}")
+            rc = fn(rows.base.data_ptr(), self._weights(kind, w), rows.K, n, rows.tv, int(bool(seed)), acc.data_ptr(),
+                    _stream())
+            self._n.check(rc, "fedavg_chain_tiled")
             return
         fn = getattr(self.lib, f"fedagg_fedavg_chain_{kind}")
-        rc = fn(self._n.ptr_array(self._rows(rows, a)), self._weights(kind, w), int(rows.shape[0]), b - a,
-                int(bool(seed)), out.data_ptr() + a * out.element_size(), _stream())
+        rc = fn(self._n.ptr_array(self._rows(rows)), self._weights(kind, w), int(rows.shape[0]), n, int(bool(seed)),
+                acc.data_ptr(), _stream())
         self._n.check(rc, "fedavg_chain")
 
-    def fedavg_products(self, sh: FedAvgShard, ws) -> None:
-        P = int(sh.pairwise_idx.size)
-        if not P or not sh.Kr:
+    def fedavg_chain(self, kind, rows, w, a: int, b: int, seed: bool, out) -> None:
+        """out[a:b] = (seed ? +0 : out[a:b]) + the clients of ``rows`` in order."""
+        if b > a:
+            self.fedavg_run(kind, rows[:, a:b], w, seed, out[a:b])
+
+    def fedavg_products_at(self, kind, rows, w, kbase: int, K: int, idx, ws) -> None:
+        """ws[p, kbase + k] = fl(rows[k, idx[p]] * w[k]) (numel == 1 products of this block)."""
+        P = int(np.asarray(idx).size)
+        if not P or not rows.shape[0]:
             return
-        kind = sh.kind
         fn = getattr(self.lib, f"fedagg_pairwise_products_{kind}")
-        idx = (ctypes.c_uint64 * P)(*[int(v) for v in sh.pairwise_idx])
-        rc = fn(self._n.ptr_array(self._rows(sh.rows)), self._weights(kind, sh.w), sh.Kr, idx, P, sh.K, sh.kbase,
+        if isinstance(rows, TiledBlock):  # client k's tile 0 as its base, indices mapped into the tiles
+            from .engine import tiled_index
+
+            for p, col in enumerate(np.asarray(idx, np.int64)):
+                t, e = rows.locate(int(col))
+                ptrs = [t.data_ptr() + k * rows.tv * 16 for k in range(rows.K)]
+                ia = (ctypes.c_uint64 * 1)(int(tiled_index(kind, rows.K, 0, e, rows.tv)))
+                rc = fn(self._n.ptr_array(ptrs), self._weights(kind, w), rows.K, ia, 1, K, kbase,
+                        ws[p:].data_ptr(), _stream())
+                self._n.check(rc, "pairwise_products")
+            return
+        ia = (ctypes.c_uint64 * P)(*[int(v) for v in np.asarray(idx)])
+        rc = fn(self._n.ptr_array(self._rows(rows)), self._weights(kind, w), int(rows.shape[0]), ia, P, K, kbase,
                 ws.data_ptr(), _stream())
         self._n.check(rc, "pairwise_products")
+
+    def fedavg_products(self, sh: FedAvgShard, ws) -> None:
+        self.fedavg_products_at(sh.kind, sh.rows, sh.w, sh.kbase, sh.K, sh.pairwise_idx, ws)
 
     def fedavg_finish(self, kind, ws, K: int, pairwise_idx, out) -> None:
         P = int(pairwise_idx.size)
@@ -231,37 +327,47 @@ class GpuShardOps:
         self.fedavg_chain(pk, parts, np.ones(parts.shape[0]), 0, M, True, out)
 
     # -- Scaffold ------------------------------------------------------------------------
+    def scaffold_run(self, kind, delta, cv, w, seed: bool, finish: bool, c, lr: float, dacc, cacc) -> None:
+        """dacc/cacc = (seed ? +0 : themselves) + this block's clients, in order; ``finish`` (the
+        last block): then ``+ c`` (``c``: the same elements of the server control variate) and
+        ``* lr``."""
+        n = int(dacc.shape[0])
+        if n == 0:
+            return
+        if delta.shape[0] == 0:  # an empty block: pass the accumulators on (start them at +0), finish them
+            if seed:
+                dacc.zero_()
+                cacc.zero_()
+            if finish:
+                self._scaffold_final(c, lr, dacc, cacc)
+            return
+        fn = getattr(self.lib, f"fedagg_scaffold_chain_{kind}")
+        wa = (ctypes.c_double * delta.shape[0])(*[float(v) for v in w])
+        rc = fn(self._n.ptr_array(self._rows(delta)), self._n.ptr_array(self._rows(cv)),
+                c.data_ptr() if finish else None, wa, int(delta.shape[0]), n, int(bool(seed)), int(bool(finish)),
+                float(lr), dacc.data_ptr(), cacc.data_ptr(), _stream())
+        self._n.check(rc, "scaffold_chain")
+
     def scaffold_chain(self, sh: ScaffoldShard, a: int, b: int, seed: bool, finish: bool, dout, cout) -> None:
         """dout/cout[a:b] = (seed ? +0 : themselves) + this block's clients, in order; ``finish``
         (last block): then ``+ c`` and ``* lr``."""
-        if b <= a:
+        if b > a:
+            self.scaffold_run(sh.kind, sh.delta[:, a:b], sh.cv[:, a:b], sh.w, seed, finish,
+                              sh.c[a:b] if finish else None, sh.lr, dout[a:b], cout[a:b])
+
+    def scaffold_products_at(self, kind, delta, cv, w, kbase: int, K: int, idx, ws) -> None:
+        P = int(np.asarray(idx).size)
+        if not P or not delta.shape[0]:
             return
-        if sh.Kr == 0:  # an empty block: pass the accumulators on (start them at +0), finish them
-            if seed:
-                dout[a:b].zero_()
-                cout[a:b].zero_()
-            if finish:
-                self._scaffold_final(sh, a, b, dout, cout)
-            return
-        fn = getattr(self.lib, f"fedagg_scaffold_chain_{sh.kind}")
-        esz = sh.delta.element_size()
-        c = sh.c.data_ptr() + a * esz if finish else None
-        w = (ctypes.c_double * sh.Kr)(*[float(v) for v in sh.w])
-        rc = fn(self._n.ptr_array(self._rows(sh.delta, a)), self._n.ptr_array(self._rows(sh.cv, a)), c, w, sh.Kr,
-                b - a, int(bool(seed)), int(bool(finish)), float(sh.lr), dout.data_ptr() + a * 8,
-                cout.data_ptr() + a * 8, _stream())
-        self._n.check(rc, "scaffold_chain")
+        fn = getattr(self.lib, f"fedagg_scaffold_products_{kind}")
+        ia = (ctypes.c_uint64 * P)(*[int(v) for v in np.asarray(idx)])
+        wa = (ctypes.c_double * delta.shape[0])(*[float(v) for v in w])
+        rc = fn(self._n.ptr_array(self._rows(delta)), self._n.ptr_array(self._rows(cv)), wa, int(delta.shape[0]),
+                kbase, K, ia, P, ws.data_ptr(), _stream())
+        self._n.check(rc, "scaffold_products")
 
     def scaffold_products(self, sh: ScaffoldShard, ws) -> None:
-        P = int(sh.pairwise_idx.size)
-        if not P or not sh.Kr:
-            return
-        fn = getattr(self.lib, f"fedagg_scaffold_products_{sh.kind}")
-        idx = (ctypes.c_uint64 * P)(*[int(v) for v in sh.pairwise_idx])
-        w = (ctypes.c_double * sh.Kr)(*[float(v) for v in sh.w])
-        rc = fn(self._n.ptr_array(self._rows(sh.delta)), self._n.ptr_array(self._rows(sh.cv)), w, sh.Kr, sh.kbase,
-                sh.K, idx, P, ws.data_ptr(), _stream())
-        self._n.check(rc, "scaffold_products")
+        self.scaffold_products_at(sh.kind, sh.delta, sh.cv, sh.w, sh.kbase, sh.K, sh.pairwise_idx, ws)
 
     def scaffold_finish(self, sh: ScaffoldShard, ws, dout, cout) -> None:
         P = int(sh.pairwise_idx.size)
@@ -273,17 +379,18 @@ class GpuShardOps:
                 _stream())
         self._n.check(rc, "scaffold_finish")
 
-    def _scaffold_final(self, sh: ScaffoldShard, a: int, b: int, dout, cout) -> None:
-        """dout[a:b] = lr * (+0 + 1.0 * dout[a:b]), cout[a:b] = +0 + 1.0 * cout[a:b] + c[a:b]: the
-        final step of scaffold.py:262-263,293 on accumulators that never hold -0.0, so exact."""
+    def _scaffold_final(self, c, lr, dacc, cacc) -> None:
+        """dacc = lr * (+0 + 1.0 * dacc), cacc = +0 + 1.0 * cacc + c: the final step of
+        scaffold.py:262-263,293 on accumulators that never hold -0.0, so exact."""
         import torch
 
-        c64 = sh.c[a:b].to(torch.float64)
+        n = int(dacc.shape[0])
+        c64 = c[:n].to(torch.float64)
         w = (ctypes.c_double * 1)(1.0)
-        d_in, c_in = dout[a:b].clone().unsqueeze(0), cout[a:b].clone().unsqueeze(0)
+        d_in, c_in = dacc.clone().unsqueeze(0), cacc.clone().unsqueeze(0)
         rc = self.lib.fedagg_scaffold_chain_f64(self._n.ptr_array(self._rows(d_in)), self._n.ptr_array(self._rows(c_in)),
-                                                c64.data_ptr(), w, 1, b - a, 1, 1, float(sh.lr),
-                                                dout.data_ptr() + a * 8, cout.data_ptr() + a * 8, _stream())
+                                                c64.data_ptr(), w, 1, n, 1, 1, float(lr), dacc.data_ptr(),
+                                                cacc.data_ptr(), _stream())
         self._n.check(rc, "scaffold_final")
 
     def scaffold_combine(self, sh: ScaffoldShard, dparts, cparts, dout, cout) -> None:
@@ -303,9 +410,14 @@ class GpuShardOps:
 # ======================================================================================
 # transports
 # ======================================================================================
+_WARMED: set = set()
+
+
 class DistTransport:
     """The exchange steps over a ``torch.distributed`` group: RCCL (backend "nccl") on device
-    tensors in the product; gloo on CPU tensors in the CPU tests.  Ranks are group ranks."""
+    tensors in the product; gloo on CPU tensors in the CPU tests.  Ranks are group ranks.  One
+    transport = one communicator; the lockstep combines issue everything through it from the
+    calling thread."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -314,23 +426,50 @@ class DistTransport:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        # one group-wide collective before the first point-to-point call: NCCL's batched P2P must
-        # not be the first operation a communicator sees on only some of its ranks (a few tens of
-        # microseconds per transport; transports are built once per aggregation, not per step)
         if self.world > 1:
+            # a group-wide collective before the first point-to-point call (NCCL's batched P2P
+            # must not be the first operation a communicator sees on only some of its ranks),
+            # then every peer pair's P2P connection, once per process and communicator
             self.all_sum_int(0)
+            key = (id(dist.group.WORLD), None if group is None else tuple(dist.get_process_group_ranks(group)))
+            if key not in _WARMED:
+                self.warm_p2p()
+                _WARMED.add(key)
 
     def _g(self, r: int) -> int:
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
 
+    def _device(self):
+        import torch
+
+        return torch.device("cuda", torch.cuda.current_device()) if self.dist.get_backend(self.group) == "nccl" \
+            else torch.device("cpu")
+
+    def warm_p2p(self) -> None:
+        """One element to and from every peer in ONE batched group, on every rank at once: RCCL
+        connects a peer pair at its first send/recv, so this keeps the connection set-up out of
+        the lockstep schedule's first groups."""
+        import torch
+
+        dev = self._device()
+        peers = [p for p in range(self.world) if p != self.rank]
+        sends = [torch.zeros(1, device=dev) for _ in peers]
+        recvs = [torch.empty(1, device=dev) for _ in peers]
+        ops = [("send", s, p) for s, p in zip(sends, peers)] + [("recv", r, p) for r, p in zip(recvs, peers)]
+        for w in self.exchange(ops):
+            w.wait()
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()
+
     def exchange(self, ops: Sequence[Tuple[str, object, int]]) -> list:
         """Batched point-to-point (``("send"|"recv", tensor, peer)``), one NCCL group; returns the
-        works (``wait()`` orders the current stream after them)."""
+        works (``wait()`` orders the current stream after them).  With NCCL the whole batch may
+        come back as ONE work (torch's coalescing manager): callers wait on every work returned."""
         if not ops:
             return []
         d = self.dist
         p2p = [d.P2POp(d.isend if kind == "send" else d.irecv, t, self._g(peer), self.group) for kind, t, peer in ops]
-        return d.batch_isend_irecv(p2p)
+        return list(d.batch_isend_irecv(p2p) or [])
 
     def reduce_sum(self, t, root: int) -> None:
         self.dist.reduce(t, dst=self._g(root), op=self.dist.ReduceOp.SUM, group=self.group)
@@ -350,9 +489,7 @@ class DistTransport:
     def all_sum_int(self, v: int) -> int:
         import torch
 
-        dev = torch.device("cuda", torch.cuda.current_device()) if self.dist.get_backend(self.group) == "nccl" \
-            else torch.device("cpu")
-        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self._device())
         self.dist.all_reduce(t, group=self.group)
         return int(t.item())
 
@@ -379,8 +516,10 @@ class _LoopbackRecv:
 class LoopbackGroup:
     """G ranks as threads of ONE process (rehearsal of the multi-rank protocol on one GPU, and
     the drift tool): point-to-point messages and collectives through in-process mailboxes.
-    Device tensors are handed over with an event recorded on the sender's current stream and
-    ``record_stream`` on the receiver's, so the ranks' streams stay ordered like RCCL's."""
+    A send posts a snapshot of the tensor (the sender may reuse its buffer at once, as after an
+    RCCL send completes); device tensors are handed over with an event recorded on the sender's
+    current stream and ``record_stream`` on the receiver's, so the ranks' streams stay ordered
+    like RCCL's."""
 
     def __init__(self, world: int):
         self.world = int(world)
@@ -433,7 +572,8 @@ class _LoopbackTransport:
         works = []
         for kind, t, peer in ops:
             if kind == "send":
-                self._put((self.rank, peer), (t, _event(t)))
+                snap = t.clone()
+                self._put((self.rank, peer), (snap, _event(snap)))
                 works.append(_Done())
             else:
                 works.append(_LoopbackRecv(self, t, peer))
@@ -489,48 +629,6 @@ class _LoopbackTransport:
 # ======================================================================================
 # the client-sharded reductions (device level)
 # ======================================================================================
-def _neighbours(rank: int, world: int) -> Tuple[int, Optional[int], Optional[int]]:
-    b = block_of(rank, world)
-    prev = chain_rank(b - 1, world) if b > 0 else None
-    nxt = chain_rank(b + 1, world) if b < world - 1 else None
-    return b, prev, nxt
-
-
-def _relay(transport, chunks, tensors: Callable[[int, int], list], run: Callable[[int, int, bool, bool], None],
-           prev: Optional[int], nxt: Optional[int]) -> None:
-    """Pipelined chain over ``chunks``: receive chunk j's accumulators from ``prev``, run this
-    block on them, send them to ``nxt``; the receives run two chunks ahead and every send is
-    batched with a receive, so the links of all ranks are busy at once."""
-    C = len(chunks)
-    recvs: Dict[int, list] = {}
-
-    def post(js):
-        ops = []
-        for j in js:
-            if prev is not None and j < C:
-                ops += [("recv", t, prev) for t in tensors(*chunks[j])]
-        return ops
-
-    pending = []
-    first = post([0, 1])
-    if first:
-        works = transport.exchange(first)
-        n0 = len(tensors(*chunks[0]))
-        recvs[0], recvs[1] = works[:n0], works[n0:]
-    for j, (a, b) in enumerate(chunks):
-        for w in recvs.pop(j, []):
-            w.wait()
-        run(a, b, prev is None, nxt is None)
-        ops = [("send", t, nxt) for t in tensors(a, b)] if nxt is not None else []
-        rops = post([j + 2])
-        works = transport.exchange(ops + rops)
-        pending += works[: len(ops)]
-        if rops:
-            recvs[j + 2] = works[len(ops):]
-    for w in pending:
-        w.wait()
-
-
 def _reduce_async(transport, t, root):
     """transport.reduce_sum_async when the transport has it (else the blocking form)."""
     fn = getattr(transport, "reduce_sum_async", None)
@@ -540,18 +638,119 @@ def _reduce_async(transport, t, root):
     return _Done()
 
 
-def client_shard_fedavg(sh: FedAvgShard, out, transport, ops, combine: str = "relay", ws=None,
-                        chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
-    """Client-sharded FedAvg (fed_avg.py:217-222) over ``transport``'s ranks: every rank passes
-    its :class:`FedAvgShard`; the result lands in ``out`` (``[>= M]``, fp32 for f32/bf16) on the
-    root (rank 0), which this returns True on.  ``ws``: optional ``[P, K]`` workspace."""
+def _slots(torch, plan, like, n_acc: int = 1, slots=None):
+    """The schedule's accumulator slots: ``[n_acc, SLOTS, slot_elems]`` of ``like``'s dtype."""
+    need = max(1, plan.slot_elems)
+    if slots is not None and slots.numel() >= n_acc * SLOTS * need and slots.dtype == like.dtype:
+        return slots.reshape(-1)[: n_acc * SLOTS * need].view(n_acc, SLOTS, need)
+    return torch.empty((n_acc, SLOTS, need), dtype=like.dtype, device=like.device)
+
+
+def lockstep_fedavg(plan: lockstep.RankPlan, blocks: Dict[int, FedAvgShard], out, transport, ops, pairwise_idx,
+                    ws=None, slots=None) -> bool:
+    """Run one rank's part of a relay / striped FedAvg schedule (fed_avg.py:217-222, bit-exact).
+    ``blocks[b]``: this rank's buffer for client block b (``rows`` ``[Kb, plan.block_len[b]]``
+    in the plan's columns, the block's GLOBAL weights, ``kbase``, ``K``); ``out``: ``[>= M]``
+    result on the root, which this returns True on; ``pairwise_idx``: the global numel == 1
+    indices (sorted).  ``ws`` / ``slots``: optional reusable workspaces."""
     import torch
 
-    if combine not in COMBINES:
-        raise ValueError(f"combine must be one of {COMBINES}")
+    sh0 = next(iter(blocks.values()))
+    kind, K = sh0.kind, sh0.K
+    acc = _slots(torch, plan, out, 1, slots)[0]
+
+    def region(loc, n):
+        where, slot, off = loc
+        return [(out if where == "out" else acc[slot])[off: off + n]]
+
+    def launch(r):
+        sh = blocks[r.block]
+        ops.fedavg_run(kind, sh.rows[:, r.col: r.col + r.n], sh.w, r.seed, region(r.acc, r.n)[0])
+
+    lockstep.run(plan, transport, region, launch)
+    pw = np.asarray(pairwise_idx, np.int64)
+    if pw.size:
+        if ws is None:
+            ws = torch.zeros((pw.size, K), dtype=ws_dtype(torch, kind), device=out.device)
+        else:
+            ws.zero_()
+        for b, p0, p1, cols in lockstep.pairwise_segments(plan, pw):
+            sh = blocks[b]
+            ops.fedavg_products_at(kind, sh.rows, sh.w, sh.kbase, K, cols, ws[p0:p1])
+        if plan.world > 1:
+            transport.reduce_sum(ws, plan.root)  # columns of other blocks are zeros: the sum is exact
+        if plan.rank == plan.root:
+            ops.fedavg_finish(kind, ws, K, pw.astype(np.uint64), out)
+    return plan.rank == plan.root
+
+
+def lockstep_scaffold(plan: lockstep.RankPlan, blocks: Dict[int, ScaffoldShard], dout, cout, transport, ops,
+                      pairwise_idx, c, lr: float, ws=None, slots=None) -> bool:
+    """One rank's part of a relay / striped Scaffold schedule (scaffold.py:262-263, 293; fp64,
+    bit-exact): the averaged update ``lr * sum_k w_k delta_k`` into ``dout`` and the new server
+    control variate ``sum_k w_k cv_k + c`` into ``cout`` on the root (True there).  ``c``: the
+    whole server control variate (global indexing), read where a stripe's last block runs (the
+    root, and for ``striped`` every rank) and on the root for the numel == 1 elements."""
+    import torch
+
+    sh0 = next(iter(blocks.values()))
+    kind, K = sh0.kind, sh0.K
+    acc = _slots(torch, plan, dout, 2, slots)
+
+    def region(loc, n):
+        where, slot, off = loc
+        if where == "out":
+            return [dout[off: off + n], cout[off: off + n]]
+        return [acc[0, slot, off: off + n], acc[1, slot, off: off + n]]
+
+    def launch(r):
+        sh = blocks[r.block]
+        d, cc = region(r.acc, r.n)
+        ops.scaffold_run(kind, sh.delta[:, r.col: r.col + r.n], sh.cv[:, r.col: r.col + r.n], sh.w, r.seed, r.final,
+                         c[r.lo: r.lo + r.n] if r.final else None, lr, d, cc)
+
+    lockstep.run(plan, transport, region, launch)
+    pw = np.asarray(pairwise_idx, np.int64)
+    P = int(pw.size)
+    if P:
+        n = P * (2 * K + 1)
+        if ws is None:
+            ws = torch.zeros(n, dtype=torch.float64, device=dout.device)
+        else:
+            ws.zero_()
+        wd, wc = ws[: P * K].view(P, K), ws[P * K:].view(P, K + 1)
+        for b, p0, p1, cols in lockstep.pairwise_segments(plan, pw):
+            sh = blocks[b]
+            if not sh.Kr:
+                continue
+            tmp = torch.zeros((p1 - p0) * (2 * K + 1), dtype=torch.float64, device=dout.device)
+            ops.scaffold_products_at(kind, sh.delta, sh.cv, sh.w, sh.kbase, K, cols, tmp)
+            wd[p0:p1] += tmp[: (p1 - p0) * K].view(p1 - p0, K)
+            wc[p0:p1] += tmp[(p1 - p0) * K:].view(p1 - p0, K + 1)
+        if plan.world > 1:
+            transport.reduce_sum(ws, plan.root)
+        if plan.rank == plan.root:
+            glob = ScaffoldShard(kind, None, None, c, np.zeros(0), 0, K, int(dout.shape[0]), lr, pw.astype(np.uint64))
+            ops.scaffold_finish(glob, ws, dout, cout)
+    return plan.rank == plan.root
+
+
+def client_shard_fedavg(sh: FedAvgShard, out, transport, ops, combine: str = "relay", ws=None,
+                        chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
+    """Client-sharded FedAvg (fed_avg.py:217-222) over ``transport``'s ranks with one client block
+    per rank (rank ``(b + 1) % G`` holds block b, :func:`block_of`): every rank passes its
+    :class:`FedAvgShard`; the result lands in ``out`` (``[>= M]``, fp32 for f32/bf16) on the root
+    (rank 0), which this returns True on.  ``ws``: optional ``[P, K]`` workspace.  (``striped``
+    holds a block per stripe instead: :func:`lockstep_fedavg` with :func:`striped_plan`.)"""
+    import torch
+
+    if combine not in ("relay", "rccl", "ordered"):
+        raise ValueError("combine must be one of ('relay', 'rccl', 'ordered') (striped: lockstep_fedavg)")
     rank, G = transport.rank, transport.world
     root = 0
-    b, prev, nxt = _neighbours(rank, G)
+    if combine == "relay" or G == 1:
+        plan = relay_plan(sh.M, G, rank, chunk_elems)
+        return lockstep_fedavg(plan, {block_of(rank, G): sh}, out, transport, ops, sh.pairwise_idx, ws=ws)
     P = int(sh.pairwise_idx.size)
     if P:
         if ws is None:
@@ -559,26 +758,20 @@ def client_shard_fedavg(sh: FedAvgShard, out, transport, ops, combine: str = "re
         else:
             ws.zero_()
         ops.fedavg_products(sh, ws)
-    if G == 1:
-        ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, out)
-    elif combine == "relay":
-        _relay(transport, relay_chunks(sh.M, chunk_elems), lambda a, b_: [out[a:b_]],
-               lambda a, b_, seed, last: ops.fedavg_chain(sh.kind, sh.rows, sh.w, a, b_, seed, out), prev, nxt)
+    if combine == "rccl":  # chunk j's reduction overlaps chunk j + 1's partial
+        works = []
+        for a, b_ in relay_chunks(sh.M, chunk_elems):
+            ops.fedavg_chain(sh.kind, sh.rows, sh.w, a, b_, True, out)  # this block's partial from +0.0
+            works.append(_reduce_async(transport, out[a:b_], root))
+        for w in works:
+            w.wait()
     else:
-        if combine == "rccl":  # chunk j's reduction overlaps chunk j + 1's partial
-            works = []
-            for a, b_ in relay_chunks(sh.M, chunk_elems):
-                ops.fedavg_chain(sh.kind, sh.rows, sh.w, a, b_, True, out)  # this block's partial from +0.0
-                works.append(_reduce_async(transport, out[a:b_], root))
-            for w in works:
-                w.wait()
-        else:
-            ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, out)  # this block's partial from +0.0
-            parts = transport.gather(out[: sh.M].contiguous(), root)
-            if rank == root:
-                stack = torch.stack([parts[chain_rank(i, G)] for i in range(G)])  # block order
-                ops.fedavg_combine(sh.kind, stack, sh.M, out)
-    if P and G > 1:
+        ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, out)  # this block's partial from +0.0
+        parts = transport.gather(out[: sh.M].contiguous(), root)
+        if rank == root:
+            stack = torch.stack([parts[chain_rank(i, G)] for i in range(G)])  # block order
+            ops.fedavg_combine(sh.kind, stack, sh.M, out)
+    if P:
         transport.reduce_sum(ws, root)  # columns of other blocks are zeros: the sum is exact
     if rank == root and P:
         ops.fedavg_finish(sh.kind, ws, sh.K, sh.pairwise_idx, out)
@@ -593,11 +786,14 @@ def client_shard_scaffold(sh: ScaffoldShard, dout, cout, transport, ops, combine
     and ``lr`` applied after the sum, on the root, in every mode."""
     import torch
 
-    if combine not in COMBINES:
-        raise ValueError(f"combine must be one of {COMBINES}")
+    if combine not in ("relay", "rccl", "ordered"):
+        raise ValueError("combine must be one of ('relay', 'rccl', 'ordered') (striped: lockstep_scaffold)")
     rank, G = transport.rank, transport.world
     root = 0
-    b, prev, nxt = _neighbours(rank, G)
+    if combine == "relay" or G == 1:
+        plan = relay_plan(sh.M, G, rank, chunk_elems)
+        return lockstep_scaffold(plan, {block_of(rank, G): sh}, dout, cout, transport, ops, sh.pairwise_idx, sh.c,
+                                 sh.lr, ws=ws)
     P = int(sh.pairwise_idx.size)
     if P:
         n = P * (2 * sh.K + 1)
@@ -606,31 +802,25 @@ def client_shard_scaffold(sh: ScaffoldShard, dout, cout, transport, ops, combine
         else:
             ws.zero_()
         ops.scaffold_products(sh, ws)
-    if G == 1:
-        ops.scaffold_chain(sh, 0, sh.M, True, True, dout, cout)
-    elif combine == "relay":
-        _relay(transport, relay_chunks(sh.M, chunk_elems), lambda a, b_: [dout[a:b_], cout[a:b_]],
-               lambda a, b_, seed, last: ops.scaffold_chain(sh, a, b_, seed, last, dout, cout), prev, nxt)
+    if combine == "rccl":  # chunk j's reductions overlap chunk j + 1's partial sums
+        works = []
+        for a, b_ in relay_chunks(sh.M, chunk_elems):
+            ops.scaffold_chain(sh, a, b_, True, False, dout, cout)  # plain fp64 partial sums
+            works += [_reduce_async(transport, dout[a:b_], root), _reduce_async(transport, cout[a:b_], root)]
+        for w in works:
+            w.wait()
+        if rank == root:  # final step: lr * (0 + 1.0 * sum), 0 + 1.0 * sum + c
+            ops.scaffold_combine(sh, dout[: sh.M].unsqueeze(0).clone(), cout[: sh.M].unsqueeze(0).clone(),
+                                 dout, cout)
     else:
-        if combine == "rccl":  # chunk j's reductions overlap chunk j + 1's partial sums
-            works = []
-            for a, b_ in relay_chunks(sh.M, chunk_elems):
-                ops.scaffold_chain(sh, a, b_, True, False, dout, cout)  # plain fp64 partial sums
-                works += [_reduce_async(transport, dout[a:b_], root), _reduce_async(transport, cout[a:b_], root)]
-            for w in works:
-                w.wait()
-            if rank == root:  # final step: lr * (0 + 1.0 * sum), 0 + 1.0 * sum + c
-                ops.scaffold_combine(sh, dout[: sh.M].unsqueeze(0).clone(), cout[: sh.M].unsqueeze(0).clone(),
-                                     dout, cout)
-        else:
-            ops.scaffold_chain(sh, 0, sh.M, True, False, dout, cout)  # plain fp64 partial sums
-            dp = transport.gather(dout[: sh.M].contiguous(), root)
-            cp = transport.gather(cout[: sh.M].contiguous(), root)
-            if rank == root:
-                order = [chain_rank(i, G) for i in range(G)]
-                ops.scaffold_combine(sh, torch.stack([dp[r] for r in order]), torch.stack([cp[r] for r in order]),
-                                     dout, cout)
-    if P and G > 1:
+        ops.scaffold_chain(sh, 0, sh.M, True, False, dout, cout)  # plain fp64 partial sums
+        dp = transport.gather(dout[: sh.M].contiguous(), root)
+        cp = transport.gather(cout[: sh.M].contiguous(), root)
+        if rank == root:
+            order = [chain_rank(i, G) for i in range(G)]
+            ops.scaffold_combine(sh, torch.stack([dp[r] for r in order]), torch.stack([cp[r] for r in order]),
+                                 dout, cout)
+    if P:
         transport.reduce_sum(ws, root)
     if rank == root and P:
         ops.scaffold_finish(sh, ws, dout, cout)
@@ -638,195 +828,7 @@ def client_shard_scaffold(sh: ScaffoldShard, dout, cout, transport, ops, combine
 
 
 # ======================================================================================
-# striped relay: S parameter stripes, each a relay over its own chain order
-# ======================================================================================
-def _units(G: int) -> List[int]:
-    """The units of Z_G (chain multipliers), alternating 1, G-1, 3, G-3, ... (for G = 8: 1 7 3 5)."""
-    import math
-
-    lo = [a for a in range(1, G) if math.gcd(a, G) == 1] or [1]
-    out, i, j = [], 0, len(lo) - 1
-    while i <= j:
-        out.append(lo[i])
-        if j != i:
-            out.append(lo[j])
-        i, j = i + 1, j - 1
-    return out
-
-
-def stripe_multipliers(G: int, stripes: Optional[int] = None) -> List[int]:
-    """One chain multiplier per stripe (default: as many as Z_G has units, at most 4)."""
-    u = _units(G)
-    n = min(len(u), 4) if stripes is None else max(1, min(int(stripes), len(u)))
-    return u[:n]
-
-
-def stripe_rank(block: int, world: int, a: int) -> int:
-    """Rank holding client block ``block`` in a stripe with multiplier ``a``: ``a * (block + 1) mod
-    G`` (a = 1 is :func:`chain_rank`); the last block is on the root for every unit ``a``."""
-    return (a * (block + 1)) % world
-
-
-def stripe_block(rank: int, world: int, a: int) -> int:
-    """Inverse of :func:`stripe_rank`: the block ``rank`` holds in that stripe."""
-    inv = pow(a, -1, world) if world > 1 else 0
-    return (inv * rank - 1) % world
-
-
-def stripe_layout(M: int, K: int, world: int, rank: int, stripes: Optional[int] = None):
-    """This rank's part of a striped client-sharded reduction: per stripe ``(lo, hi, a, block,
-    k0, k1)`` -- element range, chain multiplier, the client block it holds there and that block's
-    clients."""
-    mult = stripe_multipliers(world, stripes)
-    blocks = client_blocks(K, world)
-    out = []
-    for (lo, hi), a in zip(shard_bounds(M, len(mult)), mult):
-        b = stripe_block(rank, world, a)
-        out.append((lo, hi, a, b) + tuple(blocks[b]))
-    return out
-
-
-def _stripe_neighbours(rank: int, world: int, a: int) -> Tuple[Optional[int], Optional[int]]:
-    b = stripe_block(rank, world, a)
-    prev = stripe_rank(b - 1, world, a) if b > 0 else None
-    nxt = stripe_rank(b + 1, world, a) if b < world - 1 else None
-    return prev, nxt
-
-
-def _run_stripes(jobs: Sequence[Callable[[], None]], device) -> None:
-    """Run the stripes' relays concurrently: one host thread each, each on its own HIP stream
-    (ordered after the caller's stream, and the caller's stream after all of them), so the
-    stripes' P2P traffic (one communicator per stripe) and kernels overlap."""
-    import torch
-
-    if len(jobs) == 1:
-        jobs[0]()
-        return
-    cuda = device is not None and device.type == "cuda"
-    main = torch.cuda.current_stream(device) if cuda else None
-    streams = [torch.cuda.Stream(device) for _ in jobs] if cuda else [None] * len(jobs)
-    err: List[Optional[BaseException]] = [None] * len(jobs)
-
-    def body(i):
-        try:
-            if cuda:
-                torch.cuda.set_device(device)
-                with torch.cuda.stream(streams[i]):
-                    jobs[i]()
-            else:
-                jobs[i]()
-        except BaseException as e:  # noqa: BLE001 -- re-raised on the caller's thread
-            err[i] = e
-
-    if cuda:
-        for st in streams:
-            st.wait_stream(main)
-    th = [threading.Thread(target=body, args=(i,), name=f"stripe-{i}") for i in range(len(jobs))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if cuda:
-        for st in streams:
-            main.wait_stream(st)
-    for e in err:
-        if e is not None:
-            raise e
-
-
-def client_shard_fedavg_striped(parts: Sequence[FedAvgShard], bounds: Sequence[Tuple[int, int, int]], out,
-                                transports: Sequence, ops, pairwise_idx, ws=None,
-                                chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
-    """Striped relay FedAvg (bit-exact, see the module docstring).  Per stripe s: ``bounds[s] =
-    (lo, hi, a)``, ``parts[s]`` this rank's block for that stripe (``rows`` ``[Kb, hi - lo]``, the
-    block's global weights, ``kbase``, ``K``, ``M = hi - lo``, ``pairwise_idx`` relative to
-    ``lo``), ``transports[s]`` a transport of its own (one communicator per stripe).  The result
-    lands in ``out[:M]`` on the root (rank 0), which this returns True on; ``pairwise_idx``: the
-    global numel == 1 indices (sorted)."""
-    import torch
-
-    tr0 = transports[0]
-    rank, G = tr0.rank, tr0.world
-    kind, K = parts[0].kind, parts[0].K
-    jobs = []
-    for sh, (lo, hi, a), tr in zip(parts, bounds, transports):
-        o = out[lo:hi]
-        if G == 1:
-            jobs.append(lambda sh=sh, o=o: ops.fedavg_chain(sh.kind, sh.rows, sh.w, 0, sh.M, True, o))
-            continue
-        prev, nxt = _stripe_neighbours(rank, G, a)
-        jobs.append(lambda sh=sh, o=o, tr=tr, prev=prev, nxt=nxt: _relay(
-            tr, relay_chunks(sh.M, chunk_elems), lambda x, y: [o[x:y]],
-            lambda x, y, seed, last: ops.fedavg_chain(sh.kind, sh.rows, sh.w, x, y, seed, o), prev, nxt))
-    _run_stripes(jobs, out.device)
-    P = int(np.asarray(pairwise_idx).size)
-    if P:
-        pw = np.asarray(pairwise_idx, np.int64)
-        if ws is None:
-            ws = torch.zeros((P, K), dtype=ws_dtype(torch, kind), device=out.device)
-        else:
-            ws.zero_()
-        for sh, (lo, hi, a) in zip(parts, bounds):
-            p0, p1 = int(np.searchsorted(pw, lo)), int(np.searchsorted(pw, hi))
-            if p1 > p0:
-                ops.fedavg_products(sh, ws[p0:p1])
-        if G > 1:
-            tr0.reduce_sum(ws, 0)
-        if rank == 0:
-            ops.fedavg_finish(kind, ws, K, pw.astype(np.uint64), out)
-    return rank == 0
-
-
-def client_shard_scaffold_striped(parts: Sequence[ScaffoldShard], bounds: Sequence[Tuple[int, int, int]], dout,
-                                  cout, transports: Sequence, ops, pairwise_idx, c=None, ws=None,
-                                  chunk_elems: int = RELAY_CHUNK_ELEMS) -> bool:
-    """Striped relay Scaffold (scaffold.py:262-263, 293; bit-exact): per stripe as
-    :func:`client_shard_fedavg_striped`, ``parts[s].c`` the stripe's slice of the server control
-    variate (read by the root, which holds every stripe's last block and applies ``+ c`` and
-    ``lr`` inside its last kernel); ``c``: the whole ``c`` (root, numel == 1 elements only)."""
-    import torch
-
-    tr0 = transports[0]
-    rank, G = tr0.rank, tr0.world
-    K, lr = parts[0].K, parts[0].lr
-    jobs = []
-    for sh, (lo, hi, a), tr in zip(parts, bounds, transports):
-        d, co = dout[lo:hi], cout[lo:hi]
-        if G == 1:
-            jobs.append(lambda sh=sh, d=d, co=co: ops.scaffold_chain(sh, 0, sh.M, True, True, d, co))
-            continue
-        prev, nxt = _stripe_neighbours(rank, G, a)
-        jobs.append(lambda sh=sh, d=d, co=co, tr=tr, prev=prev, nxt=nxt: _relay(
-            tr, relay_chunks(sh.M, chunk_elems), lambda x, y: [d[x:y], co[x:y]],
-            lambda x, y, seed, last: ops.scaffold_chain(sh, x, y, seed, last, d, co), prev, nxt))
-    _run_stripes(jobs, dout.device)
-    P = int(np.asarray(pairwise_idx).size)
-    if P:
-        pw = np.asarray(pairwise_idx, np.int64)
-        n = P * (2 * K + 1)
-        if ws is None:
-            ws = torch.zeros(n, dtype=torch.float64, device=dout.device)
-        else:
-            ws.zero_()
-        wd, wc = ws[: P * K].view(P, K), ws[P * K:].view(P, K + 1)
-        for sh, (lo, hi, a) in zip(parts, bounds):
-            p0, p1 = int(np.searchsorted(pw, lo)), int(np.searchsorted(pw, hi))
-            if p1 > p0 and sh.Kr:
-                tmp = torch.zeros((p1 - p0) * (2 * K + 1), dtype=torch.float64, device=dout.device)
-                ops.scaffold_products(sh, tmp)
-                wd[p0:p1] += tmp[: (p1 - p0) * K].view(p1 - p0, K)
-                wc[p0:p1] += tmp[(p1 - p0) * K:].view(p1 - p0, K + 1)
-        if G > 1:
-            tr0.reduce_sum(ws, 0)
-        if rank == 0:
-            glob = ScaffoldShard(parts[0].kind, None, None, c, np.zeros(0), 0, K, int(dout.shape[0]), lr,
-                                 pw.astype(np.uint64))
-            ops.scaffold_finish(glob, ws, dout, cout)
-    return rank == 0
-
-
-# ======================================================================================
-# host entry points (every rank reads the same K host shared states, stages its block)
+# host entry points (every rank reads the same K host shared states, stages its blocks)
 # ======================================================================================
 def _rank_device(torch):
     return torch.device("cuda", torch.cuda.current_device())
@@ -844,106 +846,103 @@ def _one_dtype(lists, what: str) -> np.dtype:
 
 
 def _stage_block(torch, device, rows: List[List[np.ndarray]], layout: BucketLayout, dtype,
-                 lo: int = 0, hi: Optional[int] = None):
-    """The rows of this rank's clients, staged through the native session's pinned ring into a
-    ``[Kr, ld]`` device tensor of ``dtype`` (no host-side packing; stream-ordered before torch's
+                 segs: Optional[Sequence[Tuple[int, int, int]]] = None, ncols: Optional[int] = None):
+    """The rows of a client block, staged through the native session's pinned ring into a
+    ``[Kb, ld]`` device tensor of ``dtype`` (no host-side packing; stream-ordered before torch's
     work).  Rows of another float dtype are staged raw and widened exactly on the device
     (``fedagg_cast``: Scaffold's fp32 deltas beside fp64 control variates from round 2 on).
-    ``lo``/``hi``: only elements ``[lo, hi)`` of every row (a parameter stripe), into a
-    ``[Kr, hi - lo]`` view of 64-element-padded rows."""
+    ``segs``: only elements ``[lo, hi)`` of every row, each at column ``col`` of a
+    ``[Kb, ncols]`` buffer (a striped block, ``plan.blocks[b]``)."""
     from . import runtime
     from .engine import torch_dtype
 
-    full = hi is None
-    hi = layout.M if full else hi
-    n = hi - lo
-    ld = layout.ld if full else max(64, -(-n // 64) * 64)
+    full = segs is None
+    width = layout.M if full else int(ncols)
+    ld = layout.ld if full else max(64, -(-width // 64) * 64)
     t = torch.empty((max(1, len(rows)), ld), dtype=dtype, device=device)
-    if rows and n > 0:
+    todo = [(0, layout.M, 0)] if full else [(lo, hi, c) for lo, hi, c in segs if hi > lo]
+    if rows and todo:
         s = runtime.session(device.index)
         src = {a.dtype for r in rows for a in r}
         arrays = [[np.ascontiguousarray(a) for a in r] for r in rows]
         sdt = next(iter(src))
-        rng = None if full else (lo * np.dtype(sdt).itemsize, hi * np.dtype(sdt).itemsize)
+        isz = np.dtype(sdt).itemsize
+        raw = t
         if len(src) == 1 and torch_dtype(sdt) != dtype:
             raw = torch.empty((len(rows), ld), dtype=torch_dtype(sdt), device=device)
-            s.stage(raw.data_ptr(), ld * raw.element_size(), arrays, byte_range=rng)
+        for lo, hi, col in todo:
+            rng = None if full else (lo * isz, hi * isz)
+            s.stage(raw.data_ptr() + col * raw.element_size(), ld * raw.element_size(), arrays, byte_range=rng)
+        if raw is not t:
             s.cast(raw.data_ptr(), sdt, t.data_ptr(), np.dtype(str(dtype).replace("torch.", "")), len(rows) * ld)
-            s.sync()
-            del raw
-        else:
-            s.stage(t.data_ptr(), ld * t.element_size(), arrays, byte_range=rng)
-            s.sync()
-    return t[: len(rows)] if full else t[: len(rows), :n]
+        s.sync()
+        del raw
+    return t[: len(rows)] if full else t[: len(rows), :width]
 
 
-_STRIPE_GROUPS: Dict[tuple, list] = {}
+def _transport(transport, group):
+    return transport or DistTransport(group)
 
 
-def _stripe_transports(transport, group, stripes: Optional[int], transports):
-    """One transport per stripe of the striped relay: given, or one new process group each (every
-    rank creates them in the same order)."""
-    import torch.distributed as dist
+def _block_layout(torch, kind: str, Kb: int, extents, tiled) -> int:
+    """The tile (16-B vectors) a client block is re-tiled with, 0 for rows: ``tiled`` True/False,
+    or "auto" -- where the library recommends the tile-interleaved layout for EVERY run of the
+    block (its kernel for such a run walks the tiled kernel's tile)."""
+    from .engine import TILED_KINDS, tiled_recommended, tiled_tile
 
-    if transports is not None:
-        return list(transports)
-    tr = transport or DistTransport(group)
-    S = len(stripe_multipliers(tr.world, stripes))
-    if tr.world == 1:
-        return [tr] * S
-    # keyed by the default group too: a re-initialised process group gets fresh communicators
-    key = (id(dist.group.WORLD), None if group is None else tuple(dist.get_process_group_ranks(group)), S)
-    if key not in _STRIPE_GROUPS:  # communicators are set up once per process, not per aggregation
-        ranks = None if group is None else list(key[1])
-        _STRIPE_GROUPS[key] = [dist.new_group(ranks=ranks) for _ in range(S - 1)]
-    return [tr] + [DistTransport(g) for g in _STRIPE_GROUPS[key]]
+    if tiled is False or kind not in TILED_KINDS or Kb == 0 or not extents:
+        return 0
+    if tiled == "auto" and not all(tiled_recommended(kind, Kb, n) for _c, n in extents):
+        return 0
+    return tiled_tile(kind, Kb, max(n for _c, n in extents))
 
 
 def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int], group=None,
-                          combine: str = "relay", transport=None, stripes: Optional[int] = None, transports=None):
+                          combine: str = "relay", transport=None, rings: Optional[int] = None,
+                          rounds: Sequence[float] = lockstep.DEFAULT_ROUNDS, tiled="auto",
+                          chunk_elems: int = RELAY_CHUNK_ELEMS):
     """FedAvg (fed_avg.py:217-222) with the clients sharded over the process group: rank r stages
-    only its block's buckets (to its own GPU), the chain / reduce runs over RCCL and the root
+    only its blocks' buckets (to its own GPU), the chain / reduce runs over RCCL and the root
     (rank 0) returns the averaged layers; other ranks return None.  Layers must share one float
     dtype.  ``combine="relay"`` and ``"striped"`` are bit-identical to the reference
-    (``striped``: ``stripes`` parameter stripes, one process group each, see the module
-    docstring)."""
+    (``striped``: ``rings`` hop lengths and ``rounds`` of :func:`lockstep.striped_pieces`);
+    ``tiled``: their client blocks re-tiled per run (:class:`TiledBlock`; "auto": where the
+    library recommends it, fp32 / bf16)."""
     import torch
 
     from .engine import fedavg_weights, kind_of, torch_dtype
 
-    if combine == "striped":
-        trs = _stripe_transports(transport, group, stripes, transports)
-        tr = trs[0]
-    else:
-        tr = transport or DistTransport(group)
+    if combine not in COMBINES:
+        raise ValueError(f"combine must be one of {COMBINES}")
+    tr = _transport(transport, group)
     G, rank = tr.world, tr.rank
     K, L = len(parameters_updates), len(parameters_updates[0])
     dtype = _one_dtype(parameters_updates, "FedAvg")
     kind = kind_of(dtype)
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], dtype)
     dev = _rank_device(torch)
-    if combine == "striped":
-        w_all = fedavg_weights(n_samples, kind)
-        pw = layout.pairwise_idx.astype(np.int64)
-        lay = stripe_layout(layout.M, K, G, rank, len(trs))
-        parts = []
-        for lo, hi, a, b, k0, k1 in lay:
-            rows = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout,
-                                torch_dtype(kind), lo, hi)
-            parts.append(FedAvgShard(kind, rows, w_all[k0:k1], k0, K, hi - lo,
-                                     (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)))
-        out = torch.empty(layout.ld, dtype=out_dtype(torch, kind), device=dev)
-        if not client_shard_fedavg_striped(parts, [(lo, hi, a) for lo, hi, a, *_ in lay], out, trs, GpuShardOps(),
-                                           pw):
-            return None
-        flat = out[: layout.M].cpu().numpy()
-        return [a for _, a in layout.unpack(np.array(flat, copy=True))]
-    k0, k1 = client_blocks(K, G)[block_of(rank, G)]
-    rows = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, torch_dtype(kind))
-    w = fedavg_weights(n_samples, kind)[k0:k1]
+    w_all = fedavg_weights(n_samples, kind)
     out = torch.empty(layout.ld, dtype=out_dtype(torch, kind), device=dev)
-    sh = FedAvgShard(kind, rows, w, k0, K, layout.M, layout.pairwise_idx)
-    if not client_shard_fedavg(sh, out, tr, GpuShardOps(), combine):
+    if combine in ("relay", "striped"):
+        plan = (striped_plan(layout.M, G, rank, rings, rounds) if combine == "striped"
+                else relay_plan(layout.M, G, rank, chunk_elems))
+        blocks = {}
+        for b, segs in plan.blocks.items():
+            k0, k1 = client_blocks(K, G)[b]
+            rows = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout,
+                                torch_dtype(kind), segs if combine == "striped" else None, plan.block_len[b])
+            ext = TiledBlock.run_extents(plan, b)
+            tv = _block_layout(torch, kind, k1 - k0, ext, tiled)
+            if tv:
+                rows = TiledBlock.from_rows(torch, kind, rows, tv, ext)
+            blocks[b] = FedAvgShard(kind, rows, w_all[k0:k1], k0, K, plan.block_len[b], np.zeros(0, np.uint64))
+        root = lockstep_fedavg(plan, blocks, out, tr, GpuShardOps(), layout.pairwise_idx)
+    else:
+        k0, k1 = client_blocks(K, G)[block_of(rank, G)]
+        rows = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, torch_dtype(kind))
+        sh = FedAvgShard(kind, rows, w_all[k0:k1], k0, K, layout.M, layout.pairwise_idx)
+        root = client_shard_fedavg(sh, out, tr, GpuShardOps(), combine, chunk_elems=chunk_elems)
+    if not root:
         return None
     flat = out[: layout.M].cpu().numpy()
     return [a for _, a in layout.unpack(np.array(flat, copy=True))]
@@ -951,10 +950,10 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
 
 def client_sharded_scaffold(parameters_updates, control_variate_updates, server_control_variates, n_samples,
                             aggregation_lr, group=None, combine: str = "relay", transport=None,
-                            stripes: Optional[int] = None, transports=None):
+                            rings: Optional[int] = None, rounds: Sequence[float] = lockstep.DEFAULT_ROUNDS):
     """Scaffold (scaffold.py:193-196, 297-337) with the clients sharded over the process group.
-    Every rank checks its block's server control variates against client 0's on the host while
-    staging (one device copy of ``c``, needed by the root only).  Returns
+    Every rank checks its blocks' server control variates against client 0's on the host while
+    staging (``c`` itself is staged once per rank that runs a final step).  Returns
     ``(mismatches, new_server_control_variate, avg_parameters_update)`` on the root, None
     elsewhere.  fp32 or fp64 buckets (one dtype for all three lists)."""
     import torch
@@ -962,11 +961,9 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     from . import runtime
     from .engine import scaffold_weights, torch_dtype
 
-    if combine == "striped":
-        trs = _stripe_transports(transport, group, stripes, transports)
-        tr = trs[0]
-    else:
-        tr = transport or DistTransport(group)
+    if combine not in COMBINES:
+        raise ValueError(f"combine must be one of {COMBINES}")
+    tr = _transport(transport, group)
     G, rank = tr.world, tr.rank
     K, L = len(parameters_updates), len(parameters_updates[0])
     # fp32 buckets when every list is fp32 (NEP 50: the sums are fp64 either way), else fp64 with
@@ -980,58 +977,43 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     layout = BucketLayout(range(L), [a.shape for a in parameters_updates[0]], sdt)
     dev = _rank_device(torch)
     td = torch_dtype(kind)
-    if combine == "striped":
-        return _client_sharded_scaffold_striped(torch, runtime, trs, layout, kind, td, dts[2], dev, parameters_updates,
-                                                control_variate_updates, server_control_variates,
-                                                scaffold_weights(n_samples), float(aggregation_lr))
-    k0, k1 = client_blocks(K, G)[block_of(rank, G)]
-    delta = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, td)
-    cv = _stage_block(torch, dev, [control_variate_updates[k] for k in range(k0, k1)], layout, td)
-    # c: client 0's copy staged once (used by the root), this block's copies checked against it
+    w_all = scaffold_weights(n_samples)
+    lr = float(aggregation_lr)
     s = runtime.session(dev.index)
-    check_rows = [list(server_control_variates[0])] + [list(server_control_variates[k]) for k in range(k0, k1)
-                                                      if k != 0]
-    mism = s.check(check_rows, dts[2])
     c = _stage_block(torch, dev, [list(server_control_variates[0])], layout, td)[0]
-    mism = tr.all_sum_int(mism)
     dout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
     cout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
-    sh = ScaffoldShard(kind, delta, cv, c, scaffold_weights(n_samples)[k0:k1], k0, K, layout.M,
-                       float(aggregation_lr), layout.pairwise_idx)
-    if not client_shard_scaffold(sh, dout, cout, tr, GpuShardOps(), combine):
-        return None
-    d = dout[: layout.M].cpu().numpy().copy()
-    cc = cout[: layout.M].cpu().numpy().copy()
-    return mism, [a for _, a in layout.unpack(cc)], [a for _, a in layout.unpack(d)]
-
-
-def _client_sharded_scaffold_striped(torch, runtime, trs, layout, kind, td, c_dtype, dev, pus, cvs, cs, w_all, lr):
-    """client_sharded_scaffold's striped form: per stripe this rank stages its block's delta and
-    control-variate slices, checks the block's server control variates against client 0's on the
-    host over the stripe's bytes, and the root stages c once."""
-    tr = trs[0]
-    G, rank = tr.world, tr.rank
-    K = len(pus)
-    pw = layout.pairwise_idx.astype(np.int64)
-    lay = stripe_layout(layout.M, K, G, rank, len(trs))
-    s = runtime.session(dev.index)
-    isz = np.dtype(c_dtype).itemsize
-    c = _stage_block(torch, dev, [list(cs[0])], layout, td)[0] if rank == 0 else None
+    isz = np.dtype(dts[2]).itemsize
     mism = 0
-    parts = []
-    for lo, hi, a, b, k0, k1 in lay:
-        delta = _stage_block(torch, dev, [pus[k] for k in range(k0, k1)], layout, td, lo, hi)
-        cv = _stage_block(torch, dev, [cvs[k] for k in range(k0, k1)], layout, td, lo, hi)
-        check_rows = [list(cs[0])] + [list(cs[k]) for k in range(k0, k1) if k != 0]
-        if len(check_rows) > 1 and hi > lo:
-            mism += s.stage_check(0, check_rows, c_dtype, byte_range=(lo * isz, hi * isz))
-        parts.append(ScaffoldShard(kind, delta, cv, c[lo:hi] if c is not None else None, w_all[k0:k1], k0, K, hi - lo,
-                                   lr, (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)))
-    mism = tr.all_sum_int(mism)
-    dout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
-    cout = torch.empty(layout.ld, dtype=torch.float64, device=dev)
-    if not client_shard_scaffold_striped(parts, [(lo, hi, a) for lo, hi, a, *_ in lay], dout, cout, trs,
-                                         GpuShardOps(), pw, c=c):
+    if combine == "striped":
+        plan = striped_plan(layout.M, G, rank, rings, rounds)
+        blocks = {}
+        for b, segs in plan.blocks.items():
+            k0, k1 = client_blocks(K, G)[b]
+            sel = [pu for pu in range(k0, k1)]
+            delta = _stage_block(torch, dev, [parameters_updates[k] for k in sel], layout, td, segs, plan.block_len[b])
+            cv = _stage_block(torch, dev, [control_variate_updates[k] for k in sel], layout, td, segs,
+                              plan.block_len[b])
+            check_rows = [list(server_control_variates[0])] + [list(server_control_variates[k]) for k in sel if k != 0]
+            if len(check_rows) > 1:  # this block's copies of c over the elements this rank holds for it
+                for lo, hi, _col in segs:
+                    if hi > lo:
+                        mism += s.stage_check(0, check_rows, dts[2], byte_range=(lo * isz, hi * isz))
+            blocks[b] = ScaffoldShard(kind, delta, cv, None, w_all[k0:k1], k0, K, plan.block_len[b], lr,
+                                      np.zeros(0, np.uint64))
+        mism = tr.all_sum_int(mism)
+        root = lockstep_scaffold(plan, blocks, dout, cout, tr, GpuShardOps(), layout.pairwise_idx, c, lr)
+    else:
+        k0, k1 = client_blocks(K, G)[block_of(rank, G)]
+        delta = _stage_block(torch, dev, [parameters_updates[k] for k in range(k0, k1)], layout, td)
+        cv = _stage_block(torch, dev, [control_variate_updates[k] for k in range(k0, k1)], layout, td)
+        # this block's copies of c checked against client 0's on the host (pack workers)
+        check_rows = [list(server_control_variates[0])] + [list(server_control_variates[k]) for k in range(k0, k1)
+                                                          if k != 0]
+        mism = tr.all_sum_int(s.check(check_rows, dts[2]))
+        sh = ScaffoldShard(kind, delta, cv, c, w_all[k0:k1], k0, K, layout.M, lr, layout.pairwise_idx)
+        root = client_shard_scaffold(sh, dout, cout, tr, GpuShardOps(), combine)
+    if not root:
         return None
     d = dout[: layout.M].cpu().numpy().copy()
     cc = cout[: layout.M].cpu().numpy().copy()

@@ -206,6 +206,8 @@ def _nccl_world1(q, port):
     try:
         pus, ns = _data(6, seed=3)
         out = {"fedavg": {m: client_sharded_fedavg(pus, ns, combine=m) for m in ("relay", "ordered", "rccl", "striped")}}
+        for m in ("relay", "striped"):  # client blocks re-tiled on the device (TiledBlock)
+            out["fedavg"][m + "_tiled"] = client_sharded_fedavg(pus, ns, combine=m, tiled=True)
         rng = np.random.default_rng(2)
         cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
         c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
@@ -330,52 +332,59 @@ def test_relay_random_sweep(seed):
             assert np.array_equal(g.view(np.uint64), r.view(np.uint64))
 
 
-# ---- striped relay: S parameter stripes, each a relay over its own chain order ----
-def _striped(G, K, strategy="fedavg", kind="f32", stripes=None, chunk_elems=1024, shapes=SHAPES, seed=4, lr=0.9):
+# ---- striped relay: pieces rotating over the ranks on several rings (lockstep schedule) ----
+def _striped(G, K, strategy="fedavg", kind="f32", rings=None, rounds=(0.75, 0.25), shapes=SHAPES, seed=4, lr=0.9,
+             tv=0, relay=False):
     import torch
 
     from substrafl_amd.engine import fedavg_weights, scaffold_weights
     from substrafl_amd.layout import BucketLayout
-    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, LoopbackGroup, ScaffoldShard,
-                                        client_shard_fedavg_striped, client_shard_scaffold_striped, out_dtype,
-                                        stripe_layout, stripe_multipliers)
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, ScaffoldShard, TiledBlock, client_blocks,
+                                        lockstep_fedavg, lockstep_scaffold, out_dtype, relay_plan, striped_plan)
 
-    npdt = {"f32": np.float32, "f64": np.float64, "f16": np.float16}[kind]
+    npdt = {"f32": np.float32, "bf16": np.float32, "f64": np.float64, "f16": np.float16}[kind]
     pus, ns = _data(K, seed=seed, shapes=shapes)
     pus = [[a.astype(npdt) for a in c] for c in pus]
+    if kind == "bf16":  # bf16-representable values: the reference runs on the exact upcast
+        pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
     layout = BucketLayout(range(len(shapes)), shapes, npdt)
-    S = len(stripe_multipliers(G, stripes))
-    groups = [LoopbackGroup(G) for _ in range(S)]
     rng = np.random.default_rng(seed + 1)
     cvs = [[rng.standard_normal(a.shape).astype(npdt) for a in pu] for pu in pus]
     c = [rng.standard_normal(a.shape).astype(npdt) for a in pus[0]]
-    pw = layout.pairwise_idx.astype(np.int64)
 
-    def rank_fn(r, _tr):
-        trs = [g.transport(r) for g in groups]
-        lay = stripe_layout(layout.M, K, G, r, stripes)
-        bounds = [(lo, hi, a) for lo, hi, a, *_ in lay]
+    def rank_fn(r, tr):
+        plan = relay_plan(layout.M, G, r, 4096) if relay else striped_plan(layout.M, G, r, rings, rounds)
         full_c = _rows(torch, [c], layout, dtype=npdt)[0]
-        parts = []
-        for lo, hi, a, b, k0, k1 in lay:
-            loc = (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)
-            d = _rows(torch, pus[k0:k1], layout, dtype=npdt)[:, lo:hi].contiguous()
+        blocks = {}
+        for b, segs in plan.blocks.items():
+            k0, k1 = client_blocks(K, G)[b]
+
+            def packed(lists):
+                full = _rows(torch, lists, layout, dtype=npdt, tdtype=torch.bfloat16 if kind == "bf16" else None)
+                t = torch.zeros((max(1, k1 - k0), plan.block_len[b]), dtype=full.dtype, device="cuda")
+                for lo, hi, col in segs:
+                    t[: k1 - k0, col: col + hi - lo] = full[:, lo:hi]
+                return t[: k1 - k0]
+
             if strategy == "fedavg":
-                parts.append(FedAvgShard(kind, d, fedavg_weights(ns, kind)[k0:k1], k0, K, hi - lo, loc))
+                rows = packed(pus[k0:k1])
+                if tv and k1 > k0:
+                    rows = TiledBlock.from_rows(torch, kind, rows, tv, TiledBlock.run_extents(plan, b))
+                blocks[b] = FedAvgShard(kind, rows, fedavg_weights(ns, kind)[k0:k1], k0, K,
+                                        plan.block_len[b], np.zeros(0, np.uint64))
             else:
-                v = _rows(torch, cvs[k0:k1], layout, dtype=npdt)[:, lo:hi].contiguous()
-                parts.append(ScaffoldShard(kind, d, v, full_c[lo:hi], scaffold_weights(ns)[k0:k1], k0, K, hi - lo, lr,
-                                           loc))
+                blocks[b] = ScaffoldShard(kind, packed(pus[k0:k1]), packed(cvs[k0:k1]), None,
+                                          scaffold_weights(ns)[k0:k1], k0, K, plan.block_len[b], lr,
+                                          np.zeros(0, np.uint64))
         if strategy == "fedavg":
             out = torch.zeros(layout.ld, dtype=out_dtype(torch, kind), device="cuda")
-            if client_shard_fedavg_striped(parts, bounds, out, trs, GpuShardOps(), pw, chunk_elems=chunk_elems):
+            if lockstep_fedavg(plan, blocks, out, tr, GpuShardOps(), layout.pairwise_idx):
                 torch.cuda.current_stream().synchronize()
                 return out[: layout.M].cpu().numpy().copy()
             return None
         dout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
         cout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
-        if client_shard_scaffold_striped(parts, bounds, dout, cout, trs, GpuShardOps(), pw, c=full_c,
-                                         chunk_elems=chunk_elems):
+        if lockstep_scaffold(plan, blocks, dout, cout, tr, GpuShardOps(), layout.pairwise_idx, full_c, lr):
             torch.cuda.current_stream().synchronize()
             return dout[: layout.M].cpu().numpy().copy(), cout[: layout.M].cpu().numpy().copy()
         return None
@@ -390,13 +399,14 @@ def _striped(G, K, strategy="fedavg", kind="f32", stripes=None, chunk_elems=1024
     return [a for _, a in lay64.unpack(cc)] + [a for _, a in lay64.unpack(d)], rc + ra
 
 
-@pytest.mark.parametrize("G,K,kind,stripes", [(8, 20, "f32", None), (4, 9, "f32", 2), (3, 2, "f64", None),
-                                              (2, 5, "f16", None), (8, 7, "f32", 3), (1, 4, "f32", None)])
-def test_striped_relay_fedavg_bit_exact(G, K, kind, stripes):
-    """Every stripe's chain visits the blocks in client order, so each element keeps the
+@pytest.mark.parametrize("G,K,kind,rings,rounds", [(8, 20, "f32", None, (1.0,)), (4, 9, "f32", 2, (0.75, 0.25)),
+                                                   (3, 2, "f64", None, (1.0,)), (2, 5, "f16", None, (0.5, 0.5)),
+                                                   (8, 7, "f32", 3, (0.6, 0.3, 0.1)), (1, 4, "f32", None, (1.0,))])
+def test_striped_relay_fedavg_bit_exact(G, K, kind, rings, rounds):
+    """Every piece's chain visits the blocks in client order, so each element keeps the
     reference's rounding sequence; K < G leaves empty blocks in every stripe."""
     shapes = SHAPES + [(5000,), (1,)]
-    got, ref = _striped(G, K, kind=kind, stripes=stripes, shapes=shapes)
+    got, ref = _striped(G, K, kind=kind, rings=rings, rounds=rounds, shapes=shapes)
     bits = {2: np.uint16, 4: np.uint32, 8: np.uint64}
     for g, r in zip(got, ref):
         assert g.dtype == r.dtype and np.array_equal(g.view(bits[g.itemsize]), r.view(bits[r.itemsize]))
@@ -408,3 +418,16 @@ def test_striped_relay_scaffold_bit_exact(G, K, kind):
     got, ref = _striped(G, K, strategy="scaffold", kind=kind, shapes=shapes)
     for g, r in zip(got, ref):
         assert g.dtype == np.float64 and np.array_equal(g.view(np.uint64), r.view(np.uint64))
+
+
+@pytest.mark.parametrize("G,K,kind,tv,relay", [(2, 70, "f32", 8192, False), (3, 100, "f32", 2048, False),
+                                               (2, 66, "bf16", 4096, False), (4, 130, "f32", 8192, True),
+                                               (2, 64, "bf16", 4096, True), (8, 9, "f32", 2048, False)])
+def test_tiled_client_blocks_bit_exact(G, K, kind, tv, relay):
+    """Client blocks re-tiled run by run (TiledBlock: fedagg_fedavg_chain_tiled_*, >= 32 clients per
+    block, partial tiles, numel == 1 products read through the tile map) -- the striped and the
+    plain relay stay bit-identical to the reference."""
+    shapes = [(37, 29), (1,), (40000,), (1, 1), (3, 3, 3), (70001,), (1,)]
+    got, ref = _striped(G, K, kind=kind, shapes=shapes, tv=tv, relay=relay, rounds=(0.75, 0.25))
+    for g, r in zip(got, ref):
+        assert g.dtype == r.dtype and np.array_equal(g.view(np.uint32), r.view(np.uint32))

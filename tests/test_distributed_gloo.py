@@ -88,37 +88,41 @@ def _client_shard_cpu(rank, world, mode, K, strategy, chunk_elems):
 
 
 def _client_shard_striped_cpu(rank, world, K, strategy, chunk_elems, pus, ns, layout):
-    """The striped relay over gloo: one process group per stripe, the stripes' relays on their own
-    threads of every rank (the product's thread / communicator structure), NumPy per-rank ops."""
-    from substrafl_amd.sharding import (client_shard_fedavg_striped, client_shard_scaffold_striped, stripe_layout,
-                                        stripe_multipliers)
+    """The striped relay over gloo: ONE process group (the default), every rank issuing its
+    lockstep exchange groups from one thread, NumPy per-rank ops."""
+    from substrafl_amd.sharding import ScaffoldShard as SS
+    from substrafl_amd.sharding import lockstep_fedavg, lockstep_scaffold, striped_plan
 
-    S = len(stripe_multipliers(world))
-    trs = [DistTransport()] + [DistTransport(dist.new_group()) for _ in range(S - 1)]
-    lay = stripe_layout(layout.M, K, world, rank)
-    bounds = [(lo, hi, a) for lo, hi, a, *_ in lay]
-    pw = layout.pairwise_idx.astype(np.int64)
+    tr = DistTransport()
+    plan = striped_plan(layout.M, world, rank, None, (0.75, 0.25))
     rng = np.random.default_rng(5)
     cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
     c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
     ct = torch.from_numpy(_flat_rows([c], layout, np.float32)[0])
-    parts = []
-    for lo, hi, a, b, k0, k1 in lay:
-        loc = (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)
-        d = torch.from_numpy(_flat_rows(pus[k0:k1], layout, np.float32)[:, lo:hi].copy())
+    blocks = {}
+    for b, segs in plan.blocks.items():
+        k0, k1 = client_blocks(K, world)[b]
+
+        def packed(lists):
+            full = _flat_rows(lists, layout, np.float32)
+            t = np.zeros((k1 - k0, plan.block_len[b]), np.float32)
+            for lo, hi, col in segs:
+                t[:, col: col + hi - lo] = full[:, lo:hi]
+            return torch.from_numpy(t)
+
         if strategy == "fedavg":
-            parts.append(FedAvgShard("f32", d, fedavg_weights(ns, "f32")[k0:k1], k0, K, hi - lo, loc))
+            blocks[b] = FedAvgShard("f32", packed(pus[k0:k1]), fedavg_weights(ns, "f32")[k0:k1], k0, K,
+                                    plan.block_len[b], np.zeros(0, np.uint64))
         else:
-            v = torch.from_numpy(_flat_rows(cvs[k0:k1], layout, np.float32)[:, lo:hi].copy())
-            parts.append(ScaffoldShard("f32", d, v, ct[lo:hi], scaffold_weights(ns)[k0:k1], k0, K, hi - lo, 0.7, loc))
+            blocks[b] = SS("f32", packed(pus[k0:k1]), packed(cvs[k0:k1]), None, scaffold_weights(ns)[k0:k1], k0, K,
+                           plan.block_len[b], 0.7, np.zeros(0, np.uint64))
     if strategy == "fedavg":
         out = torch.zeros(layout.ld, dtype=torch.float32)
-        root = client_shard_fedavg_striped(parts, bounds, out, trs, CpuShardOps(), pw, chunk_elems=chunk_elems)
+        root = lockstep_fedavg(plan, blocks, out, tr, CpuShardOps(), layout.pairwise_idx)
         return [a for _, a in layout.unpack(out[: layout.M].numpy().copy())] if root else None
     dout = torch.zeros(layout.ld, dtype=torch.float64)
     cout = torch.zeros(layout.ld, dtype=torch.float64)
-    if not client_shard_scaffold_striped(parts, bounds, dout, cout, trs, CpuShardOps(), pw, c=ct,
-                                         chunk_elems=chunk_elems):
+    if not lockstep_scaffold(plan, blocks, dout, cout, tr, CpuShardOps(), layout.pairwise_idx, ct, 0.7):
         return None
     lay64 = BucketLayout(range(len(pus[0])), [a.shape for a in pus[0]], np.float64)
     return ([a for _, a in lay64.unpack(cout[: layout.M].numpy().copy())]
@@ -214,8 +218,8 @@ def test_client_sharded_relay_bit_exact(world, K):
 @pytest.mark.parametrize("world,K,strategy", [(2, 5, "fedavg"), (4, 9, "fedavg"), (3, 2, "fedavg"),
                                               (4, 6, "scaffold"), (2, 3, "scaffold")])
 def test_client_sharded_striped_bit_exact(world, K, strategy):
-    """The striped relay over real gloo process groups (one per stripe, driven from one thread per
-    stripe): bit-identical to the reference, empty blocks included."""
+    """The striped relay over a real gloo process group (one communicator, one issuing thread per
+    rank, the lockstep exchange groups): bit-identical to the reference, empty blocks included."""
     pus, ns = _data(K=K)
     out = _run("striped", world=world, K=K, strategy=strategy)
     assert all(out[r] is None for r in range(1, world))

@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Discrete-event model of the lockstep combines (substrafl_amd/lockstep.py) on G GPUs.
+
+Two uses:
+
+* **Deadlock check** (tests/test_client_shard_cpu.py): every rank's kernels are played in the
+  order ``lockstep.run`` issues them -- exchange group t, then the runs of step t -- under
+  either stream model:
+  ``queues="streams"``: the communicator's kernels on their own queue, the compute kernels on
+  another (group t waits for what the compute stream held when it was issued, i.e. step t - 1's
+  runs; step t's runs wait for group t - 1);
+  ``queues="single"``: EVERY kernel of a rank on ONE in-order hardware queue (the worst case of
+  streams sharing GPU_MAX_HW_QUEUES), so a blocked group blocks everything behind it.
+  A group completes once each of its messages' peer group has started (the n-th send from q to
+  r pairs with the n-th receive of r from q, whatever group either sits in).  The model reports
+  a deadlock if some kernel can never start.
+* **Timing estimate** (DESIGN.md §6): compute = elements x clients x bytes / HBM rate, a message
+  = latency + bytes / link rate (messages to one peer in a group serialised, different peers in
+  parallel, the two directions of a link independent), the gather to the root included.  Efficiency = one rank's compute alone / makespan.
+
+    python3 tools/lockstep_model.py --gpus 8 --clients-per-gpu 64 --params 125000000
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+from typing import Dict, List, Sequence
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from substrafl_amd import lockstep  # noqa: E402
+
+
+class Deadlock(RuntimeError):
+    pass
+
+
+def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", compute_s_per_elem: float = 1.0,
+             link_s_per_elem: float = 0.0, latency_s: float = 0.0) -> Dict[str, float]:
+    """Play every rank's kernels; returns {"makespan", "compute_max"} or raises Deadlock."""
+    G = len(plans)
+    kernels: List[List[dict]] = []
+    for p in plans:
+        ks = []
+        for t in range(p.n_steps + 1):
+            if p.groups[t]:
+                ks.append({"kind": "group", "t": t, "ops": p.groups[t]})
+            if t < p.n_steps and p.runs[t]:
+                ks.append({"kind": "run", "t": t, "n": sum(r.n for r in p.runs[t])})
+        kernels.append(ks)
+    # pair the n-th send q->r with the n-th receive on r from q (NCCL's per-pair FIFO)
+    seq: Dict[tuple, List[tuple]] = {}
+    for r, ks in enumerate(kernels):
+        for i, k in enumerate(ks):
+            if k["kind"] != "group":
+                continue
+            for o in k["ops"]:
+                key = (r, o.peer, "send") if o.kind == "send" else (o.peer, r, "recv")
+                seq.setdefault(key, []).append((r, i, o.n))
+    partner: Dict[tuple, tuple] = {}
+    for (q, r, kind), lst in seq.items():
+        if kind != "send":
+            continue
+        rl = seq.get((q, r, "recv"), [])
+        if len(rl) != len(lst):
+            raise Deadlock(f"{len(lst)} sends {q}->{r} but {len(rl)} receives")
+        for (sq, si, sn), (rr, ri, rn) in zip(lst, rl):
+            if sn != rn:
+                raise Deadlock(f"message size mismatch {q}->{r}: {sn} vs {rn}")
+            partner[(sq, si, "send", len([1 for x in lst if (x[0], x[1]) <= (sq, si)]))] = (rr, ri)
+    # per group: the (peer rank, peer kernel index, elements) of each of its messages
+    links: Dict[tuple, List[tuple]] = {}
+    for (q, r, kind), lst in seq.items():
+        if kind != "send":
+            continue
+        rl = seq[(q, r, "recv")]
+        for (sq, si, sn), (rr, ri, _rn) in zip(lst, rl):
+            links.setdefault((sq, si), []).append((rr, ri, sn, (r, "out")))
+            links.setdefault((rr, ri), []).append((sq, si, sn, (q, "in")))
+
+    start: Dict[tuple, float] = {}
+    end: Dict[tuple, float] = {}
+    ptr = [0] * G
+
+    def deps(r: int, i: int):
+        """Start dependencies of kernel i of rank r (None: not yet known)."""
+        k = kernels[r][i]
+        d = []
+        if queues == "single":
+            if i > 0:
+                d.append((r, i - 1))
+        else:
+            same = [j for j in range(i) if (kernels[r][j]["kind"] == "group") == (k["kind"] == "group")]
+            if same:
+                d.append((r, same[-1]))
+            if k["kind"] == "group":  # the compute stream's work issued before it (step t - 1)
+                prior = [j for j in range(i) if kernels[r][j]["kind"] == "run"]
+                if prior:
+                    d.append((r, prior[-1]))
+            else:  # step t waits for group t - 1
+                prior = [j for j in range(i) if kernels[r][j]["kind"] == "group" and kernels[r][j]["t"] < k["t"]]
+                if prior:
+                    d.append((r, prior[-1]))
+        return d
+
+    progress = True
+    while progress:
+        progress = False
+        for r in range(G):
+            for i, k in enumerate(kernels[r]):
+                if (r, i) not in start:
+                    ds = deps(r, i)
+                    if all(x in end for x in ds):
+                        start[(r, i)] = max([end[x] for x in ds], default=0.0)
+                        progress = True
+                if (r, i) in start and (r, i) not in end:
+                    if k["kind"] == "run":
+                        end[(r, i)] = start[(r, i)] + k["n"] * compute_s_per_elem
+                        progress = True
+                    else:
+                        peers = links.get((r, i), [])
+                        if all((pr, pi) in start for pr, pi, _n, _p in peers):
+                            per_peer: Dict[tuple, int] = {}  # (peer, direction): links are full duplex
+                            t0 = start[(r, i)]
+                            for pr, pi, n, peer in peers:
+                                per_peer[peer] = per_peer.get(peer, 0) + n
+                                t0 = max(t0, start[(pr, pi)])
+                            xfer = max(per_peer.values(), default=0) * link_s_per_elem
+                            end[(r, i)] = t0 + latency_s + xfer
+                            progress = True
+    missing = [(r, i) for r in range(G) for i in range(len(kernels[r])) if (r, i) not in end]
+    if missing:
+        raise Deadlock(f"{len(missing)} kernels never complete (first: rank {missing[0][0]}, "
+                       f"{kernels[missing[0][0]][missing[0][1]]['kind']} of step "
+                       f"{kernels[missing[0][0]][missing[0][1]]['t']})")
+    comp = max(sum(k["n"] for k in ks if k["kind"] == "run") for ks in kernels) * compute_s_per_elem
+    return {"makespan": max(end.values(), default=0.0), "compute_max": comp}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--clients-per-gpu", type=int, default=64)
+    ap.add_argument("--params", type=int, default=125_000_000)
+    ap.add_argument("--hbm-GBps", type=float, default=7000.0, help="bucket kernel read rate")
+    ap.add_argument("--link-GBps", type=float, default=50.0, help="one xGMI link, one direction")
+    ap.add_argument("--latency-us", type=float, default=20.0, help="per exchange group")
+    ap.add_argument("--chunk", type=int, default=2 << 20, help="relay chunk (elements)")
+    args = ap.parse_args()
+    G, Kb, M = args.gpus, args.clients_per_gpu, args.params
+    comp = Kb * 4 / (args.hbm_GBps * 1e9)  # s per element of one block (fp32 reads)
+    link = 4 / (args.link_GBps * 1e9)
+    out = {}
+    schedules = {"relay": lockstep.relay_pieces(M, G, args.chunk)}
+    for rounds in ((1.0,), (0.75, 0.25), (0.5, 0.3, 0.2)):
+        schedules[f"striped rounds={rounds}"] = lockstep.striped_pieces(M, G, None, rounds)
+    for name, pieces in schedules.items():
+        plans = [lockstep.rank_plan(pieces, G, r, cols="global" if name == "relay" else "packed") for r in range(G)]
+        res = simulate(plans, "streams", comp, link, args.latency_us * 1e-6)
+        t1 = M * comp
+        out[name] = {"steps": plans[0].n_steps, "model_ms": round(res["makespan"] * 1e3, 3),
+                     "single_gpu_ms": round(t1 * 1e3, 3), "weak_efficiency": round(t1 / res["makespan"], 3)}
+    print(json.dumps({"gpus": G, "clients_per_gpu": Kb, "params": M, "hbm_GBps": args.hbm_GBps,
+                      "link_GBps": args.link_GBps, "latency_us": args.latency_us, "schedules": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
