@@ -9,20 +9,21 @@ roofline" target is stated on.
 
 Multi-GPU (one process per GPU).  ``--gpus N`` from a plain ``python3 bench.py`` starts the N rank
 processes itself (before anything touches a GPU); under torchrun the ranks come from the
-environment, and a WORLD_SIZE that differs from --gpus is an error.  Modes:
+environment, and a WORLD_SIZE that differs from --gpus is an error.  The process group has a
+finite timeout (``pg_kwargs``).  Modes:
 
 * ``--mode param-range`` (default; SURVEY.md §8(e) primary, bit-exact): every rank reduces its own
   parameter range of all K clients -- no data-path collective.  ``--scaling weak`` (default): each
   rank owns a full M-param slice of an N*M-param model; ``--scaling strong``: the workload's own M
-  is split over the N ranks (C3 at 64 x 125M over 8 GPUs = 15.6M params per GPU).
-* ``--mode client-shard --combine relay|rccl|ordered|striped`` (the north-star mode): the clients
-  are split over the ranks, partial sums stay in HBM and are combined over RCCL/xGMI on the root
-  (``relay`` and ``striped`` bit-exact; ``striped``: the relay over up to four parameter stripes
-  whose chains hop over disjoint xGMI links, one communicator each; see
-  substrafl_amd/sharding.py).  ``--scaling weak``: every rank holds the
-  workload's K clients (N*K clients of M params in all -- the "buckets overflow one GPU" case);
-  ``--scaling strong``: the workload's K clients are split over the N ranks.  Needs one GPU per
-  rank.
+  is split over the N ranks (C3 at 64 x 125M over 8 GPUs = 15.6M params per GPU).  With N > 1 and
+  one GPU per rank the SAME line also carries ``client_shard``: the north-star client-sharded
+  mode timed right after, weak (every rank holds the workload's K clients, N*K in all), combine
+  ``--combine`` (default striped) -- step time, block-kernel time, exchange time, GB/s, fraction
+  of N x 8 TB/s, and weak efficiency against the parameter-range kernel time of one GPU.
+* ``--mode client-shard --combine relay|rccl|ordered|striped``: the client-sharded mode as the
+  line itself.  ``relay`` and ``striped`` are bit-exact lockstep schedules over ONE communicator
+  (substrafl_amd/lockstep.py); ``--scaling weak``: every rank holds the workload's K clients;
+  ``--scaling strong``: the workload's K clients are split over the N ranks.  Needs one GPU per rank.
 * ``--engine multi-device``: the drop-in's own multi-GPU path, ONE process driving N GPUs
   (MultiDeviceEngine: host buckets staged over each GPU's PCIe link, per-shard kernel time from
   HIP events on the session streams) -- an end-to-end line, not the device-resident metric.
@@ -66,7 +67,15 @@ def parse():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--mode", default="param-range", choices=["param-range", "client-shard"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--combine", default="relay", choices=["relay", "rccl", "ordered", "striped"])
+    ap.add_argument("--combine", default="striped", choices=["relay", "rccl", "ordered", "striped"],
+                    help="client-shard combine (the N > 1 line's client_shard leg and --mode client-shard)")
+    ap.add_argument("--client-shard", default="auto", choices=["auto", "off"],
+                    help="N > 1 param-range runs: also time the client-sharded (north-star) mode, weak, in the "
+                         "same invocation (auto: when every rank has its own GPU)")
+    ap.add_argument("--client-shard-steps", type=int, default=50, help="timed steps of the client-shard leg")
+    ap.add_argument("--rings", type=int, default=0, help="striped: rings (hop lengths; 0 = up to 4)")
+    ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default one round)")
+    ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
     ap.add_argument("--tile", type=int, default=0, help="tiles layout: 16-B vectors per client tile "
                     "(0: the library's choice; FEDAGG_TILE_VECTORS_*)")
@@ -84,7 +93,9 @@ def parse():
     ap.add_argument("--cpu-only", action="store_true",
                     help="run only the cpu_baseline leg (no GPU) and print its JSON")
     ap.add_argument("--cpu-full-size", action="store_true",
-                    help="cpu_baseline over the workload's full K x M instead of a bounded sample (C3: ~40 GB host)")
+                    help="cpu_baseline over the workload's full K x M (default: when the host's free RAM holds it)")
+    ap.add_argument("--cpu-sample", action="store_true",
+                    help="cpu_baseline over a bounded sample (64/128 clients x 4M) even when the full size fits")
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="tests only: run the launcher / rank / timing plumbing with no GPU (no measurement)")
     return ap.parse_args()
@@ -189,13 +200,79 @@ def read_traffic(args, sha):
 
 
 # ======================================================================================
+# process group (N > 1)
+# ======================================================================================
+PG_TIMEOUT_S = 300  # a stuck collective or exchange ends the rank instead of holding the lease
+CLIENT_SHARD_DEADLINE_S = 240  # the client-shard leg of an N > 1 line, set-up to spot check
+
+
+def pg_kwargs() -> dict:
+    """init_process_group options of every multi-rank run: a finite timeout (RCCL's watchdog
+    aborts a communicator whose work exceeds it, with TORCH_NCCL_ASYNC_ERROR_HANDLING set below,
+    so a hung rank fails instead of holding the GPUs until the driver's limit)."""
+    from datetime import timedelta
+
+    return {"timeout": timedelta(seconds=PG_TIMEOUT_S)}
+
+
+def init_group(dist, world: int, device, nccl: bool) -> str:
+    """gloo for the host-side barrier / max-over-ranks; with one GPU per rank also RCCL ("nccl")
+    for device tensors -- the client-shard exchange (one communicator, sharding.DistTransport)."""
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")  # abort the communicators, raise in the rank
+    backend = "cpu:gloo,cuda:nccl" if nccl else "gloo"
+    kw = pg_kwargs()
+    if nccl:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+    return backend
+
+
+class _Ctx:
+    """What every measurement of one rank needs."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, vals):
+        if self.world == 1:
+            return [float(v) for v in vals]
+        t = self.torch.tensor([float(v) for v in vals], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return [float(v) for v in t]
+
+
+def _timed(ctx, step, steps, warmup):
+    """W untimed steps, then EXACTLY `steps` steps bracketed by a barrier + synchronize on both
+    sides; returns this rank's wall time of the region and its HIP-event time."""
+    torch = ctx.torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(ctx.device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.barrier()
+    torch.cuda.synchronize(ctx.device)
+    t0 = time.perf_counter()
+    ev0.record(ctx.stream)
+    for _ in range(steps):
+        step()
+    ev1.record(ctx.stream)
+    torch.cuda.synchronize(ctx.device)
+    elapsed = time.perf_counter() - t0
+    ctx.barrier()
+    return elapsed, ev0.elapsed_time(ev1)
+
+
+# ======================================================================================
 # the rank path (device-resident metric)
 # ======================================================================================
 def main():
     args = parse()
     if args.cpu_only:
-        print(json.dumps(cpu_baseline(WORKLOADS[args.workload], args.cpu_seconds, full=args.cpu_full_size)),
-              flush=True)
+        print(json.dumps(cpu_baseline(WORKLOADS[args.workload], args.cpu_seconds, full=_cpu_full(args))), flush=True)
         return None
     if args.engine == "multi-device":
         return multi_device_bench(args)
@@ -216,12 +293,6 @@ def main():
     import torch.distributed as dist
 
     from substrafl_amd import _native
-    from substrafl_amd.engine import FedAvgPlan, ScaffoldPlan, fedavg_weights, scaffold_weights
-    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
-    from substrafl_amd.sharding import (DistTransport, FedAvgShard, GpuShardOps, ScaffoldShard, block_of,
-                                        client_blocks, client_shard_fedavg, client_shard_fedavg_striped,
-                                        client_shard_scaffold, client_shard_scaffold_striped, shard_bounds,
-                                        stripe_layout)
 
     ndev = torch.cuda.device_count()
     if ndev == 0:
@@ -235,11 +306,8 @@ def main():
     dev_index = local % ndev  # param-range: a 1-GPU box can rehearse N > 1 (the ranks share the GPU)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
-        if client_shard:  # the exchange is RCCL over xGMI
-            dist.init_process_group("nccl", device_id=device)
-        else:  # parameter ranges need no data-path collective: barrier + max-over-ranks only
-            dist.init_process_group("gloo")
+    nccl = world > 1 and world <= ndev
+    backend = init_group(dist, world, device, nccl) if world > 1 else None
     lib = _native.load()
     if args.grid_cap:
         _native.tune(grid_cap=args.grid_cap)
@@ -247,383 +315,599 @@ def main():
         _native.tune(nt_load=args.nontemporal)
     if args.tune:
         _native.tune(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
+    ctx = _Ctx(torch=torch, dist=dist, world=world, rank=rank, device=device, lib=lib, native=_native,
+               wl=WORKLOADS[args.workload], stream=torch.cuda.current_stream(device), backend=backend)
 
-    wl = WORKLOADS[args.workload]
-    K, M_glob, kind = wl["K"], wl["M"], wl["kind"]
-    if client_shard and args.scaling == "weak":
-        K *= world  # every rank holds the workload's K clients
-    scaffold = wl["strategy"] == "scaffold"
-    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
-    s_in = 2 if kind == "bf16" else 4
-
-    # ---- this rank's share of the job ----
     if client_shard:
-        M = M_glob
-        k0, k1 = client_blocks(K, world)[block_of(rank, world)]
-        parallelism = f"client-shard x{world} ({args.combine})" if world > 1 else "single-gpu"
-        scaling = args.scaling
-    elif args.scaling == "strong":
-        lo, hi = shard_bounds(M_glob, world)[rank]
-        M = hi - lo
-        k0, k1 = 0, K
-        parallelism = f"param-range x{world} (strong)" if world > 1 else "single-gpu"
-        scaling = "strong"
+        cs = measure_client_shard(args, ctx, args.combine or "relay", args.scaling)
+        line = client_shard_line(args, ctx, cs)
     else:
-        M = M_glob
-        k0, k1 = 0, K
-        parallelism = f"param-range x{world}" if world > 1 else "single-gpu"
-        scaling = "weak"
-    Kr = k1 - k0
-    shapes = synthetic_state_dict_shapes(M_glob if client_shard else max(M, 1))
-    layout = BucketLayout(list(range(len(shapes))), shapes, np.float32)
-    ld = layout.ld
-    pw = layout.pairwise_idx
-    seed0 = 20241016 + k0 + (1_000_003 * rank if not client_shard else 0)
-    # striped relay: this rank's block per parameter stripe, one communicator per stripe
-    striped = client_shard and args.combine == "striped" and world > 1
-    stripes = stripe_layout(M, K, world, rank) if striped else []
-    if striped:
-        strs = [DistTransport()] + [DistTransport(dist.new_group()) for _ in range(len(stripes) - 1)]
-        bounds = [(lo, hi, a) for lo, hi, a, *_ in stripes]
-        pw64 = pw.astype(np.int64)
-
-        def local_pw(lo, hi):
-            return (pw64[(pw64 >= lo) & (pw64 < hi)] - lo).astype(np.uint64)
-
-        def stripe_rows(si, lo, hi, k0s, k1s, salt=0):  # client k's stripe si: Philox seed per (k, stripe)
-            n = hi - lo
-            return synth_clients(torch, k1s - k0s, max(64, -(-n // 64) * 64), n, kind, device,
-                                 20241016 + 7919 * salt + 104729 * si + k0s)
-
-    class _Plans:  # the stripes' block kernels, back to back
-        def __init__(self, plans):
-            self.plans = plans
-
-        def launch(self, st):
-            for p in self.plans:
-                p.launch(st)
-
-        def bytes_alg(self):
-            return sum(p.bytes_alg() for p in self.plans)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    stream = torch.cuda.current_stream(device)
-    from substrafl_amd.engine import TiledFedAvgPlan, tiled_recommended, tiled_tile
-
-    tiled = (not scaffold and not client_shard and kind in ("f32", "bf16")
-             and (args.layout == "tiles" or (args.layout == "auto" and tiled_recommended(kind, K, M))))
-    tv = (args.tile or tiled_tile(kind, K, M)) if tiled else 0
-    if args.layout == "tiles" and not tiled:
-        print("bench.py: --layout tiles takes the FedAvg fp32/bf16 workloads in param-range mode", file=sys.stderr)
-        sys.exit(2)
-    if not scaffold:
-        clients = synth_tiled(torch, K, M, kind, device, seed0, tv) if tiled else \
-            synth_clients(torch, Kr, ld, M, kind, device, seed0)
-        out = torch.empty(ld, dtype=torch.float32, device=device)
-        w_all = fedavg_weights(n_samples, kind)
-        if tiled:
-            plan = TiledFedAvgPlan(kind, clients, K, w_all, M, out, pw, tv=tv)
-            kplan = plan
-
-            def step():
-                plan.launch(stream)
-        elif striped:
-            del clients
-            parts = [FedAvgShard(kind, stripe_rows(si, lo, hi, k0s, k1s), w_all[k0s:k1s], k0s, K, hi - lo,
-                                 local_pw(lo, hi)) for si, (lo, hi, a, b, k0s, k1s) in enumerate(stripes)]
-            clients = parts  # spot check
-            ops = GpuShardOps()
-            ws = torch.zeros((max(1, pw.size), K), dtype=torch.float32, device=device)
-
-            def step():
-                client_shard_fedavg_striped(parts, bounds, out, strs, ops, pw, ws=ws)
-
-            kplan = _Plans([FedAvgPlan(kind, sh.rows, sh.w, sh.M, out[lo:], None)
-                            for sh, (lo, hi, a) in zip(parts, bounds) if sh.Kr and sh.M])
-        elif client_shard:
-            sh = FedAvgShard(kind, clients, w_all[k0:k1], k0, K, M, pw)
-            ops, tr = GpuShardOps(), DistTransport() if world > 1 else None
-            ws = torch.zeros((max(1, pw.size), K), dtype=torch.float32, device=device)
-
-            def step():
-                if world > 1:
-                    client_shard_fedavg(sh, out, tr, ops, args.combine, ws=ws)
-                else:
-                    FedAvgPlan(kind, clients, w_all, M, out, pw).launch(stream)
-
-            # this block's partial kernel (a rank with no clients, K < N, has none)
-            kplan = FedAvgPlan(kind, clients, w_all[k0:k1], M, out, None) if Kr else None
-        else:
-            plan = FedAvgPlan(kind, clients, w_all, M, out, pw)
-            kplan = plan
-
-            def step():
-                plan.launch(stream)
-        bytes_job = K * M_glob * s_in + M_glob * 4
-        bytes_kernel = kplan.bytes_alg() if kplan else 0
-    else:
-        delta = synth_clients(torch, Kr, ld, M, kind, device, seed0)
-        cv = synth_clients(torch, Kr, ld, M, kind, device, seed0 + 7919)
-        gc = torch.Generator(device=device)
-        gc.manual_seed(4242)
-        c = torch.randn(ld, dtype=torch.float32, device=device, generator=gc)
-        dout = torch.empty(ld, dtype=torch.float64, device=device)
-        cout = torch.empty(ld, dtype=torch.float64, device=device)
-        w_all = scaffold_weights(n_samples)
-        if striped:
-            del delta, cv
-            parts = [ScaffoldShard(kind, stripe_rows(si, lo, hi, k0s, k1s), stripe_rows(si, lo, hi, k0s, k1s, salt=1),
-                                   c[lo:hi], w_all[k0s:k1s], k0s, K, hi - lo, 1.0, local_pw(lo, hi))
-                     for si, (lo, hi, a, b, k0s, k1s) in enumerate(stripes)]
-            delta, cv = parts, parts  # spot check
-            ops = GpuShardOps()
-
-            def step():
-                client_shard_scaffold_striped(parts, bounds, dout, cout, strs, ops, pw, c=c)
-
-            kplan = _Plans([ScaffoldPlan(kind, sh.delta, sh.cv, sh.c, sh.w, sh.M, 1.0, dout[lo:], cout[lo:], None)
-                            for sh, (lo, hi, a) in zip(parts, bounds) if sh.Kr and sh.M])
-        elif client_shard:
-            sh = ScaffoldShard(kind, delta, cv, c, w_all[k0:k1], k0, K, M, 1.0, pw)
-            ops, tr = GpuShardOps(), DistTransport() if world > 1 else None
-
-            def step():
-                if world > 1:
-                    client_shard_scaffold(sh, dout, cout, tr, ops, args.combine)
-                else:
-                    ScaffoldPlan(kind, delta, cv, c, w_all, M, 1.0, dout, cout, pw).launch(stream)
-
-            kplan = ScaffoldPlan(kind, delta, cv, c, w_all[k0:k1], M, 1.0, dout, cout, None) if Kr else None
-        else:
-            plan = ScaffoldPlan(kind, delta, cv, c, w_all, M, 1.0, dout, cout, pw)
-            kplan = plan
-
-            def step():
-                plan.launch(stream)
-        bytes_job = 2 * K * M_glob * 4 + M_glob * 4 + 2 * M_glob * 8
-        bytes_kernel = kplan.bytes_alg() if kplan else 0
-    if not client_shard and args.scaling == "weak":  # every rank reduces a full M-param slice
-        bytes_job = bytes_kernel * world
-
-    # ---- warmup (untimed) ----
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-
-    # ---- timed region: exactly `steps` steps, barrier + sync on both sides ----
-    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    ev_start.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev_end.record(stream)
-    torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0  # this rank's region; the job's time is the max over ranks
-    barrier()
-    step_ms_dev = ev_start.elapsed_time(ev_end) / args.steps
-
-    # ---- the dominant kernel alone, HIP events on its launch stream (after the timed region) ----
-    n_each = max(5, min(args.steps, 20))
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_each)]
-    for a, b in evs:
-        a.record(stream)
-        if kplan:
-            kplan.launch(stream)
-        b.record(stream)
-    torch.cuda.synchronize(device)
-    each_ms = np.array([a.elapsed_time(b) for a, b in evs])
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(max(5, min(args.steps, 50))):
-        if kplan:
-            kplan.launch(stream)
-    e1.record(stream)
-    torch.cuda.synchronize(device)
-    kern_ms = e0.elapsed_time(e1) / max(5, min(args.steps, 50))
-    if not client_shard:  # the step IS the one kernel, launched back to back: region / steps
-        kern_ms = step_ms_dev
-
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                         device=device if client_shard else torch.device("cpu"))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
-    ms_per_step = elapsed / args.steps * 1e3
-    value = bytes_job / (elapsed / args.steps) / 1e9
-
-    # ---- parity spot check (outside the timed region) ----
-    step()  # the kernel-alone launches above overwrote the outputs with a block's partial
-    torch.cuda.synchronize(device)
-    parity = spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, layout, n_samples, kind,
-                        device, locals())
-
-    # ---- read-stream ceiling on the same box (same 16-B nt load path) ----
-    src = clients if not scaffold else delta
-    if isinstance(src, list):  # striped: this rank's largest stripe block
-        src = max((p.rows if not scaffold else p.delta for p in src), key=lambda t: t.numel())
-    read_ceiling = read_probe(torch, lib, src, stream, device, _native)
-
-    # ---- CPU baseline (rank 0, N == 1): the reference call structure timed on host cores ----
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(wl, args.cpu_seconds, full=args.cpu_full_size)
-
-    sha = lib_sha256()
-    traffic, tsrc = read_traffic(args, sha) if (world == 1 or args.scaling == "weak") and not client_shard \
-        else (None, None)
-
-    achieved = bytes_kernel / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+        line, info = measure_param_range(args, ctx)
+        if world > 1 and args.client_shard != "off":
+            if nccl:  # the north-star mode beside it: client buckets sharded, exchanged over xGMI
+                line["client_shard"] = guarded_client_shard(args, ctx, info, line)
+            else:
+                line["client_shard"] = {"skipped": f"needs one GPU per rank for RCCL ({world} ranks, {ndev} GPUs)"}
     if rank == 0:
-        if not scaffold:
-            kname = f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>"
-        elif lib.fedagg_scaffold_launches(max(1, Kr), 4, M, 1) == 2:  # the library's own launch plan
-            kname = "scaffold_bucket_kernel<float> x2 (delta bucket, then control variate + c)"
-        else:
-            kname = "scaffold_kernel<float>"
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": None,
-            "dtype": "bf16-in/f32-acc" if kind == "bf16" else ("f32-in/f64-acc" if scaffold else "f32"),
-            "data": "synthetic (N(0,1) client buckets generated on device, torch Philox seeds 20241016+k; "
-                    "n_samples = default_rng(7).integers(100, 10000, K))",
-            "config": {
-                "workload": wl["name"],
-                "strategy": wl["strategy"],
-                "clients": K,
-                "clients_per_gpu": Kr,
-                "params_per_gpu": M,
-                "global_params": M_glob if (client_shard or args.scaling == "strong") else M * world,
-                "layers": len(shapes),
-                "parallelism": parallelism,
-                "layout": f"tile-interleaved ({tv} vectors per client tile)" if tiled else "rows",
-                "bytes_alg_per_step_job": bytes_job,
-                "bytes_alg_per_launch_rank0": bytes_kernel,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
-                "traffic_source": tsrc,
-                "kernel": kname,
-                "kernel_ms": round(kern_ms, 5),
-                "kernel_ms_max_over_ranks": round(kern_ms_max, 5),
-                "kernel_ms_median": round(float(np.median(each_ms)), 5),
-                "kernel_ms_min": round(float(each_ms.min()), 5),
-                "kernel_timing": "HIP events on the launch stream: timed region / steps" if not client_shard else
-                                 "HIP events on the launch stream: this rank's block kernel alone, back to back",
-                "read_stream_ceiling_GBps": round(read_ceiling, 1) if read_ceiling > 0 else None,
-                "frac_of_read_ceiling": round(achieved / read_ceiling, 4) if read_ceiling > 0 else None,
-            },
-            "cpu_baseline": cpu,
-            "parity": parity,
-            "build": {"lib_sha256": sha},
-        }
-        if client_shard and world > 1:
-            line["combine"] = {"mode": args.combine, "step_ms": round(ms_per_step, 5),
-                               "block_kernel_ms": round(kern_ms_max, 5),
-                               "exchange_and_final_ms": round(max(0.0, ms_per_step - kern_ms_max), 5),
-                               "bit_exact_by_construction": args.combine in ("relay", "striped")}
-            if striped:
-                line["combine"]["stripes"] = [{"params": hi - lo, "hop": a} for lo, hi, a in bounds]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, layout, n_samples, kind, device, env):
+def _cpu_full(args) -> bool:
+    """The CPU baseline at the workload's full K x M when the host can hold it (the reference's
+    NumPy path needs the K client lists plus a stacked copy: ~1.3 x K x M x 4 bytes)."""
+    if args.cpu_full_size:
+        return True
+    if args.cpu_sample:
+        return False
+    wl = WORKLOADS[args.workload]
+    if wl["kind"] == "bf16":  # C5: 179 GB of fp32 inputs for the reference; never on a host
+        return False
+    mult = 2 if wl["strategy"] == "scaffold" else 1
+    need = int(1.5 * mult * wl["K"] * wl["M"] * 4) + (8 << 30)
+    try:
+        import psutil
+
+        avail = psutil.virtual_memory().available
+    except Exception:  # noqa: BLE001
+        return False
+    return avail > need
+
+
+def measure_param_range(args, ctx):
+    """The device-resident metric, one process per GPU, parameter-range sharding (no data-path
+    collective): weak -- every rank reduces the workload's full K x M; strong -- the workload's
+    M split over the ranks.  Returns (line, info)."""
+    torch, world, rank, device = ctx.torch, ctx.world, ctx.rank, ctx.device
+    from substrafl_amd.engine import (FedAvgPlan, ScaffoldPlan, TiledFedAvgPlan, fedavg_weights, scaffold_weights,
+                                      tiled_recommended, tiled_tile)
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+    from substrafl_amd.sharding import shard_bounds
+
+    wl = ctx.wl
+    K, M_glob, kind = wl["K"], wl["M"], wl["kind"]
+    scaffold = wl["strategy"] == "scaffold"
+    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    s_in = 2 if kind == "bf16" else 4
+    if args.scaling == "strong":
+        lo, hi = shard_bounds(M_glob, world)[rank]
+        M = hi - lo
+        parallelism = f"param-range x{world} (strong)" if world > 1 else "single-gpu"
+    else:
+        M = M_glob
+        parallelism = f"param-range x{world}" if world > 1 else "single-gpu"
+    shapes = synthetic_state_dict_shapes(max(M, 1))
+    layout = BucketLayout(list(range(len(shapes))), shapes, np.float32)
+    ld = layout.ld
+    pw = layout.pairwise_idx
+    seed0 = 20241016 + 1_000_003 * rank
+    stream = ctx.stream
+    tiled = (not scaffold and kind in ("f32", "bf16")
+             and (args.layout == "tiles" or (args.layout == "auto" and tiled_recommended(kind, K, M))))
+    tv = (args.tile or tiled_tile(kind, K, M)) if tiled else 0
+    if args.layout == "tiles" and not tiled:
+        print("bench.py: --layout tiles takes the FedAvg fp32/bf16 workloads in param-range mode", file=sys.stderr)
+        sys.exit(2)
+    env = {"tiled": tiled, "tv": tv}
+    if not scaffold:
+        clients = synth_tiled(torch, K, M, kind, device, seed0, tv) if tiled else \
+            synth_clients(torch, K, ld, M, kind, device, seed0)
+        out = torch.empty(ld, dtype=torch.float32, device=device)
+        w_all = fedavg_weights(n_samples, kind)
+        plan = TiledFedAvgPlan(kind, clients, K, w_all, M, out, pw, tv=tv) if tiled else \
+            FedAvgPlan(kind, clients, w_all, M, out, pw)
+        env.update(clients=clients, out=out)
+    else:
+        delta = synth_clients(torch, K, ld, M, kind, device, seed0)
+        cv = synth_clients(torch, K, ld, M, kind, device, seed0 + 7919)
+        gc = torch.Generator(device=device)
+        gc.manual_seed(4242)
+        c = torch.randn(ld, dtype=torch.float32, device=device, generator=gc)
+        dout = torch.empty(ld, dtype=torch.float64, device=device)
+        cout = torch.empty(ld, dtype=torch.float64, device=device)
+        plan = ScaffoldPlan(kind, delta, cv, c, scaffold_weights(n_samples), M, 1.0, dout, cout, pw)
+        env.update(delta=delta, cv=cv, c=c, dout=dout, cout=cout)
+    bytes_kernel = plan.bytes_alg()
+    bytes_job = bytes_kernel * world if args.scaling == "weak" else (
+        K * M_glob * s_in + M_glob * 4 if not scaffold else 2 * K * M_glob * 4 + M_glob * 4 + 2 * M_glob * 8)
+
+    def step():
+        plan.launch(stream)
+
+    elapsed, ev_ms = _timed(ctx, step, args.steps, args.warmup)
+    kern_ms = ev_ms / args.steps  # the step IS the one kernel, launched back to back
+    # the kernel alone, launch by launch (HIP events on its stream): median / min for the spread
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(max(5, min(args.steps, 20)))]
+    for a, b in evs:
+        a.record(stream)
+        plan.launch(stream)
+        b.record(stream)
+    torch.cuda.synchronize(device)
+    each_ms = np.array([a.elapsed_time(b) for a, b in evs])
+    elapsed, kern_ms_max = ctx.max_over_ranks([elapsed, kern_ms])
+    ms_per_step = elapsed / args.steps * 1e3
+    value = bytes_job / (elapsed / args.steps) / 1e9
+
+    parity = spot_check(torch, world, rank, scaffold, K, M, layout, n_samples, kind, device, env)
+    read_ceiling = read_probe(torch, ctx.lib, env["clients"] if not scaffold else env["delta"], stream, device,
+                              ctx.native)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(wl, args.cpu_seconds, full=_cpu_full(args))
+    sha = lib_sha256()
+    traffic, tsrc = read_traffic(args, sha) if (world == 1 or args.scaling == "weak") else (None, None)
+    achieved = bytes_kernel / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+    if not scaffold:
+        kname = f"fedavg_kernel<{'BF16' if kind == 'bf16' else 'F32'}>"
+    elif ctx.lib.fedagg_scaffold_launches(max(1, K), 4, M, 1) == 2:  # the library's own launch plan
+        kname = "scaffold_bucket_kernel<float> x2 (delta bucket, then control variate + c)"
+    else:
+        kname = "scaffold_kernel<float>"
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "bf16-in/f32-acc" if kind == "bf16" else ("f32-in/f64-acc" if scaffold else "f32"),
+        "data": "synthetic (N(0,1) client buckets generated on device, torch Philox seeds 20241016+k; "
+                "n_samples = default_rng(7).integers(100, 10000, K))",
+        "config": {
+            "workload": wl["name"],
+            "strategy": wl["strategy"],
+            "clients": K,
+            "clients_per_gpu": K,
+            "params_per_gpu": M,
+            "global_params": M_glob if args.scaling == "strong" else M * world,
+            "layers": len(shapes),
+            "parallelism": parallelism,
+            "layout": f"tile-interleaved ({tv} vectors per client tile)" if tiled else "rows",
+            "bytes_alg_per_step_job": bytes_job,
+            "bytes_alg_per_launch_rank0": bytes_kernel,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "kernel": kname,
+            "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_max_over_ranks": round(kern_ms_max, 5),
+            "kernel_ms_median": round(float(np.median(each_ms)), 5),
+            "kernel_ms_min": round(float(each_ms.min()), 5),
+            "kernel_timing": "HIP events on the launch stream: timed region / steps",
+            "read_stream_ceiling_GBps": round(read_ceiling, 1) if read_ceiling > 0 else None,
+            "frac_of_read_ceiling": round(achieved / read_ceiling, 4) if read_ceiling > 0 else None,
+        },
+        "cpu_baseline": cpu,
+        "parity": parity,
+        "build": {"lib_sha256": sha},
+    }
+    if world > 1:
+        line["process_group"] = {"backend": ctx.backend, "timeout_s": PG_TIMEOUT_S}
+    return line, {"kern_ms": kern_ms_max, "K": K, "M": M, "tiled": tiled}
+
+
+# ======================================================================================
+# client-shard (the north-star mode) -- its own line, or a field of the N > 1 line
+# ======================================================================================
+def guarded_client_shard(args, ctx, info, line):
+    """The client-shard leg of an N > 1 line: every rank measures it after the parameter-range
+    line; an error becomes a field of the line, and a rank still inside it after
+    CLIENT_SHARD_DEADLINE_S s reports (rank 0) the parameter-range line with the failure and
+    exits, so a stuck exchange never costs the line."""
+    import threading
+
+    torch = ctx.torch
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(CLIENT_SHARD_DEADLINE_S):
+            if ctx.rank == 0:
+                out = dict(line)
+                out["client_shard"] = {"error": f"did not finish within {CLIENT_SHARD_DEADLINE_S} s"}
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+
+    torch.cuda.empty_cache()
+    try:
+        th = threading.Thread(target=watchdog, daemon=True)
+        th.start()
+        # weak (the default): every rank holds the workload's K clients, N x K in all, each element
+        # still summed in the reference's order across the N blocks
+        res = measure_client_shard(args, ctx, args.combine or "striped", "weak", t1_ms=info["kern_ms"],
+                                   t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
+    except Exception as e:  # noqa: BLE001 -- reported in the line, which is still printed
+        res = {"error": f"{type(e).__name__}: {e}"[:500]}
+    finally:
+        done.set()
+        torch.cuda.empty_cache()
+    return res
+
+
+def _synth_block(torch, kind, Kb, width, device, seed):
+    """A client block's buffer: N(0,1) from torch's device Philox stream (bf16 via fp32)."""
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}[kind]
+    t = torch.empty((max(1, Kb), max(1, width)), dtype=dt, device=device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    for k in range(Kb):
+        if kind == "bf16":
+            t[k].copy_(torch.randn(width, generator=g, device=device, dtype=torch.float32))
+        else:
+            t[k].normal_(generator=g)
+    return t[:Kb, :width]
+
+
+def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None):
+    """One rank's part of the client-sharded reduction (sharding.py; relay / striped: the
+    lockstep schedule over ONE communicator, rccl / ordered: re-associating), device-resident,
+    timed like the main line; returns the measurement as a dict (rank 0's is reported)."""
+    torch, world, rank, device = ctx.torch, ctx.world, ctx.rank, ctx.device
+    from substrafl_amd import lockstep
+    from substrafl_amd.engine import (FedAvgPlan, ScaffoldPlan, TiledFedAvgPlan, fedavg_weights, scaffold_weights,
+                                      tiled_recommended, tiled_tile)
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+    from substrafl_amd.sharding import (SLOTS, DistTransport, FedAvgShard, GpuShardOps, LoopbackGroup, ScaffoldShard,
+                                        TiledBlock, _block_layout, block_of, client_blocks, client_shard_fedavg,
+                                        client_shard_scaffold, lockstep_fedavg, lockstep_scaffold, relay_plan,
+                                        striped_plan)
+
+    wl = ctx.wl
+    K_per, M, kind = wl["K"], wl["M"], wl["kind"]
+    scaffold = wl["strategy"] == "scaffold"
+    K = K_per * world if scaling == "weak" else K_per
+    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    s_in = 2 if kind == "bf16" else 4
+    shapes = synthetic_state_dict_shapes(M)
+    layout = BucketLayout(list(range(len(shapes))), shapes, np.float32)
+    pw = layout.pairwise_idx
+    tr = DistTransport() if world > 1 else LoopbackGroup(1).transport(0)
+    ops = GpuShardOps()
+    stream = ctx.stream
+    mode = {"auto": "auto", "tiles": True, "rows": False}[args.layout]
+    lockstep_mode = combine in ("relay", "striped")
+    w_all = fedavg_weights(n_samples, kind) if not scaffold else scaffold_weights(n_samples)
+    gc = torch.Generator(device=device)
+    gc.manual_seed(4242)
+    c = torch.randn(layout.ld, dtype=torch.float32, device=device, generator=gc) if scaffold else None
+    outs = {}
+    if not scaffold:
+        outs["out"] = torch.zeros(layout.ld, dtype=torch.float32, device=device)
+    else:
+        outs["dout"] = torch.zeros(layout.ld, dtype=torch.float64, device=device)
+        outs["cout"] = torch.zeros(layout.ld, dtype=torch.float64, device=device)
+    held = {}  # block -> (k0, data, segs) for the spot check
+    tvs = set()
+    if lockstep_mode:
+        plan = striped_plan(M, world, rank, args.rings or None, _rounds(args)) if combine == "striped" else \
+            relay_plan(M, world, rank, args.chunk)
+        blocks = {}
+        for b, segs in plan.blocks.items():
+            k0, k1 = client_blocks(K, world)[b]
+            seed = 20241016 + 104729 * b + 7919 * rank
+            width = plan.block_len[b]
+            if scaffold:
+                d = _synth_block(torch, kind, k1 - k0, width, device, seed)
+                v = _synth_block(torch, kind, k1 - k0, width, device, seed + 1)
+                blocks[b] = ScaffoldShard(kind, d, v, None, w_all[k0:k1], k0, K, width, 1.0, np.zeros(0, np.uint64))
+                held[b] = (k0, (d, v), segs)
+                continue
+            ext = TiledBlock.run_extents(plan, b)
+            tv = _block_layout(torch, kind, k1 - k0, ext, mode)
+            if tv:
+                rows = TiledBlock.empty(torch, kind, k1 - k0, width, tv, ext, device)
+                g = torch.Generator(device=device)
+                g.manual_seed(seed)
+                for t, _n in rows.buckets.values():
+                    if kind == "bf16":
+                        t.copy_(torch.randn(t.numel(), generator=g, device=device, dtype=torch.float32))
+                    else:
+                        t.normal_(generator=g)
+                tvs.add(tv)
+            else:
+                rows = _synth_block(torch, kind, k1 - k0, width, device, seed)
+                tvs.add(0)
+            blocks[b] = FedAvgShard(kind, rows, w_all[k0:k1], k0, K, width, np.zeros(0, np.uint64))
+            held[b] = (k0, rows, segs)
+        slots = torch.empty(2 * SLOTS * max(1, plan.slot_elems), dtype=torch.float64 if scaffold else torch.float32,
+                            device=device)
+        ws = (torch.zeros(max(1, pw.size) * (2 * K + 1), dtype=torch.float64, device=device) if scaffold else
+              torch.zeros((max(1, pw.size), K), dtype=torch.float32, device=device))
+
+        def step():
+            if scaffold:
+                lockstep_scaffold(plan, blocks, outs["dout"], outs["cout"], tr, ops, pw, c, 1.0, ws=ws, slots=slots)
+            else:
+                lockstep_fedavg(plan, blocks, outs["out"], tr, ops, pw, ws=ws, slots=slots)
+
+        acc = slots.view(-1)
+        slot_n = max(1, plan.slot_elems)
+
+        def compute_only():  # every run of this rank back to back, no exchange (the block kernel time)
+            for runs in plan.runs:
+                for r in runs:
+                    sh = blocks[r.block]
+                    s0 = r.acc[1] if r.acc[0] == "slot" else 0
+                    a = acc[s0 * slot_n:][: r.n]
+                    if scaffold:
+                        a2 = acc[(SLOTS + s0) * slot_n:][: r.n]
+                        ops.scaffold_run(kind, sh.delta[:, r.col: r.col + r.n], sh.cv[:, r.col: r.col + r.n], sh.w,
+                                         r.seed, r.final, c[r.lo: r.lo + r.n], 1.0, a, a2)
+                    else:
+                        ops.fedavg_run(kind, sh.rows[:, r.col: r.col + r.n], sh.w, r.seed, a)
+
+        run_bytes = sum((blocks[r.block].Kr * r.n * s_in * (2 if scaffold else 1)
+                         + r.n * (8 if scaffold else 4) * (2 if scaffold else 1) * (1 if r.seed else 2))
+                        for runs in plan.runs for r in runs)
+        schedule = {"steps": plan.n_steps, "runs_per_rank": sum(len(x) for x in plan.runs),
+                    "messages_per_rank": plan.stats.get("messages_of_this_rank"),
+                    "elements_per_run": sorted({r.n for runs in plan.runs for r in runs})[-1:],
+                    "issue": "one host thread, one communicator; exchange group t pairs only with group t of the peers"}
+        if combine == "striped":
+            schedule["rings"] = lockstep.ring_multipliers(world, args.rings or None)
+            schedule["rounds"] = list(_rounds(args))
+    else:
+        k0, k1 = client_blocks(K, world)[block_of(rank, world)]
+        Kr = k1 - k0
+        seed = 20241016 + 104729 * block_of(rank, world)
+        if scaffold:
+            d = _synth_block(torch, kind, Kr, layout.ld, device, seed)
+            v = _synth_block(torch, kind, Kr, layout.ld, device, seed + 1)
+            sh = ScaffoldShard(kind, d, v, c, w_all[k0:k1], k0, K, M, 1.0, pw)
+            held[block_of(rank, world)] = (k0, (d, v), [(0, M, 0)])
+        else:
+            rows = _synth_block(torch, kind, Kr, layout.ld, device, seed)
+            sh = FedAvgShard(kind, rows, w_all[k0:k1], k0, K, M, pw)
+            held[block_of(rank, world)] = (k0, rows, [(0, M, 0)])
+        tvs.add(0)
+
+        def step():
+            if scaffold:
+                client_shard_scaffold(sh, outs["dout"], outs["cout"], tr, ops, combine)
+            else:
+                client_shard_fedavg(sh, outs["out"], tr, ops, combine)
+
+        def compute_only():
+            if scaffold:
+                ops.scaffold_chain(sh, 0, M, True, False, outs["dout"], outs["cout"])
+            else:
+                ops.fedavg_chain(kind, sh.rows, sh.w, 0, M, True, outs["out"])
+
+        run_bytes = Kr * M * s_in * (2 if scaffold else 1) + M * (16 if scaffold else 4)
+        schedule = {"issue": "dist.reduce per chunk (rccl) / dist.gather (ordered) on one communicator"}
+
+    steps = max(1, min(args.steps, args.client_shard_steps))
+    warm = max(1, min(args.warmup, 5))
+    elapsed, _ev = _timed(ctx, step, steps, warm)
+    # the block kernels alone, back to back (HIP events on their stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    compute_only()
+    e0.record(stream)
+    for _ in range(3):
+        compute_only()
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    block_ms = e0.elapsed_time(e1) / 3
+    step()  # the outputs again (compute_only overwrote the root's final runs)
+    torch.cuda.synchronize(device)
+    parity = _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held, outs, c, tvs)
+    if t1_ms is None:  # one GPU reducing the workload's own K x M: the weak-scaling reference
+        t1_ms, t1_source = _single_gpu_ms(ctx, K_per, M, kind, scaffold, layout, n_samples), \
+            "this rank, one GPU over the workload's K x M (same bench, same layout policy)"
+    elapsed, block_ms, t1_ms = ctx.max_over_ranks([elapsed, block_ms, t1_ms])
+    ms = elapsed / steps * 1e3
+    bytes_job = (K * M * s_in + M * 4) if not scaffold else (2 * K * M * 4 + M * 4 + 2 * M * 8)
+    gbps = bytes_job / (ms / 1e3) / 1e9
+    layouts = sorted(tvs)
+    res = {
+        "combine": combine,
+        "scaling": scaling,
+        "clients": K,
+        "clients_per_gpu": K // world if scaling == "weak" else -(-K // world),
+        "params": M,
+        "layout": "rows" if layouts == [0] else ", ".join(
+            "rows" if t == 0 else f"tile-interleaved ({t} vectors per client tile)" for t in layouts),
+        "steps": steps,
+        "warmup": warm,
+        "ms_per_step": round(ms, 5),
+        "GBps": round(gbps, 2),
+        "frac_of_n_x_hbm_peak": round(gbps / (world * HBM_PEAK_GBPS), 4),
+        "block_kernel_ms": round(block_ms, 5),
+        "block_kernel_GBps": round(run_bytes / (block_ms / 1e3) / 1e9, 1) if block_ms > 0 else None,
+        "exchange_and_tail_ms": round(max(0.0, ms - block_ms), 5),
+        "single_gpu_ms": round(t1_ms, 5),
+        "single_gpu_source": t1_source,
+        "bit_exact_by_construction": combine in ("relay", "striped"),
+        "schedule": schedule,
+        "hip_streams_per_rank": "2 (compute + the communicator's) <= GPU_MAX_HW_QUEUES = 4",
+        "parity": parity,
+    }
+    if scaling == "weak":
+        res["weak_efficiency"] = round(t1_ms / ms, 4) if ms > 0 else None
+    return res
+
+
+def _rounds(args):
+    from substrafl_amd import lockstep
+
+    if not args.rounds:
+        return lockstep.DEFAULT_ROUNDS
+    return tuple(float(x) for x in args.rounds.split(","))
+
+
+def _single_gpu_ms(ctx, K, M, kind, scaffold, layout, n_samples):
+    """Kernel time of one GPU reducing K clients x M (the layout the library recommends)."""
+    torch, device, stream = ctx.torch, ctx.device, ctx.stream
+    from substrafl_amd.engine import (FedAvgPlan, ScaffoldPlan, TiledFedAvgPlan, fedavg_weights, scaffold_weights,
+                                      tiled_recommended, tiled_tile)
+
+    if scaffold:
+        d = torch.empty((K, layout.ld), dtype=torch.float32, device=device).normal_()
+        v = torch.empty_like(d).normal_()
+        c = torch.randn(layout.ld, dtype=torch.float32, device=device)
+        do = torch.empty(layout.ld, dtype=torch.float64, device=device)
+        co = torch.empty_like(do)
+        plan = ScaffoldPlan(kind, d, v, c, scaffold_weights(n_samples[:K]), M, 1.0, do, co, layout.pairwise_idx)
+    else:
+        out = torch.empty(layout.ld, dtype=torch.float32, device=device)
+        w = fedavg_weights(n_samples[:K], kind)
+        if tiled_recommended(kind, K, M):
+            tv = tiled_tile(kind, K, M)
+            buf = synth_tiled(torch, K, M, kind, device, 1, tv)
+            plan = TiledFedAvgPlan(kind, buf, K, w, M, out, layout.pairwise_idx, tv=tv)
+        else:
+            buf = synth_clients(torch, K, layout.ld, M, kind, device, 1)
+            plan = FedAvgPlan(kind, buf, w, M, out, layout.pairwise_idx)
+    for _ in range(3):
+        plan.launch(stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(10):
+        plan.launch(stream)
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / 10
+    del plan
+    torch.cuda.empty_cache()
+    return ms
+
+
+def _held_values(torch, kind, data, cols, Kb):
+    """[Kb, len(cols)] fp64 values of a block buffer (rows tensor or TiledBlock) at columns."""
+    from substrafl_amd.engine import tiled_index
+    from substrafl_amd.sharding import TiledBlock
+
+    if not isinstance(data, TiledBlock):
+        return data[:, torch.from_numpy(cols).to(data.device)].to(torch.float64)
+    out = torch.empty((Kb, len(cols)), dtype=torch.float64, device=next(iter(data.buckets.values()))[0].device)
+    for j, col in enumerate(cols):
+        t, e = data.locate(int(col))
+        idx = tiled_index(kind, Kb, np.arange(Kb), e, data.tv)
+        out[:, j] = t[torch.from_numpy(idx).to(t.device)].to(torch.float64)
+    return out
+
+
+def _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held, outs, c, tvs):
+    """Sampled elements against the reference's sequential order: every rank writes the values it
+    holds into a zeroed [K, S] fp64 matrix (each (client, element) is held by exactly one rank),
+    the matrices are summed onto the root over RCCL, which recomputes the chain on the host."""
+    torch, world, rank, device = ctx.torch, ctx.world, ctx.rank, ctx.device
+    from substrafl_amd.engine import fedavg_weights, scaffold_weights
+
+    g = np.random.default_rng(123)
+    idx = np.setdiff1d(np.unique(g.integers(0, M, 2048)), layout.pairwise_idx.astype(np.int64))
+    nf = 2 if scaffold else 1
+    dense = torch.zeros((nf, K, idx.size), dtype=torch.float64, device=device)
+    for b, (k0, data, segs) in held.items():
+        parts = data if scaffold else (data,)
+        Kb = parts[0].shape[0]
+        if Kb == 0:
+            continue
+        for lo, hi, col in segs:
+            sel = np.nonzero((idx >= lo) & (idx < hi))[0]
+            if not sel.size:
+                continue
+            cols = (idx[sel] - lo + col).astype(np.int64)
+            for f, part in enumerate(parts):
+                dense[f, k0: k0 + Kb, torch.from_numpy(sel).to(device)] = _held_values(torch, kind, part, cols, Kb)
+    if world > 1:
+        ctx.dist.reduce(dense, dst=0)
+    if rank != 0:
+        return None
+    xs = dense.cpu().numpy()
+    tidx = torch.from_numpy(idx).to(device)
+    if not scaffold:
+        got = outs["out"][tidx].cpu().numpy()
+        w32 = fedavg_weights(n_samples, "f32")
+        acc = np.zeros(idx.size, np.float32)
+        for k in range(K):
+            acc = (acc + (xs[0, k].astype(np.float32) * w32[k]).astype(np.float32)).astype(np.float32)
+        bad = acc.view(np.uint32) != got.view(np.uint32)
+        return {"sampled": int(idx.size), "mismatches": int(np.sum(bad))}
+    w64 = scaffold_weights(n_samples)
+    ad, ac = np.zeros(idx.size), np.zeros(idx.size)
+    for k in range(K):
+        ad = ad + xs[0, k] * w64[k]
+        ac = ac + xs[1, k] * w64[k]
+    ad = 1.0 * ad
+    ac = ac + c[tidx].double().cpu().numpy()
+    gd, gcv = outs["dout"][tidx].cpu().numpy(), outs["cout"][tidx].cpu().numpy()
+    return {"sampled": int(idx.size), "mismatches": int(np.sum(ad.view(np.uint64) != gd.view(np.uint64))
+                                                        + np.sum(ac.view(np.uint64) != gcv.view(np.uint64)))}
+
+
+def client_shard_line(args, ctx, cs):
+    """``--mode client-shard``: the client-shard measurement as the line itself."""
+    wl = ctx.wl
+    line = {
+        "metric": METRIC,
+        "value": cs["GBps"],
+        "unit": "GB/s",
+        "n_gpus": ctx.world,
+        "steps": cs["steps"],
+        "warmup": cs["warmup"],
+        "ms_per_step": cs["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": cs["scaling"],
+        "vs_baseline": None,
+        "dtype": "bf16-in/f32-acc" if wl["kind"] == "bf16" else (
+            "f32-in/f64-acc" if wl["strategy"] == "scaffold" else "f32"),
+        "data": "synthetic (N(0,1) client blocks generated on device, torch Philox; "
+                "n_samples = default_rng(7).integers(100, 10000, K))",
+        "config": {"workload": wl["name"], "strategy": wl["strategy"], "clients": cs["clients"],
+                   "clients_per_gpu": cs["clients_per_gpu"], "global_params": cs["params"],
+                   "parallelism": f"client-shard x{ctx.world} ({cs['combine']})" if ctx.world > 1 else "single-gpu",
+                   "layout": cs["layout"]},
+        "roofline": {"bound": "hbm", "achieved": cs["block_kernel_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round((cs["block_kernel_GBps"] or 0) / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "fedavg_kernel (chain runs of the schedule)" if wl["strategy"] == "fedavg" else
+                               "scaffold chain runs", "kernel_ms": cs["block_kernel_ms"],
+                     "kernel_timing": "HIP events: this rank's block kernels alone, back to back, max over ranks"},
+        "cpu_baseline": None,
+        "parity": cs["parity"],
+        "client_shard": cs,
+        "build": {"lib_sha256": lib_sha256()},
+    }
+    if ctx.world > 1:
+        line["process_group"] = {"backend": ctx.backend, "timeout_s": PG_TIMEOUT_S}
+    return line
+
+
+def spot_check(torch, world, rank, scaffold, K, M, layout, n_samples, kind, device, env):
     """Sampled output elements against the reference's sequential order (fp32 FedAvg chain /
-    fp64 Scaffold with c last and lr after the sum); client-sharded: every rank's sampled
-    columns are gathered on the root.  numel == 1 elements are excluded here (pairwise order:
-    tests/ check them against the oracle)."""
+    fp64 Scaffold with c last and lr after the sum), on each rank's own reduction.  numel == 1
+    elements are excluded here (pairwise order: tests/ check them against the oracle)."""
     from substrafl_amd.engine import fedavg_weights, scaffold_weights
 
     g = np.random.default_rng(123)
     idx = np.setdiff1d(np.unique(g.integers(0, M, 4096)), layout.pairwise_idx.astype(np.int64))
     tidx = torch.from_numpy(idx).to(device)
-    Kr = k1 - k0
 
-    def cols_striped(parts, field):
-        """Striped relay: every rank holds a different block per stripe; gather each stripe's
-        sampled columns from its holders and assemble [K, S] on the root."""
-        from substrafl_amd.sharding import client_blocks, stripe_layout, stripe_rank
-
-        lay = stripe_layout(M, K, world, rank)
-        per = -(-K // world)
-        sel = [np.nonzero((idx >= lo) & (idx < hi))[0] for lo, hi, *_ in lay]
-        ni = max(1, max(len(x) for x in sel))
-        pad = torch.zeros((len(lay), per, ni), dtype=torch.float64, device=device)
-        for si, ((lo, hi, a, b, k0s, k1s), part) in enumerate(zip(lay, parts)):
-            rows = getattr(part, field)
-            if k1s > k0s and len(sel[si]):
-                loc = torch.from_numpy(idx[sel[si]] - lo).to(device)
-                pad[si, : k1s - k0s, : len(sel[si])] = rows[:, loc].to(torch.float64)
-        got = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
-        dist.gather(pad, gather_list=got, dst=0)
-        if rank != 0:
-            return None
-        xs = np.zeros((K, idx.size))
-        blocks = client_blocks(K, world)
-        for si, (lo, hi, a, *_rest) in enumerate(lay):
-            for b, (k0b, k1b) in enumerate(blocks):
-                if k1b > k0b and len(sel[si]):
-                    src = got[stripe_rank(b, world, a)][si, : k1b - k0b, : len(sel[si])].cpu().numpy()
-                    xs[k0b:k1b, sel[si]] = src
-        return xs
-
-    def cols(x):  # [Kr, S] sampled columns of this rank's rows, gathered on the root in block order
-        if isinstance(x, tuple):
-            return cols_striped(*x)
+    def cols(x):  # [K, S] sampled columns of the client buckets
         if env.get("tiled"):  # tile-interleaved buffer: gather each client's sampled elements
             from substrafl_amd.engine import tiled_index
 
             pos = tiled_index(kind, K, np.arange(K)[:, None], idx[None, :], env["tv"])
             return x[torch.from_numpy(pos.reshape(-1)).to(device)].view(K, -1).to(torch.float64).cpu().numpy()
-        xs = x[:, tidx].to(torch.float64) if Kr else torch.zeros((0, idx.size), dtype=torch.float64, device=device)
-        if not (client_shard and world > 1):
-            return xs.cpu().numpy()
-        from substrafl_amd.sharding import chain_rank, client_blocks
-
-        per = -(-K // world)
-        pad = torch.zeros((per, idx.size), dtype=torch.float64, device=device)
-        pad[:Kr] = xs
-        got = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
-        dist.gather(pad, gather_list=got, dst=0)
-        if rank != 0:
-            return None
-        blocks = client_blocks(K, world)
-        return np.concatenate([got[chain_rank(b, world)][: blocks[b][1] - blocks[b][0]].cpu().numpy()
-                               for b in range(world)], axis=0)
-
-    def src(name, field):
-        v = env[name]
-        return (v, field) if isinstance(v, list) else v
+        return x[:, tidx].to(torch.float64).cpu().numpy()
 
     if not scaffold:
-        xs = cols(src("clients", "rows"))
-        if rank != 0 or xs is None:
-            return None
+        xs = cols(env["clients"])
         got = env["out"][tidx].cpu().numpy()
         w32 = fedavg_weights(n_samples, "f32")
         acc = np.zeros(idx.size, np.float32)
-        for k in range(K if client_shard else xs.shape[0]):
+        for k in range(xs.shape[0]):
             acc = (acc + (xs[k].astype(np.float32) * w32[k]).astype(np.float32)).astype(np.float32)
         bad = acc.view(np.uint32) != got.view(np.uint32)
         res = {"sampled": int(idx.size), "mismatches": int(np.sum(bad))}
@@ -631,9 +915,7 @@ def spot_check(torch, dist, world, rank, client_shard, scaffold, K, k0, k1, M, l
             ia, ib = acc.view(np.int32).astype(np.int64), got.view(np.int32).astype(np.int64)
             res["max_ulp"] = int(np.max(np.abs(ia - ib)))
         return res
-    xd, xc = cols(src("delta", "delta")), cols(src("cv", "cv"))
-    if rank != 0 or xd is None:
-        return None
+    xd, xc = cols(env["delta"]), cols(env["cv"])
     cc = env["c"][tidx].double().cpu().numpy()
     w64 = scaffold_weights(n_samples)
     ad = np.zeros(idx.size)
@@ -747,12 +1029,36 @@ def multi_device_bench(args):
 # ======================================================================================
 # --rehearse-cpu (tests): the launcher / rank / timing plumbing without a GPU
 # ======================================================================================
+class _RehearsalOps:
+    """NumPy chain arithmetic for --rehearse-cpu (the schedule's plumbing over gloo, no GPU)."""
+
+    def fedavg_run(self, kind, rows, w, seed, acc):
+        a = np.zeros(acc.shape[0], np.float32) if seed else acc.numpy().copy()
+        x = rows.numpy()
+        for k in range(x.shape[0]):
+            a = (a + (x[k] * np.float32(w[k])).astype(np.float32)).astype(np.float32)
+        acc.copy_(__import__("torch").from_numpy(a))
+
+    def fedavg_products_at(self, kind, rows, w, kbase, K, idx, ws):
+        x = rows.numpy()
+        for p, i in enumerate(np.asarray(idx, np.int64)):
+            for k in range(x.shape[0]):
+                ws[p, kbase + k] = float(np.float32(x[k, i] * np.float32(w[k])))
+
+    def fedavg_finish(self, kind, ws, K, pairwise_idx, out):
+        for p, i in enumerate(np.asarray(pairwise_idx, np.int64)):
+            out[int(i)] = float(np.float32(ws[p, :K].numpy().astype(np.float32).sum()))
+
+
 def rehearse(args, world, rank):
+    """--rehearse-cpu (tests): the launcher, the process group with its timeout, the barrier /
+    max-over-ranks timing and, for N > 1, the client-shard leg's lockstep schedule over gloo on
+    a tiny synthetic problem -- the same line fields as a GPU run, nothing measured."""
     import torch
     import torch.distributed as dist
 
     if world > 1:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", **pg_kwargs())
     x = np.ones(1 << 16, np.float32)
     for _ in range(args.warmup):
         x = x * np.float32(1.0)
@@ -762,18 +1068,69 @@ def rehearse(args, world, rank):
     for _ in range(args.steps):
         x = x * np.float32(1.0)
     elapsed = time.perf_counter() - t0
+    cs = None
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+        if args.client_shard != "off":
+            cs = _rehearse_client_shard(args, world, rank)
     if rank == 0:
-        print(json.dumps({"metric": METRIC + " [CPU rehearsal of the launcher: not a measurement]",
-                          "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 6),
-                          "rehearsal": True, "ranks_seen": world}), flush=True)
+        line = {"metric": METRIC + " [CPU rehearsal of the launcher: not a measurement]",
+                "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 6),
+                "rehearsal": True, "ranks_seen": world}
+        if world > 1:
+            line["process_group"] = {"backend": dist.get_backend(), "timeout_s": PG_TIMEOUT_S}
+            line["client_shard"] = cs
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _rehearse_client_shard(args, world, rank):
+    """The striped schedule over gloo (one communicator, one issuing thread) on 2 x 3 x 4 x 512
+    elements per rank; rank 0 checks its result against a host recomputation."""
+    import torch
+
+    from substrafl_amd.sharding import (DistTransport, FedAvgShard, client_blocks, lockstep_fedavg, relay_plan,
+                                        striped_plan)
+
+    combine = args.combine if args.combine in ("relay", "striped") else "striped"
+    K, M = 3 * world, 2 * world * 4 * 512 * 3 + 77
+    rng = np.random.default_rng(11)
+    data = rng.standard_normal((K, M)).astype(np.float32)
+    w = (np.arange(1, K + 1) / np.sum(np.arange(1, K + 1))).astype(np.float32)
+    plan = striped_plan(M, world, rank) if combine == "striped" else relay_plan(M, world, rank, 4096)
+    blocks = {}
+    for b, segs in plan.blocks.items():
+        k0, k1 = client_blocks(K, world)[b]
+        t = torch.zeros((k1 - k0, plan.block_len[b]), dtype=torch.float32)
+        for lo, hi, col in segs:
+            t[:, col: col + hi - lo] = torch.from_numpy(data[k0:k1, lo:hi])
+        blocks[b] = FedAvgShard("f32", t, w[k0:k1], k0, K, plan.block_len[b], np.zeros(0, np.uint64))
+    out = torch.zeros(M, dtype=torch.float32)
+    tr = DistTransport()
+    t0 = time.perf_counter()
+    root = lockstep_fedavg(plan, blocks, out, tr, _RehearsalOps(), np.zeros(0, np.int64))
+    ms = (time.perf_counter() - t0) * 1e3
+    if not root:
+        return None
+    acc = np.zeros(M, np.float32)
+    for k in range(K):
+        acc = (acc + (data[k] * w[k]).astype(np.float32)).astype(np.float32)
+    mism = int(np.sum(acc.view(np.uint32) != out.numpy().view(np.uint32)))
+    keys = ("combine", "scaling", "clients", "clients_per_gpu", "params", "layout", "steps", "warmup", "ms_per_step",
+            "GBps", "frac_of_n_x_hbm_peak", "block_kernel_ms", "block_kernel_GBps", "exchange_and_tail_ms",
+            "single_gpu_ms", "single_gpu_source", "weak_efficiency", "bit_exact_by_construction", "schedule",
+            "hip_streams_per_rank", "parity")
+    res = {k: None for k in keys}
+    res.update(combine=combine, scaling="weak", clients=K, clients_per_gpu=K // world, params=M, layout="rows",
+               steps=1, warmup=0, ms_per_step=round(ms, 3), bit_exact_by_construction=True,
+               schedule={"steps": plan.n_steps, "issue": "one host thread, one communicator (gloo rehearsal)"},
+               parity={"sampled": M, "mismatches": mism}, rehearsal=True)
+    return res
 
 
 def cpu_baseline(wl, budget_s, full=False):

@@ -45,36 +45,23 @@ enum {
 
 int fedagg_abi_version(void);
 const char* fedagg_last_error(void);
-/* Process-wide launch knobs (defaults are the values measured best on MI355X):
+/* Process-wide launch knobs (defaults are the values measured best on MI355X).  The product
+ * library takes the knobs that choose among the shapes it holds:
  *   "grid_cap"      workgroups per launch before the kernels grid-stride (<= 0: no cap)
- *   "nt_load"       non-temporal client loads (0/1)      "nt_store"  non-temporal output stores
- *   "vpt"           16-B vectors per thread per step (0 = auto by K, size and type; 1/2/4/8/16)
- *   "unroll"        clients per load group (1/2/4/8/16, with an explicit vpt)
- *   "xcd"           1 = blocks sharing an XCD take adjacent tiles (measured slower; default 0)
- *   "tile"          a workgroup step covers vpt*256 contiguous vectors (0/1)
- *   "pipe"          software-pipelined client groups (0/1, vpt 1 only)
  *   "fuse_pairwise" patch numel==1 tensors inside the bucket launch (0/1)
- *   "sc_vpt"        Scaffold: 16-B vectors per thread per step (0 = auto by K; 1/2/4/8)
- *   "sc_pipe"       Scaffold: software-pipelined client groups (0/1)
- *   "sc_unroll"     Scaffold: clients per load group (2/4/8)
- *   "sc_split"      Scaffold: 1 = stream all delta vectors, then all control-variate vectors
- *   "sc_bsplit"     Scaffold: 1 = workgroup pairs, one streams the delta rows, one the control variates
- *   "sc_buf"        Scaffold: buffer-descriptor client loads with an explicit sc_vpt (auto: from 32
- *                   fp32 clients)
- *   "fa_occ"        FedAvg: 2-4 = register-capped (waves per SIMD) build of the 8/16-KiB tiles
- *                   (auto: 2 for fp32 from 32 clients)
- *   "buf"           FedAvg: buffer-descriptor client loads with an explicit vpt (auto: bf16 from
- *                   32 clients)
- *   "sc_cpf"        Scaffold 4x4 tile: load c with the last client group (0/1)
- *   "sc_occ"        Scaffold 4x4 tile: register-capped build, waves per SIMD (0 = uncapped)
- *   "sc_blk"        Scaffold 4x4 tile: threads per workgroup (256 / 512)
- *   "fa_blk"        FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto / 256 / 512)
+ *   "eq_vec"        16-B loads in the c-equality check (0/1)      "flat_vec"  16-B client flat ops (0/1)
  *   "st_sc1"        FedAvg output stores as write-through (sc1) stores (-1 auto: below 32 clients)
- *   "sc_sc1"        Scaffold 4 x 4 tiles: write-through (sc1) output stores
- *   "sc_2l"         Scaffold: one bucket at a time (1: a launch per bucket, 2: one launch, bucket-ordered halves)
+ *   "sc_2l"         Scaffold: 1 = one bucket per launch, 0 = both buckets in one walk, -1 = auto
  *   "tiled_few"     recommend tile-interleaved buckets below 32 fp32 clients too (0/1)
- * Returns FEDAGG_EINVAL for an unknown key. */
+ * A library built with -DFEDAGG_TUNING=1 (fedagg_tuning_build() == 1) also instantiates every
+ * variant DESIGN.md records as measured and not kept, selected by the experiment knobs "nt_load",
+ * "nt_store", "vpt", "unroll", "pipe", "tile", "xcd", "tpb", "buf", "fa_occ", "fa_blk", "sc_vpt",
+ * "sc_unroll", "sc_split", "sc_bsplit", "sc_buf", "sc_pipe", "sc_cpf", "sc_occ", "sc_blk",
+ * "sc_sc1" and "sc_2l" = 2; the product library refuses them.
+ * Returns FEDAGG_EINVAL for an unknown (or, in the product library, an experiment) key. */
 int fedagg_tune(const char* key, long long value);
+/* 1 in a FEDAGG_TUNING build (every experiment variant instantiated), 0 in the product library. */
+int fedagg_tuning_build(void);
 
 /* Workspace for the separate numel==1 path, needed only when it cannot be fused
  * (K > FEDAGG_KCHUNK (FedAvg) / FEDAGG_KCHUNK_SCAFFOLD (Scaffold), or P > FEDAGG_FUSED_PAIRWISE). */

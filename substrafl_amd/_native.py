@@ -29,6 +29,7 @@ SIGNATURES = {
     "fedagg_abi_version": (c_int, []),
     "fedagg_last_error": (ctypes.c_char_p, []),
     "fedagg_tune": (c_int, [ctypes.c_char_p, ctypes.c_longlong]),
+    "fedagg_tuning_build": (c_int, []),
     "fedagg_pairwise_ws_bytes": (c_size, [c_int, c_int, c_int]),
     "fedagg_fedavg_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
     "fedagg_fedavg_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, P(c_u64), c_int, c_void, c_void, c_void]),
@@ -173,9 +174,15 @@ def ptr_array(ptrs) -> ctypes.Array:
     return arr
 
 
+def tuning_build() -> bool:
+    """Whether the loaded library is a FEDAGG_TUNING build (every experiment variant and knob;
+    ``FEDAGG_LIB=substrafl_amd/libfedagg_tuning.so``, built by ``build(tuning=True)``)."""
+    return bool(load().fedagg_tuning_build())
+
+
 def tune(**knobs) -> None:
-    """Set launch knobs of the library (``fedagg_tune``): grid_cap, nt_load, nt_store, vpt,
-    unroll, pipe, tile, fuse_pairwise, sc_vpt, sc_unroll, sc_split, sc_bsplit, xcd."""
+    """Set launch knobs of the library (``fedagg_tune``, include/fedagg.h): the product knobs, and
+    in a tuning build the experiment knobs."""
     lib = load()
     for k, v in knobs.items():
         check(lib.fedagg_tune(k.encode(), int(v)), f"fedagg_tune({k})")

@@ -35,6 +35,15 @@
 
 #include "fedagg.h"
 
+// FEDAGG_TUNING=1 (`__graft_entry__.build(tuning=True)`, tools/): every launch variant the
+// experiment knobs of fedagg_tune select is instantiated -- the shapes, load paths, occupancy caps
+// and walks DESIGN.md records as measured and not kept.  The product library (the default) holds
+// only the shapes the default dispatch selects (shape_for, the Scaffold launch plan, the tiled
+// kernels) and refuses the experiment knobs.
+#ifndef FEDAGG_TUNING
+#define FEDAGG_TUNING 0
+#endif
+
 #define FA_BLOCK 256
 #define FA_UNROLL 8
 
@@ -67,7 +76,7 @@ int g_tile = 1;         // a workgroup step covers VPT*256 contiguous vectors
 int g_fuse_pw = 1;      // patch numel==1 tensors inside the bucket launch
 int g_sc_vpt = 0;       // Scaffold: 16-byte vectors per thread per step (1/2/4/8; 0: auto, sc_shape_for)
 int g_sc_unroll = 4;    // Scaffold: clients per load group (2/4/8, with an explicit sc_vpt)
-int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
+[[maybe_unused]] int g_sc_split = 0;     // Scaffold: phase-split walk (all delta streams, then all control-variate streams)
 int g_buf = 0;          // FedAvg: buffer-descriptor client loads (8/16-KiB tiles, fp32/bf16)
 int g_fa_occ = 0;       // FedAvg: register-capped occupancy variants (0: off; 2-4 with the 8/16-KiB shapes)
 int g_sc_buf = 0;       // Scaffold: buffer-descriptor client loads (fp32 inputs, 4- and 8-vector tiles)
@@ -76,11 +85,11 @@ int g_flat_vec = 1;     // 16-B (4-element) client flat ops when every operand i
 int g_eq_vec = 1;       // vectorised c-equality check (16-B loads) when every copy is 16-B aligned
 int g_sc_pipe = 0;      // Scaffold: software-pipelined client groups (next group's loads before this group's adds)
 int g_tpb = 1;          // consecutive tiles per workgroup (1: one step per workgroup)
-int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
-int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
-int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
+[[maybe_unused]] int g_sc_cpf = 0;       // Scaffold 4 x 4 tile: c loaded with the last client group
+[[maybe_unused]] int g_sc_occ = 0;       // Scaffold 4 x 4 tile: register-capped build (waves per SIMD, 0 = uncapped)
+[[maybe_unused]] int g_sc_blk = 256;     // Scaffold 4 x 4 tile: threads per workgroup (256 or 512)
 int g_sc_2l = -1;       // Scaffold: one bucket at a time (-1 auto: from SC_2L_MIN_K clients; 1 / 2 / 0)
-int g_sc_sc1 = 0;       // Scaffold 4 x 4 tiles: write-through (sc1) output stores
+[[maybe_unused]] int g_sc_sc1 = 0;       // Scaffold 4 x 4 tiles: write-through (sc1) output stores
 int g_tiled_few = 0;    // recommend the tile-interleaved layout below 32 fp32 clients too (fedagg_tune "tiled_few";
                         // 8 x 25M: 134.5 vs 134.4 us on rows, profiles/r02_layout_c2_*.json -- no gain)
 int g_st_sc1 = -1;      // FedAvg: write-through (sc1) output stores (-1: auto, below SC1_MAX_K clients)
@@ -1719,6 +1728,23 @@ template <typename E, int NTS>
 void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
                          int first, uint64_t nvec, uint64_t M, typename E::Out* out, Shape sh) {
 #define FA_ARGS grid, s, a, pw, kc, first, nvec, M, out
+#if !FEDAGG_TUNING
+  // product: the shapes shape_for returns under the default knobs (sc1 or nt output stores)
+  if constexpr (std::is_same<E, F64>::value) {
+    return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);  // pipelined 4 x 4
+  } else if constexpr (std::is_same<E, F16>::value) {
+    if (sh.vpt >= 16) return launch_fedavg_variant<E, true, NTS, 16, 2, false, true>(FA_ARGS);
+    return launch_fedavg_variant<E, true, NTS, 4, 4, false, true>(FA_ARGS);
+  } else {
+    if (sh.vpt >= 16) {
+      if constexpr (std::is_same<E, BF16>::value)  // client pairs over buffer descriptors
+        return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, true>(FA_ARGS);
+      else  // client pairs in 512-thread workgroups
+        return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
+    }
+    return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
+  }
+#else
   if constexpr (NTS == 2) {  // write-through (sc1) output stores: the auto shapes and their neighbours only
     if (sh.pipe) {
       if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
@@ -1812,18 +1838,27 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
   if (sh.unroll <= 4) return launch_fedavg_variant<E, true, NTS, 1, 4, false, false>(FA_ARGS);
   return launch_fedavg_variant<E, true, NTS, 1, 8, false, false>(FA_ARGS);
   }
+#endif
 #undef FA_ARGS
 }
 
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
                    int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts, bool sc1, Shape sh) {
+#if FEDAGG_TUNING
   if (nts && sc1 && g_nt_load && g_tile)
     launch_fedavg_shape<E, 2>(grid, s, a, pw, kc, first, nvec, M, out, sh);
   else if (nts)
     launch_fedavg_shape<E, 1>(grid, s, a, pw, kc, first, nvec, M, out, sh);
   else
     launch_fedavg_shape<E, 0>(grid, s, a, pw, kc, first, nvec, M, out, sh);
+#else
+  (void)nts;  // non-temporal loads and stores are fixed in the product build
+  if (sc1)
+    launch_fedavg_shape<E, 2>(grid, s, a, pw, kc, first, nvec, M, out, sh);
+  else
+    launch_fedavg_shape<E, 1>(grid, s, a, pw, kc, first, nvec, M, out, sh);
+#endif
 }
 
 // idx_in (tile-interleaved buckets): where each numel==1 element sits in the client buckets
@@ -2169,6 +2204,7 @@ void launch_scaffold_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FED
 
 // Scaffold shapes (fedagg_tune "sc_vpt" / "sc_unroll"; nt_load / nt_store shared with FedAvg).
 
+#if FEDAGG_TUNING
 template <typename TIn, int VPT, int SU>
 void launch_scaffold_bsplit_variant(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a,
                                     const PwArgs& pw, int kc, int first, int last, const TIn* c, double lr,
@@ -2195,6 +2231,8 @@ void launch_scaffold_bsplit(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDA
 #undef SC_ARGS
 }
 
+#endif
+
 // Does a Scaffold call walk one bucket per launch (scaffold_bucket_kernel x 2) or both at once?
 inline bool scaffold_one_bucket(int K, size_t in_bytes, uint64_t nvec) {
   const bool bsplit = g_sc_bsplit && nvec && g_nt_load && g_nt_store != 0;
@@ -2218,6 +2256,7 @@ void launch_scaffold_2l_variant(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_S
                      dim3(FA_BLOCK), 0, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
 }
 
+#if FEDAGG_TUNING
 // One-bucket launch pairs (sc_2l): 4 x 4, 8 x 4, 8 x 2 and 16 x 2 tiles with nt or write-through
 // (sc_sc1) stores; plain stores for the 4 x 4 tile only.
 template <typename TIn, int NTS>
@@ -2245,16 +2284,29 @@ void launch_scaffold_2l_shape(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCA
 #undef SC2_ARGS
 }
 
+#endif
+
 template <typename TIn>
 void launch_scaffold_2l(hipStream_t s, const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD>& a, const PwArgs& pw, int kc,
                         int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
                         double* cout, const int sv, const int su, const bool pipe) {
+#if !FEDAGG_TUNING
+  // product: fp32 8 x 4 tiles, fp64 pipelined 4 x 2 tiles, nt stores
+  (void)sv;
+  (void)su;
+  (void)pipe;
+  if constexpr (sizeof(TIn) == 4)
+    launch_scaffold_2l_variant<TIn, 1, 8, 4>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+  else
+    launch_scaffold_2l_variant<TIn, 1, 4, 2, true>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout);
+#else
   if (g_nt_store == 0)
     launch_scaffold_2l_shape<TIn, 0>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, pipe);
   else if (g_sc_sc1)
     launch_scaffold_2l_shape<TIn, 2>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, pipe);
   else
     launch_scaffold_2l_shape<TIn, 1>(s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, pipe);
+#endif
 }
 
 template <typename TIn>
@@ -2262,6 +2314,18 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
                      int kc, int first, int last, const TIn* c, double lr, uint64_t nvec, uint64_t M, double* dout,
                      double* cout, const int sv, const int su, const bool buf) {
 #define SC_ARGS grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout
+#if !FEDAGG_TUNING
+  // product: 4 x 4 global loads below 32 clients; from 32, fp32 8 x 4 over buffer descriptors,
+  // fp64 8 x 2 (the scalar tail of unaligned buckets runs in the same kernels)
+  (void)su;
+  (void)buf;
+  if constexpr (sizeof(TIn) == 4) {
+    if (sv >= 8) return launch_scaffold_variant<TIn, true, true, 8, 4, false, false, true>(SC_ARGS);
+  } else {
+    if (sv >= 8) return launch_scaffold_variant<TIn, true, true, 8, 2>(SC_ARGS);
+  }
+  return launch_scaffold_variant<TIn, true, true, 4, 4>(SC_ARGS);
+#else
   const bool nts = g_nt_store != 0;
   if (!g_nt_load) return launch_scaffold_variant<TIn, false, false, 1, 4>(SC_ARGS);
   if (buf && nts && !g_sc_split && !g_sc_pipe && sizeof(TIn) == 4) {  // buffer-descriptor loads
@@ -2325,6 +2389,7 @@ void launch_scaffold(unsigned grid, hipStream_t s, const ScArgs<TIn, FEDAGG_KCHU
   if (su >= 8 && nts) return launch_scaffold_variant<TIn, true, true, 1, 8>(SC_ARGS);
   if (nts) return launch_scaffold_variant<TIn, true, true, 1, 4>(SC_ARGS);
   return launch_scaffold_variant<TIn, true, false, 1, 4>(SC_ARGS);
+#endif
 #undef SC_ARGS
 }
 
@@ -2389,8 +2454,10 @@ int scaffold_launch(const TIn* const* d, const TIn* const* cv, const TIn* c, con
                               g_sc_vpt > 0 ? g_sc_vpt : (sizeof(TIn) == 4 ? 8 : 4),
                               g_sc_vpt > 0 ? g_sc_unroll : (sizeof(TIn) == 4 ? 4 : 2),
                               g_sc_vpt > 0 ? g_sc_pipe != 0 : sizeof(TIn) == 8);
+#if FEDAGG_TUNING
     else if (bsplit)
       launch_scaffold_bsplit<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su);
+#endif
     else
       launch_scaffold<TIn>(grid, s, a, pw, kc, first, last, c, lr, nvec, M, dout, cout, sv, su, buf);
     int rc = check_launch("scaffold_kernel");
@@ -2458,7 +2525,17 @@ const char* fedagg_last_error(void) { return g_err; }
 
 int fedagg_tune(const char* key, long long value) {
   if (!key) return fail(FEDAGG_EINVAL, "fedagg_tune: NULL key");
+  // knobs of the product build: they choose among the shapes it holds
   if (!strcmp(key, "grid_cap")) g_grid_cap = (int)value;
+  else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
+  else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
+  else if (!strcmp(key, "flat_vec")) g_flat_vec = value ? 1 : 0;
+  else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
+  else if (!strcmp(key, "tiled_few")) g_tiled_few = value ? 1 : 0;
+  else if (!strcmp(key, "sc_2l") && value <= 1) g_sc_2l = value < 0 ? -1 : (value == 0 ? 0 : 1);
+#if FEDAGG_TUNING
+  // experiment knobs (measured, not kept: DESIGN.md §5, §8, §9)
+  else if (!strcmp(key, "sc_2l")) g_sc_2l = 2;
   else if (!strcmp(key, "nt_load")) g_nt_load = value ? 1 : 0;
   else if (!strcmp(key, "nt_store")) g_nt_store = value < 0 ? -1 : (value ? 1 : 0);
   else if (!strcmp(key, "vpt"))
@@ -2467,7 +2544,6 @@ int fedagg_tune(const char* key, long long value) {
     g_unroll = value >= 16 ? 16 : (value <= 1 ? 1 : value <= 2 ? 2 : (value <= 4 ? 4 : 8));
   else if (!strcmp(key, "pipe")) g_pipe = value ? 1 : 0;
   else if (!strcmp(key, "tile")) g_tile = value ? 1 : 0;
-  else if (!strcmp(key, "fuse_pairwise")) g_fuse_pw = value ? 1 : 0;
   else if (!strcmp(key, "sc_vpt")) g_sc_vpt = value <= 0 ? 0 : value >= 8 ? 8 : (value >= 4 ? 4 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_unroll")) g_sc_unroll = value <= 1 ? 1 : value <= 2 ? 2 : (value >= 8 ? 8 : 4);
   else if (!strcmp(key, "sc_split")) g_sc_split = value ? 1 : 0;
@@ -2477,20 +2553,18 @@ int fedagg_tune(const char* key, long long value) {
   else if (!strcmp(key, "fa_occ")) g_fa_occ = value <= 1 ? 0 : (value >= 4 ? 4 : (int)value);
   else if (!strcmp(key, "xcd")) g_xcd = value ? 1 : 0;
   else if (!strcmp(key, "sc_pipe")) g_sc_pipe = value ? 1 : 0;
-  else if (!strcmp(key, "eq_vec")) g_eq_vec = value ? 1 : 0;
-  else if (!strcmp(key, "flat_vec")) g_flat_vec = value ? 1 : 0;
   else if (!strcmp(key, "tpb")) g_tpb = value < 1 ? 1 : (value > 64 ? 64 : (int)value);
   else if (!strcmp(key, "sc_cpf")) g_sc_cpf = value ? 1 : 0;
   else if (!strcmp(key, "sc_occ")) g_sc_occ = value <= 1 ? 0 : (int)value;
   else if (!strcmp(key, "sc_blk")) g_sc_blk = value >= 512 ? 512 : 256;
-  else if (!strcmp(key, "sc_2l")) g_sc_2l = value < 0 ? -1 : (value == 0 ? 0 : (value >= 2 ? 2 : 1));
   else if (!strcmp(key, "sc_sc1")) g_sc_sc1 = value ? 1 : 0;
-  else if (!strcmp(key, "st_sc1")) g_st_sc1 = value < 0 ? -1 : (value ? 1 : 0);
-  else if (!strcmp(key, "tiled_few")) g_tiled_few = value ? 1 : 0;
   else if (!strcmp(key, "fa_blk")) g_fa_blk = value <= 0 ? 0 : (value >= 1024 ? 1024 : (value >= 512 ? 512 : 256));
-  else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key");
+#endif
+  else return fail(FEDAGG_EINVAL, "fedagg_tune: unknown key, or an experiment knob of a FEDAGG_TUNING build");
   return FEDAGG_OK;
 }
+
+int fedagg_tuning_build(void) { return FEDAGG_TUNING; }
 
 size_t fedagg_pairwise_ws_bytes(int K, int P, int elem_bytes) {
   (void)P;

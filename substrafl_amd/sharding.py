@@ -442,7 +442,8 @@ class DistTransport:
     def _device(self):
         import torch
 
-        return torch.device("cuda", torch.cuda.current_device()) if self.dist.get_backend(self.group) == "nccl" \
+        # RCCL carries device tensors ("nccl", or the cuda half of "cpu:gloo,cuda:nccl")
+        return torch.device("cuda", torch.cuda.current_device()) if "nccl" in str(self.dist.get_backend(self.group)) \
             else torch.device("cpu")
 
     def warm_p2p(self) -> None:

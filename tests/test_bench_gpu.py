@@ -49,9 +49,24 @@ def test_scaffold_line():
     assert line["roofline"]["kernel"].startswith("scaffold_bucket_kernel<float> x2")  # 16 clients: one bucket per launch
 
 
-def test_client_shard_single_rank():
-    line = _bench("--workload", "c2", "--mode", "client-shard", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+@pytest.mark.parametrize("combine", ["striped", "relay"])
+def test_client_shard_single_rank(combine):
+    """--mode client-shard on one rank: the lockstep schedule's runs with no exchange, spot-checked
+    bit-exact, its block-kernel time and the single-GPU reference reported."""
+    line = _bench("--workload", "c2", "--mode", "client-shard", "--combine", combine, "--steps", "3", "--warmup", "1",
+                  "--no-cpu-baseline")
     assert line["parity"]["mismatches"] == 0 and line["config"]["clients_per_gpu"] == 8
+    cs = line["client_shard"]
+    assert cs["combine"] == combine and cs["block_kernel_ms"] > 0 and cs["single_gpu_ms"] > 0
+    assert cs["bit_exact_by_construction"] and 0 < cs["weak_efficiency"] < 1.5
+
+
+def test_shared_gpu_ranks_skip_the_client_shard_leg():
+    """Two ranks sharing the one GPU of a test box: the parameter-range line is measured, the
+    client-shard leg (RCCL needs a GPU per rank) is reported as skipped."""
+    line = _bench("--workload", "c2", "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert line["n_gpus"] == 2 and "skipped" in line["client_shard"]
+    assert line["process_group"]["timeout_s"] > 0
 
 
 def test_strong_scaling_two_ranks_shared_gpu():

@@ -26,18 +26,42 @@ def _line(stdout):
     return json.loads(lines[0])
 
 
+CLIENT_SHARD_FIELDS = ("combine", "scaling", "clients", "clients_per_gpu", "params", "layout", "steps", "ms_per_step",
+                       "GBps", "frac_of_n_x_hbm_peak", "block_kernel_ms", "exchange_and_tail_ms", "single_gpu_ms",
+                       "weak_efficiency", "bit_exact_by_construction", "schedule", "parity")
+
+
 def test_plain_gpus_2_launches_two_ranks():
+    """The plain N > 1 command: one line with the parameter-range fields AND the client-shard leg
+    (the north-star mode: lockstep schedule over one communicator, here gloo on a tiny problem),
+    and a process group with a finite timeout."""
     r = _run(["--gpus", "2", "--rehearse-cpu", "--steps", "3", "--warmup", "1"])
     assert r.returncode == 0, r.stderr[-3000:]
     line = _line(r.stdout)
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["rehearsal"] is True
     assert line["value"] is None  # a rehearsal is never a measurement
+    assert 0 < line["process_group"]["timeout_s"] <= 600
+    cs = line["client_shard"]
+    assert all(k in cs for k in CLIENT_SHARD_FIELDS)
+    assert cs["combine"] == "striped" and cs["scaling"] == "weak" and cs["bit_exact_by_construction"]
+    assert cs["parity"]["mismatches"] == 0 and cs["schedule"]["steps"] == 4
+
+
+def test_pg_kwargs_has_a_timeout():
+    """Every multi-rank process group the bench creates (RCCL or gloo) has a finite timeout."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    t = bench.pg_kwargs()["timeout"].total_seconds()
+    assert 0 < t <= 600 and bench.CLIENT_SHARD_DEADLINE_S < t
 
 
 def test_plain_gpus_3_launches_three_ranks():
-    r = _run(["--gpus", "3", "--rehearse-cpu", "--steps", "2", "--warmup", "0"])
+    r = _run(["--gpus", "3", "--rehearse-cpu", "--steps", "2", "--warmup", "0", "--combine", "relay"])
     assert r.returncode == 0, r.stderr[-3000:]
-    assert _line(r.stdout)["n_gpus"] == 3
+    line = _line(r.stdout)
+    assert line["n_gpus"] == 3 and line["client_shard"]["combine"] == "relay"
+    assert line["client_shard"]["parity"]["mismatches"] == 0
 
 
 def test_world_size_mismatch_is_an_error():

@@ -18,6 +18,28 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
+PRODUCT_KNOBS = {"grid_cap", "fuse_pairwise", "eq_vec", "flat_vec", "st_sc1", "tiled_few", "sc_2l"}
+
+
+def _tuning_only(*knob_dicts):
+    """Skip unless every knob is one the loaded library has: experiment knobs select variants the
+    product library does not instantiate (a FEDAGG_TUNING build does: ``build(tuning=True)``,
+    ``FEDAGG_LIB=substrafl_amd/libfedagg_tuning.so``)."""
+    from substrafl_amd import _native
+
+    keys = set().union(*[set(d) for d in knob_dicts])
+    experiment = bool(keys - PRODUCT_KNOBS - {"K"}) or any(d.get("sc_2l") == 2 for d in knob_dicts)
+    if experiment and not _native.tuning_build():
+        pytest.skip("experiment variant: needs the FEDAGG_TUNING build of libfedagg")
+
+
+def _product(d):
+    """``d`` without the experiment knobs when the product library is loaded."""
+    from substrafl_amd import _native
+
+    return dict(d) if _native.tuning_build() else {k: v for k, v in d.items() if k in PRODUCT_KNOBS}
+
+
 def _bits(a):
     a = np.asarray(a)
     return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize])
@@ -610,6 +632,8 @@ def test_launch_variants_bit_identical(torch_gpu, knobs):
     outs = []
     default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
                    fa_blk=0)
+    _tuning_only(knobs)
+    default = _product(default)
     for kn in (default, knobs):
         _native.tune(**kn)
         out = torch.empty(M + 5, device="cuda")
@@ -647,6 +671,8 @@ def test_occupancy_capped_variants_bit_identical(torch_gpu, kind, knobs):
     ns = list(range(7, 7 + K))
     default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
                    fa_blk=0, st_sc1=-1)
+    _tuning_only(knobs)
+    default = _product(default)
     outs = []
     for kn in (default, dict(default, **knobs)):
         _native.tune(**kn)
@@ -671,6 +697,8 @@ def test_fp16_buffer_load_variants_bit_identical(torch_gpu, knobs):
     x = torch.randn((K, M + 5), device="cuda").to(torch.float16)
     ns = list(range(20, 20 + K))
     default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0)
+    _tuning_only(knobs)
+    default = _product(default)
     outs = []
     for kn in (default, dict(default, **knobs)):
         _native.tune(**kn)
@@ -699,6 +727,8 @@ def test_write_through_store_variants_bit_identical(torch_gpu, kind, knobs):
     ns = list(range(11, 11 + K))
     default = dict(vpt=0, nt_load=1, nt_store=1, grid_cap=0, unroll=8, pipe=0, tile=1, xcd=0, tpb=1, fa_occ=0, buf=0,
                    fa_blk=0, st_sc1=-1)
+    _tuning_only(knobs)
+    default = _product(default)
     outs = []
     for kn in (default, dict(default, **knobs)):
         _native.tune(**kn)
@@ -723,14 +753,16 @@ def test_auto_shape_many_clients_bit_identical(torch_gpu):
     ns = list(range(100, 100 + K))
     w = fedavg_weights(ns, "f32")
     outs = []
-    for kn in (dict(vpt=0), dict(vpt=8, unroll=4)):
+    shapes = (dict(vpt=0), dict(vpt=8, unroll=4)) if _native.tuning_build() else ({},)  # product: the oracle sample
+    for kn in shapes:
         _native.tune(**kn)
         out = torch.empty(M + 3, device="cuda")
         FedAvgPlan("f32", x, w, M, out, [5, M - 1]).launch()
         torch.cuda.synchronize()
         outs.append(out[:M].clone())
-    _native.tune(vpt=0, unroll=8)
-    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    if len(outs) > 1:
+        _native.tune(vpt=0, unroll=8)
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
     idx = np.array([0, 1, 4095, 16 * 256 * 4 * 7 + 3, M // 2, M - 80, M - 2])
     xs = x[:, torch.from_numpy(idx).cuda()].cpu().numpy()
     acc = np.zeros(idx.size, np.float32)
@@ -753,14 +785,16 @@ def test_auto_shape_many_clients_bf16_bit_identical(torch_gpu):
     ns = list(range(50, 50 + K))
     w = fedavg_weights(ns, "bf16")
     outs = []
-    for kn in (dict(vpt=0, buf=0), dict(vpt=8, unroll=4, buf=0)):
+    shapes = (dict(vpt=0, buf=0), dict(vpt=8, unroll=4, buf=0)) if _native.tuning_build() else ({},)
+    for kn in shapes:
         _native.tune(**kn)
         out = torch.empty(M + 3, device="cuda")
         FedAvgPlan("bf16", x, w, M, out, [2, M - 1]).launch()
         torch.cuda.synchronize()
         outs.append(out[:M].clone())
-    _native.tune(vpt=0, unroll=8)
-    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    if len(outs) > 1:
+        _native.tune(vpt=0, unroll=8)
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
     idx = np.array([0, 1, 8191, 16 * 256 * 8 * 5 + 7, M // 3, M - 40, M - 2])
     xs = x[:, torch.from_numpy(idx).cuda()].float().cpu().numpy()
     acc = np.zeros(idx.size, np.float32)
@@ -813,6 +847,8 @@ def test_scaffold_launch_variants_bit_identical(torch_gpu, knobs):
     w = scaffold_weights(list(range(5, 5 + K)))
     default = dict(sc_vpt=0, sc_unroll=4, sc_split=0, sc_bsplit=0, sc_buf=0, sc_pipe=0, nt_store=1, nt_load=1, grid_cap=0,
                    xcd=0, tpb=1, sc_cpf=0, sc_occ=0, sc_blk=256, sc_sc1=0, sc_2l=-1)
+    _tuning_only(knobs)
+    default = _product(default)
     outs = []
     for kn in (default, knobs):
         _native.tune(**kn)
@@ -855,7 +891,9 @@ def test_scaffold_auto_shape_many_clients_bit_identical(torch_gpu, K):
     c = torch.randn(M + 1, device="cuda")
     w = scaffold_weights(list(range(9, 9 + K)))
     outs = []
-    for kn in (dict(sc_vpt=0), dict(sc_vpt=4, sc_unroll=4, sc_buf=0)):
+    pair = (dict(sc_vpt=0), dict(sc_vpt=4, sc_unroll=4, sc_buf=0)) if _native.tuning_build() else \
+        (dict(sc_2l=-1), dict(sc_2l=0))  # product: the one-bucket pair against the fused 8 x 4 walk
+    for kn in pair:
         _native.tune(**kn)
         do = torch.empty(M + 1, dtype=torch.float64, device="cuda")
         co = torch.empty(M + 1, dtype=torch.float64, device="cuda")
@@ -863,7 +901,7 @@ def test_scaffold_auto_shape_many_clients_bit_identical(torch_gpu, K):
                      do, co, [1, M - 1]).launch()
         torch.cuda.synchronize()
         outs.append((do[:M].clone(), co[:M].clone()))
-    _native.tune(sc_vpt=0, sc_unroll=4, sc_buf=0)
+    _native.tune(**_product(dict(sc_vpt=0, sc_unroll=4, sc_buf=0, sc_2l=-1)))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a.view(torch.int64), b.view(torch.int64))
 
@@ -884,6 +922,8 @@ def test_scaffold_one_bucket_launches_fp64_bit_identical(torch_gpu, K, knobs):
     c = torch.randn(M + 1, device="cuda", dtype=torch.float64)
     w = scaffold_weights(list(range(4, 4 + K)))
     base = dict(sc_2l=0, sc_vpt=0, sc_unroll=4, sc_sc1=0, sc_pipe=0)
+    _tuning_only(knobs)
+    base = _product(base)
     outs = []
     for kn in (base, dict(base, **knobs)):
         _native.tune(**kn)
