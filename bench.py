@@ -76,6 +76,11 @@ def parse():
     ap.add_argument("--rings", type=int, default=0, help="striped: rings (hop lengths; 0 = up to 4)")
     ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default one round)")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
+    ap.add_argument("--executor", default="native", choices=["native", "torch"],
+                    help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip) or the "
+                         "Python schedule over torch.distributed's RCCL process group")
+    ap.add_argument("--client-shard-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--t1-ms", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
     ap.add_argument("--tile", type=int, default=0, help="tiles layout: 16-B vectors per client tile "
                     "(0: the library's choice; FEDAGG_TILE_VECTORS_*)")
@@ -306,8 +311,10 @@ def main():
     dev_index = local % ndev  # param-range: a 1-GPU box can rehearse N > 1 (the ranks share the GPU)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    nccl = world > 1 and world <= ndev
-    backend = init_group(dist, world, device, nccl) if world > 1 else None
+    own_gpus = world <= ndev
+    # RCCL in the process group only where torch's process group carries the exchange itself
+    torch_pg_exchange = (client_shard or args.client_shard_child) and args.executor == "torch"
+    backend = init_group(dist, world, device, world > 1 and own_gpus and torch_pg_exchange) if world > 1 else None
     lib = _native.load()
     if args.grid_cap:
         _native.tune(grid_cap=args.grid_cap)
@@ -318,17 +325,25 @@ def main():
     ctx = _Ctx(torch=torch, dist=dist, world=world, rank=rank, device=device, lib=lib, native=_native,
                wl=WORKLOADS[args.workload], stream=torch.cuda.current_stream(device), backend=backend)
 
-    if client_shard:
+    if args.client_shard_child:  # one leg of an N > 1 line (see client_shard_legs)
+        try:
+            res = measure_client_shard(args, ctx, args.combine, "weak", t1_ms=args.t1_ms or None,
+                                       t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
+        except Exception as e:  # noqa: BLE001 -- reported in the parent's line
+            res = {"error": f"{type(e).__name__}: {e}"[:800]}
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+    elif client_shard:
         cs = measure_client_shard(args, ctx, args.combine or "relay", args.scaling)
         line = client_shard_line(args, ctx, cs)
     else:
         line, info = measure_param_range(args, ctx)
         if world > 1 and args.client_shard != "off":
-            if nccl:  # the north-star mode beside it: client buckets sharded, exchanged over xGMI
-                line["client_shard"] = guarded_client_shard(args, ctx, info, line)
+            if own_gpus:  # the north-star mode beside it: client buckets sharded, exchanged over xGMI
+                line.update(client_shard_legs(args, ctx, info))
             else:
                 line["client_shard"] = {"skipped": f"needs one GPU per rank for RCCL ({world} ranks, {ndev} GPUs)"}
-    if rank == 0:
+    if rank == 0 and not args.client_shard_child:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -501,38 +516,58 @@ def measure_param_range(args, ctx):
 # ======================================================================================
 # client-shard (the north-star mode) -- its own line, or a field of the N > 1 line
 # ======================================================================================
-def guarded_client_shard(args, ctx, info, line):
-    """The client-shard leg of an N > 1 line: every rank measures it after the parameter-range
-    line; an error becomes a field of the line, and a rank still inside it after
-    CLIENT_SHARD_DEADLINE_S s reports (rank 0) the parameter-range line with the failure and
-    exits, so a stuck exchange never costs the line."""
-    import threading
+def client_shard_legs(args, ctx, info):
+    """The client-shard legs of an N > 1 line, each in a CHILD process per rank (a fresh
+    interpreter with its own process group on a new port, started once this rank's parameter-range
+    buffers are freed): ``client_shard`` with the native RCCL executor, ``client_shard_torch_pg``
+    with the Python schedule over torch's RCCL process group.  A leg that fails, crashes or exceeds
+    CLIENT_SHARD_DEADLINE_S becomes an ``error`` field -- it can never cost the line."""
+    import subprocess
 
-    torch = ctx.torch
-    done = threading.Event()
-
-    def watchdog():
-        if not done.wait(CLIENT_SHARD_DEADLINE_S):
-            if ctx.rank == 0:
-                out = dict(line)
-                out["client_shard"] = {"error": f"did not finish within {CLIENT_SHARD_DEADLINE_S} s"}
-                print(json.dumps(out), flush=True)
-            os._exit(0)
-
+    torch, dist = ctx.torch, ctx.dist
     torch.cuda.empty_cache()
-    try:
-        th = threading.Thread(target=watchdog, daemon=True)
-        th.start()
-        # weak (the default): every rank holds the workload's K clients, N x K in all, each element
-        # still summed in the reference's order across the N blocks
-        res = measure_client_shard(args, ctx, args.combine or "striped", "weak", t1_ms=info["kern_ms"],
-                                   t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
-    except Exception as e:  # noqa: BLE001 -- reported in the line, which is still printed
-        res = {"error": f"{type(e).__name__}: {e}"[:500]}
-    finally:
-        done.set()
-        torch.cuda.empty_cache()
-    return res
+    ports = [[_free_port(), _free_port()]] if ctx.rank == 0 else [None]
+    dist.broadcast_object_list(ports, src=0)
+    out = {}
+    for (executor, key), port in zip((("native", "client_shard"), ("torch", "client_shard_torch_pg")), ports[0]):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+        env.update(RANK=str(ctx.rank), WORLD_SIZE=str(ctx.world), LOCAL_RANK=str(ctx.device.index),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmd = [sys.executable, str(Path(__file__).resolve()), "--client-shard-child", "--executor", executor,
+               "--gpus", str(ctx.world), "--workload", args.workload, "--combine", args.combine or "striped",
+               "--layout", args.layout, "--steps", str(args.client_shard_steps), "--warmup", "3",
+               "--client-shard-steps", str(args.client_shard_steps), "--t1-ms", str(info["kern_ms"]),
+               "--chunk", str(args.chunk), "--rings", str(args.rings), "--no-cpu-baseline"]
+        if args.rounds:
+            cmd += ["--rounds", args.rounds]
+        t0 = time.perf_counter()
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        try:
+            so, se = p.communicate(timeout=CLIENT_SHARD_DEADLINE_S)
+            res = None
+            if ctx.rank == 0:
+                lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+                res = json.loads(lines[-1]) if lines else None
+            if p.returncode != 0:
+                res = {"error": f"leg exited with {p.returncode}: {se[-600:]}"}
+            elif ctx.rank == 0 and res is None:
+                res = {"error": f"no result line: {se[-600:]}"}
+        except subprocess.TimeoutExpired:
+            p.kill()  # this rank's own child, by PID
+            p.communicate()
+            res = {"error": f"did not finish within {CLIENT_SHARD_DEADLINE_S} s"}
+        if res is not None:
+            res["wall_s"] = round(time.perf_counter() - t0, 1)
+            res["executor"] = executor
+        # every rank's leg is over before the next one starts (errors are per rank: gather them)
+        errs = [None] * ctx.world
+        dist.all_gather_object(errs, (res or {}).get("error"))
+        if ctx.rank == 0:
+            bad = {r: e for r, e in enumerate(errs) if e}
+            if bad and "error" not in res:
+                res["errors_on_other_ranks"] = bad
+            out[key] = res
+    return out
 
 
 def _synth_block(torch, kind, Kb, width, device, seed):
@@ -572,11 +607,20 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     shapes = synthetic_state_dict_shapes(M)
     layout = BucketLayout(list(range(len(shapes))), shapes, np.float32)
     pw = layout.pairwise_idx
-    tr = DistTransport() if world > 1 else LoopbackGroup(1).transport(0)
+    lockstep_mode = combine in ("relay", "striped")
+    if world == 1:
+        tr = LoopbackGroup(1).transport(0)
+    elif args.executor == "native":
+        if not lockstep_mode:
+            raise ValueError(f"the native executor runs the lockstep schedules (relay, striped), not {combine}")
+        from substrafl_amd.rccl import RcclTransport
+
+        tr = RcclTransport()
+    else:
+        tr = DistTransport()
     ops = GpuShardOps()
     stream = ctx.stream
     mode = {"auto": "auto", "tiles": True, "rows": False}[args.layout]
-    lockstep_mode = combine in ("relay", "striped")
     w_all = fedavg_weights(n_samples, kind) if not scaffold else scaffold_weights(n_samples)
     gc = torch.Generator(device=device)
     gc.manual_seed(4242)
@@ -638,10 +682,13 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
             for runs in plan.runs:
                 for r in runs:
                     sh = blocks[r.block]
-                    s0 = r.acc[1] if r.acc[0] == "slot" else 0
-                    a = acc[s0 * slot_n:][: r.n]
+                    if r.acc[0] == "out":  # the root's final runs accumulate in the output itself
+                        a = (outs["dout"] if scaffold else outs["out"])[r.acc[2]: r.acc[2] + r.n]
+                        a2 = outs["cout"][r.acc[2]: r.acc[2] + r.n] if scaffold else None
+                    else:
+                        a = acc[r.acc[1] * slot_n + r.acc[2]:][: r.n]
+                        a2 = acc[(SLOTS + r.acc[1]) * slot_n + r.acc[2]:][: r.n] if scaffold else None
                     if scaffold:
-                        a2 = acc[(SLOTS + s0) * slot_n:][: r.n]
                         ops.scaffold_run(kind, sh.delta[:, r.col: r.col + r.n], sh.cv[:, r.col: r.col + r.n], sh.w,
                                          r.seed, r.final, c[r.lo: r.lo + r.n], 1.0, a, a2)
                     else:
@@ -729,6 +776,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
         "single_gpu_ms": round(t1_ms, 5),
         "single_gpu_source": t1_source,
         "bit_exact_by_construction": combine in ("relay", "striped"),
+        "executor": ("native RCCL (csrc/lockstep.hip)" if getattr(tr, "native", False) else
+                     "Python schedule over torch.distributed" if world > 1 else "one rank (no exchange)"),
         "schedule": schedule,
         "hip_streams_per_rank": "2 (compute + the communicator's) <= GPU_MAX_HW_QUEUES = 4",
         "parity": parity,
@@ -821,11 +870,12 @@ def _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held,
             cols = (idx[sel] - lo + col).astype(np.int64)
             for f, part in enumerate(parts):
                 dense[f, k0: k0 + Kb, torch.from_numpy(sel).to(device)] = _held_values(torch, kind, part, cols, Kb)
-    if world > 1:
+    dense = dense.cpu()
+    if world > 1:  # over the host group (gloo): every leg has it
         ctx.dist.reduce(dense, dst=0)
     if rank != 0:
         return None
-    xs = dense.cpu().numpy()
+    xs = dense.numpy()
     tidx = torch.from_numpy(idx).to(device)
     if not scaffold:
         got = outs["out"][tidx].cpu().numpy()

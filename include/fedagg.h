@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 10
+#define FEDAGG_ABI_VERSION 11
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -220,6 +220,63 @@ int fedagg_scaffold_finish_f32(double* d_ws, int Ktot, const float* d_c, const u
                                double* d_delta_out, double* d_c_out, void* stream);
 int fedagg_scaffold_finish_f64(double* d_ws, int Ktot, const double* d_c, const uint64_t* h_idx, int P, double lr,
                                double* d_delta_out, double* d_c_out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Native executor of the client-sharded lockstep schedules (substrafl_amd/lockstep.py,
+ * DESIGN.md §6).  The schedule -- every run (one chain launch over a client block) and every
+ * point-to-point message of every exchange group -- is computed once on the host; this issues it
+ * from ONE thread on ONE RCCL communicator: for t = 0, 1, ...: exchange group t on the
+ * communicator's stream after the caller's stream so far (ncclGroupStart / Send / Recv / End),
+ * then step t's runs on the caller's stream after group t - 1; finally the in-place ncclReduce
+ * of the numel == 1 product workspace onto the root.  Group t of every rank pairs only with group
+ * t of its peers, so the schedule cannot deadlock.  Replaces the per-element client loop of
+ * fed_avg.py:221-222 / scaffold.py:262-263,293 across GPUs (the reference has no multi-GPU path).
+ * RCCL is dlopen'ed from rccl_path (NULL: "librccl.so.1"), reusing an instance already loaded.
+ * -------------------------------------------------------------------------*/
+enum { FEDAGG_BF16 = 12 };  /* kind of a run over bf16 buckets (fp32 accumulators)              */
+enum { FEDAGG_RUN_FEDAVG = 0, FEDAGG_RUN_FEDAVG_TILED = 1, FEDAGG_RUN_SCAFFOLD = 2 };
+typedef struct fedagg_lockstep_run {
+  int32_t step;              /* the step it runs at (runs sorted by step)                        */
+  int32_t op;                /* FEDAGG_RUN_*                                                     */
+  int32_t kind;              /* FEDAGG_F32 / FEDAGG_BF16 / FEDAGG_F64 / FEDAGG_F16 (Scaffold: F32/F64) */
+  int32_t K;                 /* clients of the block (>= 1)                                      */
+  int32_t seed, finish;      /* seed: start from +0.0; finish (Scaffold): + c, then * lr         */
+  uint64_t n;                /* elements                                                         */
+  uint64_t tile_vectors;     /* FEDAGG_RUN_FEDAVG_TILED: the tile                                */
+  const void* const* x;      /* K client pointers (tiled: x[0] = the run's tile-interleaved bucket) */
+  const void* const* x2;     /* Scaffold: the K control-variate pointers                         */
+  const void* w;             /* K weights: float (f32/bf16), double (f64, Scaffold), fp16 bits   */
+  const void* c;             /* Scaffold, finish: c of these elements                            */
+  double lr;                 /* Scaffold: aggregation_lr                                         */
+  void* acc;                 /* accumulator (Scaffold: the delta sum)                            */
+  void* acc2;                /* Scaffold: the control-variate sum                                */
+} fedagg_lockstep_run;
+typedef struct fedagg_lockstep_msg {
+  int32_t group;             /* exchange group (messages sorted by group)                        */
+  int32_t send;              /* 1 send, 0 receive                                                */
+  int32_t peer;              /* rank of the communicator                                         */
+  int32_t kind;              /* element kind: FEDAGG_F32 / FEDAGG_F64 / FEDAGG_F16               */
+  void* buf;
+  uint64_t count;
+} fedagg_lockstep_msg;
+typedef struct fedagg_comm fedagg_comm;
+/* rank 0 of the group: a fresh RCCL unique id (128 bytes) to hand to every rank */
+int fedagg_comm_unique_id(const char* rccl_path, void* id_out);
+/* every rank at once (collective): the communicator of `nranks` ranks on GPU `device` */
+int fedagg_comm_create(const char* rccl_path, int nranks, int rank, const void* unique_id, int device,
+                       fedagg_comm** out);
+int fedagg_comm_destroy(fedagg_comm* comm);
+/* ncclCommAbort (a watchdog's way out of a stuck exchange) */
+int fedagg_comm_abort(fedagg_comm* comm);
+/* 0, or FEDAGG_EHIP if RCCL reports an asynchronous error on the communicator */
+int fedagg_comm_async_error(fedagg_comm* comm);
+const char* fedagg_comm_last_error(void);
+/* Enqueue the whole schedule (asynchronous on `stream` and the communicator's stream; the
+ * caller's stream waits for everything at the end).  ws / ws_count / ws_kind: the numel == 1
+ * product workspace, reduced in place onto `root` (NULL / 0: none). */
+int fedagg_lockstep_execute(fedagg_comm* comm, const fedagg_lockstep_run* runs, int nruns,
+                            const fedagg_lockstep_msg* msgs, int nmsgs, int ngroups, void* ws, uint64_t ws_count,
+                            int ws_kind, int root, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Client-side flat-bucket ops (the producer / consumer of the buckets, SURVEY.md §8(a)

@@ -91,6 +91,15 @@ SIGNATURES = {
                                              c_void, c_void]),
     "fedagg_scaffold_finish_f32": (c_int, [c_void, c_int, c_void, P(c_u64), c_int, c_dbl, c_void, c_void, c_void]),
     "fedagg_scaffold_finish_f64": (c_int, [c_void, c_int, c_void, P(c_u64), c_int, c_dbl, c_void, c_void, c_void]),
+    # native lockstep executor over RCCL (csrc/lockstep.hip)
+    "fedagg_comm_unique_id": (c_int, [ctypes.c_char_p, c_void]),
+    "fedagg_comm_create": (c_int, [ctypes.c_char_p, c_int, c_int, c_void, c_int, P(c_void)]),
+    "fedagg_comm_destroy": (c_int, [c_void]),
+    "fedagg_comm_abort": (c_int, [c_void]),
+    "fedagg_comm_async_error": (c_int, [c_void]),
+    "fedagg_comm_last_error": (ctypes.c_char_p, []),
+    "fedagg_lockstep_execute": (c_int, [c_void, c_void, c_int, c_void, c_int, c_int, c_void, c_u64, c_int, c_int,
+                                        c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),
@@ -114,7 +123,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
@@ -128,6 +137,8 @@ FEDAGG_SESSION_EVENTS = 8
 FEDAGG_F16 = 0  # kinds (include/fedagg.h enum)
 FEDAGG_F32 = 1
 FEDAGG_F64 = 2
+FEDAGG_BF16 = 12
+FEDAGG_RUN_FEDAVG, FEDAGG_RUN_FEDAVG_TILED, FEDAGG_RUN_SCAFFOLD = 0, 1, 2
 
 
 class NativeLibraryError(RuntimeError):

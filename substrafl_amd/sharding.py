@@ -659,29 +659,36 @@ def lockstep_fedavg(plan: lockstep.RankPlan, blocks: Dict[int, FedAvgShard], out
     sh0 = next(iter(blocks.values()))
     kind, K = sh0.kind, sh0.K
     acc = _slots(torch, plan, out, 1, slots)[0]
-
-    def region(loc, n):
-        where, slot, off = loc
-        return [(out if where == "out" else acc[slot])[off: off + n]]
-
-    def launch(r):
-        sh = blocks[r.block]
-        ops.fedavg_run(kind, sh.rows[:, r.col: r.col + r.n], sh.w, r.seed, region(r.acc, r.n)[0])
-
-    lockstep.run(plan, transport, region, launch)
     pw = np.asarray(pairwise_idx, np.int64)
     if pw.size:
         if ws is None:
             ws = torch.zeros((pw.size, K), dtype=ws_dtype(torch, kind), device=out.device)
         else:
             ws.zero_()
+    native = getattr(transport, "native", False) and all(b.Kr for b in blocks.values())
+    if native:  # rccl.RcclTransport: the whole schedule issued from C++ (csrc/lockstep.hip)
+        prog = transport.program(plan=plan, blocks=blocks, accs=[acc], outs=[out], kind=kind, scaffold=False)
+        for b, p0, p1, cols in lockstep.pairwise_segments(plan, pw):  # before the schedule, same stream
+            sh = blocks[b]
+            ops.fedavg_products_at(kind, sh.rows, sh.w, sh.kbase, K, cols, ws[p0:p1])
+        transport.execute(prog, _stream(), ws=ws if pw.size else None, ws_kind="f64" if kind == "f64" else "f32")
+    else:
+        def region(loc, n):
+            where, slot, off = loc
+            return [(out if where == "out" else acc[slot])[off: off + n]]
+
+        def launch(r):
+            sh = blocks[r.block]
+            ops.fedavg_run(kind, sh.rows[:, r.col: r.col + r.n], sh.w, r.seed, region(r.acc, r.n)[0])
+
+        lockstep.run(plan, transport, region, launch)
         for b, p0, p1, cols in lockstep.pairwise_segments(plan, pw):
             sh = blocks[b]
             ops.fedavg_products_at(kind, sh.rows, sh.w, sh.kbase, K, cols, ws[p0:p1])
-        if plan.world > 1:
+        if pw.size and plan.world > 1:
             transport.reduce_sum(ws, plan.root)  # columns of other blocks are zeros: the sum is exact
-        if plan.rank == plan.root:
-            ops.fedavg_finish(kind, ws, K, pw.astype(np.uint64), out)
+    if pw.size and plan.rank == plan.root:
+        ops.fedavg_finish(kind, ws, K, pw.astype(np.uint64), out)
     return plan.rank == plan.root
 
 
@@ -697,20 +704,6 @@ def lockstep_scaffold(plan: lockstep.RankPlan, blocks: Dict[int, ScaffoldShard],
     sh0 = next(iter(blocks.values()))
     kind, K = sh0.kind, sh0.K
     acc = _slots(torch, plan, dout, 2, slots)
-
-    def region(loc, n):
-        where, slot, off = loc
-        if where == "out":
-            return [dout[off: off + n], cout[off: off + n]]
-        return [acc[0, slot, off: off + n], acc[1, slot, off: off + n]]
-
-    def launch(r):
-        sh = blocks[r.block]
-        d, cc = region(r.acc, r.n)
-        ops.scaffold_run(kind, sh.delta[:, r.col: r.col + r.n], sh.cv[:, r.col: r.col + r.n], sh.w, r.seed, r.final,
-                         c[r.lo: r.lo + r.n] if r.final else None, lr, d, cc)
-
-    lockstep.run(plan, transport, region, launch)
     pw = np.asarray(pairwise_idx, np.int64)
     P = int(pw.size)
     if P:
@@ -719,6 +712,8 @@ def lockstep_scaffold(plan: lockstep.RankPlan, blocks: Dict[int, ScaffoldShard],
             ws = torch.zeros(n, dtype=torch.float64, device=dout.device)
         else:
             ws.zero_()
+
+    def products():
         wd, wc = ws[: P * K].view(P, K), ws[P * K:].view(P, K + 1)
         for b, p0, p1, cols in lockstep.pairwise_segments(plan, pw):
             sh = blocks[b]
@@ -728,8 +723,33 @@ def lockstep_scaffold(plan: lockstep.RankPlan, blocks: Dict[int, ScaffoldShard],
             ops.scaffold_products_at(kind, sh.delta, sh.cv, sh.w, sh.kbase, K, cols, tmp)
             wd[p0:p1] += tmp[: (p1 - p0) * K].view(p1 - p0, K)
             wc[p0:p1] += tmp[(p1 - p0) * K:].view(p1 - p0, K + 1)
-        if plan.world > 1:
-            transport.reduce_sum(ws, plan.root)
+
+    native = getattr(transport, "native", False) and all(b.Kr for b in blocks.values())
+    if native:  # rccl.RcclTransport: the whole schedule issued from C++ (csrc/lockstep.hip)
+        prog = transport.program(plan=plan, blocks=blocks, accs=[acc[0], acc[1]], outs=[dout, cout], kind=kind,
+                                 scaffold=True, c=c, lr=lr)
+        if P:
+            products()
+        transport.execute(prog, _stream(), ws=ws if P else None, ws_kind="f64")
+    else:
+        def region(loc, n):
+            where, slot, off = loc
+            if where == "out":
+                return [dout[off: off + n], cout[off: off + n]]
+            return [acc[0, slot, off: off + n], acc[1, slot, off: off + n]]
+
+        def launch(r):
+            sh = blocks[r.block]
+            d, cc = region(r.acc, r.n)
+            ops.scaffold_run(kind, sh.delta[:, r.col: r.col + r.n], sh.cv[:, r.col: r.col + r.n], sh.w, r.seed,
+                             r.final, c[r.lo: r.lo + r.n] if r.final else None, lr, d, cc)
+
+        lockstep.run(plan, transport, region, launch)
+        if P:
+            products()
+            if plan.world > 1:
+                transport.reduce_sum(ws, plan.root)
+    if P:
         if plan.rank == plan.root:
             glob = ScaffoldShard(kind, None, None, c, np.zeros(0), 0, K, int(dout.shape[0]), lr, pw.astype(np.uint64))
             ops.scaffold_finish(glob, ws, dout, cout)

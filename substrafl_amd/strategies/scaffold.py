@@ -11,6 +11,8 @@ engine's ``c_check="device"`` keeps the GPU ``equal_count`` kernel as an option)
 
 from typing import List, Optional
 
+import numpy as np
+
 from ..engine import Devices, engine_for
 from ..remote import remote
 from ..schemas import ScaffoldAveragedStates, ScaffoldSharedState, StrategyName
@@ -61,10 +63,27 @@ class Scaffold(Strategy):
                 first.server_control_variate
             ), "the length of server_control_variate should be the same for each shared_state"
             for c, ci in zip(first.server_control_variate, shared_state.server_control_variate):
-                assert c.shape == ci.shape, "all server_control_variate in the shared_states are not equal"
+                if np.shape(c) == np.shape(ci):
+                    continue  # the element-wise comparison runs in the engine while c is staged
+                # np.testing.assert_array_equal (scaffold.py:193-196) broadcasts a 0-d operand against
+                # the other one and refuses any other shape mismatch
+                assert np.ndim(c) == 0 or np.ndim(ci) == 0, "all server_control_variate in the shared_states are not equal"
+                assert _all_equal(c, ci), "all server_control_variate in the shared_states are not equal"
         assert (
             len(first.control_variate_update) == len(first.server_control_variate) == len(first.parameters_update)
         ), "the length of server_control_variate, parameters_update and server_control_variate should be the same"
+
+    @staticmethod
+    def _server_control_variates(shared_states) -> List[list]:
+        """Every client's c for the engine's element-wise check; a client whose layers differ in
+        shape from client 0's (a 0-d layer, already compared value by value on the host) passes
+        client 0's arrays instead."""
+        c0 = list(shared_states[0].server_control_variate)
+        out = []
+        for s in shared_states:
+            ci = list(s.server_control_variate)
+            out.append(ci if all(np.shape(a) == np.shape(b) for a, b in zip(c0, ci)) else c0)
+        return out
 
     @remote
     def avg_shared_states(self, shared_states: List[ScaffoldSharedState]) -> ScaffoldAveragedStates:
@@ -77,8 +96,17 @@ class Scaffold(Strategy):
         check_same_shapes([*cvs, c0])  # np.sum([w*cv_k ..., c]) (scaffold.py:263)
         check_same_shapes(pus)  # np.sum([w*Δ_k ...]) (scaffold.py:293)
         mismatches, new_c, avg = self._engine().scaffold(
-            pus, cvs, [list(s.server_control_variate) for s in shared_states],
+            pus, cvs, self._server_control_variates(shared_states),
             [s.n_samples for s in shared_states], self._aggregation_lr, wire=True,
         )
         assert mismatches == 0, "all server_control_variate in the shared_states are not equal"
         return ScaffoldAveragedStates(server_control_variate=new_c, avg_parameters_update=avg)
+
+
+def _all_equal(a, b) -> bool:
+    """Value equality as np.testing.assert_array_equal has it (NaN == NaN, +0 == -0), broadcast."""
+    a, b = np.asarray(a), np.asarray(b)
+    eq = np.asarray(a == b)
+    if a.dtype.kind in "fc" and b.dtype.kind in "fc":
+        eq = eq | (np.isnan(a) & np.isnan(b))
+    return bool(np.all(eq))

@@ -431,3 +431,143 @@ def test_tiled_client_blocks_bit_exact(G, K, kind, tv, relay):
     got, ref = _striped(G, K, kind=kind, shapes=shapes, tv=tv, relay=relay, rounds=(0.75, 0.25))
     for g, r in zip(got, ref):
         assert g.dtype == r.dtype and np.array_equal(g.view(np.uint32), r.view(np.uint32))
+
+
+# ---- the native lockstep executor (csrc/lockstep.hip) over a real RCCL communicator ----
+def _native_world1(q, port):
+    import torch
+    import torch.distributed as dist
+
+    from substrafl_amd import lockstep
+    from substrafl_amd.engine import fedavg_weights, scaffold_weights
+    from substrafl_amd.layout import BucketLayout
+    from substrafl_amd.rccl import RcclTransport
+    from substrafl_amd.sharding import (FedAvgShard, GpuShardOps, LoopbackGroup, ScaffoldShard, TiledBlock,
+                                        lockstep_fedavg, lockstep_scaffold, out_dtype, striped_plan)
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    out = {}
+    try:
+        tr = RcclTransport()
+        shapes = [(37, 29), (1,), (40000,), (1, 1), (5000,)]
+        # (1) every run kind through the native executor: one rank, the schedule's runs, the
+        #     numel == 1 workspace reduce; against the Python executor and the oracle
+        for kind, tv in (("f32", 0), ("f32", 8192), ("bf16", 4096), ("f64", 0), ("f16", 0)):
+            npdt = {"f32": np.float32, "bf16": np.float32, "f64": np.float64, "f16": np.float16}[kind]
+            K = 33
+            pus, ns = _data(K, seed=7, shapes=shapes)
+            pus = [[a.astype(npdt) for a in c] for c in pus]
+            if kind == "bf16":
+                pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
+            layout = BucketLayout(range(len(shapes)), shapes, npdt)
+            plan = striped_plan(layout.M, 1, 0)
+            rows = _rows(torch, pus, layout, dtype=npdt, tdtype=torch.bfloat16 if kind == "bf16" else None)
+            segs = plan.blocks[0]
+            packed = torch.zeros((K, plan.block_len[0]), dtype=rows.dtype, device="cuda")
+            for lo, hi, col in segs:
+                packed[:, col: col + hi - lo] = rows[:, lo:hi]
+            data = TiledBlock.from_rows(torch, kind, packed, tv, TiledBlock.run_extents(plan, 0)) if tv else packed
+            blocks = {0: FedAvgShard(kind, data, fedavg_weights(ns, kind), 0, K, plan.block_len[0],
+                                     np.zeros(0, np.uint64))}
+            res = []
+            for t in (tr, LoopbackGroup(1).transport(0)):
+                o = torch.zeros(layout.ld, dtype=out_dtype(torch, kind), device="cuda")
+                lockstep_fedavg(plan, blocks, o, t, GpuShardOps(), layout.pairwise_idx)
+                torch.cuda.synchronize()
+                res.append(o[: layout.M].cpu().numpy().copy())
+            out[f"fedavg_{kind}_{tv}"] = (res[0], res[1], pus, ns, shapes, npdt)
+        # Scaffold, fp32 and fp64 buckets
+        for kind in ("f32", "f64"):
+            npdt = np.float32 if kind == "f32" else np.float64
+            K = 9
+            pus, ns = _data(K, seed=8, shapes=shapes)
+            pus = [[a.astype(npdt) for a in c] for c in pus]
+            rng = np.random.default_rng(3)
+            cvs = [[rng.standard_normal(a.shape).astype(npdt) for a in c] for c in pus]
+            c = [rng.standard_normal(a.shape).astype(npdt) for a in pus[0]]
+            layout = BucketLayout(range(len(shapes)), shapes, npdt)
+            plan = striped_plan(layout.M, 1, 0)
+
+            def packed(lists):
+                r = _rows(torch, lists, layout, dtype=npdt)
+                t = torch.zeros((len(lists), plan.block_len[0]), dtype=r.dtype, device="cuda")
+                for lo, hi, col in plan.blocks[0]:
+                    t[:, col: col + hi - lo] = r[:, lo:hi]
+                return t
+
+            blocks = {0: ScaffoldShard(kind, packed(pus), packed(cvs), None, scaffold_weights(ns), 0, K,
+                                       plan.block_len[0], 0.6, np.zeros(0, np.uint64))}
+            ct = _rows(torch, [c], layout, dtype=npdt)[0]
+            res = []
+            for t in (tr, LoopbackGroup(1).transport(0)):
+                d = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+                cc = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
+                lockstep_scaffold(plan, blocks, d, cc, t, GpuShardOps(), layout.pairwise_idx, ct, 0.6)
+                torch.cuda.synchronize()
+                res.append((d[: layout.M].cpu().numpy().copy(), cc[: layout.M].cpu().numpy().copy()))
+            out[f"scaffold_{kind}"] = (res[0], res[1], pus, cvs, c, ns, shapes, npdt)
+        # (2) the exchange path: a hand-built schedule whose relay hop goes to the rank itself
+        #     (send + receive in one RCCL group): block 0 at step 0 into a slot, group 1 moves it
+        #     into the output, block 1 continues it at step 2 -- the full client sum, in order
+        K0, K1 = 5, 6
+        pus, ns = _data(K0 + K1, seed=9, shapes=shapes)
+        layout = BucketLayout(range(len(shapes)), shapes, np.float32)
+        n = layout.M
+        plan = lockstep.RankPlan(
+            rank=0, world=1, root=0,
+            runs=[[lockstep.Run(0, 0, n, 0, ("slot", 0, 0), True, False)], [],
+                  [lockstep.Run(1, 0, n, 0, ("out", 0, 0), False, True)]],
+            groups=[[], [lockstep.Op("recv", 0, ("out", 0, 0), n, 0), lockstep.Op("send", 0, ("slot", 0, 0), n, 0)],
+                    [], []],
+            blocks={0: [(0, n, 0)], 1: [(0, n, 0)]}, block_len={0: n, 1: n}, slot_elems=n)
+        w = fedavg_weights(ns, "f32")
+        rows = _rows(torch, pus, layout)
+        blocks = {0: FedAvgShard("f32", rows[:K0], w[:K0], 0, K0 + K1, n, np.zeros(0, np.uint64)),
+                  1: FedAvgShard("f32", rows[K0:], w[K0:], K0, K0 + K1, n, np.zeros(0, np.uint64))}
+        res = []
+        for t in (tr, LoopbackGroup(1).transport(0)):
+            o = torch.zeros(layout.ld, dtype=torch.float32, device="cuda")
+            lockstep_fedavg(plan, blocks, o, t, GpuShardOps(), layout.pairwise_idx)
+            torch.cuda.synchronize()
+            res.append(o[:n].cpu().numpy().copy())
+        out["self_exchange"] = (res[0], res[1], pus, ns, shapes, np.float32)
+        tr.close()
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_lockstep_executor_world1():
+    """csrc/lockstep.hip over a one-rank RCCL communicator: every run kind (fp32 rows and tiles,
+    bf16 tiles, fp64, fp16, Scaffold fp32 / fp64) and the numel == 1 workspace reduce, and a
+    schedule whose exchange group sends to and receives from the rank itself -- bit-identical to
+    the Python executor and to the reference."""
+    import torch.multiprocessing as mp
+
+    from substrafl_amd.layout import BucketLayout
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_world1, args=(q, _free_port()))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    bits = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+    for key, val in out.items():
+        if key.startswith("scaffold"):
+            (nd, nc), (pd, pc), pus, cvs, c, ns, shapes, npdt = val
+            assert np.array_equal(nd.view(np.uint64), pd.view(np.uint64)), key
+            assert np.array_equal(nc.view(np.uint64), pc.view(np.uint64)), key
+            lay = BucketLayout(range(len(shapes)), shapes, np.float64)
+            rc, ra = scaffold_reference_structure(pus, cvs, c, ns, 0.6)
+            for g, r in zip([a for _, a in lay.unpack(nc)] + [a for _, a in lay.unpack(nd)], rc + ra):
+                assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), key
+            continue
+        nat, py, pus, ns, shapes, npdt = val
+        assert np.array_equal(nat.view(bits[nat.itemsize]), py.view(bits[py.itemsize])), key
+        lay = BucketLayout(range(len(shapes)), shapes, npdt)
+        for g, r in zip([a for _, a in lay.unpack(nat)], fedavg_reference_structure(pus, ns)):
+            assert g.dtype == r.dtype and np.array_equal(g.view(bits[g.itemsize]), r.view(bits[r.itemsize])), key

@@ -466,6 +466,53 @@ def test_baseline_config_sizes_vs_torch_sequential(torch_gpu, K, M, kind):
     assert same
 
 
+@pytest.mark.parametrize("K, M, kind", [(64, 125_000_000, "f32"), (128, 350_000_000, "bf16")])
+def test_baseline_config_sizes_tiled_as_timed(torch_gpu, K, M, kind):
+    """The headline kernels exactly as bench.py times them: C3 (64 x 125M fp32) and C5 (128 x 350M
+    bf16) on tile-interleaved buckets (TiledFedAvgPlan with the library's tile -- 8192 / 4096
+    vectors -- and the fused numel == 1 patch), checked on EVERY element: bit-exact against torch
+    eager ops applied client by client in list order, the numel == 1 elements against NumPy's
+    pairwise sum (fed_avg.py:217-222)."""
+    torch = torch_gpu
+    from substrafl_amd.engine import TiledFedAvgPlan, fedavg_weights, tiled_client_view, tiled_elems, tiled_tile
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+
+    shapes = synthetic_state_dict_shapes(M)
+    lay = BucketLayout(range(len(shapes)), shapes, np.float32)
+    tv = tiled_tile(kind, K, M)
+    assert tv == (8192 if kind == "f32" else 4096)  # the recommended layout of the headline line
+    dt = torch.bfloat16 if kind == "bf16" else torch.float32
+    buf = torch.zeros(tiled_elems(kind, K, M, tv), device="cuda", dtype=dt)
+    g = torch.Generator(device="cuda").manual_seed(13)
+    for k in range(K):
+        view = tiled_client_view(buf, kind, K, k, tv)
+        row = torch.zeros(view.numel(), device="cuda")
+        row[:M].normal_(generator=g)
+        view.copy_(row.view(view.shape))
+        del row
+    ns = [int(v) for v in np.random.default_rng(17).integers(100, 10000, K)]
+    w = fedavg_weights(ns, kind)
+    out = torch.empty(lay.ld, device="cuda")
+    TiledFedAvgPlan(kind, buf, K, w, M, out, lay.pairwise_idx, tv=tv).launch()
+    acc = torch.zeros(M, device="cuda")
+    pw = lay.pairwise_idx.astype(np.int64)
+    prods = np.zeros((pw.size, K), np.float32)
+    for k in range(K):
+        xk = tiled_client_view(buf, kind, K, k, tv).reshape(-1)[:M].float()
+        acc = acc + xk * torch.tensor(w[k], device="cuda")
+        prods[:, k] = (xk[torch.from_numpy(pw).cuda()].cpu().numpy() * w[k]).astype(np.float32)
+        del xk
+    torch.cuda.synchronize()
+    mask = torch.ones(M, dtype=torch.bool, device="cuda")
+    mask[torch.from_numpy(pw).cuda()] = False
+    same = torch.equal(out[:M][mask].view(torch.int32), acc[mask].view(torch.int32))
+    for i, p in enumerate(pw):
+        same = same and _bits(np.float32(0.0) + numpy_pairwise_sum(prods[i])) == _bits(out[p].cpu().numpy())
+    del buf, acc, mask, out
+    torch.cuda.empty_cache()
+    assert same
+
+
 @pytest.mark.parametrize("K, M", [(16, 25_000_000), (16, 5_000_011), (3, 2_000_000)])
 def test_scaffold_full_size_vs_torch_fp64(torch_gpu, K, M):
     """Scaffold at size: bit-exact against torch fp64 eager ops (w*x, +, c last, lr*) on the device."""
@@ -1378,3 +1425,33 @@ def test_session_staging_knobs_round_trip(torch_gpu, copy_streams, chunk):
             assert np.array_equal(got2[k * (hi - lo): (k + 1) * (hi - lo)], np.concatenate(rows[k])[lo:hi])
     finally:
         s.close()
+
+
+def test_scaffold_0d_server_control_variate(torch_gpu, dummy_algo_class):
+    """A client whose server control variate layer is 0-d and equal to every element of client 0's
+    layer passes the reference's np.testing.assert_array_equal (scaffold.py:193-196); the average
+    (which adds client 0's c, scaffold.py:262-263) is bit-exact; an unequal 0-d value is refused."""
+    from substrafl_amd.schemas import ScaffoldSharedState
+    from substrafl_amd.strategies import Scaffold
+
+    rng = np.random.default_rng(77)
+    shapes = [(40, 3), (7,), (1,)]
+    K = 4
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    cvs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    c0 = [np.full((40, 3), 0.375, np.float32), rng.standard_normal(7).astype(np.float32), np.ones(1, np.float32)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+
+    def states(c2):
+        cs = [c0, [a.copy() for a in c0], c2, [a.copy() for a in c0]]
+        return [ScaffoldSharedState(parameters_update=pus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                    server_control_variate=cs[k]) for k in range(K)]
+
+    good = [np.array(0.375, np.float32), c0[1].copy(), c0[2].copy()]
+    res = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.8).avg_shared_states(states(good), _skip=True)
+    rc, ra = scaffold_reference_structure(pus, cvs, c0, ns, 0.8)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)
+    bad = [np.array(0.5, np.float32), c0[1].copy(), c0[2].copy()]
+    with pytest.raises(AssertionError, match="server_control_variate"):
+        Scaffold(algo=dummy_algo_class(), aggregation_lr=0.8).avg_shared_states(states(bad), _skip=True)

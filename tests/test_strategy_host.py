@@ -140,3 +140,52 @@ def test_ingest_raises_first_failing_path_in_order(tmp_path):
         AggregationEngine(0).ingest(paths, "fedavg", load)
     good = AggregationEngine(0).ingest(paths[:2], "fedavg", load)  # no GPU here: loads, stages nothing
     assert [g["k"] for g in good] == [0, 1]
+
+
+def _reference_check_passes(c0, ci) -> bool:
+    """The reference's own check (scaffold.py:193-196): np.testing.assert_array_equal per layer."""
+    try:
+        for a, b in zip(c0, ci):
+            np.testing.assert_array_equal(a, b)
+        return True
+    except AssertionError:
+        return False
+
+
+@pytest.mark.parametrize("ci_layer, expect", [
+    (np.array(2.5, np.float32), True),  # 0-d, equal to every element: the reference accepts
+    (np.array(2.0, np.float32), False),  # 0-d, different value
+    (np.full((2, 3), 2.5, np.float32), True),
+    (np.full((3, 2), 2.5, np.float32), False),  # same size, another shape: refused
+    (np.full((1, 3), 2.5, np.float32), False),  # broadcastable but not 0-d: refused
+])
+def test_scaffold_c_check_matches_assert_array_equal(dummy_algo_class, ci_layer, expect):
+    """The host half of Scaffold's c check accepts and refuses exactly what the reference's
+    np.testing.assert_array_equal does, including a 0-d layer equal to every element of client
+    0's layer (the element-wise equal-shape case is the engine's, checked on the GPU)."""
+    c0 = [np.full((2, 3), 2.5, np.float32), np.ones(4, np.float32)]
+    ci = [ci_layer, np.ones(4, np.float32)]
+    pu = [np.zeros((2, 3), np.float32), np.zeros(4, np.float32)]
+    states = [ScaffoldSharedState(parameters_update=pu, control_variate_update=pu, n_samples=3,
+                                  server_control_variate=c)
+              for c in (c0, [a.copy() for a in c0], ci)]
+    assert _reference_check_passes(c0, ci) == expect
+    s = Scaffold(algo=dummy_algo_class())
+    if expect:
+        s._check_shared_states(states)
+        sc = s._server_control_variates(states)  # what the engine compares element-wise
+        assert all(np.shape(a) == np.shape(b) for row in sc for a, b in zip(row, c0))
+    else:
+        with pytest.raises(AssertionError, match="server_control_variate"):
+            s._check_shared_states(states)
+
+
+def test_scaffold_c_check_nan_in_0d_layer(dummy_algo_class):
+    """assert_array_equal treats NaN == NaN: a 0-d NaN against an all-NaN layer passes."""
+    c0 = [np.full(3, np.nan, np.float32)]
+    ci = [np.array(np.nan, np.float32)]
+    assert _reference_check_passes(c0, ci)
+    z = [np.zeros(3, np.float32)]
+    states = [ScaffoldSharedState(parameters_update=z, control_variate_update=z, n_samples=1, server_control_variate=c)
+              for c in (c0, ci)]
+    Scaffold(algo=dummy_algo_class())._check_shared_states(states)

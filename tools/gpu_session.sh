@@ -1,4 +1,7 @@
+#!/bin/bash
+# One GPU session of round 3 (run by gpurun from the repo root): tests, then profiling of this build.
 export TMPDIR=/tmp
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r03c_gpu_tests.log 2>&1; echo tests_rc=$? >> gpurun_out/r03c_gpu_tests.log
-FEDAGG_LIB=$PWD/substrafl_amd/libfedagg_tuning.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "variants or auto_shape or one_bucket" > gpurun_out/r03c_tuning_tests.log 2>&1; echo tests_rc=$? >> gpurun_out/r03c_tuning_tests.log
-timeout -k 10 200 python -u tools/chunk_probe.py > gpurun_out/r03c_chunk_probe.log 2>&1 && timeout -k 10 200 python -u bench.py > gpurun_out/r03c_bench_default.json 2> gpurun_out/r03c_bench_default.err && timeout -k 10 200 python -u bench.py --mode client-shard --no-cpu-baseline > gpurun_out/r03c_bench_cs1.json 2> gpurun_out/r03c_bench_cs1.err
+TAG=${1:-r03}
+timeout -k 10 300 python -u -m pytest tests/test_client_shard_gpu.py -x -v --timeout 200 --timeout-method thread -k "native or tiled_client or host_entry" > gpurun_out/${TAG}_native_tests.log 2>&1 || exit 1
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || exit 1
+timeout -k 10 900 bash tools/profile_round.sh ${TAG} c3 c2 c4 c5 > gpurun_out/${TAG}_profile.log 2>&1

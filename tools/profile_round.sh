@@ -2,7 +2,9 @@
 # One profiling session per workload, on the GPU box (DESIGN.md §5 evidence):
 #   1. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) -> HBM bytes per launch (tools/pmc_traffic.py);
 #   2. the bench line itself, whose roofline.traffic is that file (same build, same session);
-#   3. rocprofv3 --kernel-trace --stats of the same bench command (kernel average duration).
+#   3. rocprofv3 --kernel-trace --stats of the same bench command (kernel average duration);
+#   4. tools/roofline_check.py: the plain line's HIP-event kernel time, the profiled line's (the
+#      process rocprof traced) and rocprof's average / min side by side, with the fraction each gives.
 # Usage: tools/profile_round.sh TAG WORKLOAD [WORKLOAD ...]   (outputs under gpurun_out/TAG_*)
 set -euo pipefail
 TAG=$1; shift
@@ -43,5 +45,9 @@ print(_native.load().fedagg_scaffold_launches(16, 4, 25000000, 1))") ;;
     --traffic "$OUT/${TAG}_traffic_${WL}.json" > "$OUT/${TAG}_profiled_bench_${WL}.json"
   STATS=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_stats.csv' | head -1)
   cp "$STATS" "$OUT/${TAG}_${WL}_kernel_stats.csv"
+  KPFX=$([ "$KERN" = scaffold ] && echo scaffold || echo fedavg_kernel)
+  python3 "$ROOT/tools/roofline_check.py" --bench "$OUT/${TAG}_bench_${WL}.json" \
+    --profiled "$OUT/${TAG}_profiled_bench_${WL}.json" --stats "$OUT/${TAG}_${WL}_kernel_stats.csv" \
+    --kernel "$KPFX" --group $GROUP --out "$OUT/${TAG}_${WL}_roofline_check.json" > /dev/null
 done
 echo "[$TAG] done" >&2
