@@ -136,8 +136,9 @@ def striped_pieces(M: int, G: int, rings: Optional[int] = None,
 @dataclass
 class Run:
     """One launch: ``n`` elements of ``block`` starting at column ``col`` of this rank's buffer
-    for that block, accumulator at ``acc`` = ("slot", slot, offset) or ("out", 0, global lo);
-    ``lo``: global first element (the run is globally contiguous when ``final``)."""
+    for that block, accumulator at ``acc`` = ("slot", slot, offset) or ("out", 0, global lo) --
+    every final run accumulates in the rank's output buffer; ``lo``: global first element (the run
+    is globally contiguous when ``final``)."""
 
     block: int
     col: int
@@ -190,24 +191,36 @@ def _table(pieces: Sequence[Piece], G: int):
     return tab
 
 
-def rank_plan(pieces: Sequence[Piece], G: int, rank: int, root: int = 0, cols: str = "packed") -> RankPlan:
+def rank_plan(pieces: Sequence[Piece], G: int, rank: int, root: int = 0, cols: str = "packed",
+              gather_spread: int = 0) -> RankPlan:
     """This rank's runs and exchange groups.  ``cols="packed"``: the pieces a rank holds for a
     block lie back to back in its buffer for that block (in step order); ``"global"``: column =
-    global element index (one block holding every element, the plain relay)."""
+    global element index (one block holding every element, the plain relay).
+
+    A piece's LAST block accumulates straight into the output buffer of the rank running it (the
+    root's is the result; another rank's holds its stripes' finished elements until they are
+    sent).  A finished piece off the root goes to the root in ``gather_spread`` parts over the
+    exchange groups that follow (0: 2 G groups -- a round's worth -- so round k's results travel
+    under round k + 1's kernels instead of in one burst; the schedule's last groups take what is
+    left)."""
     tab = _table(pieces, G)
     n_steps = 1 + max((p.t0 + 2 * (G - 1) for p in pieces), default=-1)
+    spread = int(gather_spread) if gather_spread > 0 else 2 * G
+
+    def is_final(t: int, i: int) -> bool:
+        return t == pieces[i].t0 + 2 * (G - 1)
 
     def acc_loc(r: int, t: int, i: int) -> Tuple[str, int, int]:
         """Where rank r keeps piece i's accumulator at step t."""
         p = pieces[i]
-        if r == root and t == p.t0 + 2 * (G - 1):
+        if is_final(t, i):
             return ("out", 0, p.lo)
         off = 0
         for j, _b in tab[(r, t)]:
             q = pieces[j]
             if j == i:
                 return ("slot", t % SLOTS, off)
-            if not (r == root and t == q.t0 + 2 * (G - 1)):
+            if not is_final(t, j):
                 off += _align_up(q.hi - q.lo, COL_ALIGN)
         raise AssertionError("piece not at (rank, step)")
 
@@ -257,8 +270,12 @@ def rank_plan(pieces: Sequence[Piece], G: int, rank: int, root: int = 0, cols: s
             if b < G - 1:
                 r = p.ranks[b + 1]
                 msgs.setdefault((t + 1, q, r), []).append((p.lo, acc_loc(q, t, i), acc_loc(r, t + 2, i), n))
-            elif q != root:  # the stripe's final chunk goes to the root's output
-                msgs.setdefault((t + 1, q, root), []).append((p.lo, acc_loc(q, t, i), ("out", 0, p.lo), n))
+            elif q != root:  # the finished piece goes to the root's output, in parts over the next groups
+                D = max(1, min(spread, n_steps - t))
+                part = _align_up(-(-n // D), COL_ALIGN)
+                for d, a in enumerate(range(p.lo, p.hi, part)):
+                    e = min(p.hi, a + part)
+                    msgs.setdefault((t + 1 + d, q, root), []).append((a, ("out", 0, a), ("out", 0, a), e - a))
     groups: List[List[Op]] = [[] for _ in range(n_steps + 1)]
     n_msgs = 0
     for (g, q, r), lst in sorted(msgs.items()):

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--clients", type=int, default=64)
     ap.add_argument("--sizes", default="2e6,3.90625e6,7.8125e6,15.625e6,31.25e6,62.5e6,125e6")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--knobs", default="", help="tuning build only: rows under each knob set, "
+                    "e.g. 'vpt=4,unroll=4;vpt=2,unroll=8' (FEDAGG_LIB=substrafl_amd/libfedagg_tuning.so)")
+    ap.add_argument("--no-tiled", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -64,7 +67,15 @@ def main():
         r = rows[:, :n]
         ms = timeit(lambda: ops.fedavg_run("f32", r, w, False, acc[:n]))
         line["rows_ms"], line["rows_TBps"] = round(ms, 4), round(nbytes / ms / 1e9, 3)
-        for tv in (2048, 8192):
+        for ks in [k for k in args.knobs.split(";") if k]:
+            from substrafl_amd import _native
+
+            kv = {a: int(b) for a, b in (x.split("=") for x in ks.split(","))}
+            _native.tune(**kv)
+            ms = timeit(lambda: ops.fedavg_run("f32", r, w, False, acc[:n]))
+            _native.tune(vpt=0, unroll=8)
+            line[f"rows[{ks}]_TBps"] = round(nbytes / ms / 1e9, 3)
+        for tv in (() if args.no_tiled else (2048, 8192)):
             buf = torch.empty(tiled_elems("f32", K, n, tv), dtype=torch.float32, device=dev).normal_()
             view = TiledView("f32", buf, K, n, tv)
             ms = timeit(lambda: ops.fedavg_run("f32", view, w, False, acc[:n]))

@@ -38,9 +38,32 @@ class Deadlock(RuntimeError):
     pass
 
 
+# chain-kernel rate (TB/s of client reads) against run length at 64 clients, fp32 rows: tools/chunk_probe.py
+# on MI355X (profiles/r03_chunk_probe.log): short runs lose to launch and tail effects
+RATE_CURVE = ((2.0e6, 5.56), (3.9e6, 6.92), (7.8e6, 6.94), (15.6e6, 6.86), (31.2e6, 6.73), (62.5e6, 6.93),
+              (125e6, 6.89))
+
+
+def rate_tbps(n: float, curve=RATE_CURVE) -> float:
+    """Piecewise-linear in log(n); below the first point the rate falls in proportion to n (a
+    fixed per-launch cost)."""
+    import math
+
+    if n <= curve[0][0]:
+        return curve[0][1] * (n / curve[0][0]) ** 0.5
+    for (n0, r0), (n1, r1) in zip(curve, curve[1:]):
+        if n <= n1:
+            f = (math.log(n) - math.log(n0)) / (math.log(n1) - math.log(n0))
+            return r0 + f * (r1 - r0)
+    return curve[-1][1]
+
+
 def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", compute_s_per_elem: float = 1.0,
-             link_s_per_elem: float = 0.0, latency_s: float = 0.0) -> Dict[str, float]:
-    """Play every rank's kernels; returns {"makespan", "compute_max"} or raises Deadlock."""
+             link_s_per_elem: float = 0.0, latency_s: float = 0.0, run_time=None) -> Dict[str, float]:
+    """Play every rank's kernels; returns {"makespan", "compute_max"} or raises Deadlock.
+    ``run_time(n)``: seconds of a step's launch over n elements (default n x compute_s_per_elem)."""
+    if run_time is None:
+        run_time = lambda n: n * compute_s_per_elem  # noqa: E731
     G = len(plans)
     kernels: List[List[dict]] = []
     for p in plans:
@@ -118,7 +141,7 @@ def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", comput
                         progress = True
                 if (r, i) in start and (r, i) not in end:
                     if k["kind"] == "run":
-                        end[(r, i)] = start[(r, i)] + k["n"] * compute_s_per_elem
+                        end[(r, i)] = start[(r, i)] + run_time(k["n"])
                         progress = True
                     else:
                         peers = links.get((r, i), [])
@@ -136,7 +159,7 @@ def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", comput
         raise Deadlock(f"{len(missing)} kernels never complete (first: rank {missing[0][0]}, "
                        f"{kernels[missing[0][0]][missing[0][1]]['kind']} of step "
                        f"{kernels[missing[0][0]][missing[0][1]]['t']})")
-    comp = max(sum(k["n"] for k in ks if k["kind"] == "run") for ks in kernels) * compute_s_per_elem
+    comp = max(sum(run_time(k["n"]) for k in ks if k["kind"] == "run") for ks in kernels)
     return {"makespan": max(end.values(), default=0.0), "compute_max": comp}
 
 
@@ -145,22 +168,26 @@ def main():
     ap.add_argument("--gpus", type=int, default=8)
     ap.add_argument("--clients-per-gpu", type=int, default=64)
     ap.add_argument("--params", type=int, default=125_000_000)
-    ap.add_argument("--hbm-GBps", type=float, default=7000.0, help="bucket kernel read rate")
+    ap.add_argument("--hbm-GBps", type=float, default=0.0,
+                    help="bucket kernel read rate (0: RATE_CURVE, the measured rate against run length)")
     ap.add_argument("--link-GBps", type=float, default=50.0, help="one xGMI link, one direction")
     ap.add_argument("--latency-us", type=float, default=20.0, help="per exchange group")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay chunk (elements)")
     args = ap.parse_args()
     G, Kb, M = args.gpus, args.clients_per_gpu, args.params
-    comp = Kb * 4 / (args.hbm_GBps * 1e9)  # s per element of one block (fp32 reads)
+    if args.hbm_GBps:
+        rt = lambda n: n * Kb * 4 / (args.hbm_GBps * 1e9)  # noqa: E731
+    else:
+        rt = lambda n: n * Kb * 4 / (rate_tbps(n) * 1e12)  # noqa: E731
     link = 4 / (args.link_GBps * 1e9)
     out = {}
     schedules = {"relay": lockstep.relay_pieces(M, G, args.chunk)}
-    for rounds in ((1.0,), (0.75, 0.25), (0.5, 0.3, 0.2)):
+    for rounds in ((1.0,), (0.75, 0.25), (0.5, 0.3, 0.2), (0.4, 0.3, 0.2, 0.1), (0.6, 0.25, 0.15)):
         schedules[f"striped rounds={rounds}"] = lockstep.striped_pieces(M, G, None, rounds)
     for name, pieces in schedules.items():
         plans = [lockstep.rank_plan(pieces, G, r, cols="global" if name == "relay" else "packed") for r in range(G)]
-        res = simulate(plans, "streams", comp, link, args.latency_us * 1e-6)
-        t1 = M * comp
+        res = simulate(plans, "streams", 0.0, link, args.latency_us * 1e-6, run_time=rt)
+        t1 = rt(M)
         out[name] = {"steps": plans[0].n_steps, "model_ms": round(res["makespan"] * 1e3, 3),
                      "single_gpu_ms": round(t1 * 1e3, 3), "weak_efficiency": round(t1 / res["makespan"], 3)}
     print(json.dumps({"gpus": G, "clients_per_gpu": Kb, "params": M, "hbm_GBps": args.hbm_GBps,
