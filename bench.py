@@ -74,7 +74,8 @@ def parse():
                          "same invocation (auto: when every rank has its own GPU)")
     ap.add_argument("--client-shard-steps", type=int, default=50, help="timed steps of the client-shard leg")
     ap.add_argument("--rings", type=int, default=0, help="striped: rings (hop lengths; 0 = up to 4)")
-    ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default one round)")
+    ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default: three "
+                    "rounds with the native executor, one with the Python one)")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
     ap.add_argument("--executor", default="native", choices=["native", "torch"],
                     help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip) or the "
@@ -790,8 +791,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
 def _rounds(args):
     from substrafl_amd import lockstep
 
-    if not args.rounds:
-        return lockstep.DEFAULT_ROUNDS
+    if not args.rounds:  # the schedule's default for the executor (lockstep.py)
+        return lockstep.NATIVE_ROUNDS if args.executor == "native" else lockstep.DEFAULT_ROUNDS
     return tuple(float(x) for x in args.rounds.split(","))
 
 

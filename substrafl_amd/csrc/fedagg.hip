@@ -1705,6 +1705,14 @@ inline Shape shape_for(int K, uint64_t nvec) {
   // group's loads are already in flight (software-pipelined tiles: 8 x 25M fp64 6.0 vs 5.1 TB/s,
   // 64 x 62.5M 6.1 vs 4.9; profiles/r01_tune2_f64_*.log)
   if constexpr (std::is_same<E, F64>::value) return Shape{4, 4, true, 0};
+  // many client streams over a SHORT bucket (the runs of the client-sharded schedules, relay
+  // chunks): a tile small enough for the grid to cover the CUs twice over -- 64 x 2M fp32: 7.10
+  // TB/s with 4 x 4 against 5.59 with 8 x 4 (244 workgroups); 64 x 1M: 6.80 with 2 x 8 against
+  // 3.29; 64 x 0.5M: 6.44 against 1.84 (profiles/r03e_small_runs_probe.log)
+  if constexpr (std::is_same<E, F32>::value || std::is_same<E, BF16>::value) {
+    if (K >= 32 && nvec < (uint64_t)384 * 1024) return Shape{2, 8, false, 0, false, blk};
+    if (K >= 32 && nvec < (uint64_t)768 * 1024) return Shape{4, 4, false, 0, false, blk};
+  }
   // many client streams over a large bucket: 16 KiB per wave per stream (fewer DRAM row
   // switches; 64 x 125M fp32 +2 %, 128 x 350M bf16 +1 %, 64 x 125M fp16 +1 %), as long as the
   // grid stays >> 256 CUs
@@ -1742,6 +1750,8 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
       else  // client pairs in 512-thread workgroups
         return launch_fedavg_variant<E, true, NTS, 16, 2, false, true, 1, false, 512>(FA_ARGS);
     }
+    if (sh.vpt <= 2) return launch_fedavg_variant<E, true, NTS, 2, 8, false, true>(FA_ARGS);  // short buckets
+    if (sh.vpt <= 4) return launch_fedavg_variant<E, true, NTS, 4, 4, false, true>(FA_ARGS);
     return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
   }
 #else

@@ -101,9 +101,14 @@ def ring_multipliers(G: int, rings: Optional[int] = None) -> List[int]:
     return u[:n]
 
 
-# one round by default: 2 G steps, each long enough (C3 at G = 8: ~0.3 ms of HBM work) that issuing a
-# step from Python stays below its GPU time; more rounds shorten the gather tail but add steps
+# Round split of the striped schedule.  More rounds shorten the last round's gather tail (each
+# round's results travel under the next round's kernels) but add steps with shorter runs.  The Python
+# executor keeps ONE round: 2 G steps, each long enough (C3 at G = 8: ~0.3 ms of HBM work) that
+# issuing it from Python (~30 us per message) stays below its GPU time.  The native executor issues
+# a step in microseconds and takes three (tools/lockstep_model.py, C3 weak at G = 8: 0.95 against
+# 0.86 for one round at 65 GB/s per link direction, 0.96 against 0.88 at 80).
 DEFAULT_ROUNDS = (1.0,)
+NATIVE_ROUNDS = (0.5, 0.3, 0.2)
 
 
 def striped_pieces(M: int, G: int, rings: Optional[int] = None,

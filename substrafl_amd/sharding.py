@@ -105,10 +105,17 @@ def relay_plan(M: int, world: int, rank: int, chunk_elems: int = RELAY_CHUNK_ELE
 
 
 def striped_plan(M: int, world: int, rank: int, rings: Optional[int] = None,
-                 rounds: Sequence[float] = lockstep.DEFAULT_ROUNDS) -> lockstep.RankPlan:
+                 rounds: Optional[Sequence[float]] = None) -> lockstep.RankPlan:
     """This rank's part of the striped relay: per client block, the element ranges it holds
     (``plan.blocks[b]``: ``(lo, hi, col)``, packed into a ``[Kb, plan.block_len[b]]`` buffer)."""
-    return lockstep.rank_plan(striped_pieces(M, world, rings, rounds), world, rank, cols="packed")
+    return lockstep.rank_plan(striped_pieces(M, world, rings, rounds or lockstep.DEFAULT_ROUNDS), world, rank,
+                              cols="packed")
+
+
+def default_rounds(transport) -> Sequence[float]:
+    """The striped schedule's round split for a transport: three rounds for the native executor,
+    one for the Python one (lockstep.DEFAULT_ROUNDS / NATIVE_ROUNDS)."""
+    return lockstep.NATIVE_ROUNDS if getattr(transport, "native", False) else lockstep.DEFAULT_ROUNDS
 
 
 # ======================================================================================
@@ -920,7 +927,7 @@ def _block_layout(torch, kind: str, Kb: int, extents, tiled) -> int:
 
 def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int], group=None,
                           combine: str = "relay", transport=None, rings: Optional[int] = None,
-                          rounds: Sequence[float] = lockstep.DEFAULT_ROUNDS, tiled="auto",
+                          rounds: Optional[Sequence[float]] = None, tiled="auto",
                           chunk_elems: int = RELAY_CHUNK_ELEMS):
     """FedAvg (fed_avg.py:217-222) with the clients sharded over the process group: rank r stages
     only its blocks' buckets (to its own GPU), the chain / reduce runs over RCCL and the root
@@ -945,7 +952,7 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
     w_all = fedavg_weights(n_samples, kind)
     out = torch.empty(layout.ld, dtype=out_dtype(torch, kind), device=dev)
     if combine in ("relay", "striped"):
-        plan = (striped_plan(layout.M, G, rank, rings, rounds) if combine == "striped"
+        plan = (striped_plan(layout.M, G, rank, rings, rounds or default_rounds(tr)) if combine == "striped"
                 else relay_plan(layout.M, G, rank, chunk_elems))
         blocks = {}
         for b, segs in plan.blocks.items():
@@ -971,7 +978,7 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
 
 def client_sharded_scaffold(parameters_updates, control_variate_updates, server_control_variates, n_samples,
                             aggregation_lr, group=None, combine: str = "relay", transport=None,
-                            rings: Optional[int] = None, rounds: Sequence[float] = lockstep.DEFAULT_ROUNDS):
+                            rings: Optional[int] = None, rounds: Optional[Sequence[float]] = None):
     """Scaffold (scaffold.py:193-196, 297-337) with the clients sharded over the process group.
     Every rank checks its blocks' server control variates against client 0's on the host while
     staging (``c`` itself is staged once per rank that runs a final step).  Returns
@@ -1007,7 +1014,7 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
     isz = np.dtype(dts[2]).itemsize
     mism = 0
     if combine == "striped":
-        plan = striped_plan(layout.M, G, rank, rings, rounds)
+        plan = striped_plan(layout.M, G, rank, rings, rounds or default_rounds(tr))
         blocks = {}
         for b, segs in plan.blocks.items():
             k0, k1 = client_blocks(K, G)[b]

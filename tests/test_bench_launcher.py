@@ -56,6 +56,22 @@ def test_pg_kwargs_has_a_timeout():
     assert 0 < t <= 600 and bench.CLIENT_SHARD_DEADLINE_S < t
 
 
+def test_default_rounds_follow_the_executor():
+    """Three rounds for the native executor, one for the Python one; --rounds overrides both."""
+    import argparse
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from substrafl_amd import lockstep, sharding
+
+    ns = argparse.Namespace
+    assert bench._rounds(ns(rounds="", executor="native")) == lockstep.NATIVE_ROUNDS == (0.5, 0.3, 0.2)
+    assert bench._rounds(ns(rounds="", executor="torch")) == lockstep.DEFAULT_ROUNDS == (1.0,)
+    assert bench._rounds(ns(rounds="0.75,0.25", executor="native")) == (0.75, 0.25)
+    assert sharding.default_rounds(type("T", (), {"native": True})()) == lockstep.NATIVE_ROUNDS
+    assert sharding.default_rounds(object()) == lockstep.DEFAULT_ROUNDS
+
+
 def test_plain_gpus_3_launches_three_ranks():
     r = _run(["--gpus", "3", "--rehearse-cpu", "--steps", "2", "--warmup", "0", "--combine", "relay"])
     assert r.returncode == 0, r.stderr[-3000:]

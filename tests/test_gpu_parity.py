@@ -1455,3 +1455,32 @@ def test_scaffold_0d_server_control_variate(torch_gpu, dummy_algo_class):
     bad = [np.array(0.5, np.float32), c0[1].copy(), c0[2].copy()]
     with pytest.raises(AssertionError, match="server_control_variate"):
         Scaffold(algo=dummy_algo_class(), aggregation_lr=0.8).avg_shared_states(states(bad), _skip=True)
+
+
+@pytest.mark.parametrize("kind", ["f32", "bf16"])
+@pytest.mark.parametrize("M", [300_001, 1_000_003, 2_500_007, 3_500_011])
+def test_short_buckets_many_clients_vs_torch_sequential(torch_gpu, kind, M):
+    """The short-bucket tiles of shape_for (from 32 clients: 2 x 8 under 1.5M fp32 elements, 4 x 4
+    under 3M -- the runs of the client-sharded schedules): bit-exact against torch eager ops applied
+    client by client, as a first launch and as a chain continuing an accumulator."""
+    torch = torch_gpu
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+    from substrafl_amd.sharding import GpuShardOps
+
+    K = 64
+    dt = torch.bfloat16 if kind == "bf16" else torch.float32
+    x = torch.randn((K, M + 9), device="cuda").to(dt)
+    ns = [int(v) for v in np.random.default_rng(M).integers(100, 10000, K)]
+    w = fedavg_weights(ns, kind)
+    out = torch.empty(M + 9, device="cuda")
+    FedAvgPlan(kind, x, w, M, out, None).launch()
+    acc = torch.zeros(M, device="cuda")
+    for k in range(K):
+        acc = acc + x[k, :M].float() * torch.tensor(w[k], device="cuda")
+    half = torch.zeros(M, device="cuda")  # the chain form: clients 0..31, then 32..63 continuing it
+    ops = GpuShardOps()
+    ops.fedavg_run(kind, x[:32, :M], w[:32], True, half)
+    ops.fedavg_run(kind, x[32:, :M], w[32:], False, half)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:M].view(torch.int32), acc.view(torch.int32))
+    assert torch.equal(half.view(torch.int32), acc.view(torch.int32))

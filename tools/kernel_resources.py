@@ -17,11 +17,13 @@ ROOT = Path(__file__).resolve().parents[1]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--filter", default="", help="substring of the demangled kernel name")
+    ap.add_argument("--tuning", action="store_true", help="the FEDAGG_TUNING build (every experiment variant)")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                             "-fPIC", "-c", f"-I{ROOT / 'include'}", str(ROOT / "substrafl_amd" / "csrc" / "fedagg.hip"),
-                            "-o", str(Path(d) / "fa.o"), "-Rpass-analysis=kernel-resource-usage"],
+                            "-o", str(Path(d) / "fa.o"), "-Rpass-analysis=kernel-resource-usage"]
+                           + (["-DFEDAGG_TUNING=1"] if args.tuning else []),
                            capture_output=True, text=True)
     if r.returncode:
         sys.exit(r.stderr[-2000:])

@@ -38,10 +38,11 @@ class Deadlock(RuntimeError):
     pass
 
 
-# chain-kernel rate (TB/s of client reads) against run length at 64 clients, fp32 rows: tools/chunk_probe.py
-# on MI355X (profiles/r03_chunk_probe.log): short runs lose to launch and tail effects
-RATE_CURVE = ((2.0e6, 5.56), (3.9e6, 6.92), (7.8e6, 6.94), (15.6e6, 6.86), (31.2e6, 6.73), (62.5e6, 6.93),
-              (125e6, 6.89))
+# chain-kernel rate (TB/s of client reads) against run length at 64 clients, fp32 rows, with the short-bucket
+# tiles of shape_for: tools/chunk_probe.py on MI355X (profiles/r03_chunk_probe.log,
+# r03f_chunk_probe_short_tiles.log; two sessions averaged where both measured)
+RATE_CURVE = ((0.5e6, 5.96), (1.0e6, 6.80), (1.5e6, 6.62), (2.0e6, 7.02), (3.0e6, 6.67), (3.9e6, 6.84),
+              (7.8e6, 6.87), (15.6e6, 6.80), (31.2e6, 6.63), (62.5e6, 6.93), (125e6, 6.89))
 
 
 def rate_tbps(n: float, curve=RATE_CURVE) -> float:
