@@ -792,7 +792,7 @@ def _rounds(args):
     from substrafl_amd import lockstep
 
     if not args.rounds:  # the schedule's default for the executor (lockstep.py)
-        return lockstep.NATIVE_ROUNDS if args.executor == "native" else lockstep.DEFAULT_ROUNDS
+        return lockstep.default_rounds(args.gpus, args.executor == "native")
     return tuple(float(x) for x in args.rounds.split(","))
 
 

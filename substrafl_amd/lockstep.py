@@ -111,6 +111,12 @@ DEFAULT_ROUNDS = (1.0,)
 NATIVE_ROUNDS = (0.5, 0.3, 0.2)
 
 
+def default_rounds(world: int, native: bool) -> Tuple[float, ...]:
+    """NATIVE_ROUNDS for the native executor over >= 2 ranks; one round otherwise (one rank has no
+    gather to hide, and its runs are longest in one round)."""
+    return NATIVE_ROUNDS if native and world > 1 else DEFAULT_ROUNDS
+
+
 def striped_pieces(M: int, G: int, rings: Optional[int] = None,
                    rounds: Sequence[float] = DEFAULT_ROUNDS) -> List[Piece]:
     """The striped relay (module docstring).  ``rounds``: relative sizes of the rounds (the last

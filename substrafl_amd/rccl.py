@@ -91,6 +91,17 @@ class RcclTransport:
                "fedagg_comm_create")
         self._h = h
         self._programs: List["NativeProgram"] = []
+        self._py = None
+
+    def python_transport(self):
+        """The torch.distributed transport of the same group (sharding.DistTransport), for the paths
+        the native executor does not run: schedules with empty client blocks and the
+        re-associating combines."""
+        if self._py is None:
+            from .sharding import DistTransport
+
+            self._py = DistTransport(self.group)
+        return self._py
 
     def close(self) -> None:
         if self._h:

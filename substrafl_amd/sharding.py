@@ -113,9 +113,9 @@ def striped_plan(M: int, world: int, rank: int, rings: Optional[int] = None,
 
 
 def default_rounds(transport) -> Sequence[float]:
-    """The striped schedule's round split for a transport: three rounds for the native executor,
-    one for the Python one (lockstep.DEFAULT_ROUNDS / NATIVE_ROUNDS)."""
-    return lockstep.NATIVE_ROUNDS if getattr(transport, "native", False) else lockstep.DEFAULT_ROUNDS
+    """The striped schedule's round split for a transport: three rounds for the native executor
+    over more than one rank, else one (lockstep.DEFAULT_ROUNDS / NATIVE_ROUNDS)."""
+    return lockstep.default_rounds(getattr(transport, "world", 1), getattr(transport, "native", False))
 
 
 # ======================================================================================
@@ -673,6 +673,8 @@ def lockstep_fedavg(plan: lockstep.RankPlan, blocks: Dict[int, FedAvgShard], out
         else:
             ws.zero_()
     native = getattr(transport, "native", False) and all(b.Kr for b in blocks.values())
+    if not native:
+        transport = _python_transport(transport)
     if native:  # rccl.RcclTransport: the whole schedule issued from C++ (csrc/lockstep.hip)
         prog = transport.program(plan=plan, blocks=blocks, accs=[acc], outs=[out], kind=kind, scaffold=False)
         for b, p0, p1, cols in lockstep.pairwise_segments(plan, pw):  # before the schedule, same stream
@@ -732,6 +734,8 @@ def lockstep_scaffold(plan: lockstep.RankPlan, blocks: Dict[int, ScaffoldShard],
             wc[p0:p1] += tmp[(p1 - p0) * K:].view(p1 - p0, K + 1)
 
     native = getattr(transport, "native", False) and all(b.Kr for b in blocks.values())
+    if not native:
+        transport = _python_transport(transport)
     if native:  # rccl.RcclTransport: the whole schedule issued from C++ (csrc/lockstep.hip)
         prog = transport.program(plan=plan, blocks=blocks, accs=[acc[0], acc[1]], outs=[dout, cout], kind=kind,
                                  scaffold=True, c=c, lr=lr)
@@ -779,6 +783,7 @@ def client_shard_fedavg(sh: FedAvgShard, out, transport, ops, combine: str = "re
     if combine == "relay" or G == 1:
         plan = relay_plan(sh.M, G, rank, chunk_elems)
         return lockstep_fedavg(plan, {block_of(rank, G): sh}, out, transport, ops, sh.pairwise_idx, ws=ws)
+    transport = _python_transport(transport)
     P = int(sh.pairwise_idx.size)
     if P:
         if ws is None:
@@ -822,6 +827,7 @@ def client_shard_scaffold(sh: ScaffoldShard, dout, cout, transport, ops, combine
         plan = relay_plan(sh.M, G, rank, chunk_elems)
         return lockstep_scaffold(plan, {block_of(rank, G): sh}, dout, cout, transport, ops, sh.pairwise_idx, sh.c,
                                  sh.lr, ws=ws)
+    transport = _python_transport(transport)
     P = int(sh.pairwise_idx.size)
     if P:
         n = P * (2 * sh.K + 1)
@@ -910,6 +916,13 @@ def _stage_block(torch, device, rows: List[List[np.ndarray]], layout: BucketLayo
 
 def _transport(transport, group):
     return transport or DistTransport(group)
+
+
+def _python_transport(transport):
+    """The transport for the Python-issued paths: a native transport (rccl.RcclTransport) hands over
+    its torch.distributed counterpart for what its executor does not run (schedules with empty
+    client blocks, the re-associating combines)."""
+    return transport.python_transport() if getattr(transport, "native", False) else transport
 
 
 def _block_layout(torch, kind: str, Kb: int, extents, tiled) -> int:

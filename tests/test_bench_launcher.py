@@ -57,7 +57,7 @@ def test_pg_kwargs_has_a_timeout():
 
 
 def test_default_rounds_follow_the_executor():
-    """Three rounds for the native executor, one for the Python one; --rounds overrides both."""
+    """Three rounds for the native executor over >= 2 ranks, else one; --rounds overrides both."""
     import argparse
 
     sys.path.insert(0, str(ROOT))
@@ -65,10 +65,12 @@ def test_default_rounds_follow_the_executor():
     from substrafl_amd import lockstep, sharding
 
     ns = argparse.Namespace
-    assert bench._rounds(ns(rounds="", executor="native")) == lockstep.NATIVE_ROUNDS == (0.5, 0.3, 0.2)
-    assert bench._rounds(ns(rounds="", executor="torch")) == lockstep.DEFAULT_ROUNDS == (1.0,)
-    assert bench._rounds(ns(rounds="0.75,0.25", executor="native")) == (0.75, 0.25)
-    assert sharding.default_rounds(type("T", (), {"native": True})()) == lockstep.NATIVE_ROUNDS
+    assert bench._rounds(ns(rounds="", executor="native", gpus=8)) == lockstep.NATIVE_ROUNDS == (0.5, 0.3, 0.2)
+    assert bench._rounds(ns(rounds="", executor="native", gpus=1)) == lockstep.DEFAULT_ROUNDS == (1.0,)
+    assert bench._rounds(ns(rounds="", executor="torch", gpus=8)) == lockstep.DEFAULT_ROUNDS
+    assert bench._rounds(ns(rounds="0.75,0.25", executor="native", gpus=8)) == (0.75, 0.25)
+    assert sharding.default_rounds(type("T", (), {"native": True, "world": 4})()) == lockstep.NATIVE_ROUNDS
+    assert sharding.default_rounds(type("T", (), {"native": True, "world": 1})()) == lockstep.DEFAULT_ROUNDS
     assert sharding.default_rounds(object()) == lockstep.DEFAULT_ROUNDS
 
 

@@ -29,7 +29,9 @@ def _data(K, seed=0, shapes=SHAPES):
     return pus, ns
 
 
-def _loopback(G, fn):
+def _loopback(G, fn, transports=None):
+    """Run ``fn(rank, transport)`` for G ranks as threads on the one GPU, each on its own stream;
+    ``transports``: per-rank transports (default: one LoopbackGroup's)."""
     import torch
 
     from substrafl_amd.sharding import LoopbackGroup
@@ -42,7 +44,7 @@ def _loopback(G, fn):
             torch.cuda.set_device(0)
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
-                res[r] = fn(r, grp.transport(r))
+                res[r] = fn(r, transports[r] if transports else grp.transport(r))
             s.synchronize()
         except BaseException as e:  # noqa: BLE001
             err[r] = e
@@ -334,7 +336,7 @@ def test_relay_random_sweep(seed):
 
 # ---- striped relay: pieces rotating over the ranks on several rings (lockstep schedule) ----
 def _striped(G, K, strategy="fedavg", kind="f32", rings=None, rounds=(0.75, 0.25), shapes=SHAPES, seed=4, lr=0.9,
-             tv=0, relay=False):
+             tv=0, relay=False, transports=None, repeat=1):
     import torch
 
     from substrafl_amd.engine import fedavg_weights, scaffold_weights
@@ -376,20 +378,22 @@ def _striped(G, K, strategy="fedavg", kind="f32", rings=None, rounds=(0.75, 0.25
                 blocks[b] = ScaffoldShard(kind, packed(pus[k0:k1]), packed(cvs[k0:k1]), None,
                                           scaffold_weights(ns)[k0:k1], k0, K, plan.block_len[b], lr,
                                           np.zeros(0, np.uint64))
-        if strategy == "fedavg":
-            out = torch.zeros(layout.ld, dtype=out_dtype(torch, kind), device="cuda")
-            if lockstep_fedavg(plan, blocks, out, tr, GpuShardOps(), layout.pairwise_idx):
+        got = None
+        for _ in range(repeat):  # a repeated call reuses the compiled schedule (native executor)
+            if strategy == "fedavg":
+                out = torch.full((layout.ld,), float("nan"), dtype=out_dtype(torch, kind), device="cuda")
+                if lockstep_fedavg(plan, blocks, out, tr, GpuShardOps(), layout.pairwise_idx):
+                    torch.cuda.current_stream().synchronize()
+                    got = out[: layout.M].cpu().numpy().copy()
+                continue
+            dout = torch.full((layout.ld,), float("nan"), dtype=torch.float64, device="cuda")
+            cout = torch.full((layout.ld,), float("nan"), dtype=torch.float64, device="cuda")
+            if lockstep_scaffold(plan, blocks, dout, cout, tr, GpuShardOps(), layout.pairwise_idx, full_c, lr):
                 torch.cuda.current_stream().synchronize()
-                return out[: layout.M].cpu().numpy().copy()
-            return None
-        dout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
-        cout = torch.zeros(layout.ld, dtype=torch.float64, device="cuda")
-        if lockstep_scaffold(plan, blocks, dout, cout, tr, GpuShardOps(), layout.pairwise_idx, full_c, lr):
-            torch.cuda.current_stream().synchronize()
-            return dout[: layout.M].cpu().numpy().copy(), cout[: layout.M].cpu().numpy().copy()
-        return None
+                got = dout[: layout.M].cpu().numpy().copy(), cout[: layout.M].cpu().numpy().copy()
+        return got
 
-    res = _loopback(G, rank_fn)
+    res = _loopback(G, rank_fn, transports)
     assert all(x is None for x in res[1:])
     if strategy == "fedavg":
         return [a for _, a in layout.unpack(res[0])], fedavg_reference_structure(pus, ns)
@@ -571,3 +575,89 @@ def test_native_lockstep_executor_world1():
         lay = BucketLayout(range(len(shapes)), shapes, npdt)
         for g, r in zip([a for _, a in lay.unpack(nat)], fedavg_reference_structure(pus, ns)):
             assert g.dtype == r.dtype and np.array_equal(g.view(bits[g.itemsize]), r.view(bits[r.itemsize])), key
+
+
+# ---- the native executor with G ranks: threads on one GPU over tests/native/libthread_rccl.so ----
+THREAD_RCCL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "libthread_rccl.so")
+
+# (G, K, strategy, kind, rings, rounds, tv, relay); every block non-empty unless K < G
+NATIVE_THREAD_CASES = [
+    (8, 70, "fedavg", "f32", None, (0.5, 0.3, 0.2), 0, False),   # the bench's schedule at G = 8
+    (8, 20, "fedavg", "f32", 3, (1.0,), 0, False),
+    (4, 9, "fedavg", "f32", 2, (0.75, 0.25), 0, True),          # relay
+    (3, 100, "fedavg", "f32", None, (0.5, 0.3, 0.2), 2048, False),  # tiled blocks (>= 32 clients each)
+    (2, 66, "fedavg", "bf16", None, (0.5, 0.3, 0.2), 4096, False),
+    (3, 5, "fedavg", "f64", None, (0.6, 0.4), 0, False),
+    (2, 5, "fedavg", "f16", None, (1.0,), 0, False),
+    (8, 17, "scaffold", "f32", None, (0.5, 0.3, 0.2), 0, False),
+    (4, 6, "scaffold", "f64", None, (1.0,), 0, False),
+    (8, 5, "fedavg", "f32", None, (0.5, 0.3, 0.2), 0, False),    # K < G: empty blocks, the Python fallback
+]
+
+
+def _native_threads(q, cases):
+    import ctypes
+
+    import torch
+
+    from substrafl_amd import _native, rccl
+    from substrafl_amd.sharding import LoopbackGroup
+
+    class ThreadTransport(rccl.RcclTransport):
+        """RcclTransport over the thread-ranks stand-in (no torch process group): the native
+        executor unchanged, its RCCL calls served by tests/native/thread_rccl.hip."""
+
+        def __init__(self, uid, rank, world, py):
+            self.lib, self.rank, self.world, self.device, self.group = _native.load(), rank, world, 0, None
+            self._programs, self._py = [], py
+            h = ctypes.c_void_p()
+            rccl._check(self.lib.fedagg_comm_create(THREAD_RCCL.encode(), world, rank, uid, 0, ctypes.byref(h)),
+                        "fedagg_comm_create")
+            self._h = h
+
+        def all_sum_int(self, v):
+            return self._py.all_sum_int(v)
+
+    torch.cuda.set_device(0)
+    lib = _native.load()
+    res = {}
+    for i, (G, K, strategy, kind, rings, rounds, tv, relay) in enumerate(cases):
+        uid = (ctypes.c_char * 128)()
+        rccl._check(lib.fedagg_comm_unique_id(THREAD_RCCL.encode(), uid), "fedagg_comm_unique_id")
+        py = LoopbackGroup(G)
+        trs = [ThreadTransport(uid, r, G, py.transport(r)) for r in range(G)]
+        shapes = SHAPES + [(5000,), (1,)] if not tv else [(37, 29), (1,), (40000,), (1, 1), (3, 3, 3), (70001,), (1,)]
+        got, ref = _striped(G, K, strategy=strategy, kind=kind, rings=rings, rounds=rounds, shapes=shapes, tv=tv,
+                            relay=relay, transports=trs, repeat=2, seed=11 + i)
+        bits = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+        bad = sum(int(np.count_nonzero(g.view(bits[g.itemsize]) != r.view(bits[r.itemsize])))
+                  + int(g.dtype != r.dtype or g.shape != r.shape) for g, r in zip(got, ref))
+        programs = sum(len(t._programs) for t in trs)
+        for t in trs:
+            t.close()
+        res[i] = (bad, programs)
+    q.put(res)
+
+
+@pytest.mark.skipif(not os.path.exists(THREAD_RCCL), reason="tests/native/libthread_rccl.so not built")
+def test_native_executor_multi_rank_threads():
+    """csrc/lockstep.hip with 2-8 ranks: each rank a thread with its own stream and communicator on
+    the one GPU, RCCL's P2P / reduce served by the thread stand-in (real RCCL refuses two ranks on
+    one GPU).  Every rank's compiled run / message tables, the cross-stream event order, slot reuse
+    over 48 steps and the numel == 1 workspace reduce -- relay, striped (1-3 rounds), tiled blocks,
+    every kind, Scaffold, called twice through the cached program -- bit-identical to the
+    reference; K < G takes the Python fallback through the same transport."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_threads, args=(q, NATIVE_THREAD_CASES))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for i, case in enumerate(NATIVE_THREAD_CASES):
+        bad, programs = res[i]
+        assert bad == 0, (case, bad)
+        native = case[1] >= case[0]
+        assert (programs > 0) == native, (case, programs)  # the native path ran where it should
