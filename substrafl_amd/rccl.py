@@ -95,8 +95,9 @@ class RcclTransport:
 
     def python_transport(self):
         """The torch.distributed transport of the same group (sharding.DistTransport), for the paths
-        the native executor does not run: schedules with empty client blocks and the
-        re-associating combines."""
+        the native executor does not run: schedules with an empty client block (fewer clients than
+        ranks, or a ragged split) and the re-associating combines.  It moves device tensors, so
+        the group's backend must carry them (RCCL)."""
         if self._py is None:
             from .sharding import DistTransport
 

@@ -81,9 +81,12 @@ def pack_range(layout: BucketLayout, layers: Sequence[np.ndarray], dst: np.ndarr
 # client blocks
 # ======================================================================================
 def client_blocks(K: int, world: int) -> List[Tuple[int, int]]:
-    """Block b = clients ``[k0, k1)`` (contiguous, list order); trailing blocks may be empty."""
-    per = -(-K // world)
-    return [(min(K, b * per), min(K, (b + 1) * per)) for b in range(world)]
+    """Block b = clients ``[k0, k1)`` (contiguous, list order): sizes differ by at most one, so
+    every block holds a client once K >= world (the native executor's condition); with fewer
+    clients than ranks, one client per block and the trailing blocks empty."""
+    if K < world:
+        return [(min(K, b), min(K, b + 1)) for b in range(world)]
+    return [(b * K // world, (b + 1) * K // world) for b in range(world)]
 
 
 def block_of(rank: int, world: int) -> int:
@@ -672,7 +675,7 @@ def lockstep_fedavg(plan: lockstep.RankPlan, blocks: Dict[int, FedAvgShard], out
             ws = torch.zeros((pw.size, K), dtype=ws_dtype(torch, kind), device=out.device)
         else:
             ws.zero_()
-    native = getattr(transport, "native", False) and all(b.Kr for b in blocks.values())
+    native = _native_schedule(transport, K, plan.world)
     if not native:
         transport = _python_transport(transport)
     if native:  # rccl.RcclTransport: the whole schedule issued from C++ (csrc/lockstep.hip)
@@ -733,7 +736,7 @@ def lockstep_scaffold(plan: lockstep.RankPlan, blocks: Dict[int, ScaffoldShard],
             wd[p0:p1] += tmp[: (p1 - p0) * K].view(p1 - p0, K)
             wc[p0:p1] += tmp[(p1 - p0) * K:].view(p1 - p0, K + 1)
 
-    native = getattr(transport, "native", False) and all(b.Kr for b in blocks.values())
+    native = _native_schedule(transport, K, plan.world)
     if not native:
         transport = _python_transport(transport)
     if native:  # rccl.RcclTransport: the whole schedule issued from C++ (csrc/lockstep.hip)
@@ -916,6 +919,14 @@ def _stage_block(torch, device, rows: List[List[np.ndarray]], layout: BucketLayo
 
 def _transport(transport, group):
     return transport or DistTransport(group)
+
+
+def _native_schedule(transport, K: int, world: int) -> bool:
+    """Whether the native executor runs this schedule: a native transport and no empty client block
+    in the whole partition (client_blocks(K, world)).  A function of (K, world) alone, so every
+    rank takes the same executor -- a rank on the native communicator and a peer on the Python
+    transport would never meet."""
+    return getattr(transport, "native", False) and all(k1 > k0 for k0, k1 in client_blocks(K, world))
 
 
 def _python_transport(transport):

@@ -19,6 +19,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -75,9 +77,10 @@ struct Op {
   hipStream_t stream;
 };
 
-hipEvent_t new_event(World& w) {  // under w.mu
+hipEvent_t new_event(World& w) {  // NOT under w.mu: no HIP call is ever made holding the world's lock
   hipEvent_t e = nullptr;
   (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  std::lock_guard<std::mutex> lk(w.mu);
   w.events.push_back(e);
   return e;
 }
@@ -126,47 +129,66 @@ namespace {
 thread_local int t_depth = 0;                   // ncclGroupStart nesting on this thread
 thread_local ncclComm* t_group_comm = nullptr;  // the communicator of the open group
 
+constexpr auto kWait = std::chrono::seconds(20);  // a peer that has not posted by then never will
+
+// One group: post every send (its data-ready event recorded on the sender's stream), then serve
+// every receive (wait for the matching post, copy on the receiver's stream after the data-ready
+// event, record the consumed event), then make each send's stream wait for its consumed event.
+// HIP calls are made outside the world's lock, so a HIP call that blocks cannot stall other ranks'
+// posting.
 ncclResult_t run_group(ncclComm* c) {
   World& w = *c->w;
-  std::vector<std::pair<Op, std::shared_ptr<Posted>>> sends;
-  {
-    std::lock_guard<std::mutex> lk(w.mu);
-    for (const Op& o : c->ops) {
-      if (!o.send) continue;
-      auto p = std::make_shared<Posted>();
-      p->buf = o.buf;
-      p->bytes = o.bytes;
-      p->ready = new_event(w);
-      if (hipEventRecord(p->ready, o.stream) != hipSuccess) return ncclUnhandledCudaError;
-      w.box[{c->rank, o.peer, c->sent[o.peer]++}] = p;
-      sends.emplace_back(o, p);
-    }
+  static const bool trace = getenv("THREAD_RCCL_TRACE") != nullptr;
+  if (trace) {
+    fprintf(stderr, "[thread_rccl] rank %d group:", c->rank);
+    for (const Op& o : c->ops) fprintf(stderr, " %s%d:%zu", o.send ? "s" : "r", o.peer, o.bytes);
+    fprintf(stderr, "\n");
   }
-  w.cv.notify_all();
-  for (const Op& o : c->ops) {  // receives: wait for the matching send, copy on our stream
+  std::vector<std::pair<Op, std::shared_ptr<Posted>>> sends;
+  for (const Op& o : c->ops) {
+    if (!o.send) continue;
+    auto p = std::make_shared<Posted>();
+    p->buf = o.buf;
+    p->bytes = o.bytes;
+    p->ready = new_event(w);
+    if (hipEventRecord(p->ready, o.stream) != hipSuccess) return ncclUnhandledCudaError;
+    {
+      std::lock_guard<std::mutex> lk(w.mu);
+      w.box[{c->rank, o.peer, c->sent[o.peer]++}] = p;
+    }
+    w.cv.notify_all();
+    sends.emplace_back(o, p);
+  }
+  for (const Op& o : c->ops) {
     if (o.send) continue;
     const auto key = std::make_tuple(o.peer, c->rank, c->recvd[o.peer]++);
     std::shared_ptr<Posted> p;
     {
       std::unique_lock<std::mutex> lk(w.mu);
-      if (!w.cv.wait_for(lk, std::chrono::seconds(60), [&] { return w.box.count(key) > 0; }))
+      if (!w.cv.wait_for(lk, kWait, [&] { return w.box.count(key) > 0; }))
         return ncclSystemError;  // the peer never issued its group: a schedule bug
       p = w.box[key];
       w.box.erase(key);
-      if (p->bytes != o.bytes) return ncclInvalidUsage;  // mismatched message sizes
-      if (hipStreamWaitEvent(o.stream, p->ready, 0) != hipSuccess ||
-          hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.stream) != hipSuccess)
-        return ncclUnhandledCudaError;
-      p->done = new_event(w);
-      if (hipEventRecord(p->done, o.stream) != hipSuccess) return ncclUnhandledCudaError;
+    }
+    if (p->bytes != o.bytes) return ncclInvalidUsage;  // mismatched message sizes
+    hipEvent_t done = new_event(w);
+    if (hipStreamWaitEvent(o.stream, p->ready, 0) != hipSuccess ||
+        hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.stream) != hipSuccess ||
+        hipEventRecord(done, o.stream) != hipSuccess)
+      return ncclUnhandledCudaError;
+    {
+      std::lock_guard<std::mutex> lk(w.mu);
+      p->done = done;
       p->consumed = true;
     }
     w.cv.notify_all();
   }
-  for (auto& sp : sends) {  // sends complete once consumed
+  for (auto& sp : sends) {  // a send completes once its data has been copied out
     const std::shared_ptr<Posted>& p = sp.second;
-    std::unique_lock<std::mutex> lk(w.mu);
-    if (!w.cv.wait_for(lk, std::chrono::seconds(60), [&] { return p->consumed; })) return ncclSystemError;
+    {
+      std::unique_lock<std::mutex> lk(w.mu);
+      if (!w.cv.wait_for(lk, kWait, [&] { return p->consumed; })) return ncclSystemError;
+    }
     if (hipStreamWaitEvent(sp.first.stream, p->done, 0) != hipSuccess) return ncclUnhandledCudaError;
   }
   c->ops.clear();
@@ -281,9 +303,11 @@ ncclResult_t ncclReduce(const void* sendbuf, void* recvbuf, size_t count, ncclDa
   if (!c || op != ncclSum || root < 0 || root >= c->w->n) return ncclInvalidArgument;
   World& w = *c->w;
   const uint64_t seq = c->reduces++;
+  hipEvent_t ready = new_event(w);
+  if (hipEventRecord(ready, s) != hipSuccess) return ncclUnhandledCudaError;
   std::shared_ptr<World::Red> r;
   {
-    std::unique_lock<std::mutex> lk(w.mu);
+    std::lock_guard<std::mutex> lk(w.mu);
     auto& slot = w.red[seq];
     if (!slot) {
       slot = std::make_shared<World::Red>();
@@ -292,14 +316,15 @@ ncclResult_t ncclReduce(const void* sendbuf, void* recvbuf, size_t count, ncclDa
     }
     r = slot;
     r->buf[c->rank] = sendbuf;
-    r->ready[c->rank] = new_event(w);
-    if (hipEventRecord(r->ready[c->rank], s) != hipSuccess) return ncclUnhandledCudaError;
+    r->ready[c->rank] = ready;
     r->posted++;
   }
   w.cv.notify_all();
-  std::unique_lock<std::mutex> lk(w.mu);
   if (c->rank == root) {
-    if (!w.cv.wait_for(lk, std::chrono::seconds(60), [&] { return r->posted == w.n; })) return ncclSystemError;
+    {
+      std::unique_lock<std::mutex> lk(w.mu);
+      if (!w.cv.wait_for(lk, kWait, [&] { return r->posted == w.n; })) return ncclSystemError;
+    }
     if (sendbuf != recvbuf &&
         hipMemcpyAsync(recvbuf, sendbuf, count * type_size(t), hipMemcpyDeviceToDevice, s) != hipSuccess)
       return ncclUnhandledCudaError;
@@ -308,14 +333,22 @@ ncclResult_t ncclReduce(const void* sendbuf, void* recvbuf, size_t count, ncclDa
       if (hipStreamWaitEvent(s, r->ready[q], 0) != hipSuccess || !launch_add(recvbuf, r->buf[q], count, t, s))
         return ncclUnhandledCudaError;
     }
-    r->done = new_event(w);
-    if (hipEventRecord(r->done, s) != hipSuccess) return ncclUnhandledCudaError;
-    lk.unlock();
+    hipEvent_t done = new_event(w);
+    if (hipEventRecord(done, s) != hipSuccess) return ncclUnhandledCudaError;
+    {
+      std::lock_guard<std::mutex> lk(w.mu);
+      r->done = done;
+    }
     w.cv.notify_all();
     return ncclSuccess;
   }
-  if (!w.cv.wait_for(lk, std::chrono::seconds(60), [&] { return r->done != nullptr; })) return ncclSystemError;
-  return hipStreamWaitEvent(s, r->done, 0) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+  hipEvent_t done = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(w.mu);
+    if (!w.cv.wait_for(lk, kWait, [&] { return r->done != nullptr; })) return ncclSystemError;
+    done = r->done;
+  }
+  return hipStreamWaitEvent(s, done, 0) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
 }
 
 }  // extern "C"

@@ -49,7 +49,7 @@ def _loopback(G, fn, transports=None):
         except BaseException as e:  # noqa: BLE001
             err[r] = e
 
-    th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(G)]
     for t in th:
         t.start()
     for t in th:
@@ -580,10 +580,10 @@ def test_native_lockstep_executor_world1():
 # ---- the native executor with G ranks: threads on one GPU over tests/native/libthread_rccl.so ----
 THREAD_RCCL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "libthread_rccl.so")
 
-# (G, K, strategy, kind, rings, rounds, tv, relay); every block non-empty unless K < G
+# (G, K, strategy, kind, rings, rounds, tv, relay); client_blocks(K, G) decides native or Python
 NATIVE_THREAD_CASES = [
     (8, 70, "fedavg", "f32", None, (0.5, 0.3, 0.2), 0, False),   # the bench's schedule at G = 8
-    (8, 20, "fedavg", "f32", 3, (1.0,), 0, False),
+    (8, 20, "fedavg", "f32", 3, (1.0,), 0, False),             # ragged split (blocks of 2 and 3)
     (4, 9, "fedavg", "f32", 2, (0.75, 0.25), 0, True),          # relay
     (3, 100, "fedavg", "f32", None, (0.5, 0.3, 0.2), 2048, False),  # tiled blocks (>= 32 clients each)
     (2, 66, "fedavg", "bf16", None, (0.5, 0.3, 0.2), 4096, False),
@@ -597,8 +597,12 @@ NATIVE_THREAD_CASES = [
 
 def _native_threads(q, cases):
     import ctypes
+    import faulthandler
+    import sys
 
     import torch
+
+    faulthandler.dump_traceback_later(110, exit=True)  # a hang names its threads' stacks, then ends
 
     from substrafl_amd import _native, rccl
     from substrafl_amd.sharding import LoopbackGroup
@@ -622,6 +626,7 @@ def _native_threads(q, cases):
     lib = _native.load()
     res = {}
     for i, (G, K, strategy, kind, rings, rounds, tv, relay) in enumerate(cases):
+        print(f"[native threads] case {i}: {cases[i]}", file=sys.stderr, flush=True)
         uid = (ctypes.c_char * 128)()
         rccl._check(lib.fedagg_comm_unique_id(THREAD_RCCL.encode(), uid), "fedagg_comm_unique_id")
         py = LoopbackGroup(G)
@@ -653,11 +658,17 @@ def test_native_executor_multi_rank_threads():
     q = ctx.Queue()
     p = ctx.Process(target=_native_threads, args=(q, NATIVE_THREAD_CASES))
     p.start()
-    res = q.get(timeout=240)
-    p.join(timeout=60)
+    try:
+        res = q.get(timeout=130)
+    finally:
+        p.join(timeout=20)
+        if p.is_alive():
+            p.kill()  # our own child, by handle
     assert p.exitcode == 0
+    from substrafl_amd.sharding import client_blocks
+
     for i, case in enumerate(NATIVE_THREAD_CASES):
         bad, programs = res[i]
         assert bad == 0, (case, bad)
-        native = case[1] >= case[0]
-        assert (programs > 0) == native, (case, programs)  # the native path ran where it should
+        native = all(k1 > k0 for k0, k1 in client_blocks(case[1], case[0]))  # the same choice on every rank
+        assert (programs > 0) == native, (case, programs)

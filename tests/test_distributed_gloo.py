@@ -194,6 +194,11 @@ def test_client_blocks_and_chain():
             blocks = client_blocks(K, G)
             assert blocks[0][0] == 0 and blocks[-1][1] == K and len(blocks) == G
             assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+            sizes = [b - a for a, b in blocks]
+            if K >= G:  # balanced, never empty (the native executor runs every K >= G)
+                assert min(sizes) >= 1 and max(sizes) - min(sizes) <= 1
+            else:
+                assert sizes == [1] * K + [0] * (G - K)
             assert sorted(chain_rank(b, G) for b in range(G)) == list(range(G))
             assert chain_rank(G - 1, G) == 0  # the last block (final step) is on the root
             assert all(block_of(chain_rank(b, G), G) == b for b in range(G))
