@@ -19,7 +19,9 @@ finite timeout (``pg_kwargs``).  Modes:
   one GPU per rank the SAME line also carries ``client_shard``: the north-star client-sharded
   mode timed right after, weak (every rank holds the workload's K clients, N*K in all), combine
   ``--combine`` (default striped) -- step time, block-kernel time, exchange time, GB/s, fraction
-  of N x 8 TB/s, and weak efficiency against the parameter-range kernel time of one GPU.
+  of N x 8 TB/s, and weak efficiency against the parameter-range kernel time of one GPU -- and
+  ``multi_device``: the drop-in's one-process MultiDeviceEngine over the same N GPUs (host
+  buckets, PCIe-inclusive).
 * ``--mode client-shard --combine relay|rccl|ordered|striped``: the client-sharded mode as the
   line itself.  ``relay`` and ``striped`` are bit-exact lockstep schedules over ONE communicator
   (substrafl_amd/lockstep.py); ``--scaling weak``: every rank holds the workload's K clients;
@@ -73,6 +75,9 @@ def parse():
                     help="N > 1 param-range runs: also time the client-sharded (north-star) mode, weak, in the "
                          "same invocation (auto: when every rank has its own GPU)")
     ap.add_argument("--client-shard-steps", type=int, default=50, help="timed steps of the client-shard leg")
+    ap.add_argument("--multi-device-leg", default="auto", choices=["auto", "off"],
+                    help="N > 1: also time the drop-in's one-process MultiDeviceEngine over the N GPUs "
+                         "(host buckets, PCIe-inclusive; rank 0 runs it in a child process)")
     ap.add_argument("--rings", type=int, default=0, help="striped: rings (hop lengths; 0 = up to 4)")
     ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default: three "
                     "rounds with the native executor, one with the Python one)")
@@ -344,6 +349,8 @@ def main():
                 line.update(client_shard_legs(args, ctx, info))
             else:
                 line["client_shard"] = {"skipped": f"needs one GPU per rank for RCCL ({world} ranks, {ndev} GPUs)"}
+        if world > 1 and own_gpus and args.multi_device_leg != "off":
+            line["multi_device"] = multi_device_leg(args, ctx)
     if rank == 0 and not args.client_shard_child:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -512,6 +519,44 @@ def measure_param_range(args, ctx):
     if world > 1:
         line["process_group"] = {"backend": ctx.backend, "timeout_s": PG_TIMEOUT_S}
     return line, {"kern_ms": kern_ms_max, "K": K, "M": M, "tiled": tiled}
+
+
+MULTI_DEVICE_DEADLINE_S = 240
+
+
+def multi_device_leg(args, ctx):
+    """The N > 1 line's ``multi_device`` field: the drop-in's own multi-GPU path, ONE process driving
+    the N GPUs (MultiDeviceEngine: host buckets staged over each GPU's PCIe link, reduced, fetched
+    into one host array -- the PCIe-inclusive rate of the aggregate task), run by rank 0 as a child
+    process while the other ranks wait at the barrier (their buffers freed).  fp32 FedAvg workloads
+    (C2, C3); an error or a timeout becomes an ``error`` field."""
+    wl = ctx.wl
+    res = None
+    if ctx.rank == 0:
+        if wl["strategy"] != "fedavg" or wl["kind"] != "f32":
+            res = {"skipped": "the multi-device engine leg runs the fp32 FedAvg workloads (c2, c3)"}
+        else:
+            env = {k: v for k, v in os.environ.items()
+                   if not k.startswith("TORCHELASTIC") and k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                                     "GROUP_RANK", "MASTER_ADDR", "MASTER_PORT")}
+            cmd = [sys.executable, str(Path(__file__).resolve()), "--engine", "multi-device", "--gpus", str(ctx.world),
+                   "--workload", args.workload, "--steps", "5", "--warmup", "1"]
+            t0 = time.perf_counter()
+            p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+            try:
+                so, se = p.communicate(timeout=MULTI_DEVICE_DEADLINE_S)
+                lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+                if p.returncode != 0 or not lines:
+                    res = {"error": f"leg exited with {p.returncode}: {se[-600:]}"}
+                else:
+                    res = json.loads(lines[-1])
+            except subprocess.TimeoutExpired:
+                p.kill()  # our own child, by PID
+                p.communicate()
+                res = {"error": f"did not finish within {MULTI_DEVICE_DEADLINE_S} s"}
+            res["wall_s"] = round(time.perf_counter() - t0, 1)
+    ctx.barrier()
+    return res
 
 
 # ======================================================================================

@@ -53,7 +53,7 @@ def test_pg_kwargs_has_a_timeout():
     import bench
 
     t = bench.pg_kwargs()["timeout"].total_seconds()
-    assert 0 < t <= 600 and bench.CLIENT_SHARD_DEADLINE_S < t
+    assert 0 < t <= 600 and bench.CLIENT_SHARD_DEADLINE_S < t and bench.MULTI_DEVICE_DEADLINE_S < t
 
 
 def test_default_rounds_follow_the_executor():
