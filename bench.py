@@ -1278,7 +1278,7 @@ def cpu_baseline(wl, budget_s, full=False):
         aff = len(os.sched_getaffinity(0))
     except Exception:  # noqa: BLE001
         aff = os.cpu_count()
-    return {
+    out = {
         "value": round(nbytes / best / 1e9, 3),
         "unit": "GB/s",
         "cores": 1,
@@ -1288,6 +1288,57 @@ def cpu_baseline(wl, budget_s, full=False):
                   f"({best * 1e3:.1f} ms); oracle/aggregation.py reference call structure; "
                   f"host has {os.cpu_count()} cpus, affinity {aff}, NumPy ufuncs single-threaded",
     }
+    if wl["strategy"] == "fedavg":
+        out["threaded_variant"] = _cpu_threaded(pus, n_samples, nbytes, min(CPU_THREADS, aff or 1))
+    return out
+
+
+CPU_THREADS = 16  # the host share of one GPU on the test boxes
+
+
+def _cpu_threaded(pus, n_samples, nbytes, threads):
+    """SURVEY.md §8(d)'s optional multi-core CPU figure, NOT the reference: the same per-element
+    arithmetic (the oracle's call structure) over element chunks of the layers, the chunks spread
+    over ``threads`` threads (NumPy releases the GIL inside its ufuncs).  Chunks keep >= 2 elements,
+    and numel == 1 layers stay whole, so no chunk changes NumPy's summation order."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import fedavg_reference_structure
+
+    total = sum(a.size for a in pus[0])
+    target = max(2, total // (4 * threads))
+    chunks = []
+    for li, a in enumerate(pus[0]):
+        n = a.size
+        if n == 1:
+            chunks.append((li, 0, 1))
+            continue
+        cuts = list(range(0, n, target)) + [n]
+        if len(cuts) > 2 and cuts[-1] - cuts[-2] < 2:
+            cuts.pop(-2)
+        chunks += [(li, lo, hi) for lo, hi in zip(cuts, cuts[1:])]
+    chunks.sort(key=lambda c: c[2] - c[1], reverse=True)
+    load, parts = [0] * threads, [[] for _ in range(threads)]
+    for c in chunks:  # largest first onto the least loaded thread
+        t = load.index(min(load))
+        parts[t].append(c)
+        load[t] += c[2] - c[1]
+    views = [[[pu[li].reshape(-1)[lo:hi] for li, lo, hi in part] for pu in pus] for part in parts if part]
+
+    def run():
+        with ThreadPoolExecutor(len(views)) as ex:
+            list(ex.map(lambda v: fedavg_reference_structure(v, n_samples), views))
+
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"value": round(nbytes / best / 1e9, 3), "unit": "GB/s", "cores": len(views),
+            "kind": "port, chunked over threads -- not the reference",
+            "sample": f"the same sample, {len(chunks)} element chunks over {len(views)} threads, best of 3 "
+                      f"({best * 1e3:.1f} ms)"}
 
 
 if __name__ == "__main__":

@@ -93,3 +93,18 @@ def test_single_rank_default():
     r = _run(["--rehearse-cpu", "--steps", "2", "--warmup", "0"])
     assert r.returncode == 0, r.stderr[-3000:]
     assert _line(r.stdout)["n_gpus"] == 1
+
+
+def test_cpu_threaded_variant_is_labelled():
+    """The optional multi-core CPU figure is labelled as not the reference and
+    splits the layers into chunks of >= 2 elements (numel == 1 layers whole)."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    rng = np.random.default_rng(0)
+    shapes = [(1,), (7,), (3, 5), (1000,), (1, 1)]
+    pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(5)]
+    res = bench._cpu_threaded(pus, [3, 1, 4, 1, 5], 1000, 3)
+    assert "not the reference" in res["kind"] and 1 <= res["cores"] <= 3 and res["value"] > 0
