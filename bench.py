@@ -579,6 +579,9 @@ def client_shard_legs(args, ctx, info):
         env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
         env.update(RANK=str(ctx.rank), WORLD_SIZE=str(ctx.world), LOCAL_RANK=str(ctx.device.index),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # one node: RCCL's bootstrap over loopback (its P2P data path is xGMI either way), so an
+        # interface the container cannot route never stalls ncclCommInitRank
+        env.setdefault("NCCL_SOCKET_IFNAME", "lo")
         cmd = [sys.executable, str(Path(__file__).resolve()), "--client-shard-child", "--executor", executor,
                "--gpus", str(ctx.world), "--workload", args.workload, "--combine", args.combine or "striped",
                "--layout", args.layout, "--steps", str(args.client_shard_steps), "--warmup", "3",
