@@ -1292,21 +1292,20 @@ def cpu_baseline(wl, budget_s, full=False):
                   f"host has {os.cpu_count()} cpus, affinity {aff}, NumPy ufuncs single-threaded",
     }
     if wl["strategy"] == "fedavg":
-        out["threaded_variant"] = _cpu_threaded(pus, n_samples, nbytes, min(CPU_THREADS, aff or 1))
+        out["threaded_variant"] = _cpu_threaded(fedavg_reference_structure, pus, n_samples, nbytes,
+                                                min(CPU_THREADS, aff or 1))
     return out
 
 
 CPU_THREADS = 16  # the host share of one GPU on the test boxes
 
 
-def _cpu_threaded(pus, n_samples, nbytes, threads):
+def _cpu_threaded(reduce_fn, pus, n_samples, nbytes, threads):
     """SURVEY.md §8(d)'s optional multi-core CPU figure, NOT the reference: the same per-element
-    arithmetic (the oracle's call structure) over element chunks of the layers, the chunks spread
+    arithmetic (``reduce_fn``: cpu_baseline's oracle call structure) over element chunks of the layers, the chunks spread
     over ``threads`` threads (NumPy releases the GIL inside its ufuncs).  Chunks keep >= 2 elements,
     and numel == 1 layers stay whole, so no chunk changes NumPy's summation order."""
     from concurrent.futures import ThreadPoolExecutor
-
-    from oracle import fedavg_reference_structure
 
     total = sum(a.size for a in pus[0])
     target = max(2, total // (4 * threads))
@@ -1330,7 +1329,7 @@ def _cpu_threaded(pus, n_samples, nbytes, threads):
 
     def run():
         with ThreadPoolExecutor(len(views)) as ex:
-            list(ex.map(lambda v: fedavg_reference_structure(v, n_samples), views))
+            list(ex.map(lambda v: reduce_fn(v, n_samples), views))
 
     times = []
     for _ in range(3):

@@ -106,5 +106,7 @@ def test_cpu_threaded_variant_is_labelled():
     rng = np.random.default_rng(0)
     shapes = [(1,), (7,), (3, 5), (1000,), (1, 1)]
     pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(5)]
-    res = bench._cpu_threaded(pus, [3, 1, 4, 1, 5], 1000, 3)
+    from oracle import fedavg_reference_structure
+
+    res = bench._cpu_threaded(fedavg_reference_structure, pus, [3, 1, 4, 1, 5], 1000, 3)
     assert "not the reference" in res["kind"] and 1 <= res["cores"] <= 3 and res["value"] > 0
