@@ -214,7 +214,25 @@ def read_traffic(args, sha):
 # process group (N > 1)
 # ======================================================================================
 PG_TIMEOUT_S = 300  # a stuck collective or exchange ends the rank instead of holding the lease
-CLIENT_SHARD_DEADLINE_S = 240  # the client-shard leg of an N > 1 line, set-up to spot check
+CLIENT_SHARD_DEADLINE_S = 180  # one client-shard leg of an N > 1 line, set-up to spot check (normally 30-60 s)
+# The whole N > 1 line (parameter-range value + its legs) finishes within this many seconds of the
+# rank's start, under the driver's 600 s limit: each leg gets what is left of it (minus what the
+# legs after it and the final line need), and a leg with too little left is skipped, not started.
+LINE_BUDGET_S = float(os.environ.get("BENCH_LINE_BUDGET_S", "480"))
+LEG_MIN_S = 45  # below this a leg cannot finish; it is reported as skipped
+_T_START = time.monotonic()
+
+
+def line_time_left() -> float:
+    """Seconds left of this rank's LINE_BUDGET_S."""
+    return LINE_BUDGET_S - (time.monotonic() - _T_START)
+
+
+def leg_deadline(cap: float, reserve: float) -> float:
+    """The deadline of the next leg: at most ``cap``, and no later than the line budget minus
+    ``reserve`` (what the legs after it and the final line need); 0 means skip the leg."""
+    d = min(cap, line_time_left() - reserve)
+    return d if d >= LEG_MIN_S else 0.0
 
 
 def pg_kwargs() -> dict:
@@ -521,7 +539,7 @@ def measure_param_range(args, ctx):
     return line, {"kern_ms": kern_ms_max, "K": K, "M": M, "tiled": tiled}
 
 
-MULTI_DEVICE_DEADLINE_S = 240
+MULTI_DEVICE_DEADLINE_S = 180
 
 
 def multi_device_leg(args, ctx):
@@ -541,19 +559,23 @@ def multi_device_leg(args, ctx):
                                                                      "GROUP_RANK", "MASTER_ADDR", "MASTER_PORT")}
             cmd = [sys.executable, str(Path(__file__).resolve()), "--engine", "multi-device", "--gpus", str(ctx.world),
                    "--workload", args.workload, "--steps", "5", "--warmup", "1"]
+            deadline = leg_deadline(MULTI_DEVICE_DEADLINE_S, 15)
             t0 = time.perf_counter()
-            p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-            try:
-                so, se = p.communicate(timeout=MULTI_DEVICE_DEADLINE_S)
-                lines = [ln for ln in so.splitlines() if ln.startswith("{")]
-                if p.returncode != 0 or not lines:
-                    res = {"error": f"leg exited with {p.returncode}: {se[-600:]}"}
-                else:
-                    res = json.loads(lines[-1])
-            except subprocess.TimeoutExpired:
-                p.kill()  # our own child, by PID
-                p.communicate()
-                res = {"error": f"did not finish within {MULTI_DEVICE_DEADLINE_S} s"}
+            if not deadline:
+                res = {"skipped": f"line time budget ({LINE_BUDGET_S:.0f} s) spent: {line_time_left():.0f} s left"}
+            else:
+                p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                try:
+                    so, se = p.communicate(timeout=deadline)
+                    lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+                    if p.returncode != 0 or not lines:
+                        res = {"error": f"leg exited with {p.returncode}: {se[-600:]}"}
+                    else:
+                        res = json.loads(lines[-1])
+                except subprocess.TimeoutExpired:
+                    p.kill()  # our own child, by PID
+                    p.communicate()
+                    res = {"error": f"did not finish within {deadline:.0f} s"}
             res["wall_s"] = round(time.perf_counter() - t0, 1)
     ctx.barrier()
     return res
@@ -567,15 +589,31 @@ def client_shard_legs(args, ctx, info):
     interpreter with its own process group on a new port, started once this rank's parameter-range
     buffers are freed): ``client_shard`` with the native RCCL executor, ``client_shard_torch_pg``
     with the Python schedule over torch's RCCL process group.  A leg that fails, crashes or exceeds
-    CLIENT_SHARD_DEADLINE_S becomes an ``error`` field -- it can never cost the line."""
+    its deadline becomes an ``error`` field -- it can never cost the line.  Deadlines: rank 0's
+    ``leg_deadline`` (CLIENT_SHARD_DEADLINE_S within the line budget, keeping room for the legs
+    after it), broadcast so every rank agrees; after a leg that timed out on any rank the next
+    RCCL leg is skipped (it would wait on the same stuck bootstrap or exchange)."""
     import subprocess
 
     torch, dist = ctx.torch, ctx.dist
     torch.cuda.empty_cache()
+    legs = (("native", "client_shard"), ("torch", "client_shard_torch_pg"))
+    md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port(), _free_port()]] if ctx.rank == 0 else [None]
     dist.broadcast_object_list(ports, src=0)
     out = {}
-    for (executor, key), port in zip((("native", "client_shard"), ("torch", "client_shard_torch_pg")), ports[0]):
+    stuck = False
+    for i, ((executor, key), port) in enumerate(zip(legs, ports[0])):
+        later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
+        dl = [0.0 if stuck else leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
+        dist.broadcast_object_list(dl, src=0)
+        deadline = dl[0]
+        if not deadline:
+            if ctx.rank == 0:
+                out[key] = {"skipped": "the previous RCCL leg did not finish" if stuck else
+                            f"line time budget ({LINE_BUDGET_S:.0f} s): {line_time_left():.0f} s left",
+                            "executor": executor}
+            continue
         env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
         env.update(RANK=str(ctx.rank), WORLD_SIZE=str(ctx.world), LOCAL_RANK=str(ctx.device.index),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -592,7 +630,7 @@ def client_shard_legs(args, ctx, info):
         t0 = time.perf_counter()
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         try:
-            so, se = p.communicate(timeout=CLIENT_SHARD_DEADLINE_S)
+            so, se = p.communicate(timeout=deadline)
             res = None
             if ctx.rank == 0:
                 lines = [ln for ln in so.splitlines() if ln.startswith("{")]
@@ -604,13 +642,14 @@ def client_shard_legs(args, ctx, info):
         except subprocess.TimeoutExpired:
             p.kill()  # this rank's own child, by PID
             p.communicate()
-            res = {"error": f"did not finish within {CLIENT_SHARD_DEADLINE_S} s"}
+            res = {"error": f"did not finish within {deadline:.0f} s"}
         if res is not None:
             res["wall_s"] = round(time.perf_counter() - t0, 1)
             res["executor"] = executor
         # every rank's leg is over before the next one starts (errors are per rank: gather them)
         errs = [None] * ctx.world
         dist.all_gather_object(errs, (res or {}).get("error"))
+        stuck = stuck or any(e and e.startswith("did not finish") for e in errs)
         if ctx.rank == 0:
             bad = {r: e for r, e in enumerate(errs) if e}
             if bad and "error" not in res:

@@ -56,6 +56,26 @@ def test_pg_kwargs_has_a_timeout():
     assert 0 < t <= 600 and bench.CLIENT_SHARD_DEADLINE_S < t and bench.MULTI_DEVICE_DEADLINE_S < t
 
 
+def test_line_budget_bounds_the_legs(monkeypatch):
+    """The N > 1 line finishes under the driver's 600 s limit whatever its legs do: every leg's
+    deadline fits in what is left of LINE_BUDGET_S after the legs behind it, and a leg with less
+    than LEG_MIN_S left is skipped (deadline 0), not started."""
+    import time
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    assert bench.LINE_BUDGET_S + bench.PG_TIMEOUT_S / 10 < 600
+    monkeypatch.setattr(bench, "_T_START", time.monotonic())
+    d = bench.leg_deadline(bench.CLIENT_SHARD_DEADLINE_S, 100)
+    assert d == bench.CLIENT_SHARD_DEADLINE_S
+    monkeypatch.setattr(bench, "_T_START", time.monotonic() - (bench.LINE_BUDGET_S - 200))
+    d = bench.leg_deadline(bench.CLIENT_SHARD_DEADLINE_S, 100)
+    assert 95 <= d <= 100  # 200 s left, 100 kept for what follows
+    monkeypatch.setattr(bench, "_T_START", time.monotonic() - (bench.LINE_BUDGET_S - 60))
+    assert bench.leg_deadline(bench.CLIENT_SHARD_DEADLINE_S, 30) == 0.0  # 30 s < LEG_MIN_S: skipped
+
+
 def test_default_rounds_follow_the_executor():
     """Three rounds for the native executor over >= 2 ranks, else one; --rounds overrides both."""
     import argparse
