@@ -62,11 +62,14 @@ class FedAvg(Strategy):
         return FedAvgAveragedState(avg_parameters_update=averaged_states)
 
 
-def weighted_average(shared_states, state_name: str, device: Devices = None) -> List[np.ndarray]:
+def weighted_average(shared_states, state_name: str, device: Devices = None, wire: bool = True,
+                     empty_error=EmptySharedStatesError) -> List[np.ndarray]:
     """fed_avg.py:207-222 (also fed_pca.py:244-257): validation on the host, the weighted sum
-    of every layer on the GPU."""
+    of every layer on the GPU.  ``wire``: layers in the flat wire format (this package's own
+    schemas); False: plain NumPy arrays (the reference's schemas, :mod:`substrafl_amd.integration`).
+    ``empty_error``: the exception class raised for an empty list (the reference's own there)."""
     if len(shared_states) == 0:
-        raise EmptySharedStatesError(
+        raise empty_error(
             "Your shared_states is empty. Please ensure that "
             f"the train method of your algorithm returns a {state_name} object."
         )
@@ -84,5 +87,5 @@ def weighted_average(shared_states, state_name: str, device: Devices = None) -> 
     updates = [list(state.parameters_update) for state in shared_states]
     check_same_shapes(updates)
     engine = engine_for(device)
-    # substrafl_amd's own schemas already need this package to unpickle: return the flat wire format
-    return engine.fedavg(updates, n_samples, wire=True)
+    # substrafl_amd's own schemas already need this package to unpickle: the flat wire format
+    return engine.fedavg(updates, n_samples, wire=wire)

@@ -13,10 +13,9 @@ from typing import List, Optional
 
 import numpy as np
 
-from ..engine import Devices, engine_for
+from ..engine import Devices
 from ..remote import remote
 from ..schemas import ScaffoldAveragedStates, ScaffoldSharedState, StrategyName
-from .fed_avg import check_same_shapes
 from .strategy import Strategy
 
 
@@ -39,9 +38,6 @@ class Scaffold(Strategy):
     @property
     def name(self) -> StrategyName:
         return StrategyName.SCAFFOLD
-
-    def _engine(self):
-        return engine_for(self._device)
 
     def _check_shared_states(self, shared_states: List[ScaffoldSharedState]) -> None:
         """Host-decidable half of scaffold.py:168-202 (types, list lengths, shapes of ``c``);
@@ -89,17 +85,9 @@ class Scaffold(Strategy):
     def avg_shared_states(self, shared_states: List[ScaffoldSharedState]) -> ScaffoldAveragedStates:
         """Scaffold server step (scaffold.py:297-337): averaged weight update times
         ``aggregation_lr`` and updated server control variate, both fp64."""
-        self._check_shared_states(shared_states=shared_states)
-        cvs = [list(s.control_variate_update) for s in shared_states]
-        pus = [list(s.parameters_update) for s in shared_states]
-        c0 = list(shared_states[0].server_control_variate)
-        check_same_shapes([*cvs, c0])  # np.sum([w*cv_k ..., c]) (scaffold.py:263)
-        check_same_shapes(pus)  # np.sum([w*Δ_k ...]) (scaffold.py:293)
-        mismatches, new_c, avg = self._engine().scaffold(
-            pus, cvs, self._server_control_variates(shared_states),
-            [s.n_samples for s in shared_states], self._aggregation_lr, wire=True,
-        )
-        assert mismatches == 0, "all server_control_variate in the shared_states are not equal"
+        from ..integration import scaffold_average
+
+        new_c, avg = scaffold_average(self, shared_states, self._aggregation_lr, self._device, wire=True)
         return ScaffoldAveragedStates(server_control_variate=new_c, avg_parameters_update=avg)
 
 

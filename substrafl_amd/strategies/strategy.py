@@ -45,7 +45,7 @@ class Strategy:
             return
         from ..engine import engine_for
 
-        engine_for(getattr(self, "_device", None)).prewarm()
+        engine_for(_engine_device(self)).prewarm()
 
     def ingest_shared_states(self, method_name: str, shared_paths: Sequence, load):
         """Called by the task adapter instead of its own loading loop: loads the shared states on a
@@ -56,6 +56,11 @@ class Strategy:
             return None
         from ..engine import engine_for
 
-        dev = getattr(self, "_device", None)
-        engine = engine_for(dev)
+        engine = engine_for(_engine_device(self))
         return engine.ingest(shared_paths, kind, load)
+
+
+def _engine_device(strategy):
+    """The engine device of a mirrored strategy (``_device``) or of an ``integration.accelerate``d
+    reference class (``_fedagg_device``)."""
+    return getattr(strategy, "_fedagg_device", getattr(strategy, "_device", None))

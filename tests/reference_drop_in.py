@@ -1,0 +1,197 @@
+"""CONTAINER-ONLY checker (imports /root/reference; never runs on the GPU box): the reference's own
+experiment driver runs with ``substrafl_amd.integration.accelerate``'d strategy classes.
+
+``simulate_experiment`` (substrafl/experiment.py) drives ``accelerate(FedAvg)`` and
+``accelerate(Scaffold)`` through the reference's graph building (``perform_round``,
+``build_compute_plan``), ``@remote`` / ``RemoteStruct`` and aggregation node -- the 2-org linear
+known-answer setup of tests/golden/gen_plumbing.py -- and the final performance must equal, to the
+last bit, the one the unmodified reference produced when the G7 fixtures were captured
+(tests/golden/golden_plumbing_meta.json).  There is no GPU in this container, so the engine behind
+the accelerated methods is a test double that computes with the oracle's explicit-order
+restatement (oracle/aggregation.py, pinned bit-exact by the golden vectors); the GPU side of the
+same calls is the G7 replay in tests/test_plumbing.py.  Also checked: the generated class is
+carried by value through cloudpickle (the task process's ``RemoteStruct``), and the reference's
+error types surface unchanged.  Prints one JSON line.
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+sys.dont_write_bytecode = True  # never write into /root/reference
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(HERE / "golden"))
+from gen_golden import REF, _install_stubs  # noqa: E402
+from gen_plumbing import linear_data  # noqa: E402
+
+from oracle import fedavg_explicit, scaffold_explicit  # noqa: E402
+
+
+class OracleEngine:
+    """Test double of :class:`substrafl_amd.engine.AggregationEngine` for a GPU-less container:
+    the same two entry points, computed by the oracle; counts its calls."""
+
+    def __init__(self):
+        self.calls = {"fedavg": 0, "scaffold": 0}
+
+    def fedavg(self, parameters_updates, n_samples, wire=False):
+        assert not wire, "reference schemas take plain NumPy arrays"
+        self.calls["fedavg"] += 1
+        return fedavg_explicit(parameters_updates, n_samples)
+
+    def scaffold(self, parameters_updates, control_variate_updates, server_control_variates, n_samples,
+                 aggregation_lr, wire=False):
+        assert not wire
+        self.calls["scaffold"] += 1
+        c0 = server_control_variates[0]
+        mism = 0
+        for ci in server_control_variates[1:]:
+            for a, b in zip(c0, ci):
+                a, b = np.asarray(a), np.asarray(b)
+                mism += int(np.sum(~((a == b) | (np.isnan(a) & np.isnan(b)))))
+        new_c, avg = scaffold_explicit(parameters_updates, control_variate_updates, c0, n_samples, aggregation_lr)
+        return mism, new_c, avg
+
+
+def main():
+    if not REF.exists():
+        raise SystemExit("reference_drop_in.py needs /root/reference (build container only)")
+    _install_stubs()
+    import types
+
+    sys.modules["substra"].BackendType = types.SimpleNamespace(REMOTE="remote", LOCAL_SUBPROCESS="subprocess",
+                                                               LOCAL_DOCKER="docker")
+    sys.path.insert(0, str(REF))
+    import cloudpickle
+    import torch
+
+    import substrafl.nodes.test_data_node as tdn
+    import substrafl.nodes.train_data_node as trn
+    from substrafl import exceptions as ref_exceptions
+    from substrafl import simulate_experiment
+    from substrafl.algorithms.pytorch import TorchFedAvgAlgo, TorchScaffoldAlgo
+    from substrafl.evaluation_strategy import EvaluationStrategy
+    from substrafl.index_generator import NpIndexGenerator
+    from substrafl.nodes import AggregationNode, TestDataNode, TrainDataNode
+    from substrafl.remote.operations import RemoteOperation
+    from substrafl.strategies import FedAvg, Scaffold
+    from substrafl.strategies.schemas import FedAvgSharedState
+
+    import substrafl_amd.integration as integ
+    import substrafl_amd.strategies.fed_avg as mirror_fedavg
+
+    engine = OracleEngine()
+    integ.engine_for = mirror_fedavg.engine_for = lambda device=None: engine
+
+    data = {}
+    trn.preload_data = tdn.preload_data = lambda client, data_manager_key, data_sample_keys: data[data_sample_keys[0]]
+
+    class Client:
+        backend_mode = "subprocess"
+
+    class TorchDataset(torch.utils.data.Dataset):  # tests/conftest.py:424-441
+        def __init__(self, data_from_opener, is_inference=False):
+            self.x, self.y, self.is_inference = data_from_opener[0], data_from_opener[1], is_inference
+
+        def __getitem__(self, index):
+            x = torch.from_numpy(self.x[index]).float()
+            if self.is_inference:
+                return x
+            return x, torch.as_tensor(self.y[index]).float()
+
+        def __len__(self):
+            return len(self.x)
+
+    class Perceptron(torch.nn.Module):  # tests/conftest.py:322-341
+        def __init__(self):
+            super().__init__()
+            self.linear1 = torch.nn.Linear(2, 1)
+
+        def forward(self, x):
+            return self.linear1(x)
+
+    def mae_score(data_from_opener, predictions):  # tests/conftest.py:133-144
+        return abs(np.array(predictions) - data_from_opener[1]).mean()
+
+    split = lambda d: (d[:, :-1], d[:, -1:])  # noqa: E731
+    train = [split(linear_data(n_col=3, n_samples=1024, weights_seed=42, noise_seed=i)) for i in range(2)]
+    test = split(linear_data(n_col=3, n_samples=64, weights_seed=42, noise_seed=42))
+
+    def run(strategy_cls, algo_base, rounds=3):
+        data.clear()
+        for i, d in enumerate(train):
+            data[f"train{i}"] = d
+        data["test0"] = test
+        torch.manual_seed(42)
+        model = Perceptron()
+        nig = NpIndexGenerator(batch_size=32, num_updates=100)
+
+        class MyAlgo(algo_base):
+            def __init__(self):
+                super().__init__(optimizer=torch.optim.SGD(model.parameters(), lr=0.1), criterion=torch.nn.MSELoss(),
+                                 model=model, index_generator=nig, dataset=TorchDataset)
+
+        strategy = strategy_cls(algo=MyAlgo(), metric_functions=mae_score)
+        perf, _, _ = simulate_experiment(
+            client=Client(), strategy=strategy,
+            train_data_nodes=[TrainDataNode(f"org{i}", "ds", [f"train{i}"]) for i in range(2)],
+            evaluation_strategy=EvaluationStrategy(test_data_nodes=[TestDataNode("org0", "ds", ["test0"])],
+                                                   eval_rounds=[0, rounds]),
+            aggregation_node=AggregationNode("org0"), num_rounds=rounds, clean_models=True,
+            experiment_folder=tempfile.mkdtemp())
+        return float(perf.performance[-1]), strategy
+
+    meta = json.loads((HERE / "golden" / "golden_plumbing_meta.json").read_text())["configs"]
+    out = {}
+    AccFedAvg, AccScaffold = integ.accelerate(FedAvg), integ.accelerate(Scaffold)
+    assert issubclass(AccFedAvg, FedAvg) and issubclass(AccScaffold, Scaffold)
+    assert AccScaffold._aggregation_methods == {"avg_shared_states": "scaffold"}
+    assert callable(AccFedAvg.prewarm_aggregation) and callable(AccFedAvg.ingest_shared_states)
+    perf, strat = run(AccFedAvg, TorchFedAvgAlgo)
+    out["linear_fedavg"] = {"final": perf, "reference_final": meta["linear_fedavg"]["final_performance"],
+                            "engine_calls": engine.calls["fedavg"]}
+    perf, _ = run(AccScaffold, TorchScaffoldAlgo)
+    out["linear_scaffold"] = {"final": perf, "reference_final": meta["linear_scaffold"]["final_performance"],
+                              "engine_calls": engine.calls["scaffold"]}
+
+    # @remote: without _skip the call is a RemoteOperation naming the generated class, which
+    # cloudpickle carries by value (the task process re-creates it from the RemoteStruct)
+    states = [FedAvgSharedState(n_samples=n, parameters_update=[np.full((3,), float(n), np.float32)])
+              for n in (1, 3)]
+    op = strat.avg_shared_states(shared_states=states)
+    assert isinstance(op, RemoteOperation) and op.remote_struct._method_name == "avg_shared_states"
+    blob = cloudpickle.dumps(op.remote_struct)
+    inst = cloudpickle.loads(blob).get_remote_instance()
+    res = inst.instance.avg_shared_states(shared_states=states, _skip=True)
+    out["remote_struct_roundtrip"] = {"bytes": len(blob), "class_by_value": b"accelerate.<locals>" in blob,
+                                      "result": [float(v) for v in res.avg_parameters_update[0]]}
+
+    # the reference's error types
+    errs = {}
+    for name, call, exc in (
+            ("empty", lambda: strat.avg_shared_states(shared_states=[], _skip=True),
+             ref_exceptions.EmptySharedStatesError),
+            ("zero_samples", lambda: strat.avg_shared_states(
+                shared_states=[FedAvgSharedState(n_samples=0, parameters_update=[np.ones(2, np.float32)])] * 2,
+                _skip=True), ZeroDivisionError),
+            ("layer_count", lambda: strat.avg_shared_states(
+                shared_states=[FedAvgSharedState(n_samples=1, parameters_update=[np.ones(2, np.float32)]),
+                               FedAvgSharedState(n_samples=1, parameters_update=[])], _skip=True), AssertionError)):
+        try:
+            call()
+            errs[name] = "no exception"
+        except exc:
+            errs[name] = exc.__name__
+    out["errors"] = errs
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

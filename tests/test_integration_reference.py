@@ -1,0 +1,35 @@
+"""``substrafl_amd.integration.accelerate`` under the reference's own experiment driver
+(tests/reference_drop_in.py, run in a child process: it installs import stubs for the absent
+``substra`` packages and imports /root/reference, so it runs in the build container only)."""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+HERE = Path(__file__).resolve().parent
+
+pytestmark = pytest.mark.skipif(not Path("/root/reference/substrafl").exists(),
+                                reason="needs the reference source (build container only)")
+
+
+def test_accelerated_strategies_in_simulate_experiment(tmp_path):
+    """accelerate(FedAvg) / accelerate(Scaffold) run through simulate_experiment (graph building,
+    @remote, aggregation node of the reference) with results bit-identical to the unmodified
+    reference run of the G7 capture; the generated class travels by value in a RemoteStruct;
+    the reference's exception types surface unchanged."""
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, str(HERE / "reference_drop_in.py")], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    for name in ("linear_fedavg", "linear_scaffold"):
+        assert res[name]["final"] == res[name]["reference_final"], res[name]  # bit for bit
+        assert res[name]["engine_calls"] == 3  # one aggregation per round went through the engine
+    assert res["remote_struct_roundtrip"]["class_by_value"]
+    assert res["remote_struct_roundtrip"]["result"] == [2.5, 2.5, 2.5]  # (1*1 + 3*3) / 4
+    assert res["errors"] == {"empty": "EmptySharedStatesError", "zero_samples": "ZeroDivisionError",
+                             "layer_count": "AssertionError"}
