@@ -1,3 +1,1 @@
-"""Client-side surface the aggregation path touches (mirror of substrafl/algorithms/)."""
-
-from .algo import Algo  # noqa: F401
+"""Client-side bucket operations (substrafl/algorithms/pytorch/weight_manager.py mirror)."""
