@@ -75,6 +75,16 @@ def kind_of(np_dtype) -> str:
     raise NotImplementedError(f"no aggregation kernel for dtype {d}")
 
 
+def native_byte_order(rows):
+    """``rows`` (lists of arrays) with every array in non-native byte order (a pickle written on
+    a big-endian host) replaced by a native copy -- exact, and the byte order NumPy's ufuncs give
+    the reference's results anyway; ``rows`` itself when every array is native (the usual case)."""
+    if all(np.asarray(a).dtype.isnative for row in rows for a in row):
+        return rows
+    return [[a if np.asarray(a).dtype.isnative else np.asarray(a).astype(np.asarray(a).dtype.newbyteorder("="))
+             for a in row] for row in rows]
+
+
 def fedavg_weights(n_samples: Sequence[int], kind: str) -> np.ndarray:
     """``fl(n_k / n)``: Python-int total, double division, then rounded to the product type
     (fed_avg.py:217,221; a Python float is a weak scalar under NEP 50)."""
@@ -618,6 +628,7 @@ class AggregationEngine:
         NumPy scalars, like ``np.sum``): plain views of one owned array, or with ``wire``
         :class:`wire.BucketArray` layers that pickle as one buffer."""
         t_start = time.perf_counter()
+        parameters_updates = native_byte_order(parameters_updates)
         s = self.session()
         self.last_timing = tm = {}
         K = len(parameters_updates)
@@ -718,6 +729,8 @@ class AggregationEngine:
         count) and scaffold.py:297-337 (fp64 reductions).  Returns
         ``(mismatches, new_server_control_variate, avg_parameters_update)``."""
         t_start = time.perf_counter()
+        parameters_updates, control_variate_updates, server_control_variates = (
+            native_byte_order(x) for x in (parameters_updates, control_variate_updates, server_control_variates))
         s = self.session()
         self.last_timing = tm = {}
         K = len(parameters_updates)

@@ -35,8 +35,8 @@ import numpy as np
 
 from . import _native, runtime
 from .engine import (TILED_KINDS, AggregationEngine, FedAvgPlan, ScaffoldPlan, TiledFedAvgPlan, direct_rows,
-                     equal_count, fedavg_weights, kind_of, scaffold_weights, serialized, tiled_elems,
-                     tiled_recommended, tiled_tile)
+                     equal_count, fedavg_weights, kind_of, native_byte_order, scaffold_weights, serialized,
+                     tiled_elems, tiled_recommended, tiled_tile)
 from .layout import ROW_ALIGN_BYTES, BucketLayout
 from .sharding import SHARD_ALIGN, shard_bounds
 
@@ -194,6 +194,7 @@ class MultiDeviceEngine:
                wire: bool = False) -> List[np.ndarray]:
         """fed_avg.py:217-222 for validated inputs, sharded by parameter range over the devices."""
         t_start = time.perf_counter()
+        parameters_updates = native_byte_order(parameters_updates)
         K = len(parameters_updates)
         L = len(parameters_updates[0])
         if L == 0:
@@ -263,6 +264,8 @@ class MultiDeviceEngine:
         """scaffold.py:193-196 (c equality, as a mismatch count) and :297-337 (fp64 sums), sharded by
         parameter range.  Returns ``(mismatches, new_server_control_variate, avg_parameters_update)``."""
         t_start = time.perf_counter()
+        parameters_updates, control_variate_updates, server_control_variates = (
+            native_byte_order(x) for x in (parameters_updates, control_variate_updates, server_control_variates))
         K = len(parameters_updates)
         L = len(parameters_updates[0])
         if L == 0:

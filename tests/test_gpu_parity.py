@@ -1484,3 +1484,34 @@ def test_short_buckets_many_clients_vs_torch_sequential(torch_gpu, kind, M):
     torch.cuda.synchronize()
     assert torch.equal(out[:M].view(torch.int32), acc.view(torch.int32))
     assert torch.equal(half.view(torch.int32), acc.view(torch.int32))
+
+
+@pytest.mark.parametrize("device", [None, "all"])
+def test_non_native_byte_order_layers(torch_gpu, dummy_algo_class, device):
+    """Arrays in big-endian byte order (a pickle written on a big-endian host): NumPy's ufuncs
+    read them by value and give native-order results, so the engine converts them on the host
+    (exactly) before staging -- FedAvg fp32/fp64/int layers and Scaffold, one GPU and the
+    multi-device engine."""
+    from substrafl_amd.schemas import FedAvgSharedState, ScaffoldSharedState
+    from substrafl_amd.strategies import FedAvg, Scaffold
+
+    rng = np.random.default_rng(11)
+    K = 6
+    mk = lambda s, dt: (rng.standard_normal(s) * 30).astype(dt)  # noqa: E731
+    pus = [[mk((40, 3), ">f4"), mk((1,), ">f4"), mk((17,), ">f8"), mk((5,), ">i4"), mk((9,), np.float32)]
+           for _ in range(K)]
+    ns = [int(v) for v in rng.integers(1, 5000, K)]
+    states = [FedAvgSharedState(n_samples=n, parameters_update=p) for n, p in zip(ns, pus)]
+    got = FedAvg(algo=dummy_algo_class(), device=device).avg_shared_states(states, _skip=True).avg_parameters_update
+    _assert_same(got, fedavg_reference_structure(pus, ns))
+
+    shapes = [(13, 7), (1,), (130,)]
+    sk = lambda: [mk(s, ">f4") for s in shapes]  # noqa: E731
+    dpus, cvs, c = [sk() for _ in range(K)], [sk() for _ in range(K)], sk()
+    sstates = [ScaffoldSharedState(parameters_update=dpus[k], control_variate_update=cvs[k], n_samples=ns[k],
+                                   server_control_variate=c) for k in range(K)]
+    res = Scaffold(algo=dummy_algo_class(), aggregation_lr=0.7, device=device).avg_shared_states(
+        shared_states=sstates, _skip=True)
+    rc, ra = scaffold_reference_structure(dpus, cvs, c, ns, 0.7)
+    _assert_same(res.server_control_variate, rc)
+    _assert_same(res.avg_parameters_update, ra)
