@@ -355,6 +355,11 @@ def main():
                                        t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
         except Exception as e:  # noqa: BLE001 -- reported in the parent's line
             res = {"error": f"{type(e).__name__}: {e}"[:800]}
+        if args.executor == "torch" and world > 1 and "error" not in res:
+            try:  # the xGMI rates the schedule model needs, measured on this node (tools/lockstep_model.py)
+                res["xgmi_p2p"] = p2p_probe(torch, dist, rank, world, device, ctx.barrier, ctx.max_over_ranks)
+            except Exception as e:  # noqa: BLE001
+                res["xgmi_p2p"] = {"error": f"{type(e).__name__}: {e}"[:400]}
         if rank == 0:
             print(json.dumps(res), flush=True)
     elif client_shard:
@@ -875,6 +880,51 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     return res
 
 
+def p2p_probe(torch, dist, rank, world, device, barrier, max_over_ranks, ring_mib=256, peers_mib=64, iters=5):
+    """Point-to-point rates of this node's GPU links over the process group's RCCL (gloo on the
+    CPU rehearsal): ``ring``: every rank sends ``ring_mib`` to rank r + 1 while receiving from
+    r - 1 (one link per direction, all links of the ring busy at once -- the relay's pattern);
+    ``all_peers``: every rank sends ``peers_mib`` to each of its G - 1 peers and receives as much
+    from each, in one batch (every link of the mesh busy -- the striped schedule's pattern).
+    GB/s per rank and direction, over the slowest rank."""
+    dt = torch.float32
+    out = {"iters": iters}
+
+    def timed(fn):
+        fn()  # connects the peers and warms the path
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        return max_over_ranks([(time.perf_counter() - t0) / iters])[0]
+
+    def run(ops):
+        for w in dist.batch_isend_irecv(ops) or []:
+            w.wait()
+
+    n = ring_mib << 18
+    send, recv = torch.ones(n, dtype=dt, device=device), torch.empty(n, dtype=dt, device=device)
+    ring = [dist.P2POp(dist.isend, send, (rank + 1) % world), dist.P2POp(dist.irecv, recv, (rank - 1) % world)]
+    sec = timed(lambda: run(ring))
+    out["ring"] = {"MiB": ring_mib, "ms": round(sec * 1e3, 3), "GBps_per_direction": round(n * 4 / sec / 1e9, 2)}
+    del send, recv
+    m = peers_mib << 18
+    peers = [p for p in range(world) if p != rank]
+    sends = torch.ones((len(peers), m), dtype=dt, device=device)
+    recvs = torch.empty((len(peers), m), dtype=dt, device=device)
+    ops = [dist.P2POp(dist.isend, sends[i], p) for i, p in enumerate(peers)] + \
+          [dist.P2POp(dist.irecv, recvs[i], p) for i, p in enumerate(peers)]
+    sec = timed(lambda: run(ops))
+    out["all_peers"] = {"MiB_per_peer": peers_mib, "peers": len(peers), "ms": round(sec * 1e3, 3),
+                        "GBps_per_rank_egress": round(len(peers) * m * 4 / sec / 1e9, 2),
+                        "GBps_per_link_direction": round(m * 4 / sec / 1e9, 2)}
+    return out
+
+
 def _rounds(args):
     from substrafl_amd import lockstep
 
@@ -1214,6 +1264,10 @@ def rehearse(args, world, rank):
         elapsed = float(t[0])
         if args.client_shard != "off":
             cs = _rehearse_client_shard(args, world, rank)
+            probe = p2p_probe(torch, dist, rank, world, torch.device("cpu"), dist.barrier,
+                              lambda v: [float(x) for x in _all_max(torch, dist, v)], ring_mib=1, peers_mib=1, iters=2)
+            if cs is not None:
+                cs["xgmi_p2p"] = probe
     if rank == 0:
         line = {"metric": METRIC + " [CPU rehearsal of the launcher: not a measurement]",
                 "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -1225,6 +1279,12 @@ def rehearse(args, world, rank):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _all_max(torch, dist, vals):
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
 
 
 def _rehearse_client_shard(args, world, rank):

@@ -45,6 +45,8 @@ def test_plain_gpus_2_launches_two_ranks():
     assert all(k in cs for k in CLIENT_SHARD_FIELDS)
     assert cs["combine"] == "striped" and cs["scaling"] == "weak" and cs["bit_exact_by_construction"]
     assert cs["parity"]["mismatches"] == 0 and cs["schedule"]["steps"] == 4
+    probe = cs["xgmi_p2p"]  # the link-rate probe the N > 1 GPU line carries (here over gloo)
+    assert probe["ring"]["GBps_per_direction"] > 0 and probe["all_peers"]["peers"] == 1
 
 
 def test_pg_kwargs_has_a_timeout():
