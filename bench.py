@@ -596,8 +596,8 @@ def client_shard_legs(args, ctx, info):
     with the Python schedule over torch's RCCL process group.  A leg that fails, crashes or exceeds
     its deadline becomes an ``error`` field -- it can never cost the line.  Deadlines: rank 0's
     ``leg_deadline`` (CLIENT_SHARD_DEADLINE_S within the line budget, keeping room for the legs
-    after it), broadcast so every rank agrees; after a leg that timed out on any rank the next
-    RCCL leg is skipped (it would wait on the same stuck bootstrap or exchange)."""
+    after it), broadcast so every rank agrees.  A leg that timed out does not cancel the next one
+    (the two executors share RCCL's bootstrap but not its exchange code); the budget bounds both."""
     import subprocess
 
     torch, dist = ctx.torch, ctx.dist
@@ -607,16 +607,14 @@ def client_shard_legs(args, ctx, info):
     ports = [[_free_port(), _free_port()]] if ctx.rank == 0 else [None]
     dist.broadcast_object_list(ports, src=0)
     out = {}
-    stuck = False
     for i, ((executor, key), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
-        dl = [0.0 if stuck else leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
+        dl = [leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
         dist.broadcast_object_list(dl, src=0)
         deadline = dl[0]
         if not deadline:
             if ctx.rank == 0:
-                out[key] = {"skipped": "the previous RCCL leg did not finish" if stuck else
-                            f"line time budget ({LINE_BUDGET_S:.0f} s): {line_time_left():.0f} s left",
+                out[key] = {"skipped": f"line time budget ({LINE_BUDGET_S:.0f} s): {line_time_left():.0f} s left",
                             "executor": executor}
             continue
         env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
@@ -654,7 +652,6 @@ def client_shard_legs(args, ctx, info):
         # every rank's leg is over before the next one starts (errors are per rank: gather them)
         errs = [None] * ctx.world
         dist.all_gather_object(errs, (res or {}).get("error"))
-        stuck = stuck or any(e and e.startswith("did not finish") for e in errs)
         if ctx.rank == 0:
             bad = {r: e for r, e in enumerate(errs) if e}
             if bad and "error" not in res:
