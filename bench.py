@@ -541,6 +541,8 @@ def measure_param_range(args, ctx):
     }
     if world > 1:
         line["process_group"] = {"backend": ctx.backend, "timeout_s": PG_TIMEOUT_S}
+        # the job's fraction of N x 8 TB/s (the driver computes T(1)/T(N) itself)
+        line["frac_of_n_x_hbm_peak"] = round(value / (world * HBM_PEAK_GBPS), 4)
     return line, {"kern_ms": kern_ms_max, "K": K, "M": M, "tiled": tiled}
 
 
