@@ -351,7 +351,7 @@ def main():
 
     if args.client_shard_child:  # one leg of an N > 1 line (see client_shard_legs)
         try:
-            res = measure_client_shard(args, ctx, args.combine, "weak", t1_ms=args.t1_ms or None,
+            res = measure_client_shard(args, ctx, args.combine, args.scaling, t1_ms=args.t1_ms or None,
                                        t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
         except Exception as e:  # noqa: BLE001 -- reported in the parent's line
             res = {"error": f"{type(e).__name__}: {e}"[:800]}
@@ -604,12 +604,16 @@ def client_shard_legs(args, ctx, info):
 
     torch, dist = ctx.torch, ctx.dist
     torch.cuda.empty_cache()
-    legs = (("native", "client_shard"), ("torch", "client_shard_torch_pg"))
+    # weak (every rank holds the workload's K clients: north_star's scaling target) with both
+    # executors, then strong (the workload's K clients split over the ranks: BASELINE.json's C3
+    # as written, "64 clients ... sharded across 8 MI355X" -- the xGMI-bound regime)
+    legs = (("native", "weak", "client_shard"), ("torch", "weak", "client_shard_torch_pg"),
+            ("native", "strong", "client_shard_strong"))
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
-    ports = [[_free_port(), _free_port()]] if ctx.rank == 0 else [None]
+    ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     dist.broadcast_object_list(ports, src=0)
     out = {}
-    for i, ((executor, key), port) in enumerate(zip(legs, ports[0])):
+    for i, ((executor, scaling, key), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
         dl = [leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
         dist.broadcast_object_list(dl, src=0)
@@ -626,6 +630,7 @@ def client_shard_legs(args, ctx, info):
         # interface the container cannot route never stalls ncclCommInitRank
         env.setdefault("NCCL_SOCKET_IFNAME", "lo")
         cmd = [sys.executable, str(Path(__file__).resolve()), "--client-shard-child", "--executor", executor,
+               "--scaling", scaling,
                "--gpus", str(ctx.world), "--workload", args.workload, "--combine", args.combine or "striped",
                "--layout", args.layout, "--steps", str(args.client_shard_steps), "--warmup", "3",
                "--client-shard-steps", str(args.client_shard_steps), "--t1-ms", str(info["kern_ms"]),
@@ -876,6 +881,9 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     }
     if scaling == "weak":
         res["weak_efficiency"] = round(t1_ms / ms, 4) if ms > 0 else None
+    else:  # the same K x M over the ranks: speedup over one GPU, and that over the rank count
+        res["speedup"] = round(t1_ms / ms, 4) if ms > 0 else None
+        res["strong_efficiency"] = round(t1_ms / (world * ms), 4) if ms > 0 else None
     return res
 
 
