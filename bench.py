@@ -637,6 +637,8 @@ def client_shard_legs(args, ctx, info):
                "--chunk", str(args.chunk), "--rings", str(args.rings), "--no-cpu-baseline"]
         if args.rounds:
             cmd += ["--rounds", args.rounds]
+        elif scaling == "strong":  # exchange-bound: one round is the fastest (tools/lockstep_model.py)
+            cmd += ["--rounds", "1.0"]
         t0 = time.perf_counter()
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         try:
