@@ -71,11 +71,12 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--combine", default="striped", choices=["relay", "rccl", "ordered", "striped"],
                     help="client-shard combine (the N > 1 line's client_shard leg and --mode client-shard)")
-    ap.add_argument("--client-shard", default="auto", choices=["auto", "off"],
-                    help="N > 1 param-range runs: also time the client-sharded (north-star) mode, weak, in the "
-                         "same invocation (auto: when every rank has its own GPU)")
+    ap.add_argument("--client-shard", default="auto", choices=["auto", "off", "force"],
+                    help="N > 1 param-range runs: also time the client-sharded (north-star) mode in the same "
+                         "invocation (auto: when every rank has its own GPU; force: also at N = 1, a rehearsal "
+                         "of the legs' plumbing on one GPU)")
     ap.add_argument("--client-shard-steps", type=int, default=50, help="timed steps of the client-shard leg")
-    ap.add_argument("--multi-device-leg", default="auto", choices=["auto", "off"],
+    ap.add_argument("--multi-device-leg", default="auto", choices=["auto", "off", "force"],
                     help="N > 1: also time the drop-in's one-process MultiDeviceEngine over the N GPUs "
                          "(host buckets, PCIe-inclusive; rank 0 runs it in a child process)")
     ap.add_argument("--rings", type=int, default=0, help="striped: rings (hop lengths; 0 = up to 4)")
@@ -367,12 +368,12 @@ def main():
         line = client_shard_line(args, ctx, cs)
     else:
         line, info = measure_param_range(args, ctx)
-        if world > 1 and args.client_shard != "off":
+        if (world > 1 and args.client_shard == "auto") or args.client_shard == "force":
             if own_gpus:  # the north-star mode beside it: client buckets sharded, exchanged over xGMI
                 line.update(client_shard_legs(args, ctx, info))
             else:
                 line["client_shard"] = {"skipped": f"needs one GPU per rank for RCCL ({world} ranks, {ndev} GPUs)"}
-        if world > 1 and own_gpus and args.multi_device_leg != "off":
+        if own_gpus and ((world > 1 and args.multi_device_leg == "auto") or args.multi_device_leg == "force"):
             line["multi_device"] = multi_device_leg(args, ctx)
     if rank == 0 and not args.client_shard_child:
         print(json.dumps(line), flush=True)
@@ -611,12 +612,14 @@ def client_shard_legs(args, ctx, info):
             ("native", "strong", "client_shard_strong"))
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
-    dist.broadcast_object_list(ports, src=0)
+    if ctx.world > 1:
+        dist.broadcast_object_list(ports, src=0)
     out = {}
     for i, ((executor, scaling, key), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
         dl = [leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
-        dist.broadcast_object_list(dl, src=0)
+        if ctx.world > 1:
+            dist.broadcast_object_list(dl, src=0)
         deadline = dl[0]
         if not deadline:
             if ctx.rank == 0:
@@ -659,8 +662,9 @@ def client_shard_legs(args, ctx, info):
             res["wall_s"] = round(time.perf_counter() - t0, 1)
             res["executor"] = executor
         # every rank's leg is over before the next one starts (errors are per rank: gather them)
-        errs = [None] * ctx.world
-        dist.all_gather_object(errs, (res or {}).get("error"))
+        errs = [(res or {}).get("error")] * ctx.world
+        if ctx.world > 1:
+            dist.all_gather_object(errs, (res or {}).get("error"))
         if ctx.rank == 0:
             bad = {r: e for r, e in enumerate(errs) if e}
             if bad and "error" not in res:
