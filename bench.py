@@ -79,7 +79,8 @@ def parse():
     ap.add_argument("--multi-device-leg", default="auto", choices=["auto", "off", "force"],
                     help="N > 1: also time the drop-in's one-process MultiDeviceEngine over the N GPUs "
                          "(host buckets, PCIe-inclusive; rank 0 runs it in a child process)")
-    ap.add_argument("--rings", type=int, default=0, help="striped: rings (hop lengths; 0 = up to 4)")
+    ap.add_argument("--rings", type=int, default=0, help="striped: rings / chains (0 = the default: 6 Latin "
+                    "chains at 8 ranks, 5 at 6, else up to 4 unit rings; lockstep.ring_chains)")
     ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default: three "
                     "rounds with the native executor, one with the Python one)")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
@@ -805,7 +806,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                     "elements_per_run": sorted({r.n for runs in plan.runs for r in runs})[-1:],
                     "issue": "one host thread, one communicator; exchange group t pairs only with group t of the peers"}
         if combine == "striped":
-            schedule["rings"] = lockstep.ring_multipliers(world, args.rings or None)
+            schedule["rings"] = len(lockstep.ring_chains(world, args.rings or None))
+            schedule["ring_hops"] = lockstep.ring_hops(world, args.rings or None)
             schedule["rounds"] = list(_rounds(args))
     else:
         k0, k1 = client_blocks(K, world)[block_of(rank, world)]

@@ -25,12 +25,14 @@ Two schedules:
   chunks that are pipelined down the chain.  The root idles while the chain fills: 2 (G - 1)
   steps out of C + 2 (G - 1).
 * :func:`striped_pieces` -- the striped relay: the bucket is cut into rounds x 2 chunks x G
-  stripes x R rings of pieces; piece (k, j, s, a) places block b on rank ``a (b + 1) + s mod G``
-  (a a unit of Z_G, the ring's hop length).  At step ``2 G k + 2 p + j`` EVERY rank runs block p
-  of one piece per ring -- nobody idles, no fill -- and each rank sends on R distinct xGMI links
-  at once (hops a = 1, G - 1, 3, G - 3, ...).  Stripe s ends on rank s, whose final chunks go to
-  the root in the next exchange groups; the last round's are a tail (``rounds`` weights: a small
-  last round shortens it, at the price of more steps).  Each rank holds one client block per stripe --
+  stripes x R rings of pieces; piece (k, j, s, c) places block b on rank ``c[b] + s mod G`` for
+  ring (chain) c of :func:`ring_chains`: the unit rings ``c[b] = a (b + 1)`` (a a unit of Z_G, the
+  ring's hop length) or, at G = 6 and 8, Latin chains whose hops differ between the chains at
+  every step.  At step ``2 G k + 2 p + j`` EVERY rank runs block p of one piece per ring --
+  nobody idles, no fill -- and each rank sends on R distinct xGMI links at once (G = 8: six).
+  A stripe's final chunks go from the rank that finished them to the root in the next exchange
+  groups; the last round's are a tail (``rounds`` weights: a small last round shortens it, at
+  the price of more steps).  Each rank holds one client block per stripe --
   K M / G elements, the same bytes as the plain layout.
 
 The schedule is a pure function of (M, K, G, parameters), computed identically on every rank
@@ -95,10 +97,56 @@ def ring_units(G: int) -> List[int]:
 
 
 def ring_multipliers(G: int, rings: Optional[int] = None) -> List[int]:
-    """One hop length per ring (default: as many as Z_G has units, at most 4)."""
+    """One hop length per ring of the unit family (as many as Z_G has units, at most 4)."""
     u = ring_units(G)
     n = min(len(u), 4) if rings is None else max(1, min(int(rings), len(u)))
     return u[:n]
+
+
+# Chains beyond the unit rings: G ranks visited in an order whose hop from block b to b + 1
+# differs between the chains at EVERY b (the hop rows form a Latin rectangle over 1..G-1 and each
+# row is a sequencing of Z_G: its partial sums visit every rank once), so at every step each rank
+# sends on -- and receives from -- as many distinct links as there are chains, where the unit
+# rings (constant hops 1, G-1, 3, G-3) give Z_G's units only: 4 of the 7 links at G = 8.  Found
+# by tools/latin_rings.py (exhaustive over the (G-1)! chains; G = 6: all 5 links, G = 8: 6 of
+# the 7, no 7th found; G <= 4 gains nothing over the units).  tools/lockstep_model.py, C3 weak at
+# G = 8 with three rounds: 0.92 against 0.86 for the four unit rings at 50 GB/s per link direction,
+# 0.84 against 0.78 at 40, equal from 65.
+LATIN_HOPS = {
+    6: ((1, 1, 1, 1, 1), (2, 5, 3, 5, 2), (3, 2, 2, 3, 4), (4, 3, 4, 4, 5), (5, 4, 5, 2, 3)),
+    8: ((1, 1, 1, 1, 1, 1, 1), (2, 7, 2, 2, 7, 3, 7), (3, 6, 3, 6, 4, 7, 2), (4, 5, 4, 5, 5, 4, 3),
+        (5, 2, 5, 7, 6, 5, 4), (6, 4, 7, 3, 3, 6, 6)),
+}
+
+
+def ring_chains(G: int, rings: Optional[int] = None) -> List[Tuple[int, ...]]:
+    """The chains of the striped schedule: chain c places block b on rank ``c[b] + s mod G`` for
+    stripe s.  Default: the Latin family where it has more chains than the unit rings (G = 6, 8),
+    else the unit rings (``a (b + 1)``, at most 4).  ``rings=k``: the first k unit rings while
+    Z_G has that many units, else the first k Latin chains."""
+    units = ring_units(G)
+    latin = LATIN_HOPS.get(G, ())
+    n_units = min(len(units), 4)
+    if rings is None:
+        k, use_latin = (len(latin), True) if len(latin) > n_units else (n_units, False)
+    else:
+        k = max(1, int(rings))
+        use_latin = k > len(units) and len(latin) > len(units)
+        k = min(k, len(latin) if use_latin else len(units))
+    if not use_latin:
+        return [tuple((a * (b + 1)) % G for b in range(G)) for a in units[:k]]
+    out = []
+    for hops in latin[:k]:
+        chain = [0]
+        for h in hops:
+            chain.append((chain[-1] + h) % G)
+        out.append(tuple(chain))
+    return out
+
+
+def ring_hops(G: int, rings: Optional[int] = None) -> List[List[int]]:
+    """Hop rows of :func:`ring_chains` (reporting: the links each chain uses, step by step)."""
+    return [[(c[b + 1] - c[b]) % G for b in range(G - 1)] for c in ring_chains(G, rings)]
 
 
 # Round split of the striped schedule.  More rounds shorten the last round's gather tail (each
@@ -121,8 +169,8 @@ def striped_pieces(M: int, G: int, rings: Optional[int] = None,
                    rounds: Sequence[float] = DEFAULT_ROUNDS) -> List[Piece]:
     """The striped relay (module docstring).  ``rounds``: relative sizes of the rounds (the last
     round's final chunk is the gather tail, so it is the small one)."""
-    mult = ring_multipliers(G, rings)
-    R = len(mult)
+    chains = ring_chains(G, rings)
+    R = len(chains)
     tot = float(sum(rounds)) or 1.0
     pieces: List[Piece] = []
     base = 0
@@ -130,12 +178,13 @@ def striped_pieces(M: int, G: int, rings: Optional[int] = None,
         Mk = M - base if k == len(rounds) - 1 else min(M - base, _align_up(int(M * wk / tot)))
         m = _align_up(max(1, -(-Mk // (2 * G * R)))) if Mk > 0 else 0
         for j in range(2):
-            for s in range(G):
-                for ai, a in enumerate(mult):
-                    lo = base + ((j * G + s) * R + ai) * m
+            for f in range(G):  # the pieces that END on rank f at one step are adjacent in [0, M)
+                for ai, chain in enumerate(chains):
+                    lo = base + ((j * G + f) * R + ai) * m
                     hi = min(base + Mk, lo + m)
                     if hi > lo:
-                        ranks = tuple((a * (b + 1) + s) % G for b in range(G))
+                        s = (f - chain[G - 1]) % G  # the stripe shift that ends this chain on f
+                        ranks = tuple((chain[b] + s) % G for b in range(G))
                         pieces.append(Piece(lo, hi, ranks, 2 * G * k + j))
         base += Mk
     return pieces

@@ -274,13 +274,14 @@ def test_single_work_per_batch(G, K, combine, scaffold):
 
 
 def test_ring_chains_cover_disjoint_links():
-    """G = 8: four rings whose hops are 1, 7, 3 and 5 ranks long -- every piece of ring a visits
-    every rank once, ending on its stripe's rank, and the four rings use 4 x 8 distinct directed
-    links, so each rank sends on four links at every step."""
+    """G = 8, ``rings=4``: the unit rings, hops 1, 7, 3 and 5 ranks long -- every piece of ring a
+    visits every rank once, ending on its stripe's rank, and the four rings use 4 x 8 distinct
+    directed links, so each rank sends on four links at every step."""
     G = 8
     mult = lockstep.ring_multipliers(G)
     assert mult == [1, 7, 3, 5]
-    pieces = lockstep.striped_pieces(8 * 2 * 4 * 512 * 3, G)
+    assert lockstep.ring_chains(G, 4) == [tuple((a * (b + 1)) % G for b in range(G)) for a in mult]
+    pieces = lockstep.striped_pieces(8 * 2 * 4 * 512 * 3, G, rings=4)
     links = {}
     for p in pieces:
         assert sorted(p.ranks) == list(range(G))
@@ -289,6 +290,26 @@ def test_ring_chains_cover_disjoint_links():
         links.setdefault(hop, set()).update((p.ranks[b], p.ranks[b + 1]) for b in range(G - 1))
     assert all(len(v) == G for v in links.values())
     assert len(set().union(*links.values())) == 4 * G
+
+
+@pytest.mark.parametrize("G", [2, 3, 4, 5, 6, 7, 8])
+def test_default_chains_use_distinct_links_every_step(G):
+    """The default chains (Latin at G = 6 and 8: 5 and 6 chains; the unit rings elsewhere): every
+    chain visits every rank once, and at every step the chains' hops are distinct and non-zero --
+    with the stripe shifts, each rank sends to (and receives from) R distinct peers per step."""
+    chains = lockstep.ring_chains(G)
+    assert len(chains) == {6: 5, 8: 6}.get(G, min(len(lockstep.ring_units(G)), 4))
+    for c in chains:
+        assert sorted(c) == list(range(G))
+    pieces = lockstep.striped_pieces(G * 2 * len(chains) * 512 * 2, G)
+    for t in range(1 + max(p.t0 + 2 * (G - 1) for p in pieces)):
+        sends = {}
+        for p in pieces:
+            for b in range(G - 1):
+                if p.t0 + 2 * b == t:
+                    sends.setdefault(p.ranks[b], []).append(p.ranks[b + 1])
+        for src, dsts in sends.items():
+            assert len(set(dsts)) == len(dsts) and src not in dsts, (t, src, dsts)
 
 
 @settings(max_examples=40, deadline=None)
@@ -315,11 +336,11 @@ def test_lockstep_groups_pair_exactly(M, G, rings, rounds, chunk):
         assert sum(sum(hi - lo for lo, hi, _c in p.blocks.get(0, [])) for p in plans) == M
 
 
-@pytest.mark.parametrize("G", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("G", [2, 3, 4, 5, 6, 8])
 def test_striped_every_rank_busy_every_step(G):
     """The striped schedule has no pipeline fill: at every step every rank runs ONE launch (its
     block p of one piece per ring), and every rank holds M elements' worth of client blocks."""
-    M = 2 * G * 4 * 512 * 5
+    M = 2 * G * len(lockstep.ring_chains(G)) * 512 * 5
     plans = [striped_plan(M, G, r) for r in range(G)]
     for p in plans:
         assert [len(x) for x in p.runs] == [1] * p.n_steps

@@ -174,6 +174,7 @@ def main():
     ap.add_argument("--link-GBps", type=float, default=50.0, help="one xGMI link, one direction")
     ap.add_argument("--latency-us", type=float, default=20.0, help="per exchange group")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay chunk (elements)")
+    ap.add_argument("--rings", type=int, default=0, help="striped chains (0: lockstep.ring_chains' default)")
     args = ap.parse_args()
     G, Kb, M = args.gpus, args.clients_per_gpu, args.params
     if args.hbm_GBps:
@@ -184,7 +185,7 @@ def main():
     out = {}
     schedules = {"relay": lockstep.relay_pieces(M, G, args.chunk)}
     for rounds in ((1.0,), (0.75, 0.25), (0.5, 0.3, 0.2), (0.4, 0.3, 0.2, 0.1), (0.6, 0.25, 0.15)):
-        schedules[f"striped rounds={rounds}"] = lockstep.striped_pieces(M, G, None, rounds)
+        schedules[f"striped rounds={rounds}"] = lockstep.striped_pieces(M, G, args.rings or None, rounds)
     for name, pieces in schedules.items():
         plans = [lockstep.rank_plan(pieces, G, r, cols="global" if name == "relay" else "packed") for r in range(G)]
         res = simulate(plans, "streams", 0.0, link, args.latency_us * 1e-6, run_time=rt)
@@ -192,6 +193,7 @@ def main():
         out[name] = {"steps": plans[0].n_steps, "model_ms": round(res["makespan"] * 1e3, 3),
                      "single_gpu_ms": round(t1 * 1e3, 3), "weak_efficiency": round(t1 / res["makespan"], 3)}
     print(json.dumps({"gpus": G, "clients_per_gpu": Kb, "params": M, "hbm_GBps": args.hbm_GBps,
+                      "chains": len(lockstep.ring_chains(G, args.rings or None)),
                       "link_GBps": args.link_GBps, "latency_us": args.latency_us, "schedules": out}, indent=1))
 
 
