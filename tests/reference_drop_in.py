@@ -173,6 +173,42 @@ def main():
     out["remote_struct_roundtrip"] = {"bytes": len(blob), "class_by_value": b"accelerate.<locals>" in blob,
                                       "result": [float(v) for v in res.avg_parameters_update[0]]}
 
+    # FedPCA: both aggregation methods against the unmodified reference class on the same states
+    from substrafl.algorithms.algo import Algo
+    from substrafl.strategies import FedPCA
+    from substrafl.strategies.schemas import FedPCASharedState, StrategyName
+
+    class PcaAlgo(Algo):
+        strategies = property(lambda self: list(StrategyName))
+        model = property(lambda self: None)
+
+        def train(self, data_from_opener, shared_state):  # never called here
+            return None
+
+        def predict(self, data_from_opener, shared_state):
+            return None
+
+        def load_local_state(self, path):
+            return self
+
+        def save_local_state(self, path):
+            pass
+
+    rng = np.random.default_rng(5)
+    pca_states = [FedPCASharedState(n_samples=int(n), parameters_update=[rng.standard_normal((6, 4)),
+                                                                          rng.standard_normal((3,))])
+                  for n in (17, 5, 230)]
+    ref_pca, acc_pca = FedPCA(algo=PcaAlgo()), integ.accelerate(FedPCA)(algo=PcaAlgo())
+    same = {}
+    for meth in ("avg_shared_states", "avg_shared_states_with_qr"):
+        states = pca_states if meth == "avg_shared_states" else [
+            FedPCASharedState(n_samples=st.n_samples, parameters_update=[st.parameters_update[0]]) for st in pca_states]
+        r = getattr(ref_pca, meth)(shared_states=states, _skip=True).avg_parameters_update
+        a = getattr(acc_pca, meth)(shared_states=states, _skip=True).avg_parameters_update
+        same[meth] = len(r) == len(a) and all(x.dtype == y.dtype and np.array_equal(x.view(np.uint64), y.view(np.uint64))
+                                               for x, y in zip(r, a))
+    out["fedpca_bit_identical"] = same
+
     # the reference's error types
     errs = {}
     for name, call, exc in (

@@ -31,5 +31,6 @@ def test_accelerated_strategies_in_simulate_experiment(tmp_path):
         assert res[name]["engine_calls"] == 3  # one aggregation per round went through the engine
     assert res["remote_struct_roundtrip"]["class_by_value"]
     assert res["remote_struct_roundtrip"]["result"] == [2.5, 2.5, 2.5]  # (1*1 + 3*3) / 4
+    assert res["fedpca_bit_identical"] == {"avg_shared_states": True, "avg_shared_states_with_qr": True}
     assert res["errors"] == {"empty": "EmptySharedStatesError", "zero_samples": "ZeroDivisionError",
                              "layer_count": "AssertionError"}
