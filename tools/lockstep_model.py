@@ -175,7 +175,16 @@ def main():
     ap.add_argument("--latency-us", type=float, default=20.0, help="per exchange group")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay chunk (elements)")
     ap.add_argument("--rings", type=int, default=0, help="striped chains (0: lockstep.ring_chains' default)")
+    ap.add_argument("--from-line", default="", help="a bench.py --gpus N JSON line (file): take --gpus and the link "
+                    "rate from its client_shard_torch_pg.xgmi_p2p probe (all-peers GB/s per link direction)")
     args = ap.parse_args()
+    if args.from_line:
+        line = json.loads([ln for ln in Path(args.from_line).read_text().splitlines() if ln.startswith("{")][-1])
+        probe = (line.get("client_shard_torch_pg") or {}).get("xgmi_p2p") or {}
+        rate = (probe.get("all_peers") or {}).get("GBps_per_link_direction")
+        if not rate:
+            raise SystemExit(f"{args.from_line}: no xgmi_p2p.all_peers rate in the line")
+        args.gpus, args.link_GBps = int(line["n_gpus"]), float(rate)
     G, Kb, M = args.gpus, args.clients_per_gpu, args.params
     if args.hbm_GBps:
         rt = lambda n: n * Kb * 4 / (args.hbm_GBps * 1e9)  # noqa: E731
