@@ -60,9 +60,13 @@ def rate_tbps(n: float, curve=RATE_CURVE) -> float:
 
 
 def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", compute_s_per_elem: float = 1.0,
-             link_s_per_elem: float = 0.0, latency_s: float = 0.0, run_time=None) -> Dict[str, float]:
+             link_s_per_elem: float = 0.0, latency_s: float = 0.0, run_time=None,
+             overlap: float = 1.0) -> Dict[str, float]:
     """Play every rank's kernels; returns {"makespan", "compute_max"} or raises Deadlock.
-    ``run_time(n)``: seconds of a step's launch over n elements (default n x compute_s_per_elem)."""
+    ``run_time(n)``: seconds of a step's launch over n elements (default n x compute_s_per_elem).
+    ``overlap``: the fraction of exchange group t's own time (latency + its busiest link's bytes)
+    that hides under step t's runs on the same rank; the rest is added to those runs (1.0: full
+    overlap, the ideal; tools/executor_overlap_probe.py measures it on one GPU)."""
     if run_time is None:
         run_time = lambda n: n * compute_s_per_elem  # noqa: E731
     G = len(plans)
@@ -142,7 +146,15 @@ def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", comput
                         progress = True
                 if (r, i) in start and (r, i) not in end:
                     if k["kind"] == "run":
-                        end[(r, i)] = start[(r, i)] + run_time(k["n"])
+                        extra = 0.0
+                        if overlap < 1.0:  # the part of the concurrent group t that does not hide
+                            gi = [j for j, g in enumerate(kernels[r]) if g["kind"] == "group" and g["t"] == k["t"]]
+                            if gi:
+                                per: Dict[tuple, int] = {}
+                                for _pr, _pi, n, peer in links.get((r, gi[0]), []):
+                                    per[peer] = per.get(peer, 0) + n
+                                extra = (1.0 - overlap) * (latency_s + max(per.values(), default=0) * link_s_per_elem)
+                        end[(r, i)] = start[(r, i)] + run_time(k["n"]) + extra
                         progress = True
                     else:
                         peers = links.get((r, i), [])
@@ -175,6 +187,8 @@ def main():
     ap.add_argument("--latency-us", type=float, default=20.0, help="per exchange group")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay chunk (elements)")
     ap.add_argument("--rings", type=int, default=0, help="striped chains (0: lockstep.ring_chains' default)")
+    ap.add_argument("--overlap", type=float, default=1.0, help="fraction of a group's time hidden under the "
+                    "concurrent step's runs (1: ideal; one-GPU probe with RCCL self P2P: ~0.3)")
     ap.add_argument("--from-line", default="", help="a bench.py --gpus N JSON line (file): take --gpus and the link "
                     "rate from its client_shard_torch_pg.xgmi_p2p probe (all-peers GB/s per link direction)")
     args = ap.parse_args()
@@ -197,13 +211,14 @@ def main():
         schedules[f"striped rounds={rounds}"] = lockstep.striped_pieces(M, G, args.rings or None, rounds)
     for name, pieces in schedules.items():
         plans = [lockstep.rank_plan(pieces, G, r, cols="global" if name == "relay" else "packed") for r in range(G)]
-        res = simulate(plans, "streams", 0.0, link, args.latency_us * 1e-6, run_time=rt)
+        res = simulate(plans, "streams", 0.0, link, args.latency_us * 1e-6, run_time=rt, overlap=args.overlap)
         t1 = rt(M)
         out[name] = {"steps": plans[0].n_steps, "model_ms": round(res["makespan"] * 1e3, 3),
                      "single_gpu_ms": round(t1 * 1e3, 3), "weak_efficiency": round(t1 / res["makespan"], 3)}
     print(json.dumps({"gpus": G, "clients_per_gpu": Kb, "params": M, "hbm_GBps": args.hbm_GBps,
                       "chains": len(lockstep.ring_chains(G, args.rings or None)),
-                      "link_GBps": args.link_GBps, "latency_us": args.latency_us, "schedules": out}, indent=1))
+                      "link_GBps": args.link_GBps, "latency_us": args.latency_us, "overlap": args.overlap,
+                      "schedules": out}, indent=1))
 
 
 if __name__ == "__main__":
