@@ -609,14 +609,20 @@ def client_shard_legs(args, ctx, info):
     # weak (every rank holds the workload's K clients: north_star's scaling target) with both
     # executors, then strong (the workload's K clients split over the ranks: BASELINE.json's C3
     # as written, "64 clients ... sharded across 8 MI355X" -- the xGMI-bound regime)
-    legs = (("native", "weak", "client_shard"), ("torch", "weak", "client_shard_torch_pg"),
-            ("native", "strong", "client_shard_strong"))
+    # ... and the native weak leg again with RCCL's copy-engine P2P path (NCCL_P2P_USE_CUDA_MEMCPY:
+    # the xGMI bytes moved by SDMA engines instead of RCCL's CU kernels).  On one GPU, RCCL's P2P
+    # kernels hide only ~0.3 of their time under an HBM-saturating chain kernel while SDMA copies
+    # hide 0.87-1.0 (tools/executor_overlap_probe.py, profiles/r03m_executor_overlap_probe*.jsonl):
+    # the two weak legs side by side show which engine the node's exchange should use.
+    legs = (("native", "weak", "client_shard", {}), ("torch", "weak", "client_shard_torch_pg", {}),
+            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}),
+            ("native", "strong", "client_shard_strong", {}))
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     if ctx.world > 1:
         dist.broadcast_object_list(ports, src=0)
     out = {}
-    for i, ((executor, scaling, key), port) in enumerate(zip(legs, ports[0])):
+    for i, ((executor, scaling, key, leg_env), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
         dl = [leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
         if ctx.world > 1:
@@ -633,6 +639,7 @@ def client_shard_legs(args, ctx, info):
         # one node: RCCL's bootstrap over loopback (its P2P data path is xGMI either way), so an
         # interface the container cannot route never stalls ncclCommInitRank
         env.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        env.update(leg_env)
         cmd = [sys.executable, str(Path(__file__).resolve()), "--client-shard-child", "--executor", executor,
                "--scaling", scaling,
                "--gpus", str(ctx.world), "--workload", args.workload, "--combine", args.combine or "striped",
@@ -662,6 +669,8 @@ def client_shard_legs(args, ctx, info):
         if res is not None:
             res["wall_s"] = round(time.perf_counter() - t0, 1)
             res["executor"] = executor
+            if leg_env:
+                res["env"] = dict(leg_env)
         # every rank's leg is over before the next one starts (errors are per rank: gather them)
         errs = [(res or {}).get("error")] * ctx.world
         if ctx.world > 1:

@@ -103,18 +103,20 @@ def test_default_workload_line():
 
 
 def test_n_gt_1_legs_rehearsed_on_one_gpu():
-    """The legs an N > 1 line carries (client-shard weak with the native and the torch executor,
-    client-shard strong, the one-process multi-device engine), forced at N = 1: each runs in its
+    """The legs an N > 1 line carries (client-shard weak with the native and the torch executor
+    and with RCCL's copy-engine P2P path, client-shard strong, the one-process multi-device engine), forced at N = 1: each runs in its
     child process through the same spawn / deadline / JSON plumbing and reports without error,
     bit-exact on its spot check."""
     line = _bench("--workload", "c2", "--client-shard", "force", "--multi-device-leg", "force", "--steps", "5",
                   "--warmup", "2", "--client-shard-steps", "5", "--no-cpu-baseline", timeout=400)
     for key, scaling, executor in (("client_shard", "weak", "native"), ("client_shard_torch_pg", "weak", "torch"),
+                                   ("client_shard_copy_engine", "weak", "native"),
                                    ("client_shard_strong", "strong", "native")):
         leg = line[key]
         assert "error" not in leg, leg
         assert leg["scaling"] == scaling and leg["executor"] == executor and leg["parity"]["mismatches"] == 0
         assert leg["ms_per_step"] > 0 and leg["wall_s"] > 0
     assert line["client_shard"]["weak_efficiency"] > 0 and line["client_shard_strong"]["speedup"] > 0
+    assert line["client_shard_copy_engine"]["env"] == {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}
     md = line["multi_device"]
     assert "error" not in md and md["value"] > 0 and md["n_gpus"] == 1

@@ -32,6 +32,11 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--trials", type=int, default=7)
     ap.add_argument("--grid-cap", type=int, default=0)
+    ap.add_argument("--sdma-mib", type=float, default=0.0,
+                    help="instead of RCCL: a pinned-host -> device copy of this many MiB per step on a side stream "
+                         "(hipMemcpyAsync: an SDMA engine, like RCCL's copy-engine P2P path), beside the chain runs")
+    ap.add_argument("--d2d", action="store_true", help="with --sdma-mib: a device -> device copy instead of "
+                    "host -> device (HIP picks the engine: blit kernel or SDMA)")
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="run the chain kernels on a CU-masked stream that leaves this many CUs (spread evenly "
                          "over the mask) to the communicator's RCCL kernels")
@@ -111,12 +116,38 @@ def main():
                 v.append(e0.elapsed_time(e1))
         return float(np.median(v))
 
+    if a.sdma_mib:
+        side = torch.cuda.Stream()
+        nb = int(a.sdma_mib * (1 << 20))
+        host = torch.empty(nb, dtype=torch.uint8, device="cuda") if a.d2d else \
+            torch.empty(nb, dtype=torch.uint8).pin_memory()
+        dev = torch.empty(nb, dtype=torch.uint8, device="cuda")
+
+        def execute(with_runs, with_copies):  # noqa: F811 -- the SDMA variant of the step loop
+            evs = [torch.cuda.Event() for _ in range(S + 1)]
+            for t in range(S):
+                if with_copies:
+                    evs[t].record(stream)
+                    side.wait_event(evs[t])
+                    with torch.cuda.stream(side):
+                        dev.copy_(host, non_blocking=True)
+                if with_runs:
+                    rccl._check(lib.fedagg_lockstep_execute(h, ctypes.byref(R, t * ctypes.sizeof(rccl._Run)), 1,
+                                                            None, 0, 1, None, 0, _native.FEDAGG_F32, 0,
+                                                            stream.cuda_stream), "execute")
+            if with_copies:
+                evs[S].record(side)
+                stream.wait_event(evs[S])
+        for r in runs:
+            r.step = 0
+        R = (rccl._Run * len(runs))(*runs)
     tr, tx, tb = timed(True, False), timed(False, True), timed(True, True)
     print(json.dumps({"clients": K, "elements_per_run": n, "steps": S, "msgs_per_group": 2 * a.msgs,
-                      "MiB_per_msg": a.mib, "grid_cap": a.grid_cap, "reserved_cus": a.reserve_cus, "runs_only_ms": round(tr, 4),
+                      "MiB_per_msg": a.mib, "sdma_MiB_per_step": a.sdma_mib, "copy": "d2d" if a.d2d else "h2d", "grid_cap": a.grid_cap, "reserved_cus": a.reserve_cus, "runs_only_ms": round(tr, 4),
                       "exchange_only_ms": round(tx, 4), "both_ms": round(tb, 4),
                       "overlap": round((tr + tx - tb) / min(tr, tx), 3),
-                      "exchange_GBps_alone": round(S * a.msgs * cnt * 4 / (tx / 1e3) / 1e9, 1)}), flush=True)
+                      "exchange_GBps_alone": round((S * a.sdma_mib * (1 << 20) if a.sdma_mib else S * a.msgs * cnt * 4)
+                                                   / (tx / 1e3) / 1e9, 1)}), flush=True)
     lib.fedagg_comm_destroy(h)
 
 
