@@ -37,6 +37,8 @@ def main():
                          "(hipMemcpyAsync: an SDMA engine, like RCCL's copy-engine P2P path), beside the chain runs")
     ap.add_argument("--d2d", action="store_true", help="with --sdma-mib: a device -> device copy instead of "
                     "host -> device (HIP picks the engine: blit kernel or SDMA)")
+    ap.add_argument("--nocu", action="store_true", help="with --d2d: hipMemcpyDeviceToDeviceNoCU (an SDMA "
+                    "engine instead of a blit kernel)")
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="run the chain kernels on a CU-masked stream that leaves this many CUs (spread evenly "
                          "over the mask) to the communicator's RCCL kernels")
@@ -118,6 +120,7 @@ def main():
 
     if a.sdma_mib:
         side = torch.cuda.Stream()
+        hip = ctypes.CDLL("libamdhip64.so")
         nb = int(a.sdma_mib * (1 << 20))
         host = torch.empty(nb, dtype=torch.uint8, device="cuda") if a.d2d else \
             torch.empty(nb, dtype=torch.uint8).pin_memory()
@@ -129,8 +132,14 @@ def main():
                 if with_copies:
                     evs[t].record(stream)
                     side.wait_event(evs[t])
-                    with torch.cuda.stream(side):
-                        dev.copy_(host, non_blocking=True)
+                    if a.nocu:
+                        rc = hip.hipMemcpyAsync(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(host.data_ptr()),
+                                                ctypes.c_size_t(nb), 1024, ctypes.c_void_p(side.cuda_stream))
+                        if rc:
+                            raise RuntimeError(f"hipMemcpyAsync(NoCU): {rc}")
+                    else:
+                        with torch.cuda.stream(side):
+                            dev.copy_(host, non_blocking=True)
                 if with_runs:
                     rccl._check(lib.fedagg_lockstep_execute(h, ctypes.byref(R, t * ctypes.sizeof(rccl._Run)), 1,
                                                             None, 0, 1, None, 0, _native.FEDAGG_F32, 0,
@@ -143,7 +152,7 @@ def main():
         R = (rccl._Run * len(runs))(*runs)
     tr, tx, tb = timed(True, False), timed(False, True), timed(True, True)
     print(json.dumps({"clients": K, "elements_per_run": n, "steps": S, "msgs_per_group": 2 * a.msgs,
-                      "MiB_per_msg": a.mib, "sdma_MiB_per_step": a.sdma_mib, "copy": "d2d" if a.d2d else "h2d", "grid_cap": a.grid_cap, "reserved_cus": a.reserve_cus, "runs_only_ms": round(tr, 4),
+                      "MiB_per_msg": a.mib, "sdma_MiB_per_step": a.sdma_mib, "copy": ("d2d-nocu" if a.nocu else "d2d") if a.d2d else "h2d", "grid_cap": a.grid_cap, "reserved_cus": a.reserve_cus, "runs_only_ms": round(tr, 4),
                       "exchange_only_ms": round(tx, 4), "both_ms": round(tb, 4),
                       "overlap": round((tr + tx - tb) / min(tr, tx), 3),
                       "exchange_GBps_alone": round((S * a.sdma_mib * (1 << 20) if a.sdma_mib else S * a.msgs * cnt * 4)
