@@ -614,9 +614,10 @@ def client_shard_legs(args, ctx, info):
     # kernels hide only ~0.3 of their time under an HBM-saturating chain kernel while SDMA copies
     # hide 0.87-1.0 (tools/executor_overlap_probe.py, profiles/r03m_executor_overlap_probe*.jsonl):
     # the two weak legs side by side show which engine the node's exchange should use.
+    # (last, and with a shorter deadline: RCCL's copy-engine path has never run on this node)
     legs = (("native", "weak", "client_shard", {}), ("torch", "weak", "client_shard_torch_pg", {}),
-            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}),
-            ("native", "strong", "client_shard_strong", {}))
+            ("native", "strong", "client_shard_strong", {}),
+            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}))
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     if ctx.world > 1:
@@ -624,7 +625,8 @@ def client_shard_legs(args, ctx, info):
     out = {}
     for i, ((executor, scaling, key, leg_env), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
-        dl = [leg_deadline(CLIENT_SHARD_DEADLINE_S, later)] if ctx.rank == 0 else [None]
+        cap = CLIENT_SHARD_DEADLINE_S if not leg_env else CLIENT_SHARD_DEADLINE_S / 2
+        dl = [leg_deadline(cap, later)] if ctx.rank == 0 else [None]
         if ctx.world > 1:
             dist.broadcast_object_list(dl, src=0)
         deadline = dl[0]
