@@ -83,6 +83,9 @@ def parse():
                     "chains at 8 ranks, 5 at 6, else up to 4 unit rings; lockstep.ring_chains)")
     ap.add_argument("--rounds", default="", help="striped: relative round sizes, e.g. 0.75,0.25 (default: three "
                     "rounds with the native executor, one with the Python one)")
+    ap.add_argument("--variant-rounds", default="",
+                    help="client-shard striped: also time these round splits (';'-separated, e.g. "
+                         "'1.0;0.75,0.25') over the same communicator")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
     ap.add_argument("--executor", default="native", choices=["native", "torch"],
                     help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip) or the "
@@ -615,15 +618,18 @@ def client_shard_legs(args, ctx, info):
     # hide 0.87-1.0 (tools/executor_overlap_probe.py, profiles/r03m_executor_overlap_probe*.jsonl):
     # the two weak legs side by side show which engine the node's exchange should use.
     # (last, and with a shorter deadline: RCCL's copy-engine path has never run on this node)
-    legs = (("native", "weak", "client_shard", {}), ("torch", "weak", "client_shard_torch_pg", {}),
-            ("native", "strong", "client_shard_strong", {}),
-            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}))
+    # The native weak leg also re-times the other round splits over its communicator
+    # (rounds_variants): the model's choice of three rounds assumes full overlap.
+    legs = (("native", "weak", "client_shard", {}, ["--variant-rounds", "1.0;0.75,0.25"]),
+            ("torch", "weak", "client_shard_torch_pg", {}, []),
+            ("native", "strong", "client_shard_strong", {}, []),
+            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}, []))
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     if ctx.world > 1:
         dist.broadcast_object_list(ports, src=0)
     out = {}
-    for i, ((executor, scaling, key, leg_env), port) in enumerate(zip(legs, ports[0])):
+    for i, ((executor, scaling, key, leg_env, leg_args), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
         cap = CLIENT_SHARD_DEADLINE_S if not leg_env else CLIENT_SHARD_DEADLINE_S / 2
         dl = [leg_deadline(cap, later)] if ctx.rank == 0 else [None]
@@ -647,7 +653,7 @@ def client_shard_legs(args, ctx, info):
                "--gpus", str(ctx.world), "--workload", args.workload, "--combine", args.combine or "striped",
                "--layout", args.layout, "--steps", str(args.client_shard_steps), "--warmup", "3",
                "--client-shard-steps", str(args.client_shard_steps), "--t1-ms", str(info["kern_ms"]),
-               "--chunk", str(args.chunk), "--rings", str(args.rings), "--no-cpu-baseline"]
+               "--chunk", str(args.chunk), "--rings", str(args.rings), "--no-cpu-baseline", *leg_args]
         if args.rounds:
             cmd += ["--rounds", args.rounds]
         elif scaling == "strong":  # exchange-bound: one round is the fastest (tools/lockstep_model.py)
@@ -699,10 +705,12 @@ def _synth_block(torch, kind, Kb, width, device, seed):
     return t[:Kb, :width]
 
 
-def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None):
+def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None, tr=None, variants=True):
     """One rank's part of the client-sharded reduction (sharding.py; relay / striped: the
     lockstep schedule over ONE communicator, rccl / ordered: re-associating), device-resident,
-    timed like the main line; returns the measurement as a dict (rank 0's is reported)."""
+    timed like the main line; returns the measurement as a dict (rank 0's is reported).
+    ``--variant-rounds`` (striped): the same leg re-timed over the same communicator with each
+    listed round split (``rounds_variants``; no spot check: the schedules' parity is the tests')."""
     torch, world, rank, device = ctx.torch, ctx.world, ctx.rank, ctx.device
     from substrafl_amd import lockstep
     from substrafl_amd.engine import (FedAvgPlan, ScaffoldPlan, TiledFedAvgPlan, fedavg_weights, scaffold_weights,
@@ -723,7 +731,9 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     layout = BucketLayout(list(range(len(shapes))), shapes, np.float32)
     pw = layout.pairwise_idx
     lockstep_mode = combine in ("relay", "striped")
-    if world == 1:
+    if tr is not None:
+        pass
+    elif world == 1:
         tr = LoopbackGroup(1).transport(0)
     elif args.executor == "native":
         if not lockstep_mode:
@@ -864,7 +874,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     block_ms = e0.elapsed_time(e1) / 3
     step()  # the outputs again (compute_only overwrote the root's final runs)
     torch.cuda.synchronize(device)
-    parity = _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held, outs, c, tvs)
+    parity = _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held, outs, c, tvs) \
+        if variants else None
     if t1_ms is None:  # one GPU reducing the workload's own K x M: the weak-scaling reference
         t1_ms, t1_source = _single_gpu_ms(ctx, K_per, M, kind, scaffold, layout, n_samples), \
             "this rank, one GPU over the workload's K x M (same bench, same layout policy)"
@@ -903,6 +914,23 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     else:  # the same K x M over the ranks: speedup over one GPU, and that over the rank count
         res["speedup"] = round(t1_ms / ms, 4) if ms > 0 else None
         res["strong_efficiency"] = round(t1_ms / (world * ms), 4) if ms > 0 else None
+    if variants and combine == "striped" and getattr(args, "variant_rounds", ""):
+        # the other round splits over the same communicator, this leg's buffers freed first
+        del step, compute_only, blocks, held, slots, ws, outs
+        if hasattr(tr, "_programs"):
+            tr._programs.clear()  # compiled programs hold their buffers
+        torch.cuda.empty_cache()
+        res["rounds_variants"] = []
+        for spec in args.variant_rounds.split(";"):
+            sub = argparse.Namespace(**{**vars(args), "rounds": spec})
+            try:
+                v = measure_client_shard(sub, ctx, combine, scaling, t1_ms, t1_source, tr=tr, variants=False)
+                res["rounds_variants"].append({k: v.get(k) for k in (
+                    "ms_per_step", "weak_efficiency", "speedup", "block_kernel_ms", "exchange_and_tail_ms")}
+                    | {"rounds": v["schedule"].get("rounds"), "steps_of_schedule": v["schedule"].get("steps")})
+            except Exception as e:  # noqa: BLE001 -- a variant never costs the leg
+                res["rounds_variants"].append({"rounds": spec, "error": f"{type(e).__name__}: {e}"[:300]})
+            torch.cuda.empty_cache()
     return res
 
 

@@ -118,5 +118,8 @@ def test_n_gt_1_legs_rehearsed_on_one_gpu():
         assert leg["ms_per_step"] > 0 and leg["wall_s"] > 0
     assert line["client_shard"]["weak_efficiency"] > 0 and line["client_shard_strong"]["speedup"] > 0
     assert line["client_shard_copy_engine"]["env"] == {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}
+    variants = line["client_shard"]["rounds_variants"]  # the other round splits, same communicator
+    assert [v["rounds"] for v in variants] == [[1.0], [0.75, 0.25]], variants
+    assert all("error" not in v and v["ms_per_step"] > 0 for v in variants), variants
     md = line["multi_device"]
     assert "error" not in md and md["value"] > 0 and md["n_gpus"] == 1
