@@ -87,9 +87,10 @@ def parse():
                     help="client-shard striped: also time these round splits (';'-separated, e.g. "
                          "'1.0;0.75,0.25') over the same communicator")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
-    ap.add_argument("--executor", default="native", choices=["native", "torch"],
-                    help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip) or the "
-                         "Python schedule over torch.distributed's RCCL process group")
+    ap.add_argument("--executor", default="native", choices=["native", "torch", "push"],
+                    help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip), the "
+                         "Python schedule over torch.distributed's RCCL process group, or the push executor "
+                         "(substrafl_amd/push.py: chain kernels storing into IPC-mapped peer slots, fp32 rows)")
     ap.add_argument("--client-shard-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--t1-ms", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
@@ -623,7 +624,8 @@ def client_shard_legs(args, ctx, info):
     legs = (("native", "weak", "client_shard", {}, ["--variant-rounds", "1.0;0.75,0.25"]),
             ("torch", "weak", "client_shard_torch_pg", {}, []),
             ("native", "strong", "client_shard_strong", {}, []),
-            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}, []))
+            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}, []),
+            ("push", "weak", "client_shard_push", {}, []))
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     if ctx.world > 1:
@@ -631,7 +633,7 @@ def client_shard_legs(args, ctx, info):
     out = {}
     for i, ((executor, scaling, key, leg_env, leg_args), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
-        cap = CLIENT_SHARD_DEADLINE_S if not leg_env else CLIENT_SHARD_DEADLINE_S / 2
+        cap = CLIENT_SHARD_DEADLINE_S if not (leg_env or executor == "push") else CLIENT_SHARD_DEADLINE_S / 2
         dl = [leg_deadline(cap, later)] if ctx.rank == 0 else [None]
         if ctx.world > 1:
             dist.broadcast_object_list(dl, src=0)
@@ -735,17 +737,22 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
         pass
     elif world == 1:
         tr = LoopbackGroup(1).transport(0)
-    elif args.executor == "native":
+    elif args.executor in ("native", "push"):
         if not lockstep_mode:
-            raise ValueError(f"the native executor runs the lockstep schedules (relay, striped), not {combine}")
-        from substrafl_amd.rccl import RcclTransport
+            raise ValueError(f"the {args.executor} executor runs the lockstep schedules (relay, striped), not {combine}")
+        if args.executor == "push":
+            from substrafl_amd.push import PushTransport
 
-        tr = RcclTransport()
+            tr = PushTransport()
+        else:
+            from substrafl_amd.rccl import RcclTransport
+
+            tr = RcclTransport()
     else:
         tr = DistTransport()
     ops = GpuShardOps()
     stream = ctx.stream
-    mode = {"auto": "auto", "tiles": True, "rows": False}[args.layout]
+    mode = {"auto": "auto", "tiles": True, "rows": False}[args.layout] if args.executor != "push" else False
     w_all = fedavg_weights(n_samples, kind) if not scaffold else scaffold_weights(n_samples)
     gc = torch.Generator(device=device)
     gc.manual_seed(4242)
@@ -903,7 +910,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
         "single_gpu_ms": round(t1_ms, 5),
         "single_gpu_source": t1_source,
         "bit_exact_by_construction": combine in ("relay", "striped"),
-        "executor": ("native RCCL (csrc/lockstep.hip)" if getattr(tr, "native", False) else
+        "executor": ("push (IPC-mapped peer slots, substrafl_amd/push.py)" if getattr(tr, "push", False) else
+                     "native RCCL (csrc/lockstep.hip)" if getattr(tr, "native", False) else
                      "Python schedule over torch.distributed" if world > 1 else "one rank (no exchange)"),
         "schedule": schedule,
         "hip_streams_per_rank": "2 (compute + the communicator's) <= GPU_MAX_HW_QUEUES = 4",
@@ -983,7 +991,7 @@ def _rounds(args):
     from substrafl_amd import lockstep
 
     if not args.rounds:  # the schedule's default for the executor (lockstep.py)
-        return lockstep.default_rounds(args.gpus, args.executor == "native")
+        return lockstep.default_rounds(args.gpus, args.executor in ("native", "push"))
     return tuple(float(x) for x in args.rounds.split(","))
 
 

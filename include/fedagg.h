@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 11
+#define FEDAGG_ABI_VERSION 12
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -277,6 +277,44 @@ const char* fedagg_comm_last_error(void);
 int fedagg_lockstep_execute(fedagg_comm* comm, const fedagg_lockstep_run* runs, int nruns,
                             const fedagg_lockstep_msg* msgs, int nmsgs, int ngroups, void* ws, uint64_t ws_count,
                             int ws_kind, int root, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Push executor of the same schedules (substrafl_amd/push.py, DESIGN.md §6 "Push"): no exchange
+ * kernels.  Each run's chain kernel writes its accumulator straight into the consumer's slot (or
+ * the root's output) through an IPC mapping over xGMI, its input accumulator read as one more
+ * client of weight 1.0 (+0.0 + fl(X * 1.0) = X: a partial sum is never -0.0).  Cross-process
+ * order: one monotonic progress counter per rank in a node-shared host page; a call publishes
+ * base + 1 on entry (the rank's earlier stream work is done: peers may write into its buffers),
+ * then before step t a one-lane wait kernel polls the counters the step needs and after it a
+ * one-lane signal kernel publishes base + t + 2 (system-scope release); the next call's base is
+ * base + nsteps + 1.  Every wait points to a strictly earlier step
+ * of another rank, so no hardware-queue mapping can deadlock it; a wait that exceeds
+ * `timeout_ticks` (wall-clock ticks) gives up and records the counter index + 1 in
+ * progress[nranks + rank] (the host checks it).  Replaces the per-element client loop of
+ * fed_avg.py:221-222 across GPUs, like fedagg_lockstep_execute.
+ * -------------------------------------------------------------------------*/
+#define FEDAGG_IPC_HANDLE_BYTES 64
+/* IPC handle of the allocation holding `ptr`, and ptr's byte offset in it */
+int fedagg_ipc_get(const void* ptr, void* handle_out, uint64_t* offset_out);
+/* map another process's allocation (hipIpcOpenMemHandle, peer access enabled lazily) */
+int fedagg_ipc_open(const void* handle, void** base_out);
+int fedagg_ipc_close(void* base);
+/* page-locked, device-mapped view of host memory (a node-shared page of progress counters) */
+int fedagg_host_map(void* host, uint64_t bytes, void** dev_out);
+int fedagg_host_unmap(void* host);
+/* wall-clock ticks per second of the device timer the wait kernels use */
+int fedagg_wall_clock_hz(uint64_t* hz_out);
+typedef struct fedagg_push_wait {
+  int32_t step;              /* waited before this step's runs (nsteps: after the last step)     */
+  int32_t rank;              /* whose progress counter                                           */
+  int64_t value;             /* counter >= base + value (<= 0: nothing to wait for)              */
+} fedagg_push_wait;
+/* runs: FEDAGG_RUN_FEDAVG only (acc may be a mapped peer address); waits sorted by step;
+ * ws_src / ws_dst / ws_bytes: one device copy issued after step 0's waits (the numel == 1 products
+ * to the root's staging row; 0 bytes: none).  Asynchronous on `stream`. */
+int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
+                        int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Client-side flat-bucket ops (the producer / consumer of the buckets, SURVEY.md §8(a)

@@ -100,6 +100,15 @@ SIGNATURES = {
     "fedagg_comm_last_error": (ctypes.c_char_p, []),
     "fedagg_lockstep_execute": (c_int, [c_void, c_void, c_int, c_void, c_int, c_int, c_void, c_u64, c_int, c_int,
                                         c_void]),
+    # push executor (csrc/lockstep.hip; substrafl_amd/push.py)
+    "fedagg_ipc_get": (c_int, [c_void, c_void, P(c_u64)]),
+    "fedagg_ipc_open": (c_int, [c_void, P(c_void)]),
+    "fedagg_ipc_close": (c_int, [c_void]),
+    "fedagg_host_map": (c_int, [c_void, c_u64, P(c_void)]),
+    "fedagg_host_unmap": (c_int, [c_void]),
+    "fedagg_wall_clock_hz": (c_int, [P(c_u64)]),
+    "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64, c_u64, c_void,
+                                    c_void, c_u64, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),
@@ -123,7 +132,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

@@ -94,6 +94,103 @@ ncclDataType_t nccl_type(int kind) {
   }
 }
 
+// One run of a schedule on stream s (the chain-kernel entry points of fedagg.hip).
+int run_one(const fedagg_lockstep_run& r, hipStream_t s) {
+  if (r.K <= 0) return lfail(FEDAGG_EINVAL, "lockstep: a run needs >= 1 client");
+  int rc = FEDAGG_OK;
+  switch (r.op) {
+    case FEDAGG_RUN_FEDAVG:
+      if (r.kind == FEDAGG_F32)
+        rc = fedagg_fedavg_chain_f32((const float* const*)r.x, (const float*)r.w, r.K, r.n, r.seed,
+                                     (float*)r.acc, s);
+      else if (r.kind == FEDAGG_BF16)
+        rc = fedagg_fedavg_chain_bf16((const uint16_t* const*)r.x, (const float*)r.w, r.K, r.n, r.seed,
+                                      (float*)r.acc, s);
+      else if (r.kind == FEDAGG_F64)
+        rc = fedagg_fedavg_chain_f64((const double* const*)r.x, (const double*)r.w, r.K, r.n, r.seed,
+                                     (double*)r.acc, s);
+      else
+        rc = fedagg_fedavg_chain_f16((const uint16_t* const*)r.x, (const uint16_t*)r.w, r.K, r.n, r.seed,
+                                     (uint16_t*)r.acc, s);
+      break;
+    case FEDAGG_RUN_FEDAVG_TILED:
+      if (r.kind == FEDAGG_F32)
+        rc = fedagg_fedavg_chain_tiled_f32((const float*)r.x[0], (const float*)r.w, r.K, r.n, r.tile_vectors,
+                                           r.seed, (float*)r.acc, s);
+      else
+        rc = fedagg_fedavg_chain_tiled_bf16((const uint16_t*)r.x[0], (const float*)r.w, r.K, r.n,
+                                            r.tile_vectors, r.seed, (float*)r.acc, s);
+      break;
+    case FEDAGG_RUN_SCAFFOLD:
+      if (r.kind == FEDAGG_F32)
+        rc = fedagg_scaffold_chain_f32((const float* const*)r.x, (const float* const*)r.x2, (const float*)r.c,
+                                       (const double*)r.w, r.K, r.n, r.seed, r.finish, r.lr, (double*)r.acc,
+                                       (double*)r.acc2, s);
+      else
+        rc = fedagg_scaffold_chain_f64((const double* const*)r.x, (const double* const*)r.x2,
+                                       (const double*)r.c, (const double*)r.w, r.K, r.n, r.seed, r.finish, r.lr,
+                                       (double*)r.acc, (double*)r.acc2, s);
+      break;
+    default:
+      return lfail(FEDAGG_EINVAL, "lockstep: unknown run op");
+  }
+  return rc ? lfail(rc, "lockstep: run failed: ", fedagg_last_error()) : FEDAGG_OK;
+}
+
+
+// ---- push executor (fedagg_push_execute): progress counters in a node-shared host page ----
+constexpr int PUSH_MAX_WAITS = 16;  // counters one wait kernel polls (one lane each)
+struct PushWaitArgs {
+  uint32_t n;
+  uint32_t idx[PUSH_MAX_WAITS];
+  uint64_t val[PUSH_MAX_WAITS];
+};
+
+// Lane i polls progress[idx[i]] until it reaches val[i] (system-scope acquire: what the producer
+// released before its signal is visible to the kernels after this one); a wait that exceeds
+// `timeout` ticks gives up and records idx + 1 in *err.  Every lane reaches the end.
+__global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress, PushWaitArgs a, uint64_t timeout,
+                                                       uint64_t* err) {
+  const uint32_t i = threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(progress + a.idx[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.val[i]) {
+    if (wall_clock64() - t0 > timeout) {
+      __hip_atomic_store(err, (uint64_t)a.idx[i] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(16);
+  }
+}
+
+// progress[idx] = value after everything before it on the stream (the step's chain kernels,
+// whose stores to mapped peer memory the kernel boundary has written back), system-scope release.
+__global__ void __launch_bounds__(64) push_signal_kernel(uint64_t* progress, uint32_t idx, uint64_t value) {
+  if (threadIdx.x != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __hip_atomic_store(progress + idx, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int push_waits(const fedagg_push_wait* waits, int& wi, int nwaits, int step, uint64_t* progress, uint64_t base,
+               uint64_t timeout, uint64_t* err, hipStream_t s) {
+  while (wi < nwaits && waits[wi].step == step) {
+    PushWaitArgs a;
+    memset(&a, 0, sizeof(a));
+    for (; wi < nwaits && waits[wi].step == step && a.n < PUSH_MAX_WAITS; ++wi) {
+      const int64_t v = (int64_t)base + waits[wi].value;
+      if (v <= 0) continue;  // the counters start at 0
+      a.idx[a.n] = (uint32_t)waits[wi].rank;
+      a.val[a.n] = (uint64_t)v;
+      ++a.n;
+    }
+    if (!a.n) continue;
+    hipLaunchKernelGGL(push_wait_kernel, dim3(1), dim3(64), 0, s, (const uint64_t*)progress, a, timeout, err);
+    int rc = hip_check(hipGetLastError(), "push_wait_kernel");
+    if (rc) return rc;
+  }
+  return FEDAGG_OK;
+}
+
 }  // namespace
 
 struct fedagg_comm {
@@ -212,45 +309,7 @@ int fedagg_lockstep_execute(fedagg_comm* c, const fedagg_lockstep_run* runs, int
     // step t: after group t - 1 (the inputs of step t)
     if (t > 0 && (rc = hip_check(hipStreamWaitEvent(s, c->ev[t - 1], 0), "hipStreamWaitEvent"))) return rc;
     for (; ri < nruns && runs[ri].step == t; ++ri) {
-      const fedagg_lockstep_run& r = runs[ri];
-      if (r.K <= 0) return lfail(FEDAGG_EINVAL, "fedagg_lockstep_execute: a run needs >= 1 client");
-      switch (r.op) {
-        case FEDAGG_RUN_FEDAVG:
-          if (r.kind == FEDAGG_F32)
-            rc = fedagg_fedavg_chain_f32((const float* const*)r.x, (const float*)r.w, r.K, r.n, r.seed,
-                                         (float*)r.acc, s);
-          else if (r.kind == FEDAGG_BF16)
-            rc = fedagg_fedavg_chain_bf16((const uint16_t* const*)r.x, (const float*)r.w, r.K, r.n, r.seed,
-                                          (float*)r.acc, s);
-          else if (r.kind == FEDAGG_F64)
-            rc = fedagg_fedavg_chain_f64((const double* const*)r.x, (const double*)r.w, r.K, r.n, r.seed,
-                                         (double*)r.acc, s);
-          else
-            rc = fedagg_fedavg_chain_f16((const uint16_t* const*)r.x, (const uint16_t*)r.w, r.K, r.n, r.seed,
-                                         (uint16_t*)r.acc, s);
-          break;
-        case FEDAGG_RUN_FEDAVG_TILED:
-          if (r.kind == FEDAGG_F32)
-            rc = fedagg_fedavg_chain_tiled_f32((const float*)r.x[0], (const float*)r.w, r.K, r.n, r.tile_vectors,
-                                               r.seed, (float*)r.acc, s);
-          else
-            rc = fedagg_fedavg_chain_tiled_bf16((const uint16_t*)r.x[0], (const float*)r.w, r.K, r.n,
-                                                r.tile_vectors, r.seed, (float*)r.acc, s);
-          break;
-        case FEDAGG_RUN_SCAFFOLD:
-          if (r.kind == FEDAGG_F32)
-            rc = fedagg_scaffold_chain_f32((const float* const*)r.x, (const float* const*)r.x2, (const float*)r.c,
-                                           (const double*)r.w, r.K, r.n, r.seed, r.finish, r.lr, (double*)r.acc,
-                                           (double*)r.acc2, s);
-          else
-            rc = fedagg_scaffold_chain_f64((const double* const*)r.x, (const double* const*)r.x2,
-                                           (const double*)r.c, (const double*)r.w, r.K, r.n, r.seed, r.finish, r.lr,
-                                           (double*)r.acc, (double*)r.acc2, s);
-          break;
-        default:
-          return lfail(FEDAGG_EINVAL, "fedagg_lockstep_execute: unknown run op");
-      }
-      if (rc) return lfail(rc, "fedagg_lockstep_execute: run failed: ", fedagg_last_error());
+      if ((rc = run_one(runs[ri], s))) return rc;
     }
   }
   if (ri != nruns || mi != nmsgs)
@@ -267,6 +326,87 @@ int fedagg_lockstep_execute(fedagg_comm* c, const fedagg_lockstep_run* runs, int
       return rc;
   }
   return FEDAGG_OK;
+}
+
+
+// ---- push executor ----
+int fedagg_ipc_get(const void* ptr, void* handle_out, uint64_t* offset_out) {
+  if (!ptr || !handle_out || !offset_out) return lfail(FEDAGG_EINVAL, "fedagg_ipc_get: NULL argument");
+  static_assert(sizeof(hipIpcMemHandle_t) <= FEDAGG_IPC_HANDLE_BYTES, "IPC handle size");
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  int rc;
+  if ((rc = hip_check(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr), "hipMemGetAddressRange"))) return rc;
+  hipIpcMemHandle_t h;
+  if ((rc = hip_check(hipIpcGetMemHandle(&h, (void*)base), "hipIpcGetMemHandle"))) return rc;
+  memset(handle_out, 0, FEDAGG_IPC_HANDLE_BYTES);
+  memcpy(handle_out, &h, sizeof(h));
+  *offset_out = (uint64_t)((const char*)ptr - (const char*)base);
+  return FEDAGG_OK;
+}
+
+int fedagg_ipc_open(const void* handle, void** base_out) {
+  if (!handle || !base_out) return lfail(FEDAGG_EINVAL, "fedagg_ipc_open: NULL argument");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return hip_check(hipIpcOpenMemHandle(base_out, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+}
+
+int fedagg_ipc_close(void* base) { return base ? hip_check(hipIpcCloseMemHandle(base), "hipIpcCloseMemHandle") : 0; }
+
+int fedagg_host_map(void* host, uint64_t bytes, void** dev_out) {
+  if (!host || !bytes || !dev_out) return lfail(FEDAGG_EINVAL, "fedagg_host_map: invalid argument");
+  int rc;
+  if ((rc = hip_check(hipHostRegister(host, bytes, hipHostRegisterMapped), "hipHostRegister"))) return rc;
+  return hip_check(hipHostGetDevicePointer(dev_out, host, 0), "hipHostGetDevicePointer");
+}
+
+int fedagg_host_unmap(void* host) { return host ? hip_check(hipHostUnregister(host), "hipHostUnregister") : 0; }
+
+int fedagg_wall_clock_hz(uint64_t* hz_out) {
+  if (!hz_out) return lfail(FEDAGG_EINVAL, "fedagg_wall_clock_hz: NULL output");
+  int dev = 0, khz = 0, rc;
+  if ((rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) ||
+      (rc = hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "hipDeviceGetAttribute")))
+    return rc;
+  *hz_out = (uint64_t)khz * 1000ull;
+  return FEDAGG_OK;
+}
+
+int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
+                        int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, void* stream) {
+  if (nruns < 0 || nwaits < 0 || nsteps < 0 || (nruns && !runs) || (nwaits && !waits) || !progress || nranks < 1 ||
+      rank < 0 || rank >= nranks || (ws_bytes && (!ws_src || !ws_dst)))
+    return lfail(FEDAGG_EINVAL, "fedagg_push_execute: invalid argument");
+  for (int i = 0; i < nwaits; ++i)
+    if (waits[i].rank < 0 || waits[i].rank >= nranks || waits[i].step < 0 || waits[i].step > nsteps ||
+        (i && waits[i].step < waits[i - 1].step))
+      return lfail(FEDAGG_EINVAL, "fedagg_push_execute: waits out of range or unsorted");
+  for (int i = 0; i < nruns; ++i)
+    if (runs[i].op != FEDAGG_RUN_FEDAVG || runs[i].step < 0 || runs[i].step >= nsteps ||
+        (i && runs[i].step < runs[i - 1].step))
+      return lfail(FEDAGG_EINVAL, "fedagg_push_execute: runs must be FedAvg row runs sorted by step");
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t* err = progress + nranks + rank;
+  int rc;
+  // base + 1: this rank entered the call -- everything its stream held before (a refill of the
+  // output, the previous call's reads of its slots) is done, so peers may write into its buffers
+  hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + 1);
+  if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
+  int ri = 0, wi = 0;
+  for (int t = 0; t < nsteps; ++t) {
+    if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, s))) return rc;
+    if (t == 0 && ws_bytes &&  // after step 0's waits, which include the root's entry
+        (rc = hip_check(hipMemcpyAsync(ws_dst, ws_src, ws_bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync")))
+      return rc;
+    for (; ri < nruns && runs[ri].step == t; ++ri)
+      if ((rc = run_one(runs[ri], s))) return rc;
+    // base + t + 2: step t done (its stores into peer buffers written back)
+    hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + t + 2);
+    if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
+  }
+  return push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, s);
 }
 
 }  // extern "C"

@@ -1,0 +1,333 @@
+"""Push executor of the client-sharded lockstep schedules (``fedagg_push_execute``,
+csrc/lockstep.hip; DESIGN.md §6 "Push").
+
+The RCCL executor (:mod:`rccl`) moves each step's accumulators with RCCL's P2P kernels, which on
+MI355X hide only part of their time under an HBM-saturating chain kernel (DESIGN.md §6
+"Overlap").  Here there are no exchange kernels: a run's chain kernel writes its accumulator
+straight into the consumer's slot -- or, for a finished piece, into the root's output -- through
+an IPC mapping of the peer's buffer (xGMI stores, 1/65 of the kernel's traffic at C3), and reads
+its input accumulator as one more client of weight 1.0 (``+0.0 + fl(X * 1.0) = X`` exactly: a
+partial sum seeded with +0.0 is never -0.0).  Order across the processes: one monotonic
+progress counter per rank in a node-shared host page, polled before a step by a one-lane wait kernel and published by a
+one-lane signal kernel on entry to a call (``base + 1``: the rank's earlier stream work -- a
+refill of its output, the previous call -- is done) and after each step t (``base + t + 2``).
+Before step t a rank waits for
+
+* each producer of its step-t inputs to have finished step t - 2 (the inputs landed), and
+* each consumer of its step-t outputs to have finished step t - 2 (the consumer read the slot
+  it is about to overwrite at that step: slot t % SLOTS, SLOTS = 4), or at least to have
+  entered the call (steps 0 and 1, the root's output for finished pieces, its staging row);
+
+after the last step the root waits for every rank's last step (the finished pieces landed).
+Every wait points to a strictly earlier step of another rank, so the schedule cannot deadlock
+whatever hardware queues the kernels share.  The numel == 1 products go to a staging row of the
+root per rank (one copy after step 0's waits) and are summed on the root (one owner per column: exact).
+
+Scope: fp32 FedAvg over row-layout client blocks (the bench's C3 schedule); the other kinds keep
+the RCCL executor.  Every rank must be on this node (the counters live in ``/dev/shm``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _native, lockstep
+from .rccl import _Run
+
+PAGE = 4096
+
+
+class _Wait(ctypes.Structure):
+    _fields_ = [("step", ctypes.c_int32), ("rank", ctypes.c_int32), ("value", ctypes.c_int64)]
+
+
+assert ctypes.sizeof(_Wait) == 16  # include/fedagg.h fedagg_push_wait
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        lib = _native.load()
+        msg = lib.fedagg_comm_last_error().decode(errors="replace") or lib.fedagg_last_error().decode(errors="replace")
+        raise _native.NativeLibraryError(f"{what} failed ({rc}): {msg}")
+
+
+class PushTransport:
+    """The push executor over the ranks of ``group`` (a torch.distributed group -- gloo is
+    enough: it carries only the set-up handshakes)."""
+
+    native = True
+    push = True
+
+    def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0):
+        import torch
+        import torch.distributed as dist
+        from multiprocessing import shared_memory
+
+        self.lib = _native.load()
+        self.dist, self.group = dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        nbytes = PAGE * max(1, -(-(2 * self.world * 8) // PAGE))
+        name = [None]
+        if self.rank == 0:
+            self._shm = shared_memory.SharedMemory(create=True, size=nbytes)
+            self._shm.buf[:nbytes] = bytes(nbytes)
+            name = [self._shm.name]
+        self._src0 = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(name, src=self._src0, group=group)
+        if self.rank != 0:
+            self._shm = shared_memory.SharedMemory(name=name[0])
+        self._page = np.frombuffer(self._shm.buf, dtype=np.uint64, count=nbytes // 8)
+        dev = ctypes.c_void_p()
+        _check(self.lib.fedagg_host_map(self._page.ctypes.data, nbytes, ctypes.byref(dev)), "fedagg_host_map")
+        self._dev = dev.value
+        hz = ctypes.c_uint64()
+        _check(self.lib.fedagg_wall_clock_hz(ctypes.byref(hz)), "fedagg_wall_clock_hz")
+        self._timeout = int(timeout_s * hz.value)
+        self.base = 0
+        self._maps: Dict[bytes, int] = {}
+        self._programs: List["PushProgram"] = []
+        self._py = None
+        dist.barrier(group=group)
+
+    # -- set-up helpers --------------------------------------------------------------------
+    def ipc_info(self, t) -> Tuple[bytes, int]:
+        """(handle, byte offset) of a device tensor's first element."""
+        h = (ctypes.c_char * _native_ipc_bytes())()
+        off = ctypes.c_uint64()
+        _check(self.lib.fedagg_ipc_get(t.data_ptr(), h, ctypes.byref(off)), "fedagg_ipc_get")
+        return bytes(h.raw), int(off.value)
+
+    def remote(self, info: Tuple[bytes, int]) -> int:
+        """Address, in this process, of another rank's (handle, offset)."""
+        h, off = info
+        if h not in self._maps:
+            base = ctypes.c_void_p()
+            buf = (ctypes.c_char * len(h)).from_buffer_copy(h)
+            _check(self.lib.fedagg_ipc_open(buf, ctypes.byref(base)), "fedagg_ipc_open")
+            self._maps[h] = int(base.value)
+        return self._maps[h] + off
+
+    def all_gather(self, obj) -> list:
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def all_sum_int(self, v: int) -> int:
+        import torch
+
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        self.dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def python_transport(self):
+        """The torch.distributed transport of the same group (sharding.DistTransport) for what this
+        executor does not run; its backend must carry device tensors (RCCL)."""
+        if self._py is None:
+            from .sharding import DistTransport
+
+            self._py = DistTransport(self.group)
+        return self._py
+
+    def errors(self) -> Dict[int, int]:
+        """Ranks whose wait kernel gave up: rank -> the counter it waited for."""
+        e = self._page[self.world: 2 * self.world]
+        return {r: int(v) - 1 for r, v in enumerate(e) if v}
+
+    # -- the schedule ----------------------------------------------------------------------
+    def program(self, **kw) -> "PushProgram":
+        for p in self._programs:
+            if p.matches(**kw):
+                return p
+        p = PushProgram(self, **kw)
+        self._programs = ([p] + self._programs)[:4]
+        return p
+
+    def execute(self, prog: "PushProgram", stream: int, ws=None, ws_kind: str = "f32") -> None:
+        bad = self.errors()
+        if bad:
+            raise _native.NativeLibraryError(f"push executor: a wait timed out (rank -> counter {bad})")
+        ws_src = ws_dst = None
+        ws_bytes = 0
+        if ws is not None and self.world > 1:
+            ws_bytes = ws.numel() * ws.element_size()
+            ws_src, ws_dst = ws.data_ptr(), prog.ws_dst(ws_bytes)
+        _check(self.lib.fedagg_push_execute(ctypes.byref(prog.runs) if prog.nruns else None, prog.nruns,
+                                            ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
+                                            prog.nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
+                                            ws_src, ws_dst, ws_bytes, int(stream)), "fedagg_push_execute")
+        self.base += prog.nsteps + 1
+        if ws_bytes and self.rank == prog.plan.root:  # one owner per column: the sum is exact
+            import torch
+
+            with torch.cuda.stream(torch.cuda.ExternalStream(int(stream))):
+                ws.copy_(prog.stage.view(self.world, *ws.shape).sum(0))
+
+    def close(self) -> None:
+        if getattr(self, "_dev", None) is None:
+            return
+        import torch
+
+        torch.cuda.synchronize(self.device)
+        self.dist.barrier(group=self.group)  # nobody writes into a mapping that is going away
+        self._programs.clear()
+        for base in self._maps.values():
+            self.lib.fedagg_ipc_close(base)
+        self._maps.clear()
+        self.lib.fedagg_host_unmap(self._page.ctypes.data)
+        self._dev = None
+        self._page = None
+        self._shm.close()
+        if self.rank == 0:
+            self._shm.unlink()
+
+
+def _native_ipc_bytes() -> int:
+    return 64  # FEDAGG_IPC_HANDLE_BYTES
+
+
+class PushProgram:
+    """One rank's schedule compiled for the push executor: its runs split by consumer with
+    every output address resolved (a mapped peer slot, the root's output, or its own output),
+    and the waits of every step.  Built collectively (every rank at once)."""
+
+    def __init__(self, tr: PushTransport, plan: lockstep.RankPlan, blocks, accs, outs, kind: str, scaffold: bool,
+                 c=None, lr: float = 1.0):
+        import torch
+
+        if scaffold or kind != "f32":
+            raise ValueError("push executor: fp32 FedAvg only (the other kinds take the RCCL executor)")
+        for sh in blocks.values():
+            if not isinstance(getattr(sh, "rows", None), torch.Tensor):
+                raise ValueError("push executor: row-layout client blocks only")
+        self.plan, self.blocks, self.accs, self.outs, self.kind = plan, blocks, accs, outs, kind
+        self._keep: list = []
+        G, me, root = plan.world, plan.rank, plan.root
+        slots, out = accs[0], outs[0]
+        esz = out.element_size()
+        self.stage = None
+        pw_rows = None
+        if me == root and G > 1:  # numel == 1 product staging: one row per rank (sized at first use)
+            pw_rows = True
+        # every rank's buffers and receive ops, once
+        mine = {"slots": [tr.ipc_info(slots[s]) for s in range(slots.shape[0])] if G > 1 else [],
+                "out": tr.ipc_info(out) if G > 1 else None,
+                "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
+                         if o.kind == "recv"]}
+        infos = tr.all_gather(mine) if G > 1 else [mine]
+
+        def local(loc) -> int:
+            where, slot, off = loc
+            base = out if where == "out" else slots[slot]
+            return base.data_ptr() + off * esz
+
+        def at(rank: int, loc) -> int:
+            if rank == me:
+                return local(loc)
+            where, slot, off = loc
+            info = infos[rank]["out"] if where == "out" else infos[rank]["slots"][slot]
+            return tr.remote(info) + off * esz
+
+        recv_of = {}  # (group, sender, receiver, key) -> receiver's buffer location
+        for r, info in enumerate(infos):
+            for g, q, key, buf, n in info["recv"]:
+                recv_of[(g, q, r, key)] = (buf, n)
+
+        runs, waits = [], []
+        for t, step_runs in enumerate(plan.runs):
+            producers, consumers = set(), set()
+            # my inputs of step t arrived in group t - 1 (from the ranks that ran step t - 2)
+            inputs = [r for r in step_runs if not r.seed]
+            for o in (plan.groups[t - 1] if t >= 1 else []):
+                if o.kind == "recv" and any(_overlap(o.buf, o.n, r.acc, r.n) for r in inputs):
+                    producers.add(o.peer)
+            sends = [o for o in plan.groups[t + 1] if o.kind == "send"] if t + 1 < len(plan.groups) else []
+            for r in step_runs:
+                sh = blocks[r.block]
+                if r.final:  # a finished piece: straight into the root's output
+                    runs.append(self._run(t, sh, r, 0, r.n, at(root, ("out", 0, r.lo)), local(r.acc)))
+                    continue
+                covered = 0
+                for o in sends:
+                    a0, n0 = _intersect(o.buf, o.n, r.acc, r.n)
+                    if not n0:
+                        continue
+                    dloc, _dn = recv_of[(t + 1, me, o.peer, o.key)]
+                    d = (dloc[0], dloc[1], dloc[2] + (a0 - o.buf[2]))
+                    j = a0 - r.acc[2]
+                    runs.append(self._run(t, sh, r, j, n0, at(o.peer, d), local(r.acc) + j * esz))
+                    consumers.add(o.peer)
+                    covered += n0
+                if covered != r.n:
+                    raise AssertionError(f"push: step {t} run of {r.n} elements has {covered} consumed")
+            if t == 0 and me != root:
+                consumers.add(root)  # the root entered the call: its output and staging row are free
+            if any(r.final for r in step_runs) and me != root:
+                consumers.add(root)
+            for q in sorted(producers | consumers):  # q finished step t - 2 (or, early on, entered)
+                if q != me:
+                    waits.append(_Wait(t, q, max(t, 1)))
+        n_steps = plan.n_steps
+        if me == root:  # every finished piece landed: every rank finished its last step
+            for q in range(G):
+                if q != me:
+                    waits.append(_Wait(n_steps, q, n_steps + 1))
+        self.nruns, self.nwaits, self.nsteps = len(runs), len(waits), n_steps
+        self.runs = (_Run * max(1, len(runs)))(*runs)
+        self.waits = (_Wait * max(1, len(waits)))(*waits)
+        self._tr, self._infos, self._pw_rows = tr, infos, pw_rows
+        self._stage_info = None
+
+    def ws_dst(self, ws_bytes: int) -> int:
+        """This rank's staging row on the root for the numel == 1 products (collective at first use)."""
+        import torch
+
+        tr, G = self._tr, self.plan.world
+        if self._stage_info is None or self._stage_info[1] != ws_bytes:
+            if self.plan.rank == self.plan.root:
+                self.stage = torch.zeros(G * ws_bytes // 4, dtype=torch.float32, device=self.outs[0].device)
+                info = tr.ipc_info(self.stage)
+            else:
+                info = None
+            infos = tr.all_gather(info)
+            self._stage_info = (infos[self.plan.root], ws_bytes)
+        if self.plan.rank == self.plan.root:
+            return self.stage.data_ptr() + self.plan.rank * ws_bytes
+        return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
+
+    def _run(self, t: int, sh, r, j: int, n: int, dst: int, src: int) -> _Run:
+        rec = _Run()
+        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG, _native.FEDAGG_F32, 1, 0, n
+        rows = sh.rows
+        base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
+        ptrs = [base + k * step + (r.col + j) * esz for k in range(rows.shape[0])]
+        w = [float(v) for v in np.asarray(sh.w, np.float32)]
+        if not r.seed:  # the input accumulator: one more client of weight 1.0, first in order
+            ptrs, w = [src] + ptrs, [1.0] + w
+        rec.K = len(ptrs)
+        arr = _native.ptr_array(ptrs)
+        warr = (ctypes.c_float * len(w))(*w)
+        self._keep += [arr, warr]
+        rec.x, rec.w, rec.acc = ctypes.addressof(arr), ctypes.addressof(warr), dst
+        return rec
+
+    def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:
+        return (plan is self.plan and blocks is self.blocks and kind == self.kind and not scaffold
+                and [a.data_ptr() for a in accs] == [a.data_ptr() for a in self.accs]
+                and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
+
+
+def _intersect(loc_a, n_a: int, loc_b, n_b: int) -> Tuple[int, int]:
+    """(start, length) of the intersection of two buffer ranges (same buffer and slot), else (0, 0)."""
+    if loc_a[0] != loc_b[0] or loc_a[1] != loc_b[1]:
+        return 0, 0
+    lo = max(loc_a[2], loc_b[2])
+    hi = min(loc_a[2] + n_a, loc_b[2] + n_b)
+    return (lo, hi - lo) if hi > lo else (0, 0)
+
+
+def _overlap(loc_a, n_a: int, loc_b, n_b: int) -> bool:
+    return _intersect(loc_a, n_a, loc_b, n_b)[1] > 0

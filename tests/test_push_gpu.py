@@ -1,0 +1,121 @@
+"""Push executor (substrafl_amd/push.py, fedagg_push_execute): G rank PROCESSES on the one GPU
+(IPC-mapped slots between processes, the node-shared progress page, gloo for the set-up), each
+running its part of a relay / striped FedAvg schedule three times through the cached program;
+the root's result bit-identical to the reference (fed_avg.py:217-222).  On the 8-GPU node the
+same protocol crosses xGMI (bench.py's client_shard_push leg)."""
+
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# (G, K, rounds, relay, shapes)
+CASES = [
+    (2, 5, (1.0,), False, "default"),
+    (3, 7, (0.5, 0.3, 0.2), False, "default"),
+    (4, 9, (0.75, 0.25), True, "default"),
+    (3, 40, (0.5, 0.5), False, "wide"),
+]
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, G, K, rounds, relay, shapes_name, port, q):
+    import faulthandler
+
+    faulthandler.dump_traceback_later(100, exit=True)
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    from oracle import fedavg_reference_structure
+    from substrafl_amd.engine import fedavg_weights
+    from substrafl_amd.layout import BucketLayout
+    from substrafl_amd.push import PushTransport
+    from substrafl_amd.sharding import (SLOTS, FedAvgShard, GpuShardOps, client_blocks, lockstep_fedavg,
+                                        relay_plan, striped_plan)
+    from test_client_shard_gpu import SHAPES, _data, _rows
+
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=G, timeout=timedelta(seconds=90))
+        torch.cuda.set_device(0)
+        shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else [(1,), (130001,), (1, 1), (77777,)]
+        pus, ns = _data(K, seed=17 + G, shapes=shapes)
+        pus = [[a.astype(np.float32) for a in c] for c in pus]
+        layout = BucketLayout(range(len(shapes)), shapes, np.float32)
+        plan = relay_plan(layout.M, G, rank, 4096) if relay else striped_plan(layout.M, G, rank, None, rounds)
+        blocks = {}
+        for b, segs in plan.blocks.items():
+            k0, k1 = client_blocks(K, G)[b]
+            full = _rows(torch, pus[k0:k1], layout, dtype=np.float32)
+            t = torch.zeros((k1 - k0, plan.block_len[b]), dtype=torch.float32, device="cuda")
+            for lo, hi, col in segs:
+                t[:, col: col + hi - lo] = full[:, lo:hi]
+            blocks[b] = FedAvgShard("f32", t, fedavg_weights(ns, "f32")[k0:k1], k0, K, plan.block_len[b],
+                                    np.zeros(0, np.uint64))
+        tr = PushTransport(timeout_s=30)
+        bad, calls = [], 0
+        ref = fedavg_reference_structure(pus, ns) if rank == plan.root else None
+        out = torch.empty((layout.ld,), dtype=torch.float32, device="cuda")
+        slots = torch.empty(SLOTS * max(1, plan.slot_elems), dtype=torch.float32, device="cuda")
+        for _ in range(3):  # the cached program, and counters that keep climbing across calls
+            out.fill_(float("nan"))
+            is_root = lockstep_fedavg(plan, blocks, out, tr, GpuShardOps(), layout.pairwise_idx, slots=slots)
+            torch.cuda.synchronize()
+            calls += 1
+            if is_root:
+                got = [a for _, a in layout.unpack(out[: layout.M].cpu().numpy())]
+                bad.append(sum(int(np.count_nonzero(g.view(np.uint32) != r.view(np.uint32))) for g, r in zip(got, ref)))
+        errs = tr.errors()
+        programs = len(tr._programs)
+        tr.close()
+        dist.destroy_process_group()
+        q.put((rank, bad, errs, programs, calls, None))
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        import traceback
+
+        q.put((rank, None, None, 0, 0, traceback.format_exc()[-2000:]))
+
+
+@pytest.mark.parametrize("G,K,rounds,relay,shapes", CASES)
+def test_push_executor_processes_bit_exact(G, K, rounds, relay, shapes):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, G, K, rounds, relay, shapes, port, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(G):
+            rank, bad, errs, programs, calls, tb = q.get(timeout=110)
+            res[rank] = (bad, errs, programs, calls, tb)
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()  # our own child, by handle
+    for rank, (bad, errs, programs, calls, tb) in sorted(res.items()):
+        assert tb is None, f"rank {rank}:\n{tb}"
+        assert errs == {} and programs == 1 and calls == 3, (rank, errs, programs, calls, bad)
+    assert res[0][0] == [0, 0, 0], res[0][0]  # root: every element, every call
