@@ -1,0 +1,109 @@
+"""Per-step cost of the push executor's order kernels (fedagg_push_execute, csrc/lockstep.hip) on
+one GPU: S steps with no runs, each with a one-lane wait kernel whose counter is already there
+(``--waits`` counters per step) and the step's signal kernel; and the same S steps around the
+chain runs of a 64-client x n-element block (runs alone, through the executor's own run table,
+against runs + waits + signals).  The counters live in a page-locked host page, as in
+substrafl_amd/push.py.
+
+  python tools/push_overhead_probe.py [--steps 48] [--n 2600000] [--waits 6]
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--n", type=int, default=2_600_000)
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--waits", type=int, default=6)
+    ap.add_argument("--trials", type=int, default=9)
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from substrafl_amd import _native, push, rccl
+
+    torch.cuda.set_device(0)
+    lib = _native.load()
+    G = max(2, a.waits + 1)
+    page = np.zeros(512, np.uint64)
+    dev = ctypes.c_void_p()
+    push._check(lib.fedagg_host_map(page.ctypes.data, page.nbytes, ctypes.byref(dev)), "fedagg_host_map")
+    page[1:G] = 1 << 40  # the other "ranks" are far ahead: every wait is satisfied at once
+    K, n, S = a.clients, a.n, a.steps
+    rows = torch.randn((K, n), dtype=torch.float32, device="cuda")
+    acc = torch.zeros(n, dtype=torch.float32, device="cuda")
+    ptrs = _native.ptr_array([rows[k].data_ptr() for k in range(K)])
+    w = (ctypes.c_float * K)(*[1.0 / K] * K)
+    runs = []
+    for t in range(S):
+        r = rccl._Run()
+        r.step, r.op, r.kind, r.K, r.seed, r.finish, r.n = t, _native.FEDAGG_RUN_FEDAVG, _native.FEDAGG_F32, K, 1, 0, n
+        r.x, r.w, r.acc = ctypes.addressof(ptrs), ctypes.addressof(w), acc.data_ptr()
+        runs.append(r)
+    R = (rccl._Run * S)(*runs)
+    waits = [push._Wait(t, 1 + i, 1) for t in range(S) for i in range(a.waits)]
+    W = (push._Wait * max(1, len(waits)))(*waits)
+    stream = torch.cuda.current_stream()
+    base = [0]
+
+    def call(with_runs, with_order):
+        push._check(lib.fedagg_push_execute(ctypes.byref(R) if with_runs else None, S if with_runs else 0,
+                                            ctypes.byref(W) if with_order and waits else None,
+                                            len(waits) if with_order else 0, S, dev.value, 0, G, base[0],
+                                            1 << 40, None, None, 0, stream.cuda_stream), "fedagg_push_execute")
+        base[0] += S + 1
+
+    def timed(*cfg):
+        v = []
+        for i in range(a.trials + 1):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            call(*cfg)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if i:
+                v.append(e0.elapsed_time(e1))
+        return float(np.median(v))
+
+    def plain_runs():
+        for _ in range(S):
+            _native.check(lib.fedagg_fedavg_chain_f32(ptrs, w, K, n, 1, acc.data_ptr(), stream.cuda_stream), "chain")
+
+    def timed_plain():
+        v = []
+        for i in range(a.trials + 1):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            plain_runs()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if i:
+                v.append(e0.elapsed_time(e1))
+        return float(np.median(v))
+
+    runs_only = timed_plain()
+    order = timed(False, True)
+    runs_sig = timed(True, False)  # runs + the step signals (no waits)
+    both = timed(True, True)
+    print(json.dumps({"steps": S, "waits_per_step": a.waits, "clients": K, "elements_per_run": n,
+                      "runs_only_ms": round(runs_only, 4), "order_only_ms": round(order, 4), "order_us_per_step": round(order / S * 1e3, 2),
+                      "runs_and_signals_ms": round(runs_sig, 4), "runs_signals_waits_ms": round(both, 4),
+                      "added_us_per_step": round((both - runs_only) / S * 1e3, 2)}), flush=True)
+    lib.fedagg_host_unmap(page.ctypes.data)
+
+
+if __name__ == "__main__":
+    main()
