@@ -30,7 +30,8 @@ the RCCL executor.  Every rank must be on this node (the counters live in ``/dev
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, List, Optional, Tuple
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -208,10 +209,7 @@ class PushProgram:
         G, me, root = plan.world, plan.rank, plan.root
         slots, out = accs[0], outs[0]
         esz = out.element_size()
-        self.stage = None
-        pw_rows = None
-        if me == root and G > 1:  # numel == 1 product staging: one row per rank (sized at first use)
-            pw_rows = True
+        self.stage = None  # the root's numel == 1 product staging (one row per rank), at first use
         # every rank's buffers and receive ops, once
         mine = {"slots": [tr.ipc_info(slots[s]) for s in range(slots.shape[0])] if G > 1 else [],
                 "out": tr.ipc_info(out) if G > 1 else None,
@@ -231,54 +229,15 @@ class PushProgram:
             info = infos[rank]["out"] if where == "out" else infos[rank]["slots"][slot]
             return tr.remote(info) + off * esz
 
-        recv_of = {}  # (group, sender, receiver, key) -> receiver's buffer location
-        for r, info in enumerate(infos):
-            for g, q, key, buf, n in info["recv"]:
-                recv_of[(g, q, r, key)] = (buf, n)
-
-        runs, waits = [], []
-        for t, step_runs in enumerate(plan.runs):
-            producers, consumers = set(), set()
-            # my inputs of step t arrived in group t - 1 (from the ranks that ran step t - 2)
-            inputs = [r for r in step_runs if not r.seed]
-            for o in (plan.groups[t - 1] if t >= 1 else []):
-                if o.kind == "recv" and any(_overlap(o.buf, o.n, r.acc, r.n) for r in inputs):
-                    producers.add(o.peer)
-            sends = [o for o in plan.groups[t + 1] if o.kind == "send"] if t + 1 < len(plan.groups) else []
-            for r in step_runs:
-                sh = blocks[r.block]
-                if r.final:  # a finished piece: straight into the root's output
-                    runs.append(self._run(t, sh, r, 0, r.n, at(root, ("out", 0, r.lo)), local(r.acc)))
-                    continue
-                covered = 0
-                for o in sends:
-                    a0, n0 = _intersect(o.buf, o.n, r.acc, r.n)
-                    if not n0:
-                        continue
-                    dloc, _dn = recv_of[(t + 1, me, o.peer, o.key)]
-                    d = (dloc[0], dloc[1], dloc[2] + (a0 - o.buf[2]))
-                    j = a0 - r.acc[2]
-                    runs.append(self._run(t, sh, r, j, n0, at(o.peer, d), local(r.acc) + j * esz))
-                    consumers.add(o.peer)
-                    covered += n0
-                if covered != r.n:
-                    raise AssertionError(f"push: step {t} run of {r.n} elements has {covered} consumed")
-            if t == 0 and me != root:
-                consumers.add(root)  # the root entered the call: its output and staging row are free
-            if any(r.final for r in step_runs) and me != root:
-                consumers.add(root)
-            for q in sorted(producers | consumers):  # q finished step t - 2 (or, early on, entered)
-                if q != me:
-                    waits.append(_Wait(t, q, max(t, 1)))
+        specs, wait_list = push_schedule(plan, [info["recv"] for info in infos])
+        runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
+                          local(p.src) if p.src is not None else 0) for p in specs]
+        waits = [_Wait(t, q, v) for t, q, v in wait_list]
         n_steps = plan.n_steps
-        if me == root:  # every finished piece landed: every rank finished its last step
-            for q in range(G):
-                if q != me:
-                    waits.append(_Wait(n_steps, q, n_steps + 1))
         self.nruns, self.nwaits, self.nsteps = len(runs), len(waits), n_steps
         self.runs = (_Run * max(1, len(runs)))(*runs)
         self.waits = (_Wait * max(1, len(waits)))(*waits)
-        self._tr, self._infos, self._pw_rows = tr, infos, pw_rows
+        self._tr = tr
         self._stage_info = None
 
     def ws_dst(self, ws_bytes: int) -> int:
@@ -298,14 +257,14 @@ class PushProgram:
             return self.stage.data_ptr() + self.plan.rank * ws_bytes
         return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
 
-    def _run(self, t: int, sh, r, j: int, n: int, dst: int, src: int) -> _Run:
+    def _run(self, t: int, sh, col: int, n: int, dst: int, src: int) -> _Run:
         rec = _Run()
         rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG, _native.FEDAGG_F32, 1, 0, n
         rows = sh.rows
         base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
-        ptrs = [base + k * step + (r.col + j) * esz for k in range(rows.shape[0])]
+        ptrs = [base + k * step + col * esz for k in range(rows.shape[0])]
         w = [float(v) for v in np.asarray(sh.w, np.float32)]
-        if not r.seed:  # the input accumulator: one more client of weight 1.0, first in order
+        if src:  # the input accumulator: one more client of weight 1.0, first in order
             ptrs, w = [src] + ptrs, [1.0] + w
         rec.K = len(ptrs)
         arr = _native.ptr_array(ptrs)
@@ -318,6 +277,74 @@ class PushProgram:
         return (plan is self.plan and blocks is self.blocks and kind == self.kind and not scaffold
                 and [a.data_ptr() for a in accs] == [a.data_ptr() for a in self.accs]
                 and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
+
+
+@dataclass(frozen=True)
+class PushRun:
+    """One launch of the push executor: ``n`` elements at column ``col`` of ``block``'s buffer;
+    input accumulator at ``src`` on this rank (None: seeded with +0.0), output at ``dst`` on
+    ``dst_rank`` (locations as :class:`lockstep.Run.acc`)."""
+
+    step: int
+    block: int
+    col: int
+    n: int
+    src: Optional[Tuple[str, int, int]]
+    dst_rank: int
+    dst: Tuple[str, int, int]
+
+
+def push_schedule(plan: lockstep.RankPlan, recvs: Sequence[Sequence[tuple]]):
+    """This rank's push runs and waits (pure: a function of the plan and every rank's receive
+    ops ``(group, sender, key, buf, n)``).  A run's output goes where the lockstep schedule would
+    have received it (the matching receive of group t + 1 on the consumer; a finished piece: the
+    root's output at its global offset), split per consumer.  Waits ``(step, rank, value)``:
+    before step t, counter(rank) >= base + value, ``value = max(t, 1)`` for the producers of the
+    step's inputs and the consumers of its outputs (finished step t - 2, or entered the call),
+    the root at step 0 and wherever a finished piece goes to it; at ``n_steps`` the root waits
+    for every rank's last step (``n_steps + 1``)."""
+    G, me, root = plan.world, plan.rank, plan.root
+    recv_of = {}  # (group, sender, receiver, key) -> the receiver's buffer location
+    for r, ops in enumerate(recvs):
+        for g, q, key, buf, n in ops:
+            recv_of[(g, q, r, key)] = (buf, n)
+    specs: List[PushRun] = []
+    waits: List[Tuple[int, int, int]] = []
+    for t, step_runs in enumerate(plan.runs):
+        producers, consumers = set(), set()
+        inputs = [r for r in step_runs if not r.seed]  # they arrived in group t - 1
+        for o in (plan.groups[t - 1] if t >= 1 else []):
+            if o.kind == "recv" and any(_overlap(o.buf, o.n, r.acc, r.n) for r in inputs):
+                producers.add(o.peer)
+        sends = [o for o in plan.groups[t + 1] if o.kind == "send"] if t + 1 < len(plan.groups) else []
+        for r in step_runs:
+            src = None if r.seed else r.acc
+            if r.final:  # a finished piece: straight into the root's output
+                specs.append(PushRun(t, r.block, r.col, r.n, src, root, ("out", 0, r.lo)))
+                if me != root:
+                    consumers.add(root)
+                continue
+            covered = 0
+            for o in sends:
+                a0, n0 = _intersect(o.buf, o.n, r.acc, r.n)
+                if not n0:
+                    continue
+                dloc, _dn = recv_of[(t + 1, me, o.peer, o.key)]
+                j = a0 - r.acc[2]
+                specs.append(PushRun(t, r.block, r.col + j, n0, None if src is None else (src[0], src[1], src[2] + j),
+                                     o.peer, (dloc[0], dloc[1], dloc[2] + (a0 - o.buf[2]))))
+                consumers.add(o.peer)
+                covered += n0
+            if covered != r.n:
+                raise AssertionError(f"push: step {t} run of {r.n} elements has {covered} consumed")
+        if t == 0 and me != root:
+            consumers.add(root)  # the root entered the call: its output and staging row are free
+        for q in sorted(producers | consumers):
+            if q != me:
+                waits.append((t, q, max(t, 1)))
+    if me == root:
+        waits += [(plan.n_steps, q, plan.n_steps + 1) for q in range(G) if q != me]
+    return specs, waits
 
 
 def _intersect(loc_a, n_a: int, loc_b, n_b: int) -> Tuple[int, int]:
