@@ -378,6 +378,8 @@ def main():
                 line.update(client_shard_legs(args, ctx, info))
             else:
                 line["client_shard"] = {"skipped": f"needs one GPU per rank for RCCL ({world} ranks, {ndev} GPUs)"}
+                if args.client_shard == "force":  # the push leg needs no RCCL: rehearse it with ranks sharing GPUs
+                    line.update(client_shard_legs(args, ctx, info, only_push=True))
         if own_gpus and ((world > 1 and args.multi_device_leg == "auto") or args.multi_device_leg == "force"):
             line["multi_device"] = multi_device_leg(args, ctx)
     if rank == 0 and not args.client_shard_child:
@@ -597,7 +599,7 @@ def multi_device_leg(args, ctx):
 # ======================================================================================
 # client-shard (the north-star mode) -- its own line, or a field of the N > 1 line
 # ======================================================================================
-def client_shard_legs(args, ctx, info):
+def client_shard_legs(args, ctx, info, only_push=False):
     """The client-shard legs of an N > 1 line, each in a CHILD process per rank (a fresh
     interpreter with its own process group on a new port, started once this rank's parameter-range
     buffers are freed): ``client_shard`` with the native RCCL executor, ``client_shard_torch_pg``
@@ -626,6 +628,8 @@ def client_shard_legs(args, ctx, info):
             ("native", "strong", "client_shard_strong", {}, []),
             ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}, []),
             ("push", "weak", "client_shard_push", {}, []))
+    if only_push:
+        legs = tuple(leg for leg in legs if leg[0] == "push")
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     if ctx.world > 1:
