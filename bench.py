@@ -995,7 +995,7 @@ def _rounds(args):
     from substrafl_amd import lockstep
 
     if not args.rounds:  # the schedule's default for the executor (lockstep.py)
-        return lockstep.default_rounds(args.gpus, args.executor in ("native", "push"))
+        return lockstep.default_rounds(args.gpus, args.executor == "native")  # push: one round (no gather tail)
     return tuple(float(x) for x in args.rounds.split(","))
 
 

@@ -116,9 +116,12 @@ def striped_plan(M: int, world: int, rank: int, rings: Optional[int] = None,
 
 
 def default_rounds(transport) -> Sequence[float]:
-    """The striped schedule's round split for a transport: three rounds for the native executor
-    over more than one rank, else one (lockstep.DEFAULT_ROUNDS / NATIVE_ROUNDS)."""
-    return lockstep.default_rounds(getattr(transport, "world", 1), getattr(transport, "native", False))
+    """The striped schedule's round split for a transport: three rounds for the native RCCL
+    executor over more than one rank, else one (lockstep.DEFAULT_ROUNDS / NATIVE_ROUNDS).  The push
+    executor takes one: its finished pieces reach the root inside the final runs' own stores, so
+    there is no gather tail for more rounds to hide."""
+    native = getattr(transport, "native", False) and not getattr(transport, "push", False)
+    return lockstep.default_rounds(getattr(transport, "world", 1), native)
 
 
 # ======================================================================================
