@@ -375,9 +375,11 @@ int fedagg_wall_clock_hz(uint64_t* hz_out) {
 
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
-                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, void* stream) {
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, void* const* aux_streams, int naux,
+                        void* stream) {
   if (nruns < 0 || nwaits < 0 || nsteps < 0 || (nruns && !runs) || (nwaits && !waits) || !progress || nranks < 1 ||
-      rank < 0 || rank >= nranks || (ws_bytes && (!ws_src || !ws_dst)))
+      rank < 0 || rank >= nranks || (ws_bytes && (!ws_src || !ws_dst)) || naux < 0 || naux > 7 ||
+      (naux && !aux_streams))
     return lfail(FEDAGG_EINVAL, "fedagg_push_execute: invalid argument");
   for (int i = 0; i < nwaits; ++i)
     if (waits[i].rank < 0 || waits[i].rank >= nranks || waits[i].step < 0 || waits[i].step > nsteps ||
@@ -394,14 +396,44 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   // output, the previous call's reads of its slots) is done, so peers may write into its buffers
   hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + 1);
   if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
+  // a step's launches (one per consumer: each writes over its own xGMI link) spread over the
+  // caller's stream and the aux streams, forked from and joined back into the caller's stream
+  hipEvent_t ev[8] = {};
+  for (int i = 0; i <= naux; ++i)
+    if ((rc = hip_check(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate"))) {
+      for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+      return rc;
+    }
+  struct EvGuard {
+    hipEvent_t* e;
+    int n;
+    ~EvGuard() {
+      for (int i = 0; i < n; ++i) (void)hipEventDestroy(e[i]);
+    }
+  } guard{ev, naux + 1};
   int ri = 0, wi = 0;
   for (int t = 0; t < nsteps; ++t) {
     if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, s))) return rc;
     if (t == 0 && ws_bytes &&  // after step 0's waits, which include the root's entry
         (rc = hip_check(hipMemcpyAsync(ws_dst, ws_src, ws_bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync")))
       return rc;
-    for (; ri < nruns && runs[ri].step == t; ++ri)
-      if ((rc = run_one(runs[ri], s))) return rc;
+    int r0 = ri;
+    while (ri < nruns && runs[ri].step == t) ++ri;
+    const int nlaunch = ri - r0, used = nlaunch - 1 < naux ? nlaunch - 1 : naux;
+    if (used > 0) {  // fork: the aux streams start after the waits above
+      if ((rc = hip_check(hipEventRecord(ev[0], s), "hipEventRecord"))) return rc;
+      for (int a = 0; a < used; ++a)
+        if ((rc = hip_check(hipStreamWaitEvent((hipStream_t)aux_streams[a], ev[0], 0), "hipStreamWaitEvent")))
+          return rc;
+    }
+    for (int i = 0; i < nlaunch; ++i) {
+      hipStream_t si = (used > 0 && i % (used + 1)) ? (hipStream_t)aux_streams[i % (used + 1) - 1] : s;
+      if ((rc = run_one(runs[r0 + i], si))) return rc;
+    }
+    for (int a = 0; a < used; ++a)  // join: the step's signal after every launch of it
+      if ((rc = hip_check(hipEventRecord(ev[1 + a], (hipStream_t)aux_streams[a]), "hipEventRecord")) ||
+          (rc = hip_check(hipStreamWaitEvent(s, ev[1 + a], 0), "hipStreamWaitEvent")))
+        return rc;
     // base + t + 2: step t done (its stores into peer buffers written back)
     hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + t + 2);
     if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;

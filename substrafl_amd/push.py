@@ -62,6 +62,8 @@ class PushTransport:
     native = True
     push = True
 
+    AUX_STREAMS = 3  # with the caller's: 4 streams = GPU_MAX_HW_QUEUES
+
     def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0):
         import torch
         import torch.distributed as dist
@@ -92,6 +94,8 @@ class PushTransport:
         self._maps: Dict[bytes, int] = {}
         self._programs: List["PushProgram"] = []
         self._py = None
+        self._aux = [torch.cuda.Stream(device=self.device) for _ in range(self.AUX_STREAMS)]
+        self._aux_ptrs = _native.ptr_array([st.cuda_stream for st in self._aux])
         dist.barrier(group=group)
 
     # -- set-up helpers --------------------------------------------------------------------
@@ -159,7 +163,8 @@ class PushTransport:
         _check(self.lib.fedagg_push_execute(ctypes.byref(prog.runs) if prog.nruns else None, prog.nruns,
                                             ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
                                             prog.nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
-                                            ws_src, ws_dst, ws_bytes, int(stream)), "fedagg_push_execute")
+                                            ws_src, ws_dst, ws_bytes, self._aux_ptrs, len(self._aux), int(stream)),
+               "fedagg_push_execute")
         self.base += prog.nsteps + 1
         if ws_bytes and self.rank == prog.plan.root:  # one owner per column: the sum is exact
             import torch

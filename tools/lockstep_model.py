@@ -176,6 +176,45 @@ def simulate(plans: Sequence[lockstep.RankPlan], queues: str = "streams", comput
     return {"makespan": max(end.values(), default=0.0), "compute_max": comp}
 
 
+def simulate_push(plans: Sequence[lockstep.RankPlan], run_time, link_s_per_elem: float, launch_s: float = 2e-6,
+                  order_s: float = 4e-6, streams: int = 4) -> Dict[str, float]:
+    """The push executor (substrafl_amd/push.py): no exchange kernels.  Step t of rank r starts
+    when its step t - 1 ended and every rank it waits for (push_schedule) ended step t - 2; its
+    launches (one per consumer, the xGMI stores inside: a launch lasts at least its bytes over
+    the one link it writes to) run round-robin on ``streams`` streams at once, so the step lasts
+    the larger of its HBM work and its busiest stream's link time, plus its wait and signal
+    kernels (order_s)."""
+    from substrafl_amd.push import push_schedule
+
+    G = len(plans)
+    recvs = [[(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(p.groups) for o in ops if o.kind == "recv"]
+             for p in plans]
+    progs = [push_schedule(p, recvs) for p in plans]
+    S = plans[0].n_steps
+    end = [[0.0] * S for _ in range(G)]
+    dur = [[0.0] * S for _ in range(G)]
+    deps = [[[] for _ in range(S + 1)] for _ in range(G)]
+    for r, (specs, waits) in enumerate(progs):
+        for t in range(S):
+            launches = [s for s in specs if s.step == t]
+            lanes = [0.0] * streams  # each stream's links, in series; the HBM work shared by all
+            for i, s in enumerate(launches):
+                lanes[i % streams] += (s.n * link_s_per_elem if s.dst_rank != r else 0.0) + launch_s
+            dur[r][t] = max(sum(run_time(s.n) for s in launches), max(lanes)) if launches else 0.0
+        for t, q, _v in waits:
+            deps[r][t].append(q)
+    for t in range(S):
+        for r in range(G):
+            start = end[r][t - 1] if t else 0.0
+            for q in deps[r][t]:
+                if t >= 2:
+                    start = max(start, end[q][t - 2])
+            end[r][t] = start + dur[r][t] + order_s
+    makespan = max(max(end[r][S - 1] for r in range(G)), max(end[q][S - 1] for q in deps[plans[0].root][S]) if S else 0)
+    comp = max(sum(run_time(s.n) for s in specs) for specs, _ in progs)
+    return {"makespan": makespan, "compute_max": comp}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=8)
@@ -189,6 +228,7 @@ def main():
     ap.add_argument("--rings", type=int, default=0, help="striped chains (0: lockstep.ring_chains' default)")
     ap.add_argument("--overlap", type=float, default=1.0, help="fraction of a group's time hidden under the "
                     "concurrent step's runs (1: ideal; one-GPU probe with RCCL self P2P: ~0.3)")
+    ap.add_argument("--push", action="store_true", help="model the push executor (no exchange kernels) instead")
     ap.add_argument("--from-line", default="", help="a bench.py --gpus N JSON line (file): take --gpus and the link "
                     "rate from its client_shard_torch_pg.xgmi_p2p probe (all-peers GB/s per link direction)")
     args = ap.parse_args()
@@ -209,6 +249,16 @@ def main():
     schedules = {"relay": lockstep.relay_pieces(M, G, args.chunk)}
     for rounds in ((1.0,), (0.75, 0.25), (0.5, 0.3, 0.2), (0.4, 0.3, 0.2, 0.1), (0.6, 0.25, 0.15)):
         schedules[f"striped rounds={rounds}"] = lockstep.striped_pieces(M, G, args.rings or None, rounds)
+    if args.push:
+        for rounds in ((1.0,), (0.75, 0.25), (0.5, 0.3, 0.2)):
+            plans = [lockstep.rank_plan(lockstep.striped_pieces(M, G, args.rings or None, rounds), G, r)
+                     for r in range(G)]
+            res = simulate_push(plans, rt, link)
+            t1 = rt(M)
+            out[f"push rounds={rounds}"] = {"steps": plans[0].n_steps, "model_ms": round(res["makespan"] * 1e3, 3),
+                                            "single_gpu_ms": round(t1 * 1e3, 3),
+                                            "weak_efficiency": round(t1 / res["makespan"], 3)}
+        schedules = {}
     for name, pieces in schedules.items():
         plans = [lockstep.rank_plan(pieces, G, r, cols="global" if name == "relay" else "packed") for r in range(G)]
         res = simulate(plans, "streams", 0.0, link, args.latency_us * 1e-6, run_time=rt, overlap=args.overlap)
