@@ -302,6 +302,10 @@ int fedagg_ipc_close(void* base);
 /* page-locked, device-mapped view of host memory (a node-shared page of progress counters) */
 int fedagg_host_map(void* host, uint64_t bytes, void** dev_out);
 int fedagg_host_unmap(void* host);
+/* device memory no L2 caches (hipDeviceMallocUncached), zeroed: the push executor's landing
+ * buffers, written by peers, read by this GPU's kernels without stale cache lines */
+int fedagg_device_alloc_uncached(uint64_t bytes, void** out);
+int fedagg_device_free(void* p);
 /* wall-clock ticks per second of the device timer the wait kernels use */
 int fedagg_wall_clock_hz(uint64_t* hz_out);
 typedef struct fedagg_push_wait {

@@ -107,6 +107,8 @@ SIGNATURES = {
     "fedagg_host_map": (c_int, [c_void, c_u64, P(c_void)]),
     "fedagg_host_unmap": (c_int, [c_void]),
     "fedagg_wall_clock_hz": (c_int, [P(c_u64)]),
+    "fedagg_device_alloc_uncached": (c_int, [c_u64, P(c_void)]),
+    "fedagg_device_free": (c_int, [c_void]),
     "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64, c_u64, c_void,
                                     c_void, c_u64, c_void, c_int, c_void]),
     "fedagg_session_create": (c_void, [c_int]),

@@ -363,6 +363,16 @@ int fedagg_host_map(void* host, uint64_t bytes, void** dev_out) {
 
 int fedagg_host_unmap(void* host) { return host ? hip_check(hipHostUnregister(host), "hipHostUnregister") : 0; }
 
+int fedagg_device_alloc_uncached(uint64_t bytes, void** out) {
+  if (!out || !bytes) return lfail(FEDAGG_EINVAL, "fedagg_device_alloc_uncached: invalid argument");
+  *out = nullptr;
+  int rc;
+  if ((rc = hip_check(hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags"))) return rc;
+  return hip_check(hipMemset(*out, 0, bytes), "hipMemset");
+}
+
+int fedagg_device_free(void* p) { return p ? hip_check(hipFree(p), "hipFree") : 0; }
+
 int fedagg_wall_clock_hz(uint64_t* hz_out) {
   if (!hz_out) return lfail(FEDAGG_EINVAL, "fedagg_wall_clock_hz: NULL output");
   int dev = 0, khz = 0, rc;

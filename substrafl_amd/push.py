@@ -99,11 +99,11 @@ class PushTransport:
         dist.barrier(group=group)
 
     # -- set-up helpers --------------------------------------------------------------------
-    def ipc_info(self, t) -> Tuple[bytes, int]:
-        """(handle, byte offset) of a device tensor's first element."""
+    def ipc_info(self, ptr: int) -> Tuple[bytes, int]:
+        """(handle, byte offset) of a device address."""
         h = (ctypes.c_char * _native_ipc_bytes())()
         off = ctypes.c_uint64()
-        _check(self.lib.fedagg_ipc_get(t.data_ptr(), h, ctypes.byref(off)), "fedagg_ipc_get")
+        _check(self.lib.fedagg_ipc_get(int(ptr), h, ctypes.byref(off)), "fedagg_ipc_get")
         return bytes(h.raw), int(off.value)
 
     def remote(self, info: Tuple[bytes, int]) -> int:
@@ -166,11 +166,14 @@ class PushTransport:
                                             ws_src, ws_dst, ws_bytes, self._aux_ptrs, len(self._aux), int(stream)),
                "fedagg_push_execute")
         self.base += prog.nsteps + 1
-        if ws_bytes and self.rank == prog.plan.root:  # one owner per column: the sum is exact
-            import torch
+        if self.rank == prog.plan.root and self.world > 1:
+            prog.land_to_out(int(stream))  # the finished pieces other ranks pushed
+            if ws_bytes:  # one owner per column: the sum is exact
+                import torch
 
-            with torch.cuda.stream(torch.cuda.ExternalStream(int(stream))):
-                ws.copy_(prog.stage.view(self.world, *ws.shape).sum(0))
+                with torch.cuda.stream(torch.cuda.ExternalStream(int(stream))):
+                    _memcpy(prog.stage_t.data_ptr(), prog.stage_u.ptr, prog.stage_u.bytes, int(stream))
+                    ws.copy_(prog.stage_t.view(self.world, *ws.shape).sum(0))
 
     def close(self) -> None:
         if getattr(self, "_dev", None) is None:
@@ -195,6 +198,37 @@ def _native_ipc_bytes() -> int:
     return 64  # FEDAGG_IPC_HANDLE_BYTES
 
 
+class _Uncached:
+    """Device memory no L2 caches (fedagg_device_alloc_uncached), freed with its owner."""
+
+    def __init__(self, lib, nbytes: int):
+        self.lib, self.bytes = lib, int(nbytes)
+        p = ctypes.c_void_p()
+        _check(lib.fedagg_device_alloc_uncached(self.bytes, ctypes.byref(p)), "fedagg_device_alloc_uncached")
+        self.ptr = int(p.value)
+
+    def __del__(self):
+        try:
+            self.lib.fedagg_device_free(self.ptr)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+_HIP = None
+
+
+def _memcpy(dst: int, src: int, nbytes: int, stream: int) -> None:
+    """Device-to-device hipMemcpyAsync on ``stream``."""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_void_p]
+    rc = _HIP.hipMemcpyAsync(dst, src, nbytes, 3, stream)  # hipMemcpyDeviceToDevice
+    if rc:
+        raise _native.NativeLibraryError(f"hipMemcpyAsync failed ({rc})")
+
+
 class PushProgram:
     """One rank's schedule compiled for the push executor: its runs split by consumer with
     every output address resolved (a mapped peer slot, the root's output, or its own output),
@@ -212,29 +246,46 @@ class PushProgram:
         self.plan, self.blocks, self.accs, self.outs, self.kind = plan, blocks, accs, outs, kind
         self._keep: list = []
         G, me, root = plan.world, plan.rank, plan.root
-        slots, out = accs[0], outs[0]
+        out = outs[0]
         esz = out.element_size()
-        self.stage = None  # the root's numel == 1 product staging (one row per rank), at first use
-        # every rank's buffers and receive ops, once
-        mine = {"slots": [tr.ipc_info(slots[s]) for s in range(slots.shape[0])] if G > 1 else [],
-                "out": tr.ipc_info(out) if G > 1 else None,
+        # What peers write lands in memory no L2 caches (a consumer's L2 could still hold the lines
+        # a slot had four steps earlier): the slots, and a landing copy of the output's index space
+        # (the last block's input on every rank, the finished pieces on the root).  The caller's
+        # slots are not used; the root copies the landed finished pieces into its output.
+        se = max(1, plan.slot_elems)
+        self.slots_u = _Uncached(tr.lib, lockstep.SLOTS * se * esz)
+        self.land_u = _Uncached(tr.lib, out.numel() * esz)
+        self.stage_u = self.stage_t = None  # the root's numel == 1 product staging, at first use
+        mine = {"slots": tr.ipc_info(self.slots_u.ptr) if G > 1 else None,
+                "land": tr.ipc_info(self.land_u.ptr) if G > 1 else None,
                 "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
                          if o.kind == "recv"]}
         infos = tr.all_gather(mine) if G > 1 else [mine]
 
         def local(loc) -> int:
             where, slot, off = loc
-            base = out if where == "out" else slots[slot]
-            return base.data_ptr() + off * esz
+            if where == "out":
+                return self.land_u.ptr + off * esz
+            return self.slots_u.ptr + (slot * se + off) * esz
 
         def at(rank: int, loc) -> int:
-            if rank == me:
-                return local(loc)
             where, slot, off = loc
-            info = infos[rank]["out"] if where == "out" else infos[rank]["slots"][slot]
-            return tr.remote(info) + off * esz
+            if rank == me:
+                # the root's own finished pieces: straight into the caller's output
+                return out.data_ptr() + off * esz if where == "out" and rank == root else local(loc)
+            if where == "out":
+                return tr.remote(infos[rank]["land"]) + off * esz
+            return tr.remote(infos[rank]["slots"]) + (slot * se + off) * esz
 
         specs, wait_list = push_schedule(plan, [info["recv"] for info in infos])
+        # the output ranges other ranks finish (landed on the root, copied into its output)
+        own = sorted((p.dst[2], p.dst[2] + p.n) for p in specs if p.dst_rank == me and p.dst[0] == "out")
+        self._land_ranges, a = [], 0
+        for lo, hi in own + [(out.numel(), out.numel())]:
+            if lo > a:
+                self._land_ranges.append((a, lo))
+            a = max(a, hi)
+        self._esz, self._out = esz, out
         runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
                           local(p.src) if p.src is not None else 0) for p in specs]
         waits = [_Wait(t, q, v) for t, q, v in wait_list]
@@ -252,15 +303,22 @@ class PushProgram:
         tr, G = self._tr, self.plan.world
         if self._stage_info is None or self._stage_info[1] != ws_bytes:
             if self.plan.rank == self.plan.root:
-                self.stage = torch.zeros(G * ws_bytes // 4, dtype=torch.float32, device=self.outs[0].device)
-                info = tr.ipc_info(self.stage)
+                self.stage_u = _Uncached(tr.lib, G * ws_bytes)
+                self.stage_t = torch.empty(G * ws_bytes // 4, dtype=torch.float32, device=self.outs[0].device)
+                info = tr.ipc_info(self.stage_u.ptr)
             else:
                 info = None
             infos = tr.all_gather(info)
             self._stage_info = (infos[self.plan.root], ws_bytes)
         if self.plan.rank == self.plan.root:
-            return self.stage.data_ptr() + self.plan.rank * ws_bytes
+            return self.stage_u.ptr + self.plan.rank * ws_bytes
         return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
+
+    def land_to_out(self, stream: int) -> None:
+        """Root: the finished pieces other ranks pushed, from the landing buffer into the output."""
+        for a, b in self._land_ranges:
+            _memcpy(self._out.data_ptr() + a * self._esz, self.land_u.ptr + a * self._esz, (b - a) * self._esz,
+                    stream)
 
     def _run(self, t: int, sh, col: int, n: int, dst: int, src: int) -> _Run:
         rec = _Run()
@@ -280,7 +338,6 @@ class PushProgram:
 
     def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:
         return (plan is self.plan and blocks is self.blocks and kind == self.kind and not scaffold
-                and [a.data_ptr() for a in accs] == [a.data_ptr() for a in self.accs]
                 and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
 
 
