@@ -306,6 +306,8 @@ int fedagg_host_unmap(void* host);
  * buffers, written by peers, read by this GPU's kernels without stale cache lines */
 int fedagg_device_alloc_uncached(uint64_t bytes, void** out);
 int fedagg_device_free(void* p);
+/* device-to-device copy on `stream` (the same HIP runtime as the caller's streams) */
+int fedagg_copy_async(void* dst, const void* src, uint64_t bytes, void* stream);
 /* wall-clock ticks per second of the device timer the wait kernels use */
 int fedagg_wall_clock_hz(uint64_t* hz_out);
 typedef struct fedagg_push_wait {

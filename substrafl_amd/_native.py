@@ -109,6 +109,7 @@ SIGNATURES = {
     "fedagg_wall_clock_hz": (c_int, [P(c_u64)]),
     "fedagg_device_alloc_uncached": (c_int, [c_u64, P(c_void)]),
     "fedagg_device_free": (c_int, [c_void]),
+    "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
     "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64, c_u64, c_void,
                                     c_void, c_u64, c_void, c_int, c_void]),
     "fedagg_session_create": (c_void, [c_int]),

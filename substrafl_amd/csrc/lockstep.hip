@@ -373,6 +373,12 @@ int fedagg_device_alloc_uncached(uint64_t bytes, void** out) {
 
 int fedagg_device_free(void* p) { return p ? hip_check(hipFree(p), "hipFree") : 0; }
 
+int fedagg_copy_async(void* dst, const void* src, uint64_t bytes, void* stream) {
+  if (!bytes) return FEDAGG_OK;
+  if (!dst || !src) return lfail(FEDAGG_EINVAL, "fedagg_copy_async: NULL argument");
+  return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream), "hipMemcpyAsync");
+}
+
 int fedagg_wall_clock_hz(uint64_t* hz_out) {
   if (!hz_out) return lfail(FEDAGG_EINVAL, "fedagg_wall_clock_hz: NULL output");
   int dev = 0, khz = 0, rc;
@@ -408,19 +414,21 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
   // a step's launches (one per consumer: each writes over its own xGMI link) spread over the
   // caller's stream and the aux streams, forked from and joined back into the caller's stream
-  hipEvent_t ev[8] = {};
-  for (int i = 0; i <= naux; ++i)
-    if ((rc = hip_check(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "hipEventCreate"))) {
-      for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
-      return rc;
-    }
-  struct EvGuard {
-    hipEvent_t* e;
-    int n;
-    ~EvGuard() {
-      for (int i = 0; i < n; ++i) (void)hipEventDestroy(e[i]);
-    }
-  } guard{ev, naux + 1};
+  // fork / join events: kept for the thread's lifetime (per device), never destroyed while a
+  // wait the GPU has not run yet may still name them; re-recording one is safe (a wait takes the
+  // record current when it is enqueued)
+  static thread_local hipEvent_t ev_pool[16][8];
+  static thread_local bool ev_made[16];
+  int dev = 0;
+  if ((rc = hip_check(hipGetDevice(&dev), "hipGetDevice"))) return rc;
+  if (dev < 0 || dev >= 16) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: device index beyond 15");
+  if (!ev_made[dev]) {
+    for (int i = 0; i < 8; ++i)
+      if ((rc = hip_check(hipEventCreateWithFlags(&ev_pool[dev][i], hipEventDisableTiming), "hipEventCreate")))
+        return rc;
+    ev_made[dev] = true;
+  }
+  hipEvent_t* ev = ev_pool[dev];
   int ri = 0, wi = 0;
   for (int t = 0; t < nsteps; ++t) {
     if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, s))) return rc;

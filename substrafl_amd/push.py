@@ -214,19 +214,10 @@ class _Uncached:
             pass
 
 
-_HIP = None
-
-
 def _memcpy(dst: int, src: int, nbytes: int, stream: int) -> None:
-    """Device-to-device hipMemcpyAsync on ``stream``."""
-    global _HIP
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so")
-        _HIP.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
-                                        ctypes.c_void_p]
-    rc = _HIP.hipMemcpyAsync(dst, src, nbytes, 3, stream)  # hipMemcpyDeviceToDevice
-    if rc:
-        raise _native.NativeLibraryError(f"hipMemcpyAsync failed ({rc})")
+    """Device-to-device copy on ``stream`` through libfedagg (the process's one HIP runtime: a
+    ctypes load of libamdhip64 by another path would be a second runtime, blind to torch's streams)."""
+    _check(_native.load().fedagg_copy_async(dst, src, nbytes, stream), "fedagg_copy_async")
 
 
 class PushProgram:

@@ -83,7 +83,15 @@ def _worker(rank, G, K, rounds, relay, shapes_name, port, q):
             calls += 1
             if is_root:
                 got = [a for _, a in layout.unpack(out[: layout.M].cpu().numpy())]
-                bad.append(sum(int(np.count_nonzero(g.view(np.uint32) != r.view(np.uint32))) for g, r in zip(got, ref)))
+                nb = sum(int(np.count_nonzero(g.view(np.uint32) != r.view(np.uint32))) for g, r in zip(got, ref))
+                if nb and os.environ.get("PUSH_DEBUG"):
+                    print(f"[push debug] call {calls}: " + "; ".join(
+                        f"layer {i} {g.shape}: idx {np.nonzero(g.reshape(-1).view(np.uint32) != r.reshape(-1).view(np.uint32))[0][:4]} "
+                        f"got {g.reshape(-1)[np.nonzero(g.reshape(-1).view(np.uint32) != r.reshape(-1).view(np.uint32))[0][:2]]} "
+                        f"ref {r.reshape(-1)[np.nonzero(g.reshape(-1).view(np.uint32) != r.reshape(-1).view(np.uint32))[0][:2]]}"
+                        for i, (g, r) in enumerate(zip(got, ref)) if np.any(g.view(np.uint32) != r.view(np.uint32))),
+                        file=sys.stderr, flush=True)
+                bad.append(nb)
         errs = tr.errors()
         programs = len(tr._programs)
         tr.close()
