@@ -171,6 +171,13 @@ __global__ void __launch_bounds__(64) push_signal_kernel(uint64_t* progress, uin
   __hip_atomic_store(progress + idx, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// dst[0, n) = src[0, n) (4-byte words) with ordinary vector stores: a copy into a peer's mapped
+// memory that stays in the stream's order (a runtime copy into imported memory need not).
+__global__ void __launch_bounds__(256) push_copy_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                        uint64_t n) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) dst[i] = src[i];
+}
+
 int push_waits(const fedagg_push_wait* waits, int& wi, int nwaits, int step, uint64_t* progress, uint64_t base,
                uint64_t timeout, uint64_t* err, hipStream_t s) {
   while (wi < nwaits && waits[wi].step == step) {
@@ -432,9 +439,13 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   int ri = 0, wi = 0;
   for (int t = 0; t < nsteps; ++t) {
     if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, s))) return rc;
-    if (t == 0 && ws_bytes &&  // after step 0's waits, which include the root's entry
-        (rc = hip_check(hipMemcpyAsync(ws_dst, ws_src, ws_bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync")))
-      return rc;
+    if (t == 0 && ws_bytes) {  // after step 0's waits, which include the root's entry
+      if (ws_bytes % 4) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: ws_bytes must be a multiple of 4");
+      const uint64_t words = ws_bytes / 4;
+      const unsigned g = (unsigned)((words + 255) / 256 < 64 ? (words + 255) / 256 : 64);
+      hipLaunchKernelGGL(push_copy_kernel, dim3(g), dim3(256), 0, s, (uint32_t*)ws_dst, (const uint32_t*)ws_src, words);
+      if ((rc = hip_check(hipGetLastError(), "push_copy_kernel"))) return rc;
+    }
     int r0 = ri;
     while (ri < nruns && runs[ri].step == t) ++ri;
     const int nlaunch = ri - r0, used = nlaunch - 1 < naux ? nlaunch - 1 : naux;
