@@ -316,14 +316,19 @@ typedef struct fedagg_push_wait {
   int64_t value;             /* counter >= base + value (<= 0: nothing to wait for)              */
 } fedagg_push_wait;
 /* runs: FEDAGG_RUN_FEDAVG only (acc may be a mapped peer address); waits sorted by step;
- * ws_src / ws_dst / ws_bytes: one device copy issued after step 0's waits (the numel == 1 products
- * to the root's staging row; 0 bytes: none).  A step's launches (one per consumer, each writing
- * over its own link) are spread round-robin over `stream` and the `naux` (<= 7) aux streams,
- * forked from and joined back into `stream` around the step.  Asynchronous on `stream`. */
+ * ws_src / ws_dst / ws_bytes: the numel == 1 products (fp32) copied to this rank's staging row on
+ * the root after step 0's waits (0 bytes: none); ws_stage (root only, else NULL): the nranks
+ * staging rows, summed into ws_src after the last waits.  land / out / land_ranges (root only):
+ * nranges (element offset, count) pairs of fp32 copied from the landing buffer into the output
+ * after the last waits (the finished pieces other ranks pushed).  A step's launches (one per
+ * consumer, each writing over its own link) are spread round-robin over `stream` and the `naux`
+ * (<= 7) aux streams, forked from and joined back into `stream` around the step.  Asynchronous
+ * on `stream`. */
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
-                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, void* const* aux_streams, int naux,
-                        void* stream);
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, const void* ws_stage,
+                        const void* land, void* out, const uint64_t* land_ranges, int nranges,
+                        void* const* aux_streams, int naux, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Client-side flat-bucket ops (the producer / consumer of the buckets, SURVEY.md §8(a)

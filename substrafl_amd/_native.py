@@ -111,7 +111,7 @@ SIGNATURES = {
     "fedagg_device_free": (c_int, [c_void]),
     "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
     "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64, c_u64, c_void,
-                                    c_void, c_u64, c_void, c_int, c_void]),
+                                    c_void, c_u64, c_void, c_void, c_void, c_void, c_int, c_void, c_int, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),

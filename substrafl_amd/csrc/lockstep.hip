@@ -178,6 +178,28 @@ __global__ void __launch_bounds__(256) push_copy_kernel(uint32_t* __restrict__ d
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) dst[i] = src[i];
 }
 
+// Root: ws[i] = stage[0][i] + ... + stage[G-1][i] in rank order (one owner per column, the
+// others +0.0: exact).
+__global__ void __launch_bounds__(256) push_stage_sum_kernel(float* __restrict__ ws, const float* __restrict__ stage,
+                                                             int G, uint64_t n) {
+#pragma clang fp contract(off)
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) {
+    float a = stage[i];
+    for (int g = 1; g < G; ++g) a = a + stage[(uint64_t)g * n + i];
+    ws[i] = a;
+  }
+}
+
+int push_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
+  if (bytes % 4) return lfail(FEDAGG_EINVAL, "push: copies are whole 4-byte words");
+  const uint64_t words = bytes / 4;
+  if (!words) return FEDAGG_OK;
+  const uint64_t g = (words + 255) / 256;
+  hipLaunchKernelGGL(push_copy_kernel, dim3((unsigned)(g < 2048 ? g : 2048)), dim3(256), 0, s, (uint32_t*)dst,
+                     (const uint32_t*)src, words);
+  return hip_check(hipGetLastError(), "push_copy_kernel");
+}
+
 int push_waits(const fedagg_push_wait* waits, int& wi, int nwaits, int step, uint64_t* progress, uint64_t base,
                uint64_t timeout, uint64_t* err, hipStream_t s) {
   while (wi < nwaits && waits[wi].step == step) {
@@ -398,11 +420,12 @@ int fedagg_wall_clock_hz(uint64_t* hz_out) {
 
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
-                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, void* const* aux_streams, int naux,
-                        void* stream) {
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, const void* ws_stage,
+                        const void* land, void* out, const uint64_t* land_ranges, int nranges,
+                        void* const* aux_streams, int naux, void* stream) {
   if (nruns < 0 || nwaits < 0 || nsteps < 0 || (nruns && !runs) || (nwaits && !waits) || !progress || nranks < 1 ||
       rank < 0 || rank >= nranks || (ws_bytes && (!ws_src || !ws_dst)) || naux < 0 || naux > 7 ||
-      (naux && !aux_streams))
+      (naux && !aux_streams) || nranges < 0 || (nranges && (!land_ranges || !land || !out)))
     return lfail(FEDAGG_EINVAL, "fedagg_push_execute: invalid argument");
   for (int i = 0; i < nwaits; ++i)
     if (waits[i].rank < 0 || waits[i].rank >= nranks || waits[i].step < 0 || waits[i].step > nsteps ||
@@ -439,13 +462,9 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   int ri = 0, wi = 0;
   for (int t = 0; t < nsteps; ++t) {
     if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, s))) return rc;
-    if (t == 0 && ws_bytes) {  // after step 0's waits, which include the root's entry
-      if (ws_bytes % 4) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: ws_bytes must be a multiple of 4");
-      const uint64_t words = ws_bytes / 4;
-      const unsigned g = (unsigned)((words + 255) / 256 < 64 ? (words + 255) / 256 : 64);
-      hipLaunchKernelGGL(push_copy_kernel, dim3(g), dim3(256), 0, s, (uint32_t*)ws_dst, (const uint32_t*)ws_src, words);
-      if ((rc = hip_check(hipGetLastError(), "push_copy_kernel"))) return rc;
-    }
+    if (t == 0 && ws_bytes &&  // after step 0's waits, which include the root's entry
+        (rc = push_copy(ws_dst, ws_src, ws_bytes, s)))
+      return rc;
     int r0 = ri;
     while (ri < nruns && runs[ri].step == t) ++ri;
     const int nlaunch = ri - r0, used = nlaunch - 1 < naux ? nlaunch - 1 : naux;
@@ -467,7 +486,20 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
     hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + t + 2);
     if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
   }
-  return push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, s);
+  if ((rc = push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, s))) return rc;
+  // root, once every rank's last step is in: the finished pieces others pushed, into the output;
+  // the numel == 1 staging rows, summed into this rank's workspace
+  for (int i = 0; i < nranges; ++i) {
+    const uint64_t a = land_ranges[2 * i], n = land_ranges[2 * i + 1];
+    if ((rc = push_copy((char*)out + a * 4, (const char*)land + a * 4, n * 4, s))) return rc;
+  }
+  if (ws_stage && ws_bytes) {
+    const uint64_t n = ws_bytes / 4, g = (n + 255) / 256;
+    hipLaunchKernelGGL(push_stage_sum_kernel, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s,
+                       (float*)ws_src, (const float*)ws_stage, nranks, n);
+    if ((rc = hip_check(hipGetLastError(), "push_stage_sum_kernel"))) return rc;
+  }
+  return FEDAGG_OK;
 }
 
 }  // extern "C"

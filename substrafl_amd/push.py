@@ -160,20 +160,17 @@ class PushTransport:
         if ws is not None and self.world > 1:
             ws_bytes = ws.numel() * ws.element_size()
             ws_src, ws_dst = ws.data_ptr(), prog.ws_dst(ws_bytes)
+        root = self.rank == prog.plan.root and self.world > 1
+        stage = prog.stage_u.ptr if root and ws_bytes else None
+        ranges = prog.land_ranges if root else None
         _check(self.lib.fedagg_push_execute(ctypes.byref(prog.runs) if prog.nruns else None, prog.nruns,
                                             ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
                                             prog.nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
-                                            ws_src, ws_dst, ws_bytes, self._aux_ptrs, len(self._aux), int(stream)),
-               "fedagg_push_execute")
+                                            ws_src, ws_dst, ws_bytes, stage,
+                                            prog.land_u.ptr if root else None, prog.out_ptr if root else None,
+                                            ranges, prog.land_ranges_n // 2 if ranges is not None else 0,
+                                            self._aux_ptrs, len(self._aux), int(stream)), "fedagg_push_execute")
         self.base += prog.nsteps + 1
-        if self.rank == prog.plan.root and self.world > 1:
-            prog.land_to_out(int(stream))  # the finished pieces other ranks pushed
-            if ws_bytes:  # one owner per column: the sum is exact
-                import torch
-
-                with torch.cuda.stream(torch.cuda.ExternalStream(int(stream))):
-                    _memcpy(prog.stage_t.data_ptr(), prog.stage_u.ptr, prog.stage_u.bytes, int(stream))
-                    ws.copy_(prog.stage_t.view(self.world, *ws.shape).sum(0))
 
     def close(self) -> None:
         if getattr(self, "_dev", None) is None:
@@ -212,124 +209,6 @@ class _Uncached:
             self.lib.fedagg_device_free(self.ptr)
         except Exception:  # noqa: BLE001 -- interpreter shutdown
             pass
-
-
-def _memcpy(dst: int, src: int, nbytes: int, stream: int) -> None:
-    """Device-to-device copy on ``stream`` through libfedagg (the process's one HIP runtime: a
-    ctypes load of libamdhip64 by another path would be a second runtime, blind to torch's streams)."""
-    _check(_native.load().fedagg_copy_async(dst, src, nbytes, stream), "fedagg_copy_async")
-
-
-class PushProgram:
-    """One rank's schedule compiled for the push executor: its runs split by consumer with
-    every output address resolved (a mapped peer slot, the root's output, or its own output),
-    and the waits of every step.  Built collectively (every rank at once)."""
-
-    def __init__(self, tr: PushTransport, plan: lockstep.RankPlan, blocks, accs, outs, kind: str, scaffold: bool,
-                 c=None, lr: float = 1.0):
-        import torch
-
-        if scaffold or kind != "f32":
-            raise ValueError("push executor: fp32 FedAvg only (the other kinds take the RCCL executor)")
-        for sh in blocks.values():
-            if not isinstance(getattr(sh, "rows", None), torch.Tensor):
-                raise ValueError("push executor: row-layout client blocks only")
-        self.plan, self.blocks, self.accs, self.outs, self.kind = plan, blocks, accs, outs, kind
-        self._keep: list = []
-        G, me, root = plan.world, plan.rank, plan.root
-        out = outs[0]
-        esz = out.element_size()
-        # What peers write lands in memory no L2 caches (a consumer's L2 could still hold the lines
-        # a slot had four steps earlier): the slots, and a landing copy of the output's index space
-        # (the last block's input on every rank, the finished pieces on the root).  The caller's
-        # slots are not used; the root copies the landed finished pieces into its output.
-        se = max(1, plan.slot_elems)
-        self.slots_u = _Uncached(tr.lib, lockstep.SLOTS * se * esz)
-        self.land_u = _Uncached(tr.lib, out.numel() * esz)
-        self.stage_u = self.stage_t = None  # the root's numel == 1 product staging, at first use
-        mine = {"slots": tr.ipc_info(self.slots_u.ptr) if G > 1 else None,
-                "land": tr.ipc_info(self.land_u.ptr) if G > 1 else None,
-                "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
-                         if o.kind == "recv"]}
-        infos = tr.all_gather(mine) if G > 1 else [mine]
-
-        def local(loc) -> int:
-            where, slot, off = loc
-            if where == "out":
-                return self.land_u.ptr + off * esz
-            return self.slots_u.ptr + (slot * se + off) * esz
-
-        def at(rank: int, loc) -> int:
-            where, slot, off = loc
-            if rank == me:
-                # the root's own finished pieces: straight into the caller's output
-                return out.data_ptr() + off * esz if where == "out" and rank == root else local(loc)
-            if where == "out":
-                return tr.remote(infos[rank]["land"]) + off * esz
-            return tr.remote(infos[rank]["slots"]) + (slot * se + off) * esz
-
-        specs, wait_list = push_schedule(plan, [info["recv"] for info in infos])
-        # the output ranges other ranks finish (landed on the root, copied into its output)
-        own = sorted((p.dst[2], p.dst[2] + p.n) for p in specs if p.dst_rank == me and p.dst[0] == "out")
-        self._land_ranges, a = [], 0
-        for lo, hi in own + [(out.numel(), out.numel())]:
-            if lo > a:
-                self._land_ranges.append((a, lo))
-            a = max(a, hi)
-        self._esz, self._out = esz, out
-        runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
-                          local(p.src) if p.src is not None else 0) for p in specs]
-        waits = [_Wait(t, q, v) for t, q, v in wait_list]
-        n_steps = plan.n_steps
-        self.nruns, self.nwaits, self.nsteps = len(runs), len(waits), n_steps
-        self.runs = (_Run * max(1, len(runs)))(*runs)
-        self.waits = (_Wait * max(1, len(waits)))(*waits)
-        self._tr = tr
-        self._stage_info = None
-
-    def ws_dst(self, ws_bytes: int) -> int:
-        """This rank's staging row on the root for the numel == 1 products (collective at first use)."""
-        import torch
-
-        tr, G = self._tr, self.plan.world
-        if self._stage_info is None or self._stage_info[1] != ws_bytes:
-            if self.plan.rank == self.plan.root:
-                self.stage_u = _Uncached(tr.lib, G * ws_bytes)
-                self.stage_t = torch.empty(G * ws_bytes // 4, dtype=torch.float32, device=self.outs[0].device)
-                info = tr.ipc_info(self.stage_u.ptr)
-            else:
-                info = None
-            infos = tr.all_gather(info)
-            self._stage_info = (infos[self.plan.root], ws_bytes)
-        if self.plan.rank == self.plan.root:
-            return self.stage_u.ptr + self.plan.rank * ws_bytes
-        return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
-
-    def land_to_out(self, stream: int) -> None:
-        """Root: the finished pieces other ranks pushed, from the landing buffer into the output."""
-        for a, b in self._land_ranges:
-            _memcpy(self._out.data_ptr() + a * self._esz, self.land_u.ptr + a * self._esz, (b - a) * self._esz,
-                    stream)
-
-    def _run(self, t: int, sh, col: int, n: int, dst: int, src: int) -> _Run:
-        rec = _Run()
-        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG, _native.FEDAGG_F32, 1, 0, n
-        rows = sh.rows
-        base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
-        ptrs = [base + k * step + col * esz for k in range(rows.shape[0])]
-        w = [float(v) for v in np.asarray(sh.w, np.float32)]
-        if src:  # the input accumulator: one more client of weight 1.0, first in order
-            ptrs, w = [src] + ptrs, [1.0] + w
-        rec.K = len(ptrs)
-        arr = _native.ptr_array(ptrs)
-        warr = (ctypes.c_float * len(w))(*w)
-        self._keep += [arr, warr]
-        rec.x, rec.w, rec.acc = ctypes.addressof(arr), ctypes.addressof(warr), dst
-        return rec
-
-    def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:
-        return (plan is self.plan and blocks is self.blocks and kind == self.kind and not scaffold
-                and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
 
 
 @dataclass(frozen=True)

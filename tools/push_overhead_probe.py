@@ -61,7 +61,8 @@ def main():
         push._check(lib.fedagg_push_execute(ctypes.byref(R) if with_runs else None, S if with_runs else 0,
                                             ctypes.byref(W) if with_order and waits else None,
                                             len(waits) if with_order else 0, S, dev.value, 0, G, base[0],
-                                            1 << 40, None, None, 0, None, 0, stream.cuda_stream), "fedagg_push_execute")
+                                            1 << 40, None, None, 0, None, None, None, None, 0, None, 0,
+                                            stream.cuda_stream), "fedagg_push_execute")
         base[0] += S + 1
 
     def timed(*cfg):
