@@ -211,6 +211,112 @@ class _Uncached:
             pass
 
 
+class PushProgram:
+    """One rank's schedule compiled for the push executor: its runs split by consumer with
+    every output address resolved (a mapped peer slot, the root's output, or its own output),
+    and the waits of every step.  Built collectively (every rank at once)."""
+
+    def __init__(self, tr: PushTransport, plan: lockstep.RankPlan, blocks, accs, outs, kind: str, scaffold: bool,
+                 c=None, lr: float = 1.0):
+        import torch
+
+        if scaffold or kind != "f32":
+            raise ValueError("push executor: fp32 FedAvg only (the other kinds take the RCCL executor)")
+        for sh in blocks.values():
+            if not isinstance(getattr(sh, "rows", None), torch.Tensor):
+                raise ValueError("push executor: row-layout client blocks only")
+        self.plan, self.blocks, self.accs, self.outs, self.kind = plan, blocks, accs, outs, kind
+        self._keep: list = []
+        G, me, root = plan.world, plan.rank, plan.root
+        out = outs[0]
+        esz = out.element_size()
+        # What peers write lands in memory no L2 caches (a consumer's L2 could still hold the lines
+        # a slot had four steps earlier): the slots, and a landing copy of the output's index space
+        # (the last block's input on every rank, the finished pieces on the root).  The caller's
+        # slots are not used; the root copies the landed finished pieces into its output.
+        se = max(1, plan.slot_elems)
+        self.slots_u = _Uncached(tr.lib, lockstep.SLOTS * se * esz)
+        self.land_u = _Uncached(tr.lib, out.numel() * esz)
+        self.stage_u = None  # the root's numel == 1 product staging, at first use
+        mine = {"slots": tr.ipc_info(self.slots_u.ptr) if G > 1 else None,
+                "land": tr.ipc_info(self.land_u.ptr) if G > 1 else None,
+                "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
+                         if o.kind == "recv"]}
+        infos = tr.all_gather(mine) if G > 1 else [mine]
+
+        def local(loc) -> int:
+            where, slot, off = loc
+            if where == "out":
+                return self.land_u.ptr + off * esz
+            return self.slots_u.ptr + (slot * se + off) * esz
+
+        def at(rank: int, loc) -> int:
+            where, slot, off = loc
+            if rank == me:
+                # the root's own finished pieces: straight into the caller's output
+                return out.data_ptr() + off * esz if where == "out" and rank == root else local(loc)
+            if where == "out":
+                return tr.remote(infos[rank]["land"]) + off * esz
+            return tr.remote(infos[rank]["slots"]) + (slot * se + off) * esz
+
+        specs, wait_list = push_schedule(plan, [info["recv"] for info in infos])
+        # the output ranges other ranks finish (landed on the root, copied into its output)
+        own = sorted((p.dst[2], p.dst[2] + p.n) for p in specs if p.dst_rank == me and p.dst[0] == "out")
+        self._land_ranges, a = [], 0
+        for lo, hi in own + [(out.numel(), out.numel())]:
+            if lo > a:
+                self._land_ranges.append((a, lo))
+            a = max(a, hi)
+        flat = [v for a, b in self._land_ranges for v in (a, b - a)]
+        self.land_ranges = (ctypes.c_uint64 * max(1, len(flat)))(*flat)
+        self.land_ranges_n = len(flat)
+        self.out_ptr = out.data_ptr()
+        runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
+                          local(p.src) if p.src is not None else 0) for p in specs]
+        waits = [_Wait(t, q, v) for t, q, v in wait_list]
+        n_steps = plan.n_steps
+        self.nruns, self.nwaits, self.nsteps = len(runs), len(waits), n_steps
+        self.runs = (_Run * max(1, len(runs)))(*runs)
+        self.waits = (_Wait * max(1, len(waits)))(*waits)
+        self._tr = tr
+        self._stage_info = None
+
+    def ws_dst(self, ws_bytes: int) -> int:
+        """This rank's staging row on the root for the numel == 1 products (collective at first use)."""
+        tr, G = self._tr, self.plan.world
+        if self._stage_info is None or self._stage_info[1] != ws_bytes:
+            if self.plan.rank == self.plan.root:
+                self.stage_u = _Uncached(tr.lib, G * ws_bytes)
+                info = tr.ipc_info(self.stage_u.ptr)
+            else:
+                info = None
+            infos = tr.all_gather(info)
+            self._stage_info = (infos[self.plan.root], ws_bytes)
+        if self.plan.rank == self.plan.root:
+            return self.stage_u.ptr + self.plan.rank * ws_bytes
+        return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
+
+    def _run(self, t: int, sh, col: int, n: int, dst: int, src: int) -> _Run:
+        rec = _Run()
+        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG, _native.FEDAGG_F32, 1, 0, n
+        rows = sh.rows
+        base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
+        ptrs = [base + k * step + col * esz for k in range(rows.shape[0])]
+        w = [float(v) for v in np.asarray(sh.w, np.float32)]
+        if src:  # the input accumulator: one more client of weight 1.0, first in order
+            ptrs, w = [src] + ptrs, [1.0] + w
+        rec.K = len(ptrs)
+        arr = _native.ptr_array(ptrs)
+        warr = (ctypes.c_float * len(w))(*w)
+        self._keep += [arr, warr]
+        rec.x, rec.w, rec.acc = ctypes.addressof(arr), ctypes.addressof(warr), dst
+        return rec
+
+    def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:
+        return (plan is self.plan and blocks is self.blocks and kind == self.kind and not scaffold
+                and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
+
+
 @dataclass(frozen=True)
 class PushRun:
     """One launch of the push executor: ``n`` elements at column ``col`` of ``block``'s buffer;
