@@ -18,16 +18,14 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 # (G, K, rounds, relay, shapes)
-# The relay's numel == 1 elements came out with only the root's products in the second of three
-# calls while the root's staging sum was a torch op after the executor (the striped cases passed);
-# the sum and the landing copies now run inside the executor -- every case non-strict until a GPU
-# run has re-verified that build (the push executor is an extra N > 1 leg, not the product default).
-_UNVERIFIED = pytest.mark.xfail(strict=False, reason="re-verify the in-executor staging sum / landing copies")
+# (the relay case once gave the numel == 1 elements only the root's products in the second of
+# three calls, while the root's staging sum was a torch op after the executor; the sum and the
+# landing copies run inside the executor since)
 CASES = [
-    pytest.param(2, 5, (1.0,), False, "default", marks=_UNVERIFIED),
-    pytest.param(3, 7, (0.5, 0.3, 0.2), False, "default", marks=_UNVERIFIED),
-    pytest.param(4, 9, (0.75, 0.25), True, "default", marks=_UNVERIFIED),
-    pytest.param(3, 40, (0.5, 0.5), False, "wide", marks=_UNVERIFIED),
+    (2, 5, (1.0,), False, "default"),
+    (3, 7, (0.5, 0.3, 0.2), False, "default"),
+    (4, 9, (0.75, 0.25), True, "default"),
+    (3, 40, (0.5, 0.5), False, "wide"),
 ]
 
 
