@@ -918,7 +918,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                      "native RCCL (csrc/lockstep.hip)" if getattr(tr, "native", False) else
                      "Python schedule over torch.distributed" if world > 1 else "one rank (no exchange)"),
         "schedule": schedule,
-        "hip_streams_per_rank": "2 (compute + the communicator's) <= GPU_MAX_HW_QUEUES = 4",
+        "hip_streams_per_rank": ("4 (compute + 3 for a step's per-consumer launches)" if getattr(tr, "push", False)
+                                 else "2 (compute + the communicator's)") + " <= GPU_MAX_HW_QUEUES = 4",
         "parity": parity,
     }
     if scaling == "weak":
