@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 12
+#define FEDAGG_ABI_VERSION 13
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -170,6 +170,12 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
  * -------------------------------------------------------------------------*/
 int fedagg_fedavg_chain_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                             float* d_out, void* stream);
+/* The push executor's chain run (FEDAGG_RUN_FEDAVG_PUSH): d_out may be a peer GPU's memory mapped
+ * over xGMI; every wave of the launch ends with a system-scope release after its last store, so
+ * the stores are performed at system scope before the executor's tag / counter writes that follow
+ * the launch (fed_avg.py:221-222, the block's clients continuing the accumulator in order). */
+int fedagg_fedavg_chain_push_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
+                                 float* d_out, void* stream);
 int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                              float* d_out, void* stream);
 int fedagg_fedavg_chain_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, int seed,
@@ -234,7 +240,8 @@ int fedagg_scaffold_finish_f64(double* d_ws, int Ktot, const double* d_c, const 
  * RCCL is dlopen'ed from rccl_path (NULL: "librccl.so.1"), reusing an instance already loaded.
  * -------------------------------------------------------------------------*/
 enum { FEDAGG_BF16 = 12 };  /* kind of a run over bf16 buckets (fp32 accumulators)              */
-enum { FEDAGG_RUN_FEDAVG = 0, FEDAGG_RUN_FEDAVG_TILED = 1, FEDAGG_RUN_SCAFFOLD = 2 };
+enum { FEDAGG_RUN_FEDAVG = 0, FEDAGG_RUN_FEDAVG_TILED = 1, FEDAGG_RUN_SCAFFOLD = 2,
+       FEDAGG_RUN_FEDAVG_PUSH = 3 /* fp32 FedAvg run storing into mapped peer memory (push executor) */ };
 typedef struct fedagg_lockstep_run {
   int32_t step;              /* the step it runs at (runs sorted by step)                        */
   int32_t op;                /* FEDAGG_RUN_*                                                     */
@@ -290,8 +297,16 @@ int fedagg_lockstep_execute(fedagg_comm* comm, const fedagg_lockstep_run* runs, 
  * base + nsteps + 1.  Every wait points to a strictly earlier step
  * of another rank, so no hardware-queue mapping can deadlock it; a wait that exceeds
  * `timeout_ticks` (wall-clock ticks) gives up and records the counter index + 1 in
- * progress[nranks + rank] (the host checks it).  Replaces the per-element client loop of
- * fed_avg.py:221-222 across GPUs, like fedagg_lockstep_execute.
+ * progress[nranks + rank] (+ 2^32 when it was a landing tag; the host checks it).
+ * Landing tags: the counters travel to host memory over PCIe while the data a step pushed travels
+ * over xGMI into the consumer's HBM, so a counter is no proof that the data landed.  After step t a
+ * rank's signal kernel also writes the call's generation (base + 1) into one tag word per consumer
+ * it pushed to at step t -- in the consumer's own (uncached) HBM, over the same link as the data,
+ * after the step's runs each ended with a system-scope release -- and a consumer waits for the tag
+ * of every push it reads, after the producer's counter; a tag found missing once the counter was
+ * there is counted in progress[2 * nranks + rank] (the ordering gap, measured), and waited for.
+ * Replaces the per-element client loop of fed_avg.py:221-222 across GPUs, like
+ * fedagg_lockstep_execute.
  * -------------------------------------------------------------------------*/
 #define FEDAGG_IPC_HANDLE_BYTES 64
 /* IPC handle of the allocation holding `ptr`, and ptr's byte offset in it */
@@ -306,7 +321,8 @@ int fedagg_host_unmap(void* host);
  * buffers, written by peers, read by this GPU's kernels without stale cache lines */
 int fedagg_device_alloc_uncached(uint64_t bytes, void** out);
 int fedagg_device_free(void* p);
-/* device-to-device copy on `stream` (the same HIP runtime as the caller's streams) */
+/* device-to-device runtime copy on `stream` (the same HIP runtime as the caller's streams); tools
+ * only (tools/push_tail_probe.py): no product path uses it, and none reads peer-written memory with it */
 int fedagg_copy_async(void* dst, const void* src, uint64_t bytes, void* stream);
 /* wall-clock ticks per second of the device timer the wait kernels use */
 int fedagg_wall_clock_hz(uint64_t* hz_out);
@@ -314,8 +330,16 @@ typedef struct fedagg_push_wait {
   int32_t step;              /* waited before this step's runs (nsteps: after the last step)     */
   int32_t rank;              /* whose progress counter                                           */
   int64_t value;             /* counter >= base + value (<= 0: nothing to wait for)              */
+  const uint64_t* tag;       /* NULL, or this rank's landing tag of the producer's push: after the
+                                counter, wait for *tag >= base + 1                               */
 } fedagg_push_wait;
-/* runs: FEDAGG_RUN_FEDAVG only (acc may be a mapped peer address); waits sorted by step;
+typedef struct fedagg_push_tag {
+  int32_t step;              /* written after this step's runs (tags sorted by step)             */
+  int32_t reserved;
+  uint64_t* tag;             /* a consumer's landing tag (mapped peer memory): *tag = base + 1   */
+} fedagg_push_tag;
+/* runs: FEDAGG_RUN_FEDAVG / FEDAGG_RUN_FEDAVG_PUSH (acc: a mapped peer address) sorted by step;
+ * waits sorted by step; tags: the landing tags this rank writes, sorted by step (<= 16 a step);
  * ws_src / ws_dst / ws_bytes: the numel == 1 products (fp32) copied to this rank's staging row on
  * the root after step 0's waits (0 bytes: none); ws_stage (root only, else NULL): the nranks
  * staging rows, summed into ws_src after the last waits.  land / out / land_ranges (root only):
@@ -325,6 +349,7 @@ typedef struct fedagg_push_wait {
  * (<= 7) aux streams, forked from and joined back into `stream` around the step.  Asynchronous
  * on `stream`. */
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
+                        const fedagg_push_tag* tags, int ntags,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
                         const void* ws_src, void* ws_dst, uint64_t ws_bytes, const void* ws_stage,
                         const void* land, void* out, const uint64_t* land_ranges, int nranges,

@@ -65,6 +65,7 @@ SIGNATURES = {
     "fedagg_scale_cast": (c_int, [c_void, c_int, c_dbl, c_void, c_int, c_u64, c_void]),
     # client-sharded building blocks (chain / split pairwise trees)
     "fedagg_fedavg_chain_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_push_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_int, c_void, c_void]),
@@ -110,8 +111,9 @@ SIGNATURES = {
     "fedagg_device_alloc_uncached": (c_int, [c_u64, P(c_void)]),
     "fedagg_device_free": (c_int, [c_void]),
     "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
-    "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64, c_u64, c_void,
-                                    c_void, c_u64, c_void, c_void, c_void, c_void, c_int, c_void, c_int, c_void]),
+    "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64,
+                                    c_u64, c_void, c_void, c_u64, c_void, c_void, c_void, c_void, c_int, c_void, c_int,
+                                    c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),
@@ -135,7 +137,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
@@ -150,7 +152,7 @@ FEDAGG_F16 = 0  # kinds (include/fedagg.h enum)
 FEDAGG_F32 = 1
 FEDAGG_F64 = 2
 FEDAGG_BF16 = 12
-FEDAGG_RUN_FEDAVG, FEDAGG_RUN_FEDAVG_TILED, FEDAGG_RUN_SCAFFOLD = 0, 1, 2
+FEDAGG_RUN_FEDAVG, FEDAGG_RUN_FEDAVG_TILED, FEDAGG_RUN_SCAFFOLD, FEDAGG_RUN_FEDAVG_PUSH = 0, 1, 2, 3
 
 
 class NativeLibraryError(RuntimeError):

@@ -95,6 +95,14 @@ int g_tiled_few = 0;    // recommend the tile-interleaved layout below 32 fp32 c
 int g_st_sc1 = -1;      // FedAvg: write-through (sc1) output stores (-1: auto, below SC1_MAX_K clients)
 int g_fa_blk = 0;       // FedAvg fp32/bf16 global-load tiles: threads per workgroup (0 auto, 256, 512)
 int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take adjacent tiles)
+// Push runs (fedagg_fedavg_chain_push_f32): the accumulator is a peer GPU's memory mapped over
+// xGMI.  Their output stores are system-scope write-through stores (st16<3>: sc0 sc1) and every
+// wave waits for their acknowledgements before it retires (s_waitcnt vmcnt(0)), so the stores are
+// performed at system scope before the executor's tag / counter writes that follow the launch.
+// (A per-wave system-scope release fence -- buffer_wbl2 sc0 sc1 -- does the same for stores that
+// sit in this GPU's L2, which these never do; it cost 26-204 % of the run's time on one MI355X,
+// profiles/r04_push_overhead.jsonl, for nothing the write-through stores do not already give.)
+thread_local int g_rel_sys = 0;
 constexpr int NT_STORE_MIN_K = 16;
 // Output stores as device-scope write-through (sc1) instead of non-temporal: 8 x 25M fp32 133.6
 // vs 140.0 us, fp16 71.5 vs 75.0, fp64 280 vs 298; from 32 clients the output is <= 3 % of the
@@ -208,10 +216,12 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 
 // Store policy SP: 0 plain, 1 non-temporal, 2 device-scope write-through (sc1) as a buffer store
 // based at the first active lane's address (callers' lanes store at ascending addresses within
-// one wave, so every lane offset is a small non-negative 32-bit number).
+// one wave, so every lane offset is a small non-negative 32-bit number), 3 the same store at system
+// scope (sc0 sc1: written through to memory -- a peer GPU's over xGMI -- and acknowledged from
+// there; the push executor's runs, which then wait for their acknowledgements before retiring).
 template <int SP>
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
-  if constexpr (SP == 2) {
+  if constexpr (SP == 2 || SP == 3) {
     const uint64_t addr = reinterpret_cast<uint64_t>(p);
     // readfirstlane returns int: widen through unsigned (a sign-extended low word would corrupt
     // the high address bits)
@@ -220,7 +230,7 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
     const uint64_t base = ((uint64_t)hi << 32) | (uint64_t)lo;
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(addr - base), 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(addr - base), 0, SP == 3 ? 17 : 16);  // sc0 = 1, sc1 = 16
   } else if constexpr (SP == 1) {
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
   } else {
@@ -569,7 +579,7 @@ template <typename E, int KC, bool NT, int NTS, int VPT, int U, bool PIPE, bool 
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
                   const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb,
-                  const uint64_t pitch) {
+                  const uint64_t pitch, const int rel) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
@@ -642,8 +652,12 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     }
     for (int p = 0; p < pw.n; ++p)
       if (pw.idx[p] == i) acc = fedavg_pairwise_elem<E, KC>(a, K, ii);
-    out[i] = E::out(acc);
+    if constexpr (NTS == 3 && std::is_same<typename E::Out, float>::value)  // push runs: system scope too
+      __hip_atomic_store(out + i, E::out(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      out[i] = E::out(acc);
   }
+  if (rel) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // push runs: this wave's sc0 sc1 stores acknowledged
 }
 
 // ------------------------------------------------------------------------------------
@@ -1678,7 +1692,7 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out, uint64_t pitch = 0) {
   if (BLK != FA_BLOCK) grid = (grid + BLK / FA_BLOCK - 1) / (BLK / FA_BLOCK);  // the caller sized it for 256
   hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF, BLK, INTER ? VPT * BLK : 0>),
-                     dim3(grid), dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb, pitch);
+                     dim3(grid), dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb, pitch, g_rel_sys);
 }
 
 // Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
@@ -1755,7 +1769,7 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
     return launch_fedavg_variant<E, true, NTS, 8, 4, false, true>(FA_ARGS);
   }
 #else
-  if constexpr (NTS == 2) {  // write-through (sc1) output stores: the auto shapes and their neighbours only
+  if constexpr (NTS == 2 || NTS == 3) {  // write-through (sc1 / sc0 sc1) output stores: the auto shapes and their neighbours only
     if (sh.pipe) {
       if (sh.vpt >= 8) return launch_fedavg_variant<E, true, NTS, 8, 2, true, true>(FA_ARGS);
       return launch_fedavg_variant<E, true, NTS, 4, 4, true, true>(FA_ARGS);
@@ -1855,6 +1869,9 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
                    int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts, bool sc1, Shape sh) {
+  if constexpr (std::is_same<E, F32>::value) {
+    if (g_rel_sys) return launch_fedavg_shape<E, 3>(grid, s, a, pw, kc, first, nvec, M, out, sh);  // push runs
+  }
 #if FEDAGG_TUNING
   if (nts && sc1 && g_nt_load && g_tile)
     launch_fedavg_shape<E, 2>(grid, s, a, pw, kc, first, nvec, M, out, sh);
@@ -2693,6 +2710,13 @@ int fedagg_scale_cast(const void* d_in, int in_kind, double w, void* d_out, int 
 int fedagg_fedavg_chain_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                             float* d_out, void* stream) {
   return fedavg_launch<F32>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
+}
+int fedagg_fedavg_chain_push_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
+                                 float* d_out, void* stream) {
+  g_rel_sys = 1;
+  const int rc = fedavg_launch<F32>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
+  g_rel_sys = 0;
+  return rc;
 }
 int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                              float* d_out, void* stream) {

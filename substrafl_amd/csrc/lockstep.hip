@@ -113,6 +113,10 @@ int run_one(const fedagg_lockstep_run& r, hipStream_t s) {
         rc = fedagg_fedavg_chain_f16((const uint16_t* const*)r.x, (const uint16_t*)r.w, r.K, r.n, r.seed,
                                      (uint16_t*)r.acc, s);
       break;
+    case FEDAGG_RUN_FEDAVG_PUSH:  // the accumulator is mapped peer memory: system-scope release per wave
+      if (r.kind != FEDAGG_F32) return lfail(FEDAGG_EINVAL, "lockstep: push runs are fp32");
+      rc = fedagg_fedavg_chain_push_f32((const float* const*)r.x, (const float*)r.w, r.K, r.n, r.seed, (float*)r.acc, s);
+      break;
     case FEDAGG_RUN_FEDAVG_TILED:
       if (r.kind == FEDAGG_F32)
         rc = fedagg_fedavg_chain_tiled_f32((const float*)r.x[0], (const float*)r.w, r.K, r.n, r.tile_vectors,
@@ -139,43 +143,82 @@ int run_one(const fedagg_lockstep_run& r, hipStream_t s) {
 
 
 // ---- push executor (fedagg_push_execute): progress counters in a node-shared host page ----
-constexpr int PUSH_MAX_WAITS = 16;  // counters one wait kernel polls (one lane each)
+constexpr int PUSH_MAX_WAITS = 32;  // counters / tags one wait kernel polls (one lane each)
+constexpr int PUSH_MAX_TAGS = 16;   // landing tags one signal kernel writes (one lane each)
+constexpr uint64_t PUSH_TAG_ERR = 1ull << 32;  // err word: a landing tag (not a counter) timed out
 struct PushWaitArgs {
   uint32_t n;
   uint32_t idx[PUSH_MAX_WAITS];
   uint64_t val[PUSH_MAX_WAITS];
+  const uint64_t* tag[PUSH_MAX_WAITS];
+};
+struct PushSignalArgs {
+  uint32_t n;
+  uint64_t* tag[PUSH_MAX_TAGS];
 };
 
+__device__ __forceinline__ uint64_t ld_acquire_sys(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Lane i polls progress[idx[i]] until it reaches val[i] (system-scope acquire: what the producer
-// released before its signal is visible to the kernels after this one); a wait that exceeds
-// `timeout` ticks gives up and records idx + 1 in *err.  Every lane reaches the end.
-__global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress, PushWaitArgs a, uint64_t timeout,
-                                                       uint64_t* err) {
+// released before its signal is visible to the kernels after this one); then, for a landing tag,
+// its tag word until it holds this call's generation `gen` -- a tag still missing when the counter
+// was already there is the ordering gap between the PCIe counter and the xGMI data: counted in
+// *late and waited out.  A wait that exceeds `timeout` ticks gives up and records idx + 1 (+
+// PUSH_TAG_ERR for a tag) in *err.  Every lane reaches the end (the late count is a wave ballot).
+__global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress, PushWaitArgs a, uint64_t gen,
+                                                       uint64_t timeout, uint64_t* err, uint64_t* late) {
   const uint32_t i = threadIdx.x;
-  if (i >= a.n) return;
-  const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(progress + a.idx[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.val[i]) {
-    if (wall_clock64() - t0 > timeout) {
-      __hip_atomic_store(err, (uint64_t)a.idx[i] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
+  bool was_late = false;
+  if (i < a.n) {
+    const uint64_t t0 = wall_clock64();
+    bool ok = true;
+    while (ld_acquire_sys(progress + a.idx[i]) < a.val[i]) {
+      if (wall_clock64() - t0 > timeout) {
+        __hip_atomic_store(err, (uint64_t)a.idx[i] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(16);
     }
-    __builtin_amdgcn_s_sleep(16);
+    if (ok && a.tag[i] && ld_acquire_sys(a.tag[i]) < gen) {
+      was_late = true;
+      while (ld_acquire_sys(a.tag[i]) < gen) {
+        if (wall_clock64() - t0 > timeout) {
+          __hip_atomic_store(err, (uint64_t)a.idx[i] + 1 + PUSH_TAG_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(16);
+      }
+    }
+  }
+  const uint64_t m = __ballot(was_late);
+  if (i == 0 && m) {  // only this rank's wait kernels (one stream, in order) write its late word
+    const uint64_t v = __hip_atomic_load(late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(late, v + (uint64_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
-// progress[idx] = value after everything before it on the stream (the step's chain kernels,
-// whose stores to mapped peer memory the kernel boundary has written back), system-scope release.
-__global__ void __launch_bounds__(64) push_signal_kernel(uint64_t* progress, uint32_t idx, uint64_t value) {
-  if (threadIdx.x != 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __hip_atomic_store(progress + idx, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// After everything before it on the stream (the step's chain kernels, each wave of which ended
+// with a system-scope release of its peer stores): the landing tags of the consumers this step
+// pushed to (peer HBM, the data's own path), then a system-scope release, then
+// progress[idx] = value (the node-shared host page).
+__global__ void __launch_bounds__(64) push_signal_kernel(uint64_t* progress, uint32_t idx, uint64_t value,
+                                                         PushSignalArgs t, uint64_t gen) {
+  const uint32_t i = threadIdx.x;
+  if (i < t.n) __hip_atomic_store(t.tag[i], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the wave's tag stores performed before the counter
+  if (i == 0) __hip_atomic_store(progress + idx, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // dst[0, n) = src[0, n) (4-byte words) with ordinary vector stores: a copy into a peer's mapped
-// memory that stays in the stream's order (a runtime copy into imported memory need not).
+// memory that stays in the stream's order (a runtime copy into imported memory need not), ended
+// by a system-scope release like the push runs.
 __global__ void __launch_bounds__(256) push_copy_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
                                                         uint64_t n) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) dst[i] = src[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // Root: ws[i] = stage[0][i] + ... + stage[G-1][i] in rank order (one owner per column, the
@@ -190,6 +233,18 @@ __global__ void __launch_bounds__(256) push_stage_sum_kernel(float* __restrict__
   }
 }
 
+int push_signal(uint64_t* progress, int rank, uint64_t value, const fedagg_push_tag* tags, int& ti, int ntags,
+                int step, uint64_t gen, hipStream_t s) {
+  PushSignalArgs a;
+  memset(&a, 0, sizeof(a));
+  for (; ti < ntags && tags[ti].step == step; ++ti) {
+    if (a.n >= (uint32_t)PUSH_MAX_TAGS) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: > 16 landing tags a step");
+    a.tag[a.n++] = tags[ti].tag;
+  }
+  hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, value, a, gen);
+  return hip_check(hipGetLastError(), "push_signal_kernel");
+}
+
 int push_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
   if (bytes % 4) return lfail(FEDAGG_EINVAL, "push: copies are whole 4-byte words");
   const uint64_t words = bytes / 4;
@@ -201,19 +256,21 @@ int push_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
 }
 
 int push_waits(const fedagg_push_wait* waits, int& wi, int nwaits, int step, uint64_t* progress, uint64_t base,
-               uint64_t timeout, uint64_t* err, hipStream_t s) {
+               uint64_t timeout, uint64_t* err, uint64_t* late, hipStream_t s) {
   while (wi < nwaits && waits[wi].step == step) {
     PushWaitArgs a;
     memset(&a, 0, sizeof(a));
     for (; wi < nwaits && waits[wi].step == step && a.n < PUSH_MAX_WAITS; ++wi) {
       const int64_t v = (int64_t)base + waits[wi].value;
-      if (v <= 0) continue;  // the counters start at 0
+      if (v <= 0 && !waits[wi].tag) continue;  // the counters start at 0
       a.idx[a.n] = (uint32_t)waits[wi].rank;
-      a.val[a.n] = (uint64_t)v;
+      a.val[a.n] = (uint64_t)(v > 0 ? v : 0);
+      a.tag[a.n] = waits[wi].tag;
       ++a.n;
     }
     if (!a.n) continue;
-    hipLaunchKernelGGL(push_wait_kernel, dim3(1), dim3(64), 0, s, (const uint64_t*)progress, a, timeout, err);
+    hipLaunchKernelGGL(push_wait_kernel, dim3(1), dim3(64), 0, s, (const uint64_t*)progress, a, base + 1, timeout, err,
+                       late);
     int rc = hip_check(hipGetLastError(), "push_wait_kernel");
     if (rc) return rc;
   }
@@ -419,11 +476,13 @@ int fedagg_wall_clock_hz(uint64_t* hz_out) {
 }
 
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
+                        const fedagg_push_tag* tags, int ntags,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
                         const void* ws_src, void* ws_dst, uint64_t ws_bytes, const void* ws_stage,
                         const void* land, void* out, const uint64_t* land_ranges, int nranges,
                         void* const* aux_streams, int naux, void* stream) {
-  if (nruns < 0 || nwaits < 0 || nsteps < 0 || (nruns && !runs) || (nwaits && !waits) || !progress || nranks < 1 ||
+  if (nruns < 0 || nwaits < 0 || ntags < 0 || nsteps < 0 || (nruns && !runs) || (nwaits && !waits) ||
+      (ntags && !tags) || !progress || nranks < 1 ||
       rank < 0 || rank >= nranks || (ws_bytes && (!ws_src || !ws_dst)) || naux < 0 || naux > 7 ||
       (naux && !aux_streams) || nranges < 0 || (nranges && (!land_ranges || !land || !out)))
     return lfail(FEDAGG_EINVAL, "fedagg_push_execute: invalid argument");
@@ -432,16 +491,20 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
         (i && waits[i].step < waits[i - 1].step))
       return lfail(FEDAGG_EINVAL, "fedagg_push_execute: waits out of range or unsorted");
   for (int i = 0; i < nruns; ++i)
-    if (runs[i].op != FEDAGG_RUN_FEDAVG || runs[i].step < 0 || runs[i].step >= nsteps ||
-        (i && runs[i].step < runs[i - 1].step))
+    if ((runs[i].op != FEDAGG_RUN_FEDAVG && runs[i].op != FEDAGG_RUN_FEDAVG_PUSH) || runs[i].step < 0 ||
+        runs[i].step >= nsteps || (i && runs[i].step < runs[i - 1].step))
       return lfail(FEDAGG_EINVAL, "fedagg_push_execute: runs must be FedAvg row runs sorted by step");
+  for (int i = 0; i < ntags; ++i)
+    if (!tags[i].tag || tags[i].step < 0 || tags[i].step >= nsteps || (i && tags[i].step < tags[i - 1].step))
+      return lfail(FEDAGG_EINVAL, "fedagg_push_execute: tags out of range or unsorted");
   hipStream_t s = (hipStream_t)stream;
   uint64_t* err = progress + nranks + rank;
-  int rc;
+  uint64_t* late = progress + 2 * nranks + rank;
+  const uint64_t gen = base + 1;  // this call's generation: its entry value, unique and > 0
+  int rc, ti = 0;
   // base + 1: this rank entered the call -- everything its stream held before (a refill of the
   // output, the previous call's reads of its slots) is done, so peers may write into its buffers
-  hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + 1);
-  if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
+  if ((rc = push_signal(progress, rank, base + 1, tags, ti, 0, -1, gen, s))) return rc;
   // a step's launches (one per consumer: each writes over its own xGMI link) spread over the
   // caller's stream and the aux streams, forked from and joined back into the caller's stream
   // fork / join events: kept for the thread's lifetime (per device), never destroyed while a
@@ -461,7 +524,7 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   hipEvent_t* ev = ev_pool[dev];
   int ri = 0, wi = 0;
   for (int t = 0; t < nsteps; ++t) {
-    if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, s))) return rc;
+    if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, late, s))) return rc;
     if (t == 0 && ws_bytes &&  // after step 0's waits, which include the root's entry
         (rc = push_copy(ws_dst, ws_src, ws_bytes, s)))
       return rc;
@@ -482,11 +545,11 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
       if ((rc = hip_check(hipEventRecord(ev[1 + a], (hipStream_t)aux_streams[a]), "hipEventRecord")) ||
           (rc = hip_check(hipStreamWaitEvent(s, ev[1 + a], 0), "hipStreamWaitEvent")))
         return rc;
-    // base + t + 2: step t done (its stores into peer buffers written back)
-    hipLaunchKernelGGL(push_signal_kernel, dim3(1), dim3(64), 0, s, progress, (uint32_t)rank, base + t + 2);
-    if ((rc = hip_check(hipGetLastError(), "push_signal_kernel"))) return rc;
+    // step t done: its consumers' landing tags, then base + t + 2
+    if ((rc = push_signal(progress, rank, base + t + 2, tags, ti, ntags, t, gen, s))) return rc;
   }
-  if ((rc = push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, s))) return rc;
+  if ((rc = push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, late, s))) return rc;
+  if (ti != ntags || wi != nwaits) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: tags / waits beyond the last step");
   // root, once every rank's last step is in: the finished pieces others pushed, into the output;
   // the numel == 1 staging rows, summed into this rank's workspace
   for (int i = 0; i < nranges; ++i) {

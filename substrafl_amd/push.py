@@ -18,9 +18,19 @@ Before step t a rank waits for
   it is about to overwrite at that step: slot t % SLOTS, SLOTS = 4), or at least to have
   entered the call (steps 0 and 1, the root's output for finished pieces, its staging row);
 
-after the last step the root waits for every rank's last step (the finished pieces landed).
-Every wait points to a strictly earlier step of another rank, so the schedule cannot deadlock
-whatever hardware queues the kernels share.  The numel == 1 products go to a staging row of the
+after the last step the root waits for every rank's last step.
+
+A counter reaches host memory over PCIe while the data of the same step travels over xGMI into
+the consumer's HBM, so the counter alone does not prove the data landed.  Landing tags close that
+gap: a run storing into a peer ends every wave with a system-scope release
+(``FEDAGG_RUN_FEDAVG_PUSH``), and the step's signal kernel then writes the call's generation into
+one tag word per consumer it pushed to -- in the consumer's own HBM, over the same link as the
+data -- before it publishes the counter.  A consumer waits for the producer's counter AND the tag
+before it reads the pushes (at step t + 2, or after its last step for finished pieces and the
+staging row); a tag found missing once the counter was there is counted (``late_tags``: the gap,
+measured on the node) and waited out, and one that never comes is a timeout error, not a wrong
+number.  Every wait points to a strictly earlier step of another rank, so the schedule cannot
+deadlock whatever hardware queues the kernels share.  The numel == 1 products go to a staging row of the
 root per rank (one copy after step 0's waits) and are summed on the root (one owner per column: exact).
 
 Scope: fp32 FedAvg over row-layout client blocks (the bench's C3 schedule); the other kinds keep
@@ -30,6 +40,7 @@ the RCCL executor.  Every rank must be on this node (the counters live in ``/dev
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -42,10 +53,26 @@ PAGE = 4096
 
 
 class _Wait(ctypes.Structure):
-    _fields_ = [("step", ctypes.c_int32), ("rank", ctypes.c_int32), ("value", ctypes.c_int64)]
+    _fields_ = [("step", ctypes.c_int32), ("rank", ctypes.c_int32), ("value", ctypes.c_int64),
+                ("tag", ctypes.c_void_p)]
 
 
-assert ctypes.sizeof(_Wait) == 16  # include/fedagg.h fedagg_push_wait
+class _Tag(ctypes.Structure):
+    _fields_ = [("step", ctypes.c_int32), ("reserved", ctypes.c_int32), ("tag", ctypes.c_void_p)]
+
+
+assert ctypes.sizeof(_Wait) == 24 and ctypes.sizeof(_Tag) == 16  # include/fedagg.h fedagg_push_wait / _tag
+
+GPU_MAX_HW_QUEUES = 4  # HIP's hardware queues per process on the boxes (GPU_MAX_HW_QUEUES, HIP's default)
+RCCL_STREAMS = 3  # a live fedagg_comm: its own stream + RCCL's internal device and host streams
+
+
+def aux_stream_budget(hw_queues: int = GPU_MAX_HW_QUEUES, rccl_live: bool = False) -> int:
+    """Aux streams the push executor may spread a step's per-consumer launches over: what the
+    hardware queues leave after the caller's stream (and, with a native RCCL communicator live in
+    the same process, after its stream and RCCL's own two), at most 3.  More streams than queues
+    share queues and serialise anyway (DESIGN.md §6 "Streams")."""
+    return max(0, min(3, hw_queues - 1 - (RCCL_STREAMS if rccl_live else 0)))
 
 
 def _check(rc: int, what: str) -> None:
@@ -62,9 +89,8 @@ class PushTransport:
     native = True
     push = True
 
-    AUX_STREAMS = 3  # with the caller's: 4 streams = GPU_MAX_HW_QUEUES
-
-    def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0):
+    def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0,
+                 aux_streams: Optional[int] = None):
         import torch
         import torch.distributed as dist
         from multiprocessing import shared_memory
@@ -73,7 +99,8 @@ class PushTransport:
         self.dist, self.group = dist, group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.device = torch.cuda.current_device() if device is None else int(device)
-        nbytes = PAGE * max(1, -(-(2 * self.world * 8) // PAGE))
+        # counters [0, G), wait errors [G, 2G), late landing tags [2G, 3G)
+        nbytes = PAGE * max(1, -(-(3 * self.world * 8) // PAGE))
         name = [None]
         if self.rank == 0:
             self._shm = shared_memory.SharedMemory(create=True, size=nbytes)
@@ -94,7 +121,8 @@ class PushTransport:
         self._maps: Dict[bytes, int] = {}
         self._programs: List["PushProgram"] = []
         self._py = None
-        self._aux = [torch.cuda.Stream(device=self.device) for _ in range(self.AUX_STREAMS)]
+        n_aux = aux_stream_budget(_hw_queues()) if aux_streams is None else int(aux_streams)
+        self._aux = [torch.cuda.Stream(device=self.device) for _ in range(n_aux)]
         self._aux_ptrs = _native.ptr_array([st.cuda_stream for st in self._aux])
         dist.barrier(group=group)
 
@@ -137,10 +165,17 @@ class PushTransport:
             self._py = DistTransport(self.group)
         return self._py
 
-    def errors(self) -> Dict[int, int]:
-        """Ranks whose wait kernel gave up: rank -> the counter it waited for."""
+    def errors(self) -> Dict[int, str]:
+        """Ranks whose wait kernel gave up: rank -> what it waited for (a rank's progress counter,
+        or the landing tag of a rank's push)."""
         e = self._page[self.world: 2 * self.world]
-        return {r: int(v) - 1 for r, v in enumerate(e) if v}
+        return {r: (f"landing tag of rank {(int(v) & 0xFFFFFFFF) - 1}" if int(v) >> 32 else
+                    f"counter of rank {int(v) - 1}") for r, v in enumerate(e) if v}
+
+    def late_tags(self) -> List[int]:
+        """Per rank: landing-tag waits that found the producer's counter published but its data's
+        tag not yet landed (the PCIe-counter / xGMI-data ordering gap, waited out), cumulative."""
+        return [int(v) for v in self._page[2 * self.world: 3 * self.world]]
 
     # -- the schedule ----------------------------------------------------------------------
     def program(self, **kw) -> "PushProgram":
@@ -165,6 +200,7 @@ class PushTransport:
         ranges = prog.land_ranges if root else None
         _check(self.lib.fedagg_push_execute(ctypes.byref(prog.runs) if prog.nruns else None, prog.nruns,
                                             ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
+                                            ctypes.byref(prog.tags) if prog.ntags else None, prog.ntags,
                                             prog.nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
                                             ws_src, ws_dst, ws_bytes, stage,
                                             prog.land_u.ptr if root else None, prog.out_ptr if root else None,
@@ -193,6 +229,13 @@ class PushTransport:
 
 def _native_ipc_bytes() -> int:
     return 64  # FEDAGG_IPC_HANDLE_BYTES
+
+
+def _hw_queues() -> int:
+    try:
+        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", GPU_MAX_HW_QUEUES)))
+    except ValueError:
+        return GPU_MAX_HW_QUEUES
 
 
 class _Uncached:
@@ -237,9 +280,13 @@ class PushProgram:
         se = max(1, plan.slot_elems)
         self.slots_u = _Uncached(tr.lib, lockstep.SLOTS * se * esz)
         self.land_u = _Uncached(tr.lib, out.numel() * esz)
+        # landing tags: word q * n_steps + t = the generation of the call whose step-t pushes of
+        # rank q into this rank landed (written by q after its data, over the same link)
+        self.tags_u = _Uncached(tr.lib, max(1, G * plan.n_steps) * 8)
         self.stage_u = None  # the root's numel == 1 product staging, at first use
         mine = {"slots": tr.ipc_info(self.slots_u.ptr) if G > 1 else None,
                 "land": tr.ipc_info(self.land_u.ptr) if G > 1 else None,
+                "tags": tr.ipc_info(self.tags_u.ptr) if G > 1 else None,
                 "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
                          if o.kind == "recv"]}
         infos = tr.all_gather(mine) if G > 1 else [mine]
@@ -272,12 +319,22 @@ class PushProgram:
         self.land_ranges_n = len(flat)
         self.out_ptr = out.data_ptr()
         runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
-                          local(p.src) if p.src is not None else 0) for p in specs]
-        waits = [_Wait(t, q, v) for t, q, v in wait_list]
+                          local(p.src) if p.src is not None else 0, remote=p.dst_rank != me) for p in specs]
         n_steps = plan.n_steps
-        self.nruns, self.nwaits, self.nsteps = len(runs), len(waits), n_steps
+        outgoing = push_outgoing(plan, specs)
+        everyone = tr.all_gather(outgoing) if G > 1 else [outgoing]
+        tag_waits = push_tag_waits(me, n_steps, everyone)
+        # counter waits first within a step, then the tag waits (each after its own producer's counter)
+        waits = sorted([(t, 0, q, v, None) for t, q, v in wait_list] +
+                       [(t, 1, q, v, self.tags_u.ptr + idx * 8) for t, q, v, idx in tag_waits],
+                       key=lambda x: (x[0], x[1]))
+        waits = [_Wait(t, q, v, tag) for t, _k, q, v, tag in waits]
+        tags = [_Tag(t, 0, tr.remote(infos[c]["tags"]) + (me * n_steps + t) * 8) for t, c, _e in outgoing]
+        self.outgoing, self.tag_waits = outgoing, tag_waits
+        self.nruns, self.nwaits, self.ntags, self.nsteps = len(runs), len(waits), len(tags), n_steps
         self.runs = (_Run * max(1, len(runs)))(*runs)
         self.waits = (_Wait * max(1, len(waits)))(*waits)
+        self.tags = (_Tag * max(1, len(tags)))(*tags)
         self._tr = tr
         self._stage_info = None
 
@@ -296,9 +353,11 @@ class PushProgram:
             return self.stage_u.ptr + self.plan.rank * ws_bytes
         return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
 
-    def _run(self, t: int, sh, col: int, n: int, dst: int, src: int) -> _Run:
+    def _run(self, t: int, sh, col: int, n: int, dst: int, src: int, remote: bool = False) -> _Run:
         rec = _Run()
-        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG, _native.FEDAGG_F32, 1, 0, n
+        # a run storing into a peer's memory ends every wave with a system-scope release
+        op = _native.FEDAGG_RUN_FEDAVG_PUSH if remote else _native.FEDAGG_RUN_FEDAVG
+        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, op, _native.FEDAGG_F32, 1, 0, n
         rows = sh.rows
         base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
         ptrs = [base + k * step + col * esz for k in range(rows.shape[0])]
@@ -330,6 +389,7 @@ class PushRun:
     src: Optional[Tuple[str, int, int]]
     dst_rank: int
     dst: Tuple[str, int, int]
+    final: bool = False  # a finished piece (read by the root after the last step, not at step + 2)
 
 
 def push_schedule(plan: lockstep.RankPlan, recvs: Sequence[Sequence[tuple]]):
@@ -358,7 +418,7 @@ def push_schedule(plan: lockstep.RankPlan, recvs: Sequence[Sequence[tuple]]):
         for r in step_runs:
             src = None if r.seed else r.acc
             if r.final:  # a finished piece: straight into the root's output
-                specs.append(PushRun(t, r.block, r.col, r.n, src, root, ("out", 0, r.lo)))
+                specs.append(PushRun(t, r.block, r.col, r.n, src, root, ("out", 0, r.lo), final=True))
                 if me != root:
                     consumers.add(root)
                 continue
@@ -383,6 +443,38 @@ def push_schedule(plan: lockstep.RankPlan, recvs: Sequence[Sequence[tuple]]):
     if me == root:
         waits += [(plan.n_steps, q, plan.n_steps + 1) for q in range(G) if q != me]
     return specs, waits
+
+
+def push_outgoing(plan: lockstep.RankPlan, specs: Sequence[PushRun]) -> List[Tuple[int, int, bool]]:
+    """``(step, consumer, at_end)`` of every landing tag this rank writes: one per consumer its
+    step pushed to, and at step 0 always one to the root (its numel == 1 staging row is copied
+    there after step 0's waits).  ``at_end``: the consumer reads those pushes only after its last
+    step (finished pieces and the staging row on the root), not at step + 2.  Sorted by step."""
+    ends: Dict[Tuple[int, int], bool] = {}
+    for s in specs:
+        if s.dst_rank != plan.rank:
+            key = (s.step, s.dst_rank)
+            ends[key] = ends.get(key, True) and s.final
+    if plan.rank != plan.root and plan.n_steps > 0:
+        ends.setdefault((0, plan.root), True)
+    return sorted((t, c, e) for (t, c), e in ends.items())
+
+
+def push_tag_waits(me: int, n_steps: int, outgoing: Sequence[Sequence[Tuple[int, int, bool]]]
+                   ) -> List[Tuple[int, int, int, int]]:
+    """This rank's landing-tag waits from every rank's :func:`push_outgoing`: ``(wait step,
+    producer q, counter value, tag index)``.  A push of q at step t is an input of this rank's step
+    t + 2 (computed at t, consumed at t + 2), or is read after the last step (``at_end``); its tag is
+    waited for before that step, after q's counter says step t is done (value t + 2) -- a wait on a
+    strictly earlier step of another rank, like every other wait of the schedule."""
+    res = []
+    for q, lst in enumerate(outgoing):
+        if q == me:
+            continue
+        for t, c, at_end in lst:
+            if c == me:
+                res.append((n_steps if at_end else min(t + 2, n_steps), q, t + 2, q * n_steps + t))
+    return sorted(res)
 
 
 def _intersect(loc_a, n_a: int, loc_b, n_b: int) -> Tuple[int, int]:

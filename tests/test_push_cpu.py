@@ -19,8 +19,13 @@ import numpy as np
 import pytest
 
 from substrafl_amd import lockstep
-from substrafl_amd.push import push_schedule
+from substrafl_amd.push import push_outgoing, push_schedule, push_tag_waits
 from substrafl_amd.sharding import relay_plan, striped_plan
+
+
+class TagTimeout(AssertionError):
+    """A rank is stuck on a landing tag that can never arrive (the executor's wait kernel times out
+    and the host raises on the error word instead of computing with what is in the buffer)."""
 
 
 def _plans(M, G, rounds, relay, rings):
@@ -30,43 +35,62 @@ def _plans(M, G, rounds, relay, rings):
 
 
 def _programs(plans):
+    """Per rank: (specs, counter waits, landing tags written, landing-tag waits) -- push.py's."""
     recvs = [[(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(p.groups) for o in ops if o.kind == "recv"]
              for p in plans]
-    return [push_schedule(p, recvs) for p in plans]
+    sched = [push_schedule(p, recvs) for p in plans]
+    outgoing = [push_outgoing(p, specs) for p, (specs, _w) in zip(plans, sched)]
+    return [(specs, waits, outgoing[p.rank], push_tag_waits(p.rank, p.n_steps, outgoing))
+            for p, (specs, waits) in zip(plans, sched)]
 
 
-def _ops(plan, specs, waits, base, root_fill):
+def _ops(plan, specs, waits, outgoing, tag_waits, base, root_fill):
     """One call of one rank as a list of events, in its stream's order."""
     ops = []
     if root_fill:
         ops.append(("fill",))
-    ops.append(("signal", base + 1))
+    ops.append(("signal", base + 1, []))
     by_step = {}
     for t, q, v in waits:
         by_step.setdefault(t, []).append(("wait", q, base + v))
+    for t, q, v, idx in tag_waits:
+        by_step.setdefault(t, []).append(("twait", q, base + v, idx))
+    tags_of = {}
+    for t, c, _e in outgoing:
+        tags_of.setdefault(t, []).append((c, plan.rank * plan.n_steps + t))
     for t in range(plan.n_steps):
         ops += by_step.get(t, [])
         for s in (s for s in specs if s.step == t):
             ops += [("start", s), ("end", s)]
-        ops.append(("signal", base + t + 2))
+        ops.append(("signal", base + t + 2, tags_of.get(t, [])))
     ops += by_step.get(plan.n_steps, [])
     return ops
 
 
-def _replay(plans, progs, M, calls, seed):
+def _replay(plans, progs, M, calls, seed, delay=False, drop=None):
+    """Random interleavings of the ranks' event lists.  ``delay``: a store into a peer's memory is
+    in flight on its (producer, consumer) link until a random later ``land`` event, in order per
+    link, while the counter a signal publishes is visible at once (it travels over another path) --
+    the ordering gap the landing tags close; the signal's tag writes follow the step's data on each
+    link.  ``drop = (rank, step, consumer)``: that rank's step-``step`` stores to ``consumer`` and
+    their tag never land (a lost piece) in the last call."""
     G = len(plans)
     rng = random.Random(seed)
     root = plans[0].root
     slot_elems = max(max(1, p.slot_elems) for p in plans)
     bufs = [{"slot": np.full((lockstep.SLOTS, slot_elems), -1, np.int64), "out": np.full(M, -1, np.int64)}
             for _ in range(G)]
+    tags = [dict() for _ in range(G)]
     progress = [0] * G
+    links = {}  # (producer, consumer) -> FIFO of pending writes
     for call in range(calls):
         expect = call + 1  # the call's tag: a value left over from the previous call never matches
         for b in range(G):
             expect = expect * (G + 1) + b + 1
         base = call * (plans[0].n_steps + 1)
-        queues = [_ops(plans[r], *progs[r], base, r == root) for r in range(G)]
+        gen = base + 1
+        queues = [_ops(plans[r], progs[r][0], progs[r][1], progs[r][2], progs[r][3], base, r == root)
+                  for r in range(G)]
         pcs = [0] * G
         pending = [None] * G  # a started run's output, written at its end
 
@@ -74,16 +98,43 @@ def _replay(plans, progs, M, calls, seed):
             where, slot, off = loc
             return bufs[r]["out"][off: off + n] if where == "out" else bufs[r]["slot"][slot, off: off + n]
 
+        def post(src, dst, write, step):
+            if drop is not None and call == calls - 1 and (src, step, dst) == drop:
+                return  # lost on the link
+            if delay and src != dst:
+                links.setdefault((src, dst), []).append(write)
+            else:
+                write()
+
+        def blocked(r):
+            op = queues[r][pcs[r]]
+            if op[0] == "wait":
+                return progress[op[1]] < op[2]
+            if op[0] == "twait":
+                return progress[op[1]] < op[2] or tags[r].get(op[3], 0) < gen
+            return False
+
         while any(pcs[r] < len(queues[r]) for r in range(G)):
-            ready = [r for r in range(G) if pcs[r] < len(queues[r])
-                     and not (queues[r][pcs[r]][0] == "wait" and progress[queues[r][pcs[r]][1]] < queues[r][pcs[r]][2])]
-            assert ready, f"deadlock (call {call}): {[queues[r][pcs[r]] if pcs[r] < len(queues[r]) else None for r in range(G)]}"
+            ready = [r for r in range(G) if pcs[r] < len(queues[r]) and not blocked(r)]
+            inflight = [k for k, v in links.items() if v]
+            if not ready and not inflight:
+                stuck = [queues[r][pcs[r]] for r in range(G) if pcs[r] < len(queues[r])]
+                if any(op[0] == "twait" for op in stuck):
+                    raise TagTimeout(f"call {call}: stuck on a landing tag: {stuck}")
+                raise AssertionError(f"deadlock (call {call}): {stuck}")
+            if inflight and (not ready or rng.random() < 0.5):
+                write = links[rng.choice(inflight)].pop(0)
+                write()
+                continue
             r = rng.choice(ready)
             op = queues[r][pcs[r]]
             pcs[r] += 1
             if op[0] == "fill":
                 bufs[r]["out"][:] = -7
             elif op[0] == "signal":
+                step = op[1] - base - 2
+                for c, idx in op[2]:
+                    post(r, c, lambda c=c, idx=idx: tags[c].__setitem__(idx, gen), step)
                 progress[r] = op[1]
             elif op[0] == "start":
                 s = op[1]
@@ -91,8 +142,14 @@ def _replay(plans, progs, M, calls, seed):
                 pending[r] = np.where(x < 0, -99, x * (G + 1) + s.block + 1)  # garbage stays garbage
             elif op[0] == "end":
                 s = op[1]
-                region(s.dst_rank, s.dst, s.n)[:] = pending[r]
+                val = pending[r]
+
+                def write(s=s, val=val):
+                    region(s.dst_rank, s.dst, s.n)[:] = val
+
+                post(r, s.dst_rank, write, s.step)
                 pending[r] = None
+        assert not any(links.values())
         got = bufs[root]["out"][:M]
         bad = int(np.count_nonzero(got != expect))
         assert bad == 0, f"call {call}: {bad} of {M} elements wrong (seed {seed})"
@@ -112,6 +169,8 @@ def test_push_protocol_random_interleavings(M, G, rounds, relay, rings):
     progs = _programs(plans)
     for seed in range(12 if G <= 4 else 4):
         _replay(plans, progs, M, calls=2, seed=seed)
+        # the stores in flight on their links after the counters (the ordering gap): the tags hold
+        _replay(plans, progs, M, calls=2, seed=100 + seed, delay=True)
 
 
 def test_push_runs_cover_every_output_once():
@@ -119,7 +178,7 @@ def test_push_runs_cover_every_output_once():
     location, or (finished) the root's output at its global offset."""
     M, G = 50000, 8
     plans = _plans(M, G, (0.5, 0.3, 0.2), False, None)
-    for p, (specs, waits) in zip(plans, _programs(plans)):
+    for p, (specs, waits, _o, _tw) in zip(plans, _programs(plans)):
         assert sum(s.n for s in specs) == sum(r.n for runs in p.runs for r in runs)
         for s in specs:
             if s.block == G - 1:  # finished: the root's output (the last block's input sits in "out" too)
@@ -138,8 +197,8 @@ def test_push_entry_wait_protects_the_refilled_output():
     progs = _programs(plans)
     root = plans[0].root
     stripped = [(specs, [(t, q, v) for t, q, v in waits if not (q == root and p.rank != root and v == max(t, 1)
-                                                                  and not _is_producer(p, t, q))])
-                for p, (specs, waits) in zip(plans, progs)]
+                                                                  and not _is_producer(p, t, q))], o, tw)
+                for p, (specs, waits, o, tw) in zip(plans, progs)]
     failures = 0
     for seed in range(30):
         try:
@@ -162,8 +221,8 @@ def test_push_waits_catch_a_missing_wait():
     plans = _plans(M, G, (0.5, 0.3, 0.2), False, None)
     progs = _programs(plans)
     stripped = []
-    for p, (specs, waits) in zip(plans, progs):
-        stripped.append((specs, [(t, q, v) for t, q, v in waits if t == p.n_steps]))  # only the root's end waits
+    for p, (specs, waits, o, _tw) in zip(plans, progs):
+        stripped.append((specs, [(t, q, v) for t, q, v in waits if t == p.n_steps], o, []))  # only the root's end waits
     failures = 0
     for seed in range(20):
         try:
@@ -171,3 +230,52 @@ def test_push_waits_catch_a_missing_wait():
         except AssertionError:
             failures += 1
     assert failures > 0
+
+
+@pytest.mark.parametrize("relay", [False, True])
+def test_counters_alone_miss_late_data(relay):
+    """Without the landing tags, a store still in flight on its link when the producer's counter
+    is published is read stale in some interleaving: the gap is real in this model, and the tags
+    are what closes it (test_push_protocol_random_interleavings)."""
+    M, G = 30000, 4
+    plans = _plans(M, G, (0.5, 0.5), relay, None)
+    progs = [(specs, waits, o, []) for specs, waits, o, _tw in _programs(plans)]
+    failures = 0
+    for seed in range(30):
+        try:
+            _replay(plans, progs, M, calls=2, seed=seed, delay=True)
+        except AssertionError:
+            failures += 1
+    assert failures > 0
+
+
+@pytest.mark.parametrize("relay", [False, True])
+def test_landing_tags_reject_a_dropped_piece(relay):
+    """A push that never lands (its data and its tag lost on the link) stops the consumer at that
+    tag -- the executor's wait times out and the host raises (PushTransport.execute / errors()) --
+    instead of letting it compute with what the buffer held.  Every (rank, step, consumer) push is
+    dropped in turn on a small schedule."""
+    M, G = 12000, 3
+    plans = _plans(M, G, (1.0,), relay, None)
+    progs = _programs(plans)
+    pushes = [(r, t, c) for r, (_s, _w, o, _tw) in enumerate(progs) for t, c, _e in o]
+    assert pushes
+    for i, drop in enumerate(pushes):
+        with pytest.raises(TagTimeout):
+            _replay(plans, progs, M, calls=2, seed=i, delay=True, drop=drop)
+
+
+def test_tag_waits_point_to_earlier_steps():
+    """Every landing-tag wait names another rank's strictly earlier step (the deadlock argument),
+    and every tag a rank writes is waited for by its consumer exactly once."""
+    M, G = 50000, 8
+    plans = _plans(M, G, (0.5, 0.3, 0.2), False, None)
+    progs = _programs(plans)
+    written = {(r, t, c) for r, (_s, _w, o, _tw) in enumerate(progs) for t, c, _e in o}
+    waited = set()
+    for p, (_s, _w, _o, tw) in zip(plans, progs):
+        for t_wait, q, v, idx in tw:
+            t_push = idx - q * p.n_steps
+            assert q != p.rank and t_push < t_wait and v == t_push + 2
+            waited.add((q, t_push, p.rank))
+    assert waited == written

@@ -19,8 +19,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 # (G, K, rounds, relay, shapes)
 # (the relay case once gave the numel == 1 elements only the root's products in the second of
-# three calls, while the root's staging sum was a torch op after the executor; the sum and the
-# landing copies run inside the executor since)
+# three calls, while the root's staging sum was a torch reduction between the executor and the
+# pairwise finish (tools/push_tail_probe.py); the sum and the landing copies run
+# inside the executor since, so no torch op sits between libfedagg launches on this path)
 CASES = [
     (2, 5, (1.0,), False, "default"),
     (3, 7, (0.5, 0.3, 0.2), False, "default"),
@@ -97,6 +98,10 @@ def _worker(rank, G, K, rounds, relay, shapes_name, port, q):
                 bad.append(nb)
         errs = tr.errors()
         programs = len(tr._programs)
+        prog = tr._programs[0]
+        # every rank writes landing tags (at least the root's staging tag) and the root waits for them
+        assert prog.ntags > 0 if rank != plan.root else sum(1 for w in prog.tag_waits) > 0, (rank, prog.ntags)
+        print(f"[push] rank {rank}: late landing tags {tr.late_tags()[rank]}", file=sys.stderr, flush=True)
         tr.close()
         dist.destroy_process_group()
         q.put((rank, bad, errs, programs, calls, None))
