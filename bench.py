@@ -87,10 +87,12 @@ def parse():
                     help="client-shard striped: also time these round splits (';'-separated, e.g. "
                          "'1.0;0.75,0.25') over the same communicator")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
-    ap.add_argument("--executor", default="native", choices=["native", "torch", "push"],
+    ap.add_argument("--executor", default="native", choices=["native", "torch", "push", "gather"],
                     help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip), the "
                          "Python schedule over torch.distributed's RCCL process group, or the push executor "
-                         "(substrafl_amd/push.py: chain kernels storing into IPC-mapped peer slots, fp32 rows)")
+                         "(substrafl_amd/push.py: chain kernels storing into IPC-mapped peer slots, fp32 rows); "
+                         "gather (N > 1 line's param_range_strong_gather leg: the workload's M split over the ranks, "
+                         "the result slices gathered to rank 0 over RCCL inside the timed step)")
     ap.add_argument("--client-shard-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--t1-ms", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
@@ -343,7 +345,7 @@ def main():
     device = torch.device("cuda", dev_index)
     own_gpus = world <= ndev
     # RCCL in the process group only where torch's process group carries the exchange itself
-    torch_pg_exchange = (client_shard or args.client_shard_child) and args.executor == "torch"
+    torch_pg_exchange = (client_shard or args.client_shard_child) and args.executor in ("torch", "gather")
     backend = init_group(dist, world, device, world > 1 and own_gpus and torch_pg_exchange) if world > 1 else None
     lib = _native.load()
     if args.grid_cap:
@@ -357,8 +359,11 @@ def main():
 
     if args.client_shard_child:  # one leg of an N > 1 line (see client_shard_legs)
         try:
-            res = measure_client_shard(args, ctx, args.combine, args.scaling, t1_ms=args.t1_ms or None,
-                                       t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
+            if args.executor == "gather":
+                res = measure_param_range_gather(args, ctx, t1_ms=args.t1_ms or None)
+            else:
+                res = measure_client_shard(args, ctx, args.combine, args.scaling, t1_ms=args.t1_ms or None,
+                                           t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
         except Exception as e:  # noqa: BLE001 -- reported in the parent's line
             res = {"error": f"{type(e).__name__}: {e}"[:800]}
         if args.executor == "torch" and world > 1 and "error" not in res:
@@ -514,7 +519,10 @@ def measure_param_range(args, ctx):
         "data": "synthetic (N(0,1) client buckets generated on device, torch Philox seeds 20241016+k; "
                 "n_samples = default_rng(7).integers(100, 10000, K))",
         "config": {
-            "workload": wl["name"],
+            # N > 1 weak: every rank reduces its own K x M (an N x M-param model, no bytes between
+            # GPUs) -- per GPU the workload; BASELINE's C3 as written (M split over the GPUs, the
+            # result gathered to rank 0) is the param_range_strong_gather leg of the same line
+            "workload": wl["name"] + ("_per_gpu" if world > 1 and args.scaling == "weak" else ""),
             "strategy": wl["strategy"],
             "clients": K,
             "clients_per_gpu": K,
@@ -599,6 +607,19 @@ def multi_device_leg(args, ctx):
 # ======================================================================================
 # client-shard (the north-star mode) -- its own line, or a field of the N > 1 line
 # ======================================================================================
+# (executor, scaling, line key, extra environment, extra arguments), in the order the N > 1 line
+# runs them (client_shard_legs): the decisive comparison first -- the push executor,
+# whose full output is compared with the native executor's on the same client blocks, and the
+# native weak leg -- then C3 as written (M split over the GPUs, the result gathered to rank 0 over
+# RCCL inside the step), then the rest
+LEGS = (("push", "weak", "client_shard_push", {}, []),
+        ("native", "weak", "client_shard", {}, ["--variant-rounds", "1.0;0.75,0.25"]),
+        ("gather", "strong", "param_range_strong_gather", {}, []),
+        ("torch", "weak", "client_shard_torch_pg", {}, []),
+        ("native", "strong", "client_shard_strong", {}, []),
+        ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}, []))
+
+
 def client_shard_legs(args, ctx, info, only_push=False):
     """The client-shard legs of an N > 1 line, each in a CHILD process per rank (a fresh
     interpreter with its own process group on a new port, started once this rank's parameter-range
@@ -623,21 +644,21 @@ def client_shard_legs(args, ctx, info, only_push=False):
     # (last, and with a shorter deadline: RCCL's copy-engine path has never run on this node)
     # The native weak leg also re-times the other round splits over its communicator
     # (rounds_variants): the model's choice of three rounds assumes full overlap.
-    legs = (("native", "weak", "client_shard", {}, ["--variant-rounds", "1.0;0.75,0.25"]),
-            ("torch", "weak", "client_shard_torch_pg", {}, []),
-            ("native", "strong", "client_shard_strong", {}, []),
-            ("native", "weak", "client_shard_copy_engine", {"NCCL_P2P_USE_CUDA_MEMCPY": "1"}, []),
-            ("push", "weak", "client_shard_push", {}, []))
+    # the decisive comparison first: the push executor (its full output compared
+    # with the native executor's on the same client blocks) and the native weak leg, then C3 as
+    # written (M split over the GPUs, the result gathered to rank 0 over RCCL inside the step),
+    # then the rest
+    legs = LEGS
     if only_push:
         legs = tuple(leg for leg in legs if leg[0] == "push")
     md_reserve = MULTI_DEVICE_DEADLINE_S if args.multi_device_leg != "off" else 0
+    out = {"legs_order": [leg[2] for leg in legs]}
     ports = [[_free_port() for _ in legs]] if ctx.rank == 0 else [None]
     if ctx.world > 1:
         dist.broadcast_object_list(ports, src=0)
-    out = {}
     for i, ((executor, scaling, key, leg_env, leg_args), port) in enumerate(zip(legs, ports[0])):
         later = (len(legs) - 1 - i) * LEG_MIN_S + min(md_reserve, LEG_MIN_S) + 15
-        cap = CLIENT_SHARD_DEADLINE_S if not (leg_env or executor == "push") else CLIENT_SHARD_DEADLINE_S / 2
+        cap = CLIENT_SHARD_DEADLINE_S if not (leg_env or executor in ("push", "gather")) else CLIENT_SHARD_DEADLINE_S / 2
         dl = [leg_deadline(cap, later)] if ctx.rank == 0 else [None]
         if ctx.world > 1:
             dist.broadcast_object_list(dl, src=0)
@@ -887,6 +908,10 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     torch.cuda.synchronize(device)
     parity = _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held, outs, c, tvs) \
         if variants else None
+    full_compare = None
+    if variants and getattr(tr, "push", False) and world > 1 and lockstep_mode and not scaffold:
+        # every element (numel == 1 ones included) against a second, independent transport
+        full_compare = _push_vs_native(ctx, plan, blocks, outs["out"], ops, pw, ws, slots, M)
     if t1_ms is None:  # one GPU reducing the workload's own K x M: the weak-scaling reference
         t1_ms, t1_source = _single_gpu_ms(ctx, K_per, M, kind, scaffold, layout, n_samples), \
             "this rank, one GPU over the workload's K x M (same bench, same layout policy)"
@@ -918,10 +943,20 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                      "native RCCL (csrc/lockstep.hip)" if getattr(tr, "native", False) else
                      "Python schedule over torch.distributed" if world > 1 else "one rank (no exchange)"),
         "schedule": schedule,
-        "hip_streams_per_rank": ("4 (compute + 3 for a step's per-consumer launches)" if getattr(tr, "push", False)
-                                 else "2 (compute + the communicator's)") + " <= GPU_MAX_HW_QUEUES = 4",
+        "hip_streams_per_rank": (f"{1 + len(tr._aux)} (compute + {len(tr._aux)} for a step's per-consumer launches)"
+                                 if getattr(tr, "push", False) else
+                                 "4 (compute + the communicator's + RCCL's device and host streams)"
+                                 if getattr(tr, "native", False) and world > 1 else
+                                 "2 (compute + the communicator's)") + " <= GPU_MAX_HW_QUEUES = 4",
         "parity": parity,
     }
+    if getattr(tr, "push", False):
+        res["late_landing_tags"] = int(sum(tr.late_tags()))  # every rank's count: one shared page
+        res["wait_errors"] = tr.errors()
+        if full_compare is not None or rank == 0:
+            res["full_compare"] = full_compare
+    elif getattr(tr, "comm_count", None) is not None:
+        res["rccl_comm_count"] = tr.comm_count()
     if scaling == "weak":
         res["weak_efficiency"] = round(t1_ms / ms, 4) if ms > 0 else None
     else:  # the same K x M over the ranks: speedup over one GPU, and that over the rank count
@@ -944,6 +979,142 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
             except Exception as e:  # noqa: BLE001 -- a variant never costs the leg
                 res["rounds_variants"].append({"rounds": spec, "error": f"{type(e).__name__}: {e}"[:300]})
             torch.cuda.empty_cache()
+    return res
+
+
+def _push_vs_native(ctx, plan, blocks, out, ops, pw, ws, slots, M):
+    """The push leg's whole output against the native RCCL executor's on the same plan and client
+    blocks: two independent transports (stores into IPC-mapped peer memory against RCCL's P2P),
+    one expected bit pattern -- both follow the reference's client order (fed_avg.py:221-222).
+    Collective; returns the comparison on the root (every element, numel == 1 ones included)."""
+    torch = ctx.torch
+    from substrafl_amd.rccl import RcclTransport
+    from substrafl_amd.sharding import lockstep_fedavg
+
+    if torch.cuda.device_count() < ctx.world:
+        return {"skipped": f"{ctx.world} ranks share {torch.cuda.device_count()} GPU(s): RCCL refuses duplicate GPUs"}
+    push_out = out.clone()
+    nat = RcclTransport()  # created after the push leg's timing: never live beside a push step
+    try:
+        count = nat.comm_count()
+        out.fill_(float("nan"))
+        lockstep_fedavg(plan, blocks, out, nat, ops, pw, ws=ws, slots=slots)
+        torch.cuda.synchronize(ctx.device)
+        res = None
+        if plan.rank == plan.root:
+            a, b = push_out[:M].view(torch.int32), out[:M].view(torch.int32)
+            res = {"against": "native RCCL executor (csrc/lockstep.hip), same plan and client blocks",
+                   "elements": M, "mismatches": int((a != b).sum().item()), "rccl_comm_count": count}
+    finally:
+        nat.close()
+        out.copy_(push_out)
+    return res
+
+
+def measure_param_range_gather(args, ctx, t1_ms=None):
+    """BASELINE.json's C3 as written on N GPUs ("64 clients x 125M ... sharded across 8 MI355X"),
+    strong: rank r reduces elements [lo_r, hi_r) of all K clients with the single-GPU kernel
+    (parameter-range sharding, bit-exact), and the timed step includes the RCCL gather of the N
+    result slices into ONE full result on rank 0 (torch.distributed gather over the NCCL backend:
+    (N - 1) / N of M * 4 bytes into rank 0 over its xGMI links).  Parity: every rank's sampled
+    elements against the reference's sequential order, and rank 0's gathered slices against every
+    rank's own by checksum."""
+    torch, world, rank, device, dist = ctx.torch, ctx.world, ctx.rank, ctx.device, ctx.dist
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+    from substrafl_amd.layout import BucketLayout, synthetic_state_dict_shapes
+    from substrafl_amd.sharding import shard_bounds
+
+    wl = ctx.wl
+    if wl["strategy"] != "fedavg" or wl["kind"] != "f32":
+        return {"skipped": "the gather leg runs the fp32 FedAvg workloads (c2, c3)"}
+    K, M = wl["K"], wl["M"]
+    layout = BucketLayout(list(range(len(synthetic_state_dict_shapes(M)))), synthetic_state_dict_shapes(M), np.float32)
+    bounds = shard_bounds(M, world)
+    lo, hi = bounds[rank]
+    n = hi - lo
+    chunk = bounds[0][1] - bounds[0][0]
+    pw = layout.pairwise_idx.astype(np.int64)
+    pw_local = (pw[(pw >= lo) & (pw < hi)] - lo).astype(np.uint64)
+    n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
+    ld = max(64, -(-max(1, n) // 64) * 64)
+    x = synth_clients(torch, K, ld, max(1, n), "f32", device, 20241016 + 1_000_003 * rank)
+    send = torch.zeros(chunk, dtype=torch.float32, device=device)
+    plan = FedAvgPlan("f32", x, fedavg_weights(n_samples, "f32"), n, send, pw_local)
+    full = (torch.empty(world * chunk, dtype=torch.float32, device=device) if world > 1 else send) if rank == 0 else None
+    glist = [full[r * chunk:(r + 1) * chunk] for r in range(world)] if rank == 0 else None
+    stream = ctx.stream
+
+    def gather():
+        if world > 1:  # one rank: its slice is the whole result, already where it belongs
+            dist.gather(send, gather_list=glist, dst=0)
+
+    def step():
+        plan.launch(stream)
+        gather()
+
+    steps = max(1, min(args.steps, args.client_shard_steps))
+    warm = max(1, min(args.warmup, 5))
+    elapsed, _ev = _timed(ctx, step, steps, warm)
+
+    def timed_alone(fn, reps=10):
+        torch.cuda.synchronize(device)
+        ctx.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(device)
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    kern_ms = timed_alone(lambda: plan.launch(stream))
+    gather_ms = timed_alone(gather)
+    # parity: sampled elements of this rank's slice against the sequential fp32 chain
+    g = np.random.default_rng(123 + rank)
+    idx = np.setdiff1d(np.unique(g.integers(0, max(1, n), 1024)), pw_local.astype(np.int64)) if n else np.zeros(0, np.int64)
+    mism = 0
+    if idx.size:
+        tidx = torch.from_numpy(idx).to(device)
+        xs = x[:, tidx].double().cpu().numpy()
+        w32 = fedavg_weights(n_samples, "f32")
+        acc = np.zeros(idx.size, np.float32)
+        for k in range(K):
+            acc = (acc + (xs[k].astype(np.float32) * w32[k]).astype(np.float32)).astype(np.float32)
+        mism = int(np.sum(acc.view(np.uint32) != send[tidx].cpu().numpy().view(np.uint32)))
+    # the gathered slices on rank 0 against each rank's own slice, by checksum of the bit patterns
+    step()
+    torch.cuda.synchronize(device)
+    mine = int(send[:n].view(torch.int32).to(torch.int64).sum().item()) if n else 0
+    sums = [(mine, mism)] * world
+    if world > 1:
+        dist.all_gather_object(sums, (mine, mism))
+    elapsed, kern_ms, gather_ms = ctx.max_over_ranks([elapsed, kern_ms, gather_ms])
+    if rank != 0:
+        return {}
+    got = [int(full[r * chunk: r * chunk + (b - a)].view(torch.int32).to(torch.int64).sum().item()) if b > a else 0
+           for r, (a, b) in enumerate(bounds)]
+    ms = elapsed / steps * 1e3
+    bytes_job = K * M * 4 + M * 4
+    res = {
+        "workload": wl["name"] + " (BASELINE.json C3 as written: M split over the GPUs)",
+        "scaling": "strong",
+        "clients": K,
+        "params": M,
+        "params_per_gpu": chunk,
+        "steps": steps,
+        "warmup": warm,
+        "ms_per_step": round(ms, 5),
+        "GBps": round(bytes_job / (ms / 1e3) / 1e9, 2),
+        "frac_of_n_x_hbm_peak": round(bytes_job / (ms / 1e3) / 1e9 / (world * HBM_PEAK_GBPS), 4),
+        "kernel_ms": round(kern_ms, 5),
+        "gather_ms": round(gather_ms, 5),
+        "gather": "torch.distributed gather (NCCL backend = RCCL) of the N result slices into one buffer on rank 0",
+        "gather_bytes_into_rank0": (world - 1) * chunk * 4,
+        "parity": {"sampled_per_rank": 1024, "mismatches": int(sum(v[1] for v in sums)),
+                   "gathered_slice_checksum_mismatches": int(sum(1 for r in range(world) if got[r] != sums[r][0]))},
+    }
+    if t1_ms:
+        res["single_gpu_ms"] = round(t1_ms, 5)
+        res["speedup"] = round(t1_ms / ms, 4) if ms > 0 else None
+        res["strong_efficiency"] = round(t1_ms / (world * ms), 4) if ms > 0 else None
     return res
 
 
@@ -1323,7 +1494,7 @@ def rehearse(args, world, rank):
     for _ in range(args.steps):
         x = x * np.float32(1.0)
     elapsed = time.perf_counter() - t0
-    cs = None
+    cs = gather_leg = None
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -1335,14 +1506,20 @@ def rehearse(args, world, rank):
                               lambda v: [float(x) for x in _all_max(torch, dist, v)], ring_mib=1, peers_mib=1, iters=2)
             if cs is not None:
                 cs["xgmi_p2p"] = probe
+            gather_leg = _rehearse_gather(world, rank)
     if rank == 0:
         line = {"metric": METRIC + " [CPU rehearsal of the launcher: not a measurement]",
                 "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 6),
                 "rehearsal": True, "ranks_seen": world}
+        wl = WORKLOADS[args.workload]
+        line["config"] = {"workload": wl["name"] + ("_per_gpu" if world > 1 and args.scaling == "weak" else ""),
+                          "parallelism": f"param-range x{world}" if world > 1 else "single-gpu"}
         if world > 1:
             line["process_group"] = {"backend": dist.get_backend(), "timeout_s": PG_TIMEOUT_S}
             line["client_shard"] = cs
+            line["legs_order"] = [leg[2] for leg in LEGS]
+            line["param_range_strong_gather"] = gather_leg
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -1380,12 +1557,28 @@ def _rehearse_client_shard(args, world, rank):
     t0 = time.perf_counter()
     root = lockstep_fedavg(plan, blocks, out, tr, _RehearsalOps(), np.zeros(0, np.int64))
     ms = (time.perf_counter() - t0) * 1e3
+    # the full comparison the push leg makes against the native executor, rehearsed as the other
+    # lockstep schedule over the same blocks (one expected bit pattern)
+    other = "relay" if combine == "striped" else "striped"
+    plan2 = relay_plan(M, world, rank, 4096) if other == "relay" else striped_plan(M, world, rank)
+    blocks2 = {}
+    for b, segs in plan2.blocks.items():
+        k0, k1 = client_blocks(K, world)[b]
+        t = torch.zeros((k1 - k0, plan2.block_len[b]), dtype=torch.float32)
+        for lo, hi, col in segs:
+            t[:, col: col + hi - lo] = torch.from_numpy(data[k0:k1, lo:hi])
+        blocks2[b] = FedAvgShard("f32", t, w[k0:k1], k0, K, plan2.block_len[b], np.zeros(0, np.uint64))
+    out2 = torch.zeros(M, dtype=torch.float32)
+    lockstep_fedavg(plan2, blocks2, out2, tr, _RehearsalOps(), np.zeros(0, np.int64))
     if not root:
         return None
     acc = np.zeros(M, np.float32)
     for k in range(K):
         acc = (acc + (data[k] * w[k]).astype(np.float32)).astype(np.float32)
     mism = int(np.sum(acc.view(np.uint32) != out.numpy().view(np.uint32)))
+    full = {"against": f"the {other} schedule over the same client blocks (gloo rehearsal; on GPUs: the native "
+                       "RCCL executor)", "elements": M,
+            "mismatches": int(np.sum(out.numpy().view(np.uint32) != out2.numpy().view(np.uint32)))}
     keys = ("combine", "scaling", "clients", "clients_per_gpu", "params", "layout", "steps", "warmup", "ms_per_step",
             "GBps", "frac_of_n_x_hbm_peak", "block_kernel_ms", "block_kernel_GBps", "exchange_and_tail_ms",
             "single_gpu_ms", "single_gpu_source", "weak_efficiency", "bit_exact_by_construction", "schedule",
@@ -1394,7 +1587,54 @@ def _rehearse_client_shard(args, world, rank):
     res.update(combine=combine, scaling="weak", clients=K, clients_per_gpu=K // world, params=M, layout="rows",
                steps=1, warmup=0, ms_per_step=round(ms, 3), bit_exact_by_construction=True,
                schedule={"steps": plan.n_steps, "issue": "one host thread, one communicator (gloo rehearsal)"},
-               parity={"sampled": M, "mismatches": mism}, rehearsal=True)
+               parity={"sampled": M, "mismatches": mism}, rehearsal=True, full_compare=full,
+               late_landing_tags=None, rccl_comm_count=world)
+    return res
+
+
+def _rehearse_gather(world, rank):
+    """The param_range_strong_gather leg over gloo on a tiny problem: every rank reduces its
+    parameter range (NumPy, the reference's order), the slices are gathered into one buffer on
+    rank 0, checked by checksum and against a host recomputation of the whole result."""
+    import torch
+    import torch.distributed as dist
+
+    from substrafl_amd.sharding import shard_bounds
+
+    K, M = 5, 3 * 4096 + 77
+    rng = np.random.default_rng(5)
+    data = rng.standard_normal((K, M)).astype(np.float32)
+    w = (np.arange(1, K + 1) / np.sum(np.arange(1, K + 1))).astype(np.float32)
+    bounds = shard_bounds(M, world)
+    lo, hi = bounds[rank]
+    chunk = bounds[0][1] - bounds[0][0]
+    acc = np.zeros(hi - lo, np.float32)
+    for k in range(K):
+        acc = (acc + (data[k, lo:hi] * w[k]).astype(np.float32)).astype(np.float32)
+    send = torch.zeros(chunk, dtype=torch.float32)
+    send[: hi - lo] = torch.from_numpy(acc)
+    full = torch.zeros(world * chunk, dtype=torch.float32) if rank == 0 else None
+    dist.gather(send, gather_list=[full[r * chunk:(r + 1) * chunk] for r in range(world)] if rank == 0 else None,
+                dst=0)
+    mine = int(send[: hi - lo].view(torch.int32).to(torch.int64).sum().item())
+    sums = [None] * world
+    dist.all_gather_object(sums, mine)
+    if rank != 0:
+        return None
+    ref = np.zeros(M, np.float32)
+    for k in range(K):
+        ref = (ref + (data[k] * w[k]).astype(np.float32)).astype(np.float32)
+    got = [int(full[r * chunk: r * chunk + (b - a)].view(torch.int32).to(torch.int64).sum().item())
+           for r, (a, b) in enumerate(bounds)]
+    keys = ("workload", "scaling", "clients", "params", "params_per_gpu", "steps", "warmup", "ms_per_step", "GBps",
+            "frac_of_n_x_hbm_peak", "kernel_ms", "gather_ms", "gather", "gather_bytes_into_rank0", "parity",
+            "single_gpu_ms", "speedup", "strong_efficiency")
+    res = {k: None for k in keys}
+    res.update(scaling="strong", clients=K, params=M, params_per_gpu=chunk, rehearsal=True,
+               gather="torch.distributed gather (gloo rehearsal; on GPUs: NCCL backend = RCCL)",
+               gather_bytes_into_rank0=(world - 1) * chunk * 4,
+               parity={"mismatches": int(np.sum(full[:M].numpy().view(np.uint32) != ref.view(np.uint32))),
+                       "gathered_slice_checksum_mismatches": int(sum(1 for r in range(world) if got[r] != sums[r]))})
     return res
 
 

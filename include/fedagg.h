@@ -275,6 +275,8 @@ int fedagg_comm_create(const char* rccl_path, int nranks, int rank, const void* 
 int fedagg_comm_destroy(fedagg_comm* comm);
 /* ncclCommAbort (a watchdog's way out of a stuck exchange) */
 int fedagg_comm_abort(fedagg_comm* comm);
+/* ncclCommCount: the ranks RCCL itself counts in the communicator (the N > 1 bench line reports it) */
+int fedagg_comm_count(fedagg_comm* comm, int* count_out);
 /* 0, or FEDAGG_EHIP if RCCL reports an asynchronous error on the communicator */
 int fedagg_comm_async_error(fedagg_comm* comm);
 const char* fedagg_comm_last_error(void);

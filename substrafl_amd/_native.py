@@ -98,6 +98,7 @@ SIGNATURES = {
     "fedagg_comm_destroy": (c_int, [c_void]),
     "fedagg_comm_abort": (c_int, [c_void]),
     "fedagg_comm_async_error": (c_int, [c_void]),
+    "fedagg_comm_count": (c_int, [c_void, P(c_int)]),
     "fedagg_comm_last_error": (ctypes.c_char_p, []),
     "fedagg_lockstep_execute": (c_int, [c_void, c_void, c_int, c_void, c_int, c_int, c_void, c_u64, c_int, c_int,
                                         c_void]),

@@ -50,6 +50,7 @@ struct Rccl {
   decltype(&ncclRecv) Recv = nullptr;
   decltype(&ncclReduce) Reduce = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclCommCount) CommCount = nullptr;
 };
 
 Rccl g_rccl;
@@ -68,7 +69,7 @@ int rccl_load(const char* path) {
   r.f = reinterpret_cast<decltype(r.f)>(dlsym(h, "nccl" #f));                         \
   if (!r.f) return lfail(FEDAGG_EINVAL, "fedagg_comm: RCCL lacks nccl", #f);
   SYM(GetUniqueId) SYM(CommInitRank) SYM(CommDestroy) SYM(CommAbort) SYM(CommGetAsyncError) SYM(GroupStart)
-  SYM(GroupEnd) SYM(Send) SYM(Recv) SYM(Reduce) SYM(GetErrorString)
+  SYM(GroupEnd) SYM(Send) SYM(Recv) SYM(Reduce) SYM(GetErrorString) SYM(CommCount)
 #undef SYM
   g_rccl = r;
   return FEDAGG_OK;
@@ -345,6 +346,11 @@ int fedagg_comm_abort(fedagg_comm* c) {
   int rc = nccl_check(g_rccl.CommAbort(c->comm), "ncclCommAbort");
   c->comm = nullptr;
   return rc;
+}
+
+int fedagg_comm_count(fedagg_comm* c, int* count_out) {
+  if (!c || !c->comm || !count_out) return lfail(FEDAGG_EINVAL, "fedagg_comm_count: invalid argument");
+  return nccl_check(g_rccl.CommCount(c->comm, count_out), "ncclCommCount");
 }
 
 int fedagg_comm_async_error(fedagg_comm* c) {

@@ -198,6 +198,10 @@ class PushTransport:
         root = self.rank == prog.plan.root and self.world > 1
         stage = prog.stage_u.ptr if root and ws_bytes else None
         ranges = prog.land_ranges if root else None
+        # a native RCCL communicator live in this process holds three streams of the hardware queues
+        from .rccl import RcclTransport
+
+        naux = min(len(self._aux), aux_stream_budget(_hw_queues(), RcclTransport.live() > 0))
         _check(self.lib.fedagg_push_execute(ctypes.byref(prog.runs) if prog.nruns else None, prog.nruns,
                                             ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
                                             ctypes.byref(prog.tags) if prog.ntags else None, prog.ntags,
@@ -205,7 +209,7 @@ class PushTransport:
                                             ws_src, ws_dst, ws_bytes, stage,
                                             prog.land_u.ptr if root else None, prog.out_ptr if root else None,
                                             ranges, prog.land_ranges_n // 2 if ranges is not None else 0,
-                                            self._aux_ptrs, len(self._aux), int(stream)), "fedagg_push_execute")
+                                            self._aux_ptrs if naux else None, naux, int(stream)), "fedagg_push_execute")
         self.base += prog.nsteps + 1
 
     def close(self) -> None:

@@ -92,6 +92,19 @@ class RcclTransport:
         self._h = h
         self._programs: List["NativeProgram"] = []
         self._py = None
+        RcclTransport._live += 1  # push.aux_stream_budget counts the live communicators
+
+    _live = 0  # communicators of this process not yet closed
+
+    @classmethod
+    def live(cls) -> int:
+        return cls._live
+
+    def comm_count(self) -> int:
+        """ncclCommCount: the ranks RCCL counts in this communicator."""
+        n = ctypes.c_int()
+        _check(self.lib.fedagg_comm_count(self._h, ctypes.byref(n)), "fedagg_comm_count")
+        return int(n.value)
 
     def python_transport(self):
         """The torch.distributed transport of the same group (sharding.DistTransport), for the paths
@@ -106,8 +119,9 @@ class RcclTransport:
 
     def close(self) -> None:
         if self._h:
-            _check(self.lib.fedagg_comm_destroy(self._h), "fedagg_comm_destroy")
-            self._h = None
+            h, self._h = self._h, None
+            RcclTransport._live -= 1
+            _check(self.lib.fedagg_comm_destroy(h), "fedagg_comm_destroy")
 
     def abort(self) -> None:
         if self._h:

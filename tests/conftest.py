@@ -1,3 +1,4 @@
+import os
 import sys
 from pathlib import Path
 
@@ -10,6 +11,40 @@ if str(ROOT) not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libfedagg.so on the GPU)")
+    config.addinivalue_line("markers", "tuning: an experiment launch variant; needs the FEDAGG_TUNING build "
+                                       "(FEDAGG_LIB=substrafl_amd/libfedagg_tuning.so); deselected otherwise")
+
+
+# fedagg_tune knobs the product library accepts; any other knob selects an experiment variant
+# that only the FEDAGG_TUNING build instantiates (DESIGN.md §5 "Product and tuning builds")
+PRODUCT_KNOBS = {"grid_cap", "fuse_pairwise", "eq_vec", "flat_vec", "st_sc1", "tiled_few", "sc_2l"}
+
+
+def experiment_knobs(*knob_dicts) -> bool:
+    keys = set().union(*[set(d) for d in knob_dicts])
+    return bool(keys - PRODUCT_KNOBS - {"K"}) or any(d.get("sc_2l") == 2 for d in knob_dicts)
+
+
+def tuning_requested() -> bool:
+    return "tuning" in os.environ.get("FEDAGG_LIB", "") or os.environ.get("FEDAGG_TUNING_TESTS") == "1"
+
+
+def pytest_collection_modifyitems(config, items):
+    """Experiment-variant tests (a ``knobs`` parameter naming experiment knobs) are marked
+    ``tuning`` and deselected unless the tuning build is loaded: the product library does not
+    instantiate them, so they would only ever skip there."""
+    keep, drop = [], []
+    for it in items:
+        knobs = getattr(getattr(it, "callspec", None), "params", {}).get("knobs")
+        if isinstance(knobs, dict) and experiment_knobs(knobs):
+            it.add_marker(pytest.mark.tuning)
+            if not tuning_requested():
+                drop.append(it)
+                continue
+        keep.append(it)
+    if drop:
+        config.hook.pytest_deselected(items=drop)
+        items[:] = keep
 
 
 class DummyAlgo:

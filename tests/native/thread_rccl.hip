@@ -260,6 +260,12 @@ ncclResult_t ncclCommDestroy(ncclComm_t c) {
 
 ncclResult_t ncclCommAbort(ncclComm_t c) { return ncclCommDestroy(c); }
 
+ncclResult_t ncclCommCount(const ncclComm_t c, int* count) {
+  if (!c || !count) return ncclInvalidArgument;
+  *count = (int)c->sent.size();  // one entry per rank of the world
+  return ncclSuccess;
+}
+
 ncclResult_t ncclCommGetAsyncError(ncclComm_t, ncclResult_t* st) {
   if (st) *st = ncclSuccess;
   return ncclSuccess;

@@ -69,6 +69,19 @@ def test_shared_gpu_ranks_skip_the_client_shard_leg():
     assert line["process_group"]["timeout_s"] > 0
 
 
+def test_shared_gpu_ranks_push_leg_forced():
+    """Two ranks sharing the GPU, legs forced: the push leg runs (IPC between the rank processes,
+    landing tags), bit-exact on its spot check, with no late tag and no wait error; its full
+    comparison against the native executor is reported as skipped (RCCL refuses two ranks on one
+    GPU) instead of failing the leg."""
+    line = _bench("--workload", "c2", "--gpus", "2", "--client-shard", "force", "--multi-device-leg", "off",
+                  "--steps", "3", "--warmup", "1", "--client-shard-steps", "3", "--no-cpu-baseline", timeout=400)
+    push = line["client_shard_push"]
+    assert "error" not in push, push
+    assert push["parity"]["mismatches"] == 0 and push["wait_errors"] == {}
+    assert "skipped" in push["full_compare"]
+
+
 def test_strong_scaling_two_ranks_shared_gpu():
     line = _bench("--workload", "c2", "--scaling", "strong", "--gpus", "2", "--steps", "3", "--warmup", "1",
                   "--no-cpu-baseline")
@@ -123,3 +136,13 @@ def test_n_gt_1_legs_rehearsed_on_one_gpu():
     assert all("error" not in v and v["ms_per_step"] > 0 for v in variants), variants
     md = line["multi_device"]
     assert "error" not in md and md["value"] > 0 and md["n_gpus"] == 1
+    assert line["legs_order"][:3] == ["client_shard_push", "client_shard", "param_range_strong_gather"]
+    push = line["client_shard_push"]  # one rank: the full comparison needs a peer
+    assert "error" not in push, push
+    assert push["parity"]["mismatches"] == 0 and push["late_landing_tags"] == 0 and push["wait_errors"] == {}
+    assert "full_compare" in push
+    assert line["client_shard"]["rccl_comm_count"] == 1  # ncclCommCount of the native leg's communicator
+    g = line["param_range_strong_gather"]  # C3 as written, here on one rank (no gather)
+    assert "error" not in g, g
+    assert g["parity"] == {"sampled_per_rank": 1024, "mismatches": 0, "gathered_slice_checksum_mismatches": 0}
+    assert g["kernel_ms"] > 0 and g["speedup"] > 0 and g["params_per_gpu"] >= 25_000_000

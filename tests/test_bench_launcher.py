@@ -47,6 +47,29 @@ def test_plain_gpus_2_launches_two_ranks():
     assert cs["parity"]["mismatches"] == 0 and cs["schedule"]["steps"] == 4
     probe = cs["xgmi_p2p"]  # the link-rate probe the N > 1 GPU line carries (here over gloo)
     assert probe["ring"]["GBps_per_direction"] > 0 and probe["all_peers"]["peers"] == 1
+    # VERDICT r03 "make the N > 1 line self-validating and its headline honest":
+    # the parameter-range value is labelled per GPU ...
+    assert line["config"]["workload"] == "fedavg_fp32_64x125M_per_gpu"
+    # ... the decisive legs run first ...
+    assert line["legs_order"][:3] == ["client_shard_push", "client_shard", "param_range_strong_gather"]
+    # ... the client-shard output is compared in full against a second, independent path ...
+    fc = cs["full_compare"]
+    assert fc["elements"] == cs["params"] and fc["mismatches"] == 0 and "native RCCL" in fc["against"]
+    assert "late_landing_tags" in cs and cs["rccl_comm_count"] == 2
+    # ... and C3 as written (M split over the ranks, result gathered to rank 0) is its own leg
+    g = line["param_range_strong_gather"]
+    assert g["scaling"] == "strong" and g["params_per_gpu"] * 2 >= g["params"]
+    assert g["parity"] == {"mismatches": 0, "gathered_slice_checksum_mismatches": 0}
+    for k in ("ms_per_step", "GBps", "kernel_ms", "gather_ms", "speedup", "strong_efficiency"):
+        assert k in g
+
+
+def test_single_gpu_line_keeps_its_workload_name():
+    """N = 1: the line is the workload itself (no per-GPU suffix, no legs)."""
+    r = _run(["--rehearse-cpu", "--steps", "2", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _line(r.stdout)
+    assert line["config"]["workload"] == "fedavg_fp32_64x125M" and "legs_order" not in line
 
 
 def test_pg_kwargs_has_a_timeout():

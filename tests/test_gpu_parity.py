@@ -18,18 +18,17 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
-PRODUCT_KNOBS = {"grid_cap", "fuse_pairwise", "eq_vec", "flat_vec", "st_sc1", "tiled_few", "sc_2l"}
+from conftest import PRODUCT_KNOBS, experiment_knobs  # noqa: E402
 
 
 def _tuning_only(*knob_dicts):
     """Skip unless every knob is one the loaded library has: experiment knobs select variants the
     product library does not instantiate (a FEDAGG_TUNING build does: ``build(tuning=True)``,
-    ``FEDAGG_LIB=substrafl_amd/libfedagg_tuning.so``)."""
+    ``FEDAGG_LIB=substrafl_amd/libfedagg_tuning.so``).  Such tests are deselected at collection
+    unless that build is requested (conftest.py), so this only guards a mismatched FEDAGG_LIB."""
     from substrafl_amd import _native
 
-    keys = set().union(*[set(d) for d in knob_dicts])
-    experiment = bool(keys - PRODUCT_KNOBS - {"K"}) or any(d.get("sc_2l") == 2 for d in knob_dicts)
-    if experiment and not _native.tuning_build():
+    if experiment_knobs(*knob_dicts) and not _native.tuning_build():
         pytest.skip("experiment variant: needs the FEDAGG_TUNING build of libfedagg")
 
 
