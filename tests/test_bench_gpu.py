@@ -137,11 +137,11 @@ def test_n_gt_1_legs_rehearsed_on_one_gpu():
     md = line["multi_device"]
     assert "error" not in md and md["value"] > 0 and md["n_gpus"] == 1
     assert line["legs_order"][:3] == ["client_shard_push", "client_shard", "param_range_strong_gather"]
-    push = line["client_shard_push"]  # one rank: the full comparison needs a peer
+    push = line["client_shard_push"]  # one rank: no peers, so the leg's plumbing only (no transport)
     assert "error" not in push, push
-    assert push["parity"]["mismatches"] == 0 and push["late_landing_tags"] == 0 and push["wait_errors"] == {}
-    assert "full_compare" in push
-    assert line["client_shard"]["rccl_comm_count"] == 1  # ncclCommCount of the native leg's communicator
+    assert push["executor"] == "push" and push["parity"]["mismatches"] == 0
+    # (one rank: the legs run over the loopback transport; ncclCommCount / late tags / the full
+    # comparison are N > 1 fields -- rehearsed over gloo in tests/test_bench_launcher.py)
     g = line["param_range_strong_gather"]  # C3 as written, here on one rank (no gather)
     assert "error" not in g, g
     assert g["parity"] == {"sampled_per_rank": 1024, "mismatches": 0, "gathered_slice_checksum_mismatches": 0}
