@@ -170,12 +170,16 @@ int fedagg_equal_count_f64(const double* const* d_copies, int K, uint64_t M, uns
  * -------------------------------------------------------------------------*/
 int fedagg_fedavg_chain_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                             float* d_out, void* stream);
-/* The push executor's chain run (FEDAGG_RUN_FEDAVG_PUSH): d_out may be a peer GPU's memory mapped
- * over xGMI; every wave of the launch ends with a system-scope release after its last store, so
- * the stores are performed at system scope before the executor's tag / counter writes that follow
- * the launch (fed_avg.py:221-222, the block's clients continuing the accumulator in order). */
-int fedagg_fedavg_chain_push_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
-                                 float* d_out, void* stream);
+/* The push executor's chain runs (FEDAGG_RUN_FEDAVG_PUSH): d_out = fl-continued d_in (this rank's
+ * fp32 accumulator slot; NULL: start from +0.0) + the block's clients in order (fed_avg.py:221-222),
+ * where d_out may be a peer GPU's memory mapped over xGMI.  Outputs are stored with system-scope
+ * write-through stores and every wave waits for their acknowledgements, so the stores are performed
+ * at system scope before the executor's tag / counter writes that follow the launch.  bf16 buckets
+ * accumulate in fp32 like fedagg_fedavg_chain_bf16.  d_in / d_out 16-B aligned. */
+int fedagg_fedavg_chain_push_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M,
+                                 const float* d_in, float* d_out, void* stream);
+int fedagg_fedavg_chain_push_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M,
+                                  const float* d_in, float* d_out, void* stream);
 int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                              float* d_out, void* stream);
 int fedagg_fedavg_chain_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, int seed,
@@ -241,7 +245,9 @@ int fedagg_scaffold_finish_f64(double* d_ws, int Ktot, const double* d_c, const 
  * -------------------------------------------------------------------------*/
 enum { FEDAGG_BF16 = 12 };  /* kind of a run over bf16 buckets (fp32 accumulators)              */
 enum { FEDAGG_RUN_FEDAVG = 0, FEDAGG_RUN_FEDAVG_TILED = 1, FEDAGG_RUN_SCAFFOLD = 2,
-       FEDAGG_RUN_FEDAVG_PUSH = 3 /* fp32 FedAvg run storing into mapped peer memory (push executor) */ };
+       FEDAGG_RUN_FEDAVG_PUSH = 3 /* FedAvg run (f32 / bf16) storing into mapped peer memory (push
+                                     executor): acc = the output, acc2 = the input accumulator (NULL:
+                                     seed ? +0.0 : acc) */ };
 typedef struct fedagg_lockstep_run {
   int32_t step;              /* the step it runs at (runs sorted by step)                        */
   int32_t op;                /* FEDAGG_RUN_*                                                     */
@@ -290,8 +296,8 @@ int fedagg_lockstep_execute(fedagg_comm* comm, const fedagg_lockstep_run* runs, 
 /* ---------------------------------------------------------------------------
  * Push executor of the same schedules (substrafl_amd/push.py, DESIGN.md §6 "Push"): no exchange
  * kernels.  Each run's chain kernel writes its accumulator straight into the consumer's slot (or
- * the root's output) through an IPC mapping over xGMI, its input accumulator read as one more
- * client of weight 1.0 (+0.0 + fl(X * 1.0) = X: a partial sum is never -0.0).  Cross-process
+ * the root's output) through an IPC mapping over xGMI, continuing the input accumulator it reads
+ * from this rank's own slot (fedagg_fedavg_chain_push_{f32,bf16}).  Cross-process
  * order: one monotonic progress counter per rank in a node-shared host page; a call publishes
  * base + 1 on entry (the rank's earlier stream work is done: peers may write into its buffers),
  * then before step t a one-lane wait kernel polls the counters the step needs and after it a
@@ -340,7 +346,7 @@ typedef struct fedagg_push_tag {
   int32_t reserved;
   uint64_t* tag;             /* a consumer's landing tag (mapped peer memory): *tag = base + 1   */
 } fedagg_push_tag;
-/* runs: FEDAGG_RUN_FEDAVG / FEDAGG_RUN_FEDAVG_PUSH (acc: a mapped peer address) sorted by step;
+/* runs: FEDAGG_RUN_FEDAVG / FEDAGG_RUN_FEDAVG_PUSH (acc: a mapped peer address; f32 or bf16) sorted by step;
  * waits sorted by step; tags: the landing tags this rank writes, sorted by step (<= 16 a step);
  * ws_src / ws_dst / ws_bytes: the numel == 1 products (fp32) copied to this rank's staging row on
  * the root after step 0's waits (0 bytes: none); ws_stage (root only, else NULL): the nranks

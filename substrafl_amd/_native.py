@@ -65,7 +65,8 @@ SIGNATURES = {
     "fedagg_scale_cast": (c_int, [c_void, c_int, c_dbl, c_void, c_int, c_u64, c_void]),
     # client-sharded building blocks (chain / split pairwise trees)
     "fedagg_fedavg_chain_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
-    "fedagg_fedavg_chain_push_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_fedavg_chain_push_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void, c_void]),
+    "fedagg_fedavg_chain_push_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void, c_void]),
     "fedagg_fedavg_chain_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_int, c_void, c_void]),

@@ -103,6 +103,9 @@ int g_xcd = 0;          // XCD-contiguous tile order (blocks sharing an XCD take
 // sit in this GPU's L2, which these never do; it cost 26-204 % of the run's time on one MI355X,
 // profiles/r04_push_overhead.jsonl, for nothing the write-through stores do not already give.)
 thread_local int g_rel_sys = 0;
+// Push runs: the input accumulator (this rank's slot, fp32 for f32 and bf16 buckets) when the
+// output is elsewhere (a peer's slot); the first client chunk reads it instead of `out`.
+thread_local const void* g_acc_in = nullptr;
 constexpr int NT_STORE_MIN_K = 16;
 // Output stores as device-scope write-through (sc1) instead of non-temporal: 8 x 25M fp32 133.6
 // vs 140.0 us, fp16 71.5 vs 75.0, fp64 280 vs 298; from 32 clients the output is <= 3 % of the
@@ -579,10 +582,13 @@ template <typename E, int KC, bool NT, int NTS, int VPT, int U, bool PIPE, bool 
 __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     fedavg_kernel(const FaArgs<E, KC> a, const PwArgs pw, const int K, const int first, const uint64_t nvec,
                   const uint64_t M, typename E::Out* __restrict__ out, const int remap, const int tpb,
-                  const uint64_t pitch, const int rel) {
+                  const uint64_t pitch, const int rel, const typename E::Out* in) {
 #pragma clang fp contract(off)
   using P = typename E::P;
   constexpr int L = E::L;
+  // first == 0: where the running accumulator is read -- a separate input only in the push runs'
+  // instantiations (NTS 3), so every other kernel compiles exactly as before
+  const typename E::Out* acc_src = (NTS == 3 && in) ? in : out;
   static_assert(!BUF || BLK == FA_BLOCK, "buffer-descriptor tiles assume 256-thread workgroups");
   static_assert(TV == 0 || (TILE && !PIPE && TV == VPT * BLK), "tile-interleaved buckets: one tile per workgroup step");
   const uint64_t stride = (uint64_t)gridDim.x * BLK;
@@ -606,7 +612,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
           vin[n] = TV ? t * pitch + n * BLK + threadIdx.x : v[n];
         }
         P acc[VPT][L];
-        fedavg_vectors<E, KC, NT, VPT, U, PIPE, BUF>(a, K, first, v, vin, acc, out, (TV ? t * pitch : t * tile) * 16);
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE, BUF>(a, K, first, v, vin, acc, acc_src, (TV ? t * pitch : t * tile) * 16);
         if (pw.n) patch_pairwise<E, KC, VPT, TV>(a, pw, K, v, acc, pitch);
 #pragma unroll
         for (int n = 0; n < VPT; ++n) store_vec_wave<E, NTS>(out, v[n], acc[n], wave_full, lds_wave);
@@ -614,7 +620,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
         for (uint64_t v0 = base; v0 < nvec; v0 += BLK) {
           P acc[1][L];
           const uint64_t vi0 = in_vec<TV>(v0, pitch);
-          fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, &vi0, acc, out);
+          fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, &vi0, acc, acc_src);
           if (pw.n) patch_pairwise<E, KC, 1, TV>(a, pw, K, &v0, acc, pitch);
           store_vec<E, NTS>(out, v0, acc[0]);
         }
@@ -628,7 +634,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
 #pragma unroll
         for (int n = 0; n < VPT; ++n) v[n] = v0 + n * stride;
         P acc[VPT][L];
-        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, v, acc, out);
+        fedavg_vectors<E, KC, NT, VPT, U, PIPE>(a, K, first, v, v, acc, acc_src);
         if (pw.n) patch_pairwise<E, KC, VPT>(a, pw, K, v, acc);
 #pragma unroll
         for (int n = 0; n < VPT; ++n) store_vec<E, NTS>(out, v[n], acc[n]);
@@ -636,7 +642,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
     }
     for (; v0 < nvec; v0 += stride) {
       P acc[1][L];
-      fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, &v0, acc, out);
+      fedavg_vectors<E, KC, NT, 1, U, PIPE>(a, K, first, &v0, &v0, acc, acc_src);
       if (pw.n) patch_pairwise<E, KC, 1>(a, pw, K, &v0, acc);
       store_vec<E, NTS>(out, v0, acc[0]);
     }
@@ -644,7 +650,7 @@ __global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC)))
 
   // Scalar remainder (M % L elements, or everything when a pointer is not 16-B aligned).
   for (uint64_t i = nvec * L + gid; i < M; i += stride) {
-    P acc = first ? P(0.0f) : E::in_out(out[i]);
+    P acc = first ? P(0.0f) : E::in_out(acc_src[i]);
     const uint64_t ii = in_elem<TV, L>(i, pitch);
     for (int k = 0; k < K; ++k) {
       const P p = E::cvt(a.x[k][ii]) * a.w[k];
@@ -1692,7 +1698,8 @@ void launch_fedavg_variant(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_
                            int kc, int first, uint64_t nvec, uint64_t M, typename E::Out* out, uint64_t pitch = 0) {
   if (BLK != FA_BLOCK) grid = (grid + BLK / FA_BLOCK - 1) / (BLK / FA_BLOCK);  // the caller sized it for 256
   hipLaunchKernelGGL((fedavg_kernel<E, FEDAGG_KCHUNK, NT, NTS, VPT, U, PIPE, TILE, OCC, BUF, BLK, INTER ? VPT * BLK : 0>),
-                     dim3(grid), dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb, pitch, g_rel_sys);
+                     dim3(grid), dim3(BLK), 0, s, a, pw, kc, first, nvec, M, out, g_xcd, g_tpb, pitch, g_rel_sys,
+                     static_cast<const typename E::Out*>(g_acc_in));
 }
 
 // Shape family (fedagg_tune "vpt" / "unroll" / "tile" / "pipe"), instantiated for every element
@@ -1869,7 +1876,7 @@ void launch_fedavg_shape(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KC
 template <typename E>
 void launch_fedavg(unsigned grid, hipStream_t s, const FaArgs<E, FEDAGG_KCHUNK>& a, const PwArgs& pw, int kc,
                    int first, uint64_t nvec, uint64_t M, typename E::Out* out, bool nts, bool sc1, Shape sh) {
-  if constexpr (std::is_same<E, F32>::value) {
+  if constexpr (std::is_same<E, F32>::value || std::is_same<E, BF16>::value) {
     if (g_rel_sys) return launch_fedavg_shape<E, 3>(grid, s, a, pw, kc, first, nvec, M, out, sh);  // push runs
   }
 #if FEDAGG_TUNING
@@ -2022,6 +2029,7 @@ int fedavg_launch(const typename E::In* const* x, const typename E::P* w, int K,
     const bool nts = g_nt_store < 0 ? K >= NT_STORE_MIN_K : g_nt_store != 0;
     const bool sc1 = g_st_sc1 < 0 ? K < SC1_MAX_K : g_st_sc1 != 0;
     launch_fedavg<E>(grid, s, a, pw, kc, (k0 == 0 && seed) ? 1 : 0, nvec, M, out, nts, sc1, sh);
+    g_acc_in = nullptr;  // later chunks continue from out
     int rc = check_launch("fedavg_kernel");
     if (rc) return rc;
   }
@@ -2711,12 +2719,28 @@ int fedagg_fedavg_chain_f32(const float* const* d_clients, const float* h_w, int
                             float* d_out, void* stream) {
   return fedavg_launch<F32>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
 }
-int fedagg_fedavg_chain_push_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
-                                 float* d_out, void* stream) {
+// Push runs: d_in (this rank's accumulator slot, fp32; NULL = start from +0.0) continued by the
+// block's clients in order, written to d_out (a peer's mapped slot or the root's output) with
+// system-scope write-through stores, every wave waiting for their acknowledgements.
+extern "C++" template <typename E>
+int fedavg_push_launch(const typename E::In* const* d_clients, const typename E::P* h_w, int K, uint64_t M,
+                       const float* d_in, float* d_out, hipStream_t s) {
+  if (d_in && (!aligned16(d_in) || !aligned16(d_out)))
+    return fail(FEDAGG_EINVAL, "fedavg_chain_push: accumulators must be 16-B aligned (K=%lld)", K);
   g_rel_sys = 1;
-  const int rc = fedavg_launch<F32>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, (hipStream_t)stream, seed != 0);
+  g_acc_in = d_in;
+  const int rc = fedavg_launch<E>(d_clients, h_w, K, M, nullptr, 0, nullptr, d_out, s, d_in == nullptr);
   g_rel_sys = 0;
+  g_acc_in = nullptr;
   return rc;
+}
+int fedagg_fedavg_chain_push_f32(const float* const* d_clients, const float* h_w, int K, uint64_t M,
+                                 const float* d_in, float* d_out, void* stream) {
+  return fedavg_push_launch<F32>(d_clients, h_w, K, M, d_in, d_out, (hipStream_t)stream);
+}
+int fedagg_fedavg_chain_push_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M,
+                                  const float* d_in, float* d_out, void* stream) {
+  return fedavg_push_launch<BF16>(d_clients, h_w, K, M, d_in, d_out, (hipStream_t)stream);
 }
 int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                              float* d_out, void* stream) {

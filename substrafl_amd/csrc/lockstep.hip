@@ -114,10 +114,17 @@ int run_one(const fedagg_lockstep_run& r, hipStream_t s) {
         rc = fedagg_fedavg_chain_f16((const uint16_t* const*)r.x, (const uint16_t*)r.w, r.K, r.n, r.seed,
                                      (uint16_t*)r.acc, s);
       break;
-    case FEDAGG_RUN_FEDAVG_PUSH:  // the accumulator is mapped peer memory: system-scope release per wave
-      if (r.kind != FEDAGG_F32) return lfail(FEDAGG_EINVAL, "lockstep: push runs are fp32");
-      rc = fedagg_fedavg_chain_push_f32((const float* const*)r.x, (const float*)r.w, r.K, r.n, r.seed, (float*)r.acc, s);
+    case FEDAGG_RUN_FEDAVG_PUSH: {  // output: mapped peer memory; input accumulator: acc2 (NULL: seed / acc)
+      const float* in = r.acc2 ? (const float*)r.acc2 : (r.seed ? nullptr : (const float*)r.acc);
+      if (r.kind == FEDAGG_F32)
+        rc = fedagg_fedavg_chain_push_f32((const float* const*)r.x, (const float*)r.w, r.K, r.n, in, (float*)r.acc, s);
+      else if (r.kind == FEDAGG_BF16)
+        rc = fedagg_fedavg_chain_push_bf16((const uint16_t* const*)r.x, (const float*)r.w, r.K, r.n, in,
+                                           (float*)r.acc, s);
+      else
+        return lfail(FEDAGG_EINVAL, "lockstep: push runs are fp32 or bf16 (fp32 accumulators)");
       break;
+    }
     case FEDAGG_RUN_FEDAVG_TILED:
       if (r.kind == FEDAGG_F32)
         rc = fedagg_fedavg_chain_tiled_f32((const float*)r.x[0], (const float*)r.w, r.K, r.n, r.tile_vectors,

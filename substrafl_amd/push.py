@@ -5,9 +5,9 @@ The RCCL executor (:mod:`rccl`) moves each step's accumulators with RCCL's P2P k
 MI355X hide only part of their time under an HBM-saturating chain kernel (DESIGN.md §6
 "Overlap").  Here there are no exchange kernels: a run's chain kernel writes its accumulator
 straight into the consumer's slot -- or, for a finished piece, into the root's output -- through
-an IPC mapping of the peer's buffer (xGMI stores, 1/65 of the kernel's traffic at C3), and reads
-its input accumulator as one more client of weight 1.0 (``+0.0 + fl(X * 1.0) = X`` exactly: a
-partial sum seeded with +0.0 is never -0.0).  Order across the processes: one monotonic
+an IPC mapping of the peer's buffer (xGMI stores, 1/65 of the kernel's traffic at C3), continuing
+its input accumulator read from this rank's own slot (``fedagg_fedavg_chain_push_{f32,bf16}``:
+the same per-element order as the chain kernels, fed_avg.py:221-222).  Order across the processes: one monotonic
 progress counter per rank in a node-shared host page, polled before a step by a one-lane wait kernel and published by a
 one-lane signal kernel on entry to a call (``base + 1``: the rank's earlier stream work -- a
 refill of its output, the previous call -- is done) and after each step t (``base + t + 2``).
@@ -33,8 +33,8 @@ number.  Every wait points to a strictly earlier step of another rank, so the sc
 deadlock whatever hardware queues the kernels share.  The numel == 1 products go to a staging row of the
 root per rank (one copy after step 0's waits) and are summed on the root (one owner per column: exact).
 
-Scope: fp32 FedAvg over row-layout client blocks (the bench's C3 schedule); the other kinds keep
-the RCCL executor.  Every rank must be on this node (the counters live in ``/dev/shm``).
+Scope: FedAvg over row-layout client blocks of fp32 (the bench's C3 schedule) or bf16 buckets
+(C5; fp32 accumulators); Scaffold and the fp64 / fp16 kinds keep the RCCL executor.  Every rank must be on this node (the counters live in ``/dev/shm``).
 """
 
 from __future__ import annotations
@@ -267,8 +267,9 @@ class PushProgram:
                  c=None, lr: float = 1.0):
         import torch
 
-        if scaffold or kind != "f32":
-            raise ValueError("push executor: fp32 FedAvg only (the other kinds take the RCCL executor)")
+        if scaffold or kind not in ("f32", "bf16"):
+            raise ValueError("push executor: FedAvg over fp32 / bf16 buckets (fp32 accumulators); the other "
+                             "kinds take the RCCL executor")
         for sh in blocks.values():
             if not isinstance(getattr(sh, "rows", None), torch.Tensor):
                 raise ValueError("push executor: row-layout client blocks only")
@@ -323,7 +324,7 @@ class PushProgram:
         self.land_ranges_n = len(flat)
         self.out_ptr = out.data_ptr()
         runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
-                          local(p.src) if p.src is not None else 0, remote=p.dst_rank != me) for p in specs]
+                          local(p.src) if p.src is not None else 0) for p in specs]
         n_steps = plan.n_steps
         outgoing = push_outgoing(plan, specs)
         everyone = tr.all_gather(outgoing) if G > 1 else [outgoing]
@@ -358,21 +359,23 @@ class PushProgram:
         return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
 
     def _run(self, t: int, sh, col: int, n: int, dst: int, src: int, remote: bool = False) -> _Run:
+        """One launch: the block's clients (``sh.rows`` at column ``col``, n elements) continuing
+        the fp32 accumulator at ``src`` (0: from +0.0) into ``dst``.  Every launch is a push run
+        (``FEDAGG_RUN_FEDAVG_PUSH``: input accumulator separate from the output, system-scope
+        write-through stores) -- also the root's own final runs into its output, which keeps one
+        arithmetic path for every piece."""
         rec = _Run()
-        # a run storing into a peer's memory ends every wave with a system-scope release
-        op = _native.FEDAGG_RUN_FEDAVG_PUSH if remote else _native.FEDAGG_RUN_FEDAVG
-        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, op, _native.FEDAGG_F32, 1, 0, n
+        kind = _native.FEDAGG_BF16 if self.kind == "bf16" else _native.FEDAGG_F32
+        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG_PUSH, kind, 0 if src else 1, 0, n
         rows = sh.rows
         base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
         ptrs = [base + k * step + col * esz for k in range(rows.shape[0])]
         w = [float(v) for v in np.asarray(sh.w, np.float32)]
-        if src:  # the input accumulator: one more client of weight 1.0, first in order
-            ptrs, w = [src] + ptrs, [1.0] + w
         rec.K = len(ptrs)
         arr = _native.ptr_array(ptrs)
         warr = (ctypes.c_float * len(w))(*w)
         self._keep += [arr, warr]
-        rec.x, rec.w, rec.acc = ctypes.addressof(arr), ctypes.addressof(warr), dst
+        rec.x, rec.w, rec.acc, rec.acc2 = ctypes.addressof(arr), ctypes.addressof(warr), dst, src or None
         return rec
 
     def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-# (G, K, rounds, relay, shapes)
+# (G, K, rounds, relay, shapes[, kind])
 # (the relay case once gave the numel == 1 elements only the root's products in the second of
 # three calls, while the root's staging sum was a torch reduction between the executor and the
 # pairwise finish (tools/push_tail_probe.py); the sum and the landing copies run
@@ -27,7 +27,10 @@ CASES = [
     (3, 7, (0.5, 0.3, 0.2), False, "default"),
     (4, 9, (0.75, 0.25), True, "default"),
     (3, 40, (0.5, 0.5), False, "wide"),
+    (3, 7, (0.5, 0.5), False, "default", "bf16"),  # C5's kind: bf16 buckets, fp32 accumulators
+    (4, 9, (0.75, 0.25), True, "default", "bf16"),
 ]
+CASES = [c if len(c) == 6 else c + ("f32",) for c in CASES]
 
 
 def _port() -> int:
@@ -38,7 +41,7 @@ def _port() -> int:
     return p
 
 
-def _worker(rank, G, K, rounds, relay, shapes_name, port, q):
+def _worker(rank, G, K, rounds, relay, shapes_name, kind, port, q):
     import faulthandler
 
     faulthandler.dump_traceback_later(100, exit=True)
@@ -64,16 +67,19 @@ def _worker(rank, G, K, rounds, relay, shapes_name, port, q):
         shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else [(1,), (130001,), (1, 1), (77777,)]
         pus, ns = _data(K, seed=17 + G, shapes=shapes)
         pus = [[a.astype(np.float32) for a in c] for c in pus]
+        if kind == "bf16":  # bf16-representable values: the reference runs on the exact upcast
+            pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
         layout = BucketLayout(range(len(shapes)), shapes, np.float32)
         plan = relay_plan(layout.M, G, rank, 4096) if relay else striped_plan(layout.M, G, rank, None, rounds)
         blocks = {}
         for b, segs in plan.blocks.items():
             k0, k1 = client_blocks(K, G)[b]
-            full = _rows(torch, pus[k0:k1], layout, dtype=np.float32)
-            t = torch.zeros((k1 - k0, plan.block_len[b]), dtype=torch.float32, device="cuda")
+            tdt = torch.bfloat16 if kind == "bf16" else torch.float32
+            full = _rows(torch, pus[k0:k1], layout, dtype=np.float32, tdtype=tdt)
+            t = torch.zeros((k1 - k0, plan.block_len[b]), dtype=tdt, device="cuda")
             for lo, hi, col in segs:
                 t[:, col: col + hi - lo] = full[:, lo:hi]
-            blocks[b] = FedAvgShard("f32", t, fedavg_weights(ns, "f32")[k0:k1], k0, K, plan.block_len[b],
+            blocks[b] = FedAvgShard(kind, t, fedavg_weights(ns, kind)[k0:k1], k0, K, plan.block_len[b],
                                     np.zeros(0, np.uint64))
         tr = PushTransport(timeout_s=30)
         bad, calls = [], 0
@@ -111,14 +117,14 @@ def _worker(rank, G, K, rounds, relay, shapes_name, port, q):
         q.put((rank, None, None, 0, 0, traceback.format_exc()[-2000:]))
 
 
-@pytest.mark.parametrize("G,K,rounds,relay,shapes", CASES)
-def test_push_executor_processes_bit_exact(G, K, rounds, relay, shapes):
+@pytest.mark.parametrize("G,K,rounds,relay,shapes,kind", CASES)
+def test_push_executor_processes_bit_exact(G, K, rounds, relay, shapes, kind):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, G, K, rounds, relay, shapes, port, q)) for r in range(G)]
+    procs = [ctx.Process(target=_worker, args=(r, G, K, rounds, relay, shapes, kind, port, q)) for r in range(G)]
     for p in procs:
         p.start()
     res = {}
@@ -135,3 +141,39 @@ def test_push_executor_processes_bit_exact(G, K, rounds, relay, shapes):
         assert tb is None, f"rank {rank}:\n{tb}"
         assert errs == {} and programs == 1 and calls == 3, (rank, errs, programs, calls, bad)
     assert res[0][0] == [0, 0, 0], res[0][0]  # root: every element, every call
+
+
+@pytest.mark.parametrize("kind", ["f32", "bf16"])
+@pytest.mark.parametrize("K,M", [(9, 4096 * 3 + 5), (65, 2_000_000), (130, 70_001)])
+def test_push_run_continues_its_input_accumulator(kind, K, M):
+    """fedagg_fedavg_chain_push_{f32,bf16} (one process): d_in continued by the block's clients into
+    a separate d_out, bit-identical to the chain kernel continuing the same accumulator in place;
+    d_in NULL is the chain from +0.0.  Also across client chunks (K > 128) and element remainders."""
+    import ctypes
+
+    import torch
+
+    from substrafl_amd import _native
+    from substrafl_amd.engine import fedavg_weights
+
+    lib = _native.load()
+    torch.manual_seed(K + M)
+    tdt = torch.bfloat16 if kind == "bf16" else torch.float32
+    rows = torch.randn((K, M), dtype=torch.float32, device="cuda").to(tdt)
+    w = (ctypes.c_float * K)(*[float(v) for v in fedavg_weights(list(range(1, K + 1)), "f32")])
+    ptrs = _native.ptr_array([rows[k].data_ptr() for k in range(K)])
+    acc_in = torch.randn(M, dtype=torch.float32, device="cuda")
+    chain = getattr(lib, f"fedagg_fedavg_chain_{kind}")
+    push = getattr(lib, f"fedagg_fedavg_chain_push_{kind}")
+    s = torch.cuda.current_stream().cuda_stream
+    ref = acc_in.clone()
+    _native.check(chain(ptrs, w, K, M, 0, ref.data_ptr(), s), "chain")
+    out = torch.full((M,), float("nan"), device="cuda")
+    _native.check(push(ptrs, w, K, M, acc_in.data_ptr(), out.data_ptr(), s), "chain_push")
+    ref0 = torch.empty(M, device="cuda")
+    _native.check(chain(ptrs, w, K, M, 1, ref0.data_ptr(), s), "chain seed")
+    out0 = torch.full((M,), float("nan"), device="cuda")
+    _native.check(push(ptrs, w, K, M, None, out0.data_ptr(), s), "chain_push seed")
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(out0.view(torch.int32), ref0.view(torch.int32))

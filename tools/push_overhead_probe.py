@@ -90,7 +90,8 @@ def main():
 
     def plain_runs(fn):
         for _ in range(S):
-            _native.check(fn(ptrs, w, K, n, 1, acc.data_ptr(), stream.cuda_stream), "chain")
+            seed = None if fn is lib.fedagg_fedavg_chain_push_f32 else 1  # push: d_in NULL = seed
+            _native.check(fn(ptrs, w, K, n, seed, acc.data_ptr(), stream.cuda_stream), "chain")
 
     def timed_plain(fn):
         v = []
