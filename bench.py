@@ -715,7 +715,44 @@ def client_shard_legs(args, ctx, info, only_push=False):
             if bad and "error" not in res:
                 res["errors_on_other_ranks"] = bad
             out[key] = res
+    if ctx.rank == 0:  # every weak leg reduced the same K x M values: one expected output
+        sums = {k: v.get("output_checksum") for k, v in out.items()
+                if isinstance(v, dict) and v.get("scaling") == "weak" and v.get("checksum_comparable")
+                and v.get("output_checksum") is not None}
+        out["client_shard_output_checksums"] = {"legs": sorted(sums), "agree": len({tuple(c) for c in sums.values()}) <= 1
+                                                if sums else None}
     return out
+
+
+def _synth_block_elems(torch, kind, k0, Kb, width, segs, device):
+    """A client block's row buffer whose value at (client k, global element e) is a hash of (k, e)
+    in [-1, 1): the same wherever a plan puts (k, e) -- so every weak client-shard leg (push,
+    native, torch, copy-engine, any round split) reduces the very same K x M problem and their
+    full outputs must agree bit for bit (``output_checksum``)."""
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}[kind]
+    t = torch.zeros((max(1, Kb), max(1, width)), dtype=dt, device=device)
+    if Kb == 0:
+        return t[:0, :width]
+    kk = torch.arange(k0, k0 + Kb, device=device, dtype=torch.int64)[:, None]
+    step = 1 << 20
+    for lo, hi, col in segs:
+        for a in range(lo, hi, step):
+            b = min(hi, a + step)
+            e = torch.arange(a, b, device=device, dtype=torch.int64)[None, :]
+            h = (e * 2654435761 + kk * 40503 + 12345) & 0xFFFFFFFF
+            h = ((h ^ (h >> 15)) * 2246822519) & 0xFFFFFFFF
+            h = ((h ^ (h >> 13)) * 3266489917) & 0xFFFFFFFF
+            h = h ^ (h >> 16)
+            v = ((h & 0xFFFFFF).to(torch.float32) - 8388608.0) * (1.0 / 8388608.0)
+            t[:Kb, col + a - lo: col + b - lo] = v.to(dt)
+    return t[:Kb, :width]
+
+
+def _output_checksum(torch, out, M):
+    """Two sums of the output's bit patterns (plain, and position-weighted so a permutation shows)."""
+    x = out[:M].contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(M, device=out.device, dtype=torch.int64) % 1021 + 1
+    return [int(x.sum().item()), int((x * w).sum().item())]
 
 
 def _synth_block(torch, kind, Kb, width, device, seed):
@@ -816,8 +853,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                     else:
                         t.normal_(generator=g)
                 tvs.add(tv)
-            else:
-                rows = _synth_block(torch, kind, k1 - k0, width, device, seed)
+            else:  # rows: values addressed by (client, element), the same in every leg and round split
+                rows = _synth_block_elems(torch, kind, k0, k1 - k0, width, segs, device)
                 tvs.add(0)
             blocks[b] = FedAvgShard(kind, rows, w_all[k0:k1], k0, K, width, np.zeros(0, np.uint64))
             held[b] = (k0, rows, segs)
@@ -912,6 +949,10 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     if variants and getattr(tr, "push", False) and world > 1 and lockstep_mode and not scaffold:
         # every element (numel == 1 ones included) against a second, independent transport
         full_compare = _push_vs_native(ctx, plan, blocks, outs["out"], ops, pw, ws, slots, M)
+    # the whole output, summarised: every weak leg holds the same (client, element) values (rows),
+    # so their checksums must be equal (client_shard_legs compares them across the legs)
+    comparable = not scaffold and lockstep_mode and tvs == {0}
+    checksum = _output_checksum(torch, outs["out"], M) if (not scaffold and rank == 0) else None
     if t1_ms is None:  # one GPU reducing the workload's own K x M: the weak-scaling reference
         t1_ms, t1_source = _single_gpu_ms(ctx, K_per, M, kind, scaffold, layout, n_samples), \
             "this rank, one GPU over the workload's K x M (same bench, same layout policy)"
@@ -949,6 +990,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                                  if getattr(tr, "native", False) and world > 1 else
                                  "2 (compute + the communicator's)") + " <= GPU_MAX_HW_QUEUES = 4",
         "parity": parity,
+        "output_checksum": checksum,
+        "checksum_comparable": comparable,
     }
     if getattr(tr, "push", False):
         res["late_landing_tags"] = int(sum(tr.late_tags()))  # every rank's count: one shared page
@@ -975,7 +1018,11 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                 v = measure_client_shard(sub, ctx, combine, scaling, t1_ms, t1_source, tr=tr, variants=False)
                 res["rounds_variants"].append({k: v.get(k) for k in (
                     "ms_per_step", "weak_efficiency", "speedup", "block_kernel_ms", "exchange_and_tail_ms")}
-                    | {"rounds": v["schedule"].get("rounds"), "steps_of_schedule": v["schedule"].get("steps")})
+                    | {"rounds": v["schedule"].get("rounds"), "steps_of_schedule": v["schedule"].get("steps"),
+                       # the whole output of this round split against the leg's own (same values)
+                       "output_matches_leg": (v.get("output_checksum") == res["output_checksum"]
+                                              if res["checksum_comparable"] and v.get("checksum_comparable")
+                                              and rank == 0 else None)})
             except Exception as e:  # noqa: BLE001 -- a variant never costs the leg
                 res["rounds_variants"].append({"rounds": spec, "error": f"{type(e).__name__}: {e}"[:300]})
             torch.cuda.empty_cache()
@@ -1519,6 +1566,7 @@ def rehearse(args, world, rank):
             line["process_group"] = {"backend": dist.get_backend(), "timeout_s": PG_TIMEOUT_S}
             line["client_shard"] = cs
             line["legs_order"] = [leg[2] for leg in LEGS]
+            line["client_shard_output_checksums"] = {"legs": ["client_shard"], "agree": True} if cs else None
             line["param_range_strong_gather"] = gather_leg
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -1588,7 +1636,8 @@ def _rehearse_client_shard(args, world, rank):
                steps=1, warmup=0, ms_per_step=round(ms, 3), bit_exact_by_construction=True,
                schedule={"steps": plan.n_steps, "issue": "one host thread, one communicator (gloo rehearsal)"},
                parity={"sampled": M, "mismatches": mism}, rehearsal=True, full_compare=full,
-               late_landing_tags=None, rccl_comm_count=world)
+               late_landing_tags=None, rccl_comm_count=world, checksum_comparable=True,
+               output_checksum=_output_checksum(torch, out, M))
     return res
 
 

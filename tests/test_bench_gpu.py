@@ -142,6 +142,10 @@ def test_n_gt_1_legs_rehearsed_on_one_gpu():
     assert push["executor"] == "push" and push["parity"]["mismatches"] == 0
     # (one rank: the legs run over the loopback transport; ncclCommCount / late tags / the full
     # comparison are N > 1 fields -- rehearsed over gloo in tests/test_bench_launcher.py)
+    # every weak leg reduced the same (client, element) values: one output, whatever the executor
+    sums = line["client_shard_output_checksums"]
+    assert sums["agree"] is True and {"client_shard", "client_shard_push", "client_shard_torch_pg"} <= set(sums["legs"])
+    assert all(v["output_matches_leg"] is True for v in variants), variants
     g = line["param_range_strong_gather"]  # C3 as written, here on one rank (no gather)
     assert "error" not in g, g
     assert g["parity"] == {"sampled_per_rank": 1024, "mismatches": 0, "gathered_slice_checksum_mismatches": 0}

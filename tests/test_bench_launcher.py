@@ -56,6 +56,8 @@ def test_plain_gpus_2_launches_two_ranks():
     fc = cs["full_compare"]
     assert fc["elements"] == cs["params"] and fc["mismatches"] == 0 and "native RCCL" in fc["against"]
     assert "late_landing_tags" in cs and cs["rccl_comm_count"] == 2
+    assert cs["checksum_comparable"] and len(cs["output_checksum"]) == 2
+    assert line["client_shard_output_checksums"]["agree"] is True
     # ... and C3 as written (M split over the ranks, result gathered to rank 0) is its own leg
     g = line["param_range_strong_gather"]
     assert g["scaling"] == "strong" and g["params_per_gpu"] * 2 >= g["params"]
