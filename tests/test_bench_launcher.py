@@ -157,3 +157,32 @@ def test_cpu_threaded_variant_is_labelled():
 
     res = bench._cpu_threaded(fedavg_reference_structure, pus, [3, 1, 4, 1, 5], 1000, 3)
     assert "not the reference" in res["kind"] and 1 <= res["cores"] <= 3 and res["value"] > 0
+
+
+def test_client_shard_block_data_is_element_addressed():
+    """The client-shard legs' row buffers hold a hash of (client, element) wherever a plan puts the
+    element, so two plans (round splits, executors) hold the same values and their outputs are
+    comparable bit for bit (bench._synth_block_elems, the legs' output checksums)."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from substrafl_amd.sharding import client_blocks, striped_plan
+
+    M, G, K = 40_000, 4, 12
+    seen = []
+    for rounds in ((1.0,), (0.5, 0.3, 0.2)):
+        vals = np.full((K, M), np.nan, np.float32)
+        for r in range(G):
+            plan = striped_plan(M, G, r, None, rounds)
+            for b, segs in plan.blocks.items():
+                k0, k1 = client_blocks(K, G)[b]
+                t = bench._synth_block_elems(torch, "f32", k0, k1 - k0, plan.block_len[b], segs, torch.device("cpu"))
+                for lo, hi, col in segs:
+                    vals[k0:k1, lo:hi] = t[:, col: col + hi - lo].numpy()
+        assert not np.isnan(vals).any() and np.abs(vals).max() <= 1.0
+        seen.append(vals)
+    assert np.array_equal(seen[0].view(np.uint32), seen[1].view(np.uint32))
+    out = torch.from_numpy(seen[0][0].copy())
+    assert bench._output_checksum(torch, out, M) == bench._output_checksum(torch, out.clone(), M)
