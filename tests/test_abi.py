@@ -112,3 +112,23 @@ def test_c_demo_runs_bit_exact(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches=0" in r.stdout
+
+
+def _declared_arity():
+    """Function name -> number of parameters, from include/fedagg.h (comments stripped)."""
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"(fedagg_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_ctypes_binding_matches_every_declared_arity():
+    """Each ctypes binding takes as many arguments as its C declaration (a signature that drifted,
+    like fedagg_push_execute's landing-tag arguments of ABI 13, would shift every argument after it)."""
+    arity = _declared_arity()
+    assert "fedagg_push_execute" in arity and arity["fedagg_push_execute"] == 23
+    bad = {n: (arity[n], len(_native.SIGNATURES[n][1])) for n in arity
+           if n in _native.SIGNATURES and arity[n] != len(_native.SIGNATURES[n][1])}
+    assert not bad, bad
