@@ -186,10 +186,17 @@ class PushTransport:
         self._programs = ([p] + self._programs)[:4]
         return p
 
-    def execute(self, prog: "PushProgram", stream: int, ws=None, ws_kind: str = "f32") -> None:
+    def raise_errors(self) -> None:
+        """Raise if any rank's wait kernel gave up: that rank went on with inputs that had not
+        landed, so the call's result is wrong.  Read it once the executing stream is synchronised
+        (the root's last wait follows every rank's last step, so its synchronisation covers all
+        ranks' waits); :meth:`execute` also checks it before issuing the next call."""
         bad = self.errors()
         if bad:
-            raise _native.NativeLibraryError(f"push executor: a wait timed out (rank -> counter {bad})")
+            raise _native.NativeLibraryError(f"push executor: a wait timed out (rank -> what it waited for: {bad})")
+
+    def execute(self, prog: "PushProgram", stream: int, ws=None, ws_kind: str = "f32") -> None:
+        self.raise_errors()
         ws_src = ws_dst = None
         ws_bytes = 0
         if ws is not None and self.world > 1:

@@ -1000,7 +1000,16 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
     if not root:
         return None
     flat = out[: layout.M].cpu().numpy()
+    _raise_transport_errors(tr)  # after the copy's synchronisation: a push wait that gave up is an error
     return [a for _, a in layout.unpack(np.array(flat, copy=True))]
+
+
+def _raise_transport_errors(transport) -> None:
+    """A transport's own record of a failed exchange (push.PushTransport: a wait kernel that timed
+    out and let its rank go on without the data), checked once the result is synchronised."""
+    fn = getattr(transport, "raise_errors", None)
+    if fn is not None:
+        fn()
 
 
 def client_sharded_scaffold(parameters_updates, control_variate_updates, server_control_variates, n_samples,
@@ -1072,6 +1081,7 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
         return None
     d = dout[: layout.M].cpu().numpy().copy()
     cc = cout[: layout.M].cpu().numpy().copy()
+    _raise_transport_errors(tr)
     return mism, [a for _, a in layout.unpack(cc)], [a for _, a in layout.unpack(d)]
 
 

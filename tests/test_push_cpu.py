@@ -279,3 +279,25 @@ def test_tag_waits_point_to_earlier_steps():
             assert q != p.rank and t_push < t_wait and v == t_push + 2
             waited.add((q, t_push, p.rank))
     assert waited == written
+
+
+def test_raise_errors_reports_a_timed_out_wait():
+    """A wait kernel that gave up leaves its rank's error word set in the shared page: the root's
+    check after synchronising (sharding._raise_transport_errors) raises instead of returning the
+    numbers computed without the data."""
+    from substrafl_amd import _native
+    from substrafl_amd.push import PushTransport
+    from substrafl_amd.sharding import _raise_transport_errors
+
+    tr = PushTransport.__new__(PushTransport)
+    tr.world = 3
+    tr._page = np.zeros(3 * tr.world, dtype=np.uint64)
+    _raise_transport_errors(tr)  # clean page: nothing to report
+    tr._page[tr.world + 2] = 1 + 0  # rank 2 gave up on rank 0's counter
+    with pytest.raises(_native.NativeLibraryError, match="counter of rank 0"):
+        _raise_transport_errors(tr)
+    tr._page[tr.world + 2] = (1 << 32) + 1 + 1  # ... or on rank 1's landing tag
+    assert tr.errors() == {2: "landing tag of rank 1"}
+    with pytest.raises(_native.NativeLibraryError, match="landing tag of rank 1"):
+        tr.raise_errors()
+    _raise_transport_errors(object())  # transports without a record of their own: no-op
