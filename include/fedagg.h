@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 13
+#define FEDAGG_ABI_VERSION 14
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -182,6 +182,19 @@ int fedagg_fedavg_chain_push_bf16(const uint16_t* const* d_clients, const float*
                                   const float* d_in, float* d_out, void* stream);
 int fedagg_fedavg_chain_bf16(const uint16_t* const* d_clients, const float* h_w, int K, uint64_t M, int seed,
                              float* d_out, void* stream);
+/* The push executor's Scaffold runs (FEDAGG_RUN_SCAFFOLD_PUSH_DELTA / _CV): ONE bucket of a client
+ * block -- phase 0 the K delta rows, phase 1 the K control-variate rows -- d_out = the fp64
+ * accumulator d_in (this rank's slot; NULL: start from +0.0) continued by fl(h_w[k] * x_k) in
+ * client order; finish: phase 0 then multiplies by lr (scaffold.py:293), phase 1 adds d_c
+ * (scaffold.py:262-263).  The arithmetic of fedagg_scaffold_chain_*'s two sums, one bucket at a
+ * time; the stores as fedagg_fedavg_chain_push_* (system scope, acknowledged before the wave
+ * retires).  d_rows / d_in / d_out / d_c 16-B aligned for the vector path. */
+int fedagg_scaffold_chain_push_f32(const float* const* d_rows, const double* h_w, int K, uint64_t M, int phase,
+                                   const float* d_c, double lr, int finish, const double* d_in, double* d_out,
+                                   void* stream);
+int fedagg_scaffold_chain_push_f64(const double* const* d_rows, const double* h_w, int K, uint64_t M, int phase,
+                                   const double* d_c, double lr, int finish, const double* d_in, double* d_out,
+                                   void* stream);
 int fedagg_fedavg_chain_f64(const double* const* d_clients, const double* h_w, int K, uint64_t M, int seed,
                             double* d_out, void* stream);
 int fedagg_fedavg_chain_f16(const uint16_t* const* d_clients, const uint16_t* h_w, int K, uint64_t M, int seed,
@@ -247,7 +260,11 @@ enum { FEDAGG_BF16 = 12 };  /* kind of a run over bf16 buckets (fp32 accumulator
 enum { FEDAGG_RUN_FEDAVG = 0, FEDAGG_RUN_FEDAVG_TILED = 1, FEDAGG_RUN_SCAFFOLD = 2,
        FEDAGG_RUN_FEDAVG_PUSH = 3 /* FedAvg run (f32 / bf16) storing into mapped peer memory (push
                                      executor): acc = the output, acc2 = the input accumulator (NULL:
-                                     seed ? +0.0 : acc) */ };
+                                     seed ? +0.0 : acc) */,
+       FEDAGG_RUN_SCAFFOLD_PUSH_DELTA = 4, /* Scaffold push run (f32 / f64 buckets, fp64 accumulators):
+                                              x = the block's K delta rows, acc / acc2 as
+                                              FEDAGG_RUN_FEDAVG_PUSH; finish: x lr */
+       FEDAGG_RUN_SCAFFOLD_PUSH_CV = 5     /* the same over the K control-variate rows; finish: + c */ };
 typedef struct fedagg_lockstep_run {
   int32_t step;              /* the step it runs at (runs sorted by step)                        */
   int32_t op;                /* FEDAGG_RUN_*                                                     */
@@ -297,7 +314,7 @@ int fedagg_lockstep_execute(fedagg_comm* comm, const fedagg_lockstep_run* runs, 
  * Push executor of the same schedules (substrafl_amd/push.py, DESIGN.md §6 "Push"): no exchange
  * kernels.  Each run's chain kernel writes its accumulator straight into the consumer's slot (or
  * the root's output) through an IPC mapping over xGMI, continuing the input accumulator it reads
- * from this rank's own slot (fedagg_fedavg_chain_push_{f32,bf16}).  Cross-process
+ * from this rank's own slot (fedagg_fedavg_chain_push_{f32,bf16}, fedagg_scaffold_chain_push_*).  Cross-process
  * order: one monotonic progress counter per rank in a node-shared host page; a call publishes
  * base + 1 on entry (the rank's earlier stream work is done: peers may write into its buffers),
  * then before step t a one-lane wait kernel polls the counters the step needs and after it a
@@ -346,22 +363,28 @@ typedef struct fedagg_push_tag {
   int32_t reserved;
   uint64_t* tag;             /* a consumer's landing tag (mapped peer memory): *tag = base + 1   */
 } fedagg_push_tag;
-/* runs: FEDAGG_RUN_FEDAVG / FEDAGG_RUN_FEDAVG_PUSH (acc: a mapped peer address; f32 or bf16) sorted by step;
+typedef struct fedagg_push_copy {
+  void* dst;                 /* the root's output                                                */
+  const void* src;           /* its landing buffer (what other ranks pushed)                     */
+  uint64_t bytes;            /* a multiple of 4                                                  */
+} fedagg_push_copy;
+/* runs: FEDAGG_RUN_FEDAVG / FEDAGG_RUN_FEDAVG_PUSH (acc: a mapped peer address; f32 or bf16) or
+ * FEDAGG_RUN_SCAFFOLD_PUSH_DELTA / _CV (f32 or f64 buckets) sorted by step;
  * waits sorted by step; tags: the landing tags this rank writes, sorted by step (<= 16 a step);
- * ws_src / ws_dst / ws_bytes: the numel == 1 products (fp32) copied to this rank's staging row on
- * the root after step 0's waits (0 bytes: none); ws_stage (root only, else NULL): the nranks
- * staging rows, summed into ws_src after the last waits.  land / out / land_ranges (root only):
- * nranges (element offset, count) pairs of fp32 copied from the landing buffer into the output
- * after the last waits (the finished pieces other ranks pushed).  A step's launches (one per
- * consumer, each writing over its own link) are spread round-robin over `stream` and the `naux`
- * (<= 7) aux streams, forked from and joined back into `stream` around the step.  Asynchronous
- * on `stream`. */
+ * ws_src / ws_dst / ws_bytes: the numel == 1 products (ws_kind FEDAGG_F32 for FedAvg, FEDAGG_F64
+ * for Scaffold) copied to this rank's staging row on the root after step 0's waits (0 bytes:
+ * none); ws_stage (root only, else NULL): the nranks staging rows, summed in rank order into
+ * ws_src after the last waits.  copies (root only): the finished pieces other ranks pushed,
+ * copied from the landing buffers into the outputs after the last waits.  A step's launches (one
+ * per consumer and bucket, each writing over its own link) are spread round-robin over `stream`
+ * and the `naux` (<= 7) aux streams, forked from and joined back into `stream` around the step.
+ * Asynchronous on `stream`. */
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
                         const fedagg_push_tag* tags, int ntags,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
-                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, const void* ws_stage,
-                        const void* land, void* out, const uint64_t* land_ranges, int nranges,
-                        void* const* aux_streams, int naux, void* stream);
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, int ws_kind, const void* ws_stage,
+                        const fedagg_push_copy* copies, int ncopies, void* const* aux_streams, int naux,
+                        void* stream);
 
 /* ---------------------------------------------------------------------------
  * Client-side flat-bucket ops (the producer / consumer of the buckets, SURVEY.md §8(a)

@@ -68,6 +68,10 @@ SIGNATURES = {
     "fedagg_fedavg_chain_push_f32": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void, c_void]),
     "fedagg_fedavg_chain_push_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_void, c_void, c_void]),
     "fedagg_fedavg_chain_bf16": (c_int, [P(c_void), P(ctypes.c_float), c_int, c_u64, c_int, c_void, c_void]),
+    "fedagg_scaffold_chain_push_f32": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_dbl, c_int, c_void,
+                                               c_void, c_void]),
+    "fedagg_scaffold_chain_push_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_dbl, c_int, c_void,
+                                               c_void, c_void]),
     "fedagg_fedavg_chain_f64": (c_int, [P(c_void), P(c_dbl), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_f16": (c_int, [P(c_void), P(ctypes.c_uint16), c_int, c_u64, c_int, c_void, c_void]),
     "fedagg_fedavg_chain_tiled_f32": (c_int, [c_void, P(ctypes.c_float), c_int, c_u64, c_u64, c_int, c_void, c_void]),
@@ -114,8 +118,7 @@ SIGNATURES = {
     "fedagg_device_free": (c_int, [c_void]),
     "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
     "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64,
-                                    c_u64, c_void, c_void, c_u64, c_void, c_void, c_void, c_void, c_int, c_void, c_int,
-                                    c_void]),
+                                    c_u64, c_void, c_void, c_u64, c_int, c_void, c_void, c_int, c_void, c_int, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),
@@ -139,7 +142,7 @@ SIGNATURES = {
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
@@ -155,6 +158,7 @@ FEDAGG_F32 = 1
 FEDAGG_F64 = 2
 FEDAGG_BF16 = 12
 FEDAGG_RUN_FEDAVG, FEDAGG_RUN_FEDAVG_TILED, FEDAGG_RUN_SCAFFOLD, FEDAGG_RUN_FEDAVG_PUSH = 0, 1, 2, 3
+FEDAGG_RUN_SCAFFOLD_PUSH_DELTA, FEDAGG_RUN_SCAFFOLD_PUSH_CV = 4, 5
 
 
 class NativeLibraryError(RuntimeError):

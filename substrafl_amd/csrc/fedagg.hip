@@ -922,18 +922,25 @@ __device__ __forceinline__ void scaffold_phase_add(const ScArgs<TIn, KC>& a, con
 }
 
 // PIPE: the next client group's loads are issued before this group's fp64 products and adds.
-template <typename TIn, int KC, bool NT, int NTS, int N, int SU, int PH, bool PIPE = false>
+// SEPIN (push runs only, scaffold_push_kernel): the running accumulator is read from `in`
+// instead of `out`; every other instantiation compiles exactly as before.
+template <typename TIn, int KC, bool NT, int NTS, int N, int SU, int PH, bool PIPE = false, bool SEPIN = false>
 __device__ __forceinline__ void scaffold_phase(const ScArgs<TIn, KC>& a, const PwArgs& pw, const int K,
                                                const int first, const int last, const TIn* __restrict__ c,
                                                const double lr, const uint64_t* v, double* __restrict__ out,
-                                               bool wave_full, u32x4* lds_wave) {
+                                               bool wave_full, u32x4* lds_wave, const double* in = nullptr) {
 #pragma clang fp contract(off)
   constexpr int L = 16 / sizeof(TIn);
   double acc[N][L];
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
-    for (int j = 0; j < L; ++j) acc[n][j] = first ? 0.0 : out[v[n] * L + j];
+    for (int j = 0; j < L; ++j) {
+      if constexpr (SEPIN)
+        acc[n][j] = first ? 0.0 : in[v[n] * L + j];
+      else
+        acc[n][j] = first ? 0.0 : out[v[n] * L + j];
+    }
   int k = 0;
   if constexpr (PIPE) {
     if (K >= SU) {
@@ -1214,6 +1221,54 @@ __global__ void __launch_bounds__(FA_BLOCK)
     scaffold_bucket_walk<TIn, KC, NT, NTS, VPT, SU, PH, PIPE>(a, pw, K, first, last, c, lr, nvec, M, PH == 0 ? dout : cout,
                                                          blockIdx.x, gridDim.x, lds_wave);
   }
+}
+
+// Push runs of the client-sharded Scaffold schedules (fedagg_scaffold_chain_push_*): ONE bucket
+// of a client block -- PH 0 the delta rows (x lr at the finish), PH 1 the control-variate rows
+// (+ c at the finish) -- continuing the fp64 accumulator `in` (this rank's slot, or the output
+// itself for a later client chunk; first: from +0.0) into `out`, a peer's mapped slot or the
+// root's output, with system-scope write-through stores (st16<3>); every wave waits for their
+// acknowledgements before it retires.  Per-element arithmetic and order: scaffold_bucket_walk's
+// (scaffold.py:262-263, 293).  SEP: the accumulator is read from `in` (a chain's first client
+// chunk continuing a slot); otherwise from `out` (later chunks; `in` unused).
+template <typename TIn, int VPT, int SU, int PH, bool PIPE, bool SEP>
+__global__ void __launch_bounds__(FA_BLOCK)
+    scaffold_push_kernel(const ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a, const int K, const int first, const int last,
+                         const TIn* __restrict__ c, const double lr, const uint64_t nvec, const uint64_t M,
+                         const double* __restrict__ in, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  constexpr int L = 16 / sizeof(TIn);
+  __shared__ u32x4 stage[FA_BLOCK / 64][128];
+  u32x4* lds_wave = stage[threadIdx.x / 64];
+  PwArgs pw;  // chain runs carry no numel == 1 patch (the schedule's products / finish do)
+  pw.n = 0;
+  const uint64_t tile = (uint64_t)VPT * FA_BLOCK;
+  for (uint64_t t = blockIdx.x; t * tile < nvec; t += gridDim.x) {
+    const uint64_t base = t * tile + threadIdx.x;
+    const bool wave_full = (base - (threadIdx.x & 63)) + 63 + (VPT - 1) * FA_BLOCK < nvec;
+    if (base + (VPT - 1) * FA_BLOCK < nvec) {
+      uint64_t v[VPT];
+#pragma unroll
+      for (int n = 0; n < VPT; ++n) v[n] = base + n * FA_BLOCK;
+      scaffold_phase<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, 3, VPT, SU, PH, PIPE, SEP>(a, pw, K, first, last, c, lr, v, out,
+                                                                                  wave_full, lds_wave, in);
+    } else {
+      for (uint64_t v0 = base; v0 < nvec; v0 += FA_BLOCK)
+        scaffold_phase<TIn, FEDAGG_KCHUNK_SCAFFOLD, true, 3, 1, SU, PH, false, SEP>(a, pw, K, first, last, c, lr, &v0,
+                                                                                  out, false, lds_wave, in);
+    }
+  }
+  for (uint64_t i = nvec * L + (uint64_t)blockIdx.x * FA_BLOCK + threadIdx.x; i < M;
+       i += (uint64_t)gridDim.x * FA_BLOCK) {  // scalar remainder
+    double acc = first ? 0.0 : (SEP ? in[i] : out[i]);
+    for (int k = 0; k < K; ++k) {
+      const double p = a.w[k] * (double)(PH == 0 ? a.d[k][i] : a.cv[k][i]);
+      acc = acc + p;
+    }
+    if (last) acc = PH == 0 ? lr * acc : acc + (double)c[i];
+    __hip_atomic_store(out + i, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc0 sc1 stores acknowledged
 }
 
 // ------------------------------------------------------------------------------------
@@ -2810,6 +2865,63 @@ int fedagg_scaffold_chain_f64(const double* const* d_delta, const double* const*
                               double* d_delta_out, double* d_c_out, void* stream) {
   return scaffold_launch<double>(d_delta, d_cv, d_c, h_w, K, M, nullptr, 0, nullptr, lr, d_delta_out, d_c_out,
                                  (hipStream_t)stream, seed != 0, finish != 0);
+}
+// Scaffold push runs: one bucket (phase 0: delta, phase 1: control variate) of a client block,
+// d_in (this rank's fp64 accumulator slot; NULL = from +0.0) continued by the block's K rows into
+// d_out (a peer's mapped slot or the root's output); finish: x lr (phase 0) or + d_c (phase 1).
+// The tiles of the product's one-bucket launches (fp32 8 x 4, fp64 pipelined 4 x 2).
+extern "C++" template <typename TIn>
+int scaffold_push_launch(const TIn* const* d_rows, const double* h_w, int K, uint64_t M, int phase, const TIn* d_c,
+                         double lr, int finish, const double* d_in, double* d_out, hipStream_t s) {
+  if (K <= 0 || !d_rows || !h_w || !d_out || (phase != 0 && phase != 1) || (finish && phase == 1 && !d_c))
+    return fail(FEDAGG_EINVAL, "scaffold_chain_push: invalid argument (K=%lld)", K);
+  if (M == 0) return FEDAGG_OK;
+  bool vec = aligned16(d_out) && (!d_in || aligned16(d_in)) && (!(finish && phase == 1) || aligned16(d_c));
+  for (int k = 0; k < K; ++k) {
+    if (!d_rows[k]) return fail(FEDAGG_EINVAL, "scaffold_chain_push: client pointer %lld is NULL", k);
+    vec = vec && aligned16(d_rows[k]);
+  }
+  constexpr int L = 16 / sizeof(TIn);
+  constexpr int VPT = sizeof(TIn) == 4 ? 8 : 4, SU = sizeof(TIn) == 4 ? 4 : 2;
+  constexpr bool PIPE = sizeof(TIn) == 8;
+  const uint64_t nvec = vec ? M / L : 0;
+  const unsigned grid = grid_for(nvec ? (nvec + VPT - 1) / VPT : M);
+  for (int k0 = 0; k0 < K; k0 += FEDAGG_KCHUNK_SCAFFOLD) {
+    const int kc = (K - k0) < FEDAGG_KCHUNK_SCAFFOLD ? (K - k0) : FEDAGG_KCHUNK_SCAFFOLD;
+    ScArgs<TIn, FEDAGG_KCHUNK_SCAFFOLD> a;
+    memset(&a, 0, sizeof(a));
+    for (int k = 0; k < kc; ++k) {
+      a.d[k] = d_rows[k0 + k];
+      a.cv[k] = d_rows[k0 + k];
+      a.w[k] = h_w[k0 + k];
+    }
+    const int first = k0 == 0 && !d_in, last = (k0 + kc) == K && finish;
+    const bool sep = k0 == 0 && d_in;  // later chunks continue the output itself
+#define SCP(PH, SEP)                                                                                            \
+  hipLaunchKernelGGL((scaffold_push_kernel<TIn, VPT, SU, PH, PIPE, SEP>), dim3(grid), dim3(FA_BLOCK), 0, s, a, kc, \
+                     first, last, d_c, lr, nvec, M, d_in, d_out)
+    if (phase == 0) {
+      if (sep) SCP(0, true);
+      else SCP(0, false);
+    } else {
+      if (sep) SCP(1, true);
+      else SCP(1, false);
+    }
+#undef SCP
+    const int rc = check_launch("scaffold_push_kernel");
+    if (rc) return rc;
+  }
+  return FEDAGG_OK;
+}
+int fedagg_scaffold_chain_push_f32(const float* const* d_rows, const double* h_w, int K, uint64_t M, int phase,
+                                   const float* d_c, double lr, int finish, const double* d_in, double* d_out,
+                                   void* stream) {
+  return scaffold_push_launch<float>(d_rows, h_w, K, M, phase, d_c, lr, finish, d_in, d_out, (hipStream_t)stream);
+}
+int fedagg_scaffold_chain_push_f64(const double* const* d_rows, const double* h_w, int K, uint64_t M, int phase,
+                                   const double* d_c, double lr, int finish, const double* d_in, double* d_out,
+                                   void* stream) {
+  return scaffold_push_launch<double>(d_rows, h_w, K, M, phase, d_c, lr, finish, d_in, d_out, (hipStream_t)stream);
 }
 int fedagg_scaffold_products_f32(const float* const* d_delta, const float* const* d_cv, const double* h_w, int K,
                                  int kbase, int Ktot, const uint64_t* h_idx, int P, double* d_ws, void* stream) {

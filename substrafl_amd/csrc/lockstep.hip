@@ -125,6 +125,20 @@ int run_one(const fedagg_lockstep_run& r, hipStream_t s) {
         return lfail(FEDAGG_EINVAL, "lockstep: push runs are fp32 or bf16 (fp32 accumulators)");
       break;
     }
+    case FEDAGG_RUN_SCAFFOLD_PUSH_DELTA:
+    case FEDAGG_RUN_SCAFFOLD_PUSH_CV: {  // one bucket: x = its K rows; acc = output, acc2 = input
+      const int ph = r.op == FEDAGG_RUN_SCAFFOLD_PUSH_CV;
+      const double* in = r.acc2 ? (const double*)r.acc2 : (r.seed ? nullptr : (const double*)r.acc);
+      if (r.kind == FEDAGG_F32)
+        rc = fedagg_scaffold_chain_push_f32((const float* const*)r.x, (const double*)r.w, r.K, r.n, ph,
+                                            (const float*)r.c, r.lr, r.finish, in, (double*)r.acc, s);
+      else if (r.kind == FEDAGG_F64)
+        rc = fedagg_scaffold_chain_push_f64((const double* const*)r.x, (const double*)r.w, r.K, r.n, ph,
+                                            (const double*)r.c, r.lr, r.finish, in, (double*)r.acc, s);
+      else
+        return lfail(FEDAGG_EINVAL, "lockstep: Scaffold push runs take fp32 or fp64 buckets (fp64 accumulators)");
+      break;
+    }
     case FEDAGG_RUN_FEDAVG_TILED:
       if (r.kind == FEDAGG_F32)
         rc = fedagg_fedavg_chain_tiled_f32((const float*)r.x[0], (const float*)r.w, r.K, r.n, r.tile_vectors,
@@ -230,12 +244,13 @@ __global__ void __launch_bounds__(256) push_copy_kernel(uint32_t* __restrict__ d
 }
 
 // Root: ws[i] = stage[0][i] + ... + stage[G-1][i] in rank order (one owner per column, the
-// others +0.0: exact).
-__global__ void __launch_bounds__(256) push_stage_sum_kernel(float* __restrict__ ws, const float* __restrict__ stage,
-                                                             int G, uint64_t n) {
+// others +0.0: exact).  T: fp32 (FedAvg's products) or fp64 (Scaffold's).
+template <typename T>
+__global__ void __launch_bounds__(256) push_stage_sum_kernel(T* __restrict__ ws, const T* __restrict__ stage, int G,
+                                                             uint64_t n) {
 #pragma clang fp contract(off)
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull) {
-    float a = stage[i];
+    T a = stage[i];
     for (int g = 1; g < G; ++g) a = a + stage[(uint64_t)g * n + i];
     ws[i] = a;
   }
@@ -491,22 +506,27 @@ int fedagg_wall_clock_hz(uint64_t* hz_out) {
 int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg_push_wait* waits, int nwaits,
                         const fedagg_push_tag* tags, int ntags,
                         int nsteps, uint64_t* progress, int rank, int nranks, uint64_t base, uint64_t timeout_ticks,
-                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, const void* ws_stage,
-                        const void* land, void* out, const uint64_t* land_ranges, int nranges,
-                        void* const* aux_streams, int naux, void* stream) {
+                        const void* ws_src, void* ws_dst, uint64_t ws_bytes, int ws_kind, const void* ws_stage,
+                        const fedagg_push_copy* copies, int ncopies, void* const* aux_streams, int naux,
+                        void* stream) {
   if (nruns < 0 || nwaits < 0 || ntags < 0 || nsteps < 0 || (nruns && !runs) || (nwaits && !waits) ||
       (ntags && !tags) || !progress || nranks < 1 ||
       rank < 0 || rank >= nranks || (ws_bytes && (!ws_src || !ws_dst)) || naux < 0 || naux > 7 ||
-      (naux && !aux_streams) || nranges < 0 || (nranges && (!land_ranges || !land || !out)))
+      (naux && !aux_streams) || ncopies < 0 || (ncopies && !copies) ||
+      (ws_bytes && ws_kind != FEDAGG_F32 && ws_kind != FEDAGG_F64) ||
+      (ws_bytes % (ws_kind == FEDAGG_F64 ? 8 : 4)))
     return lfail(FEDAGG_EINVAL, "fedagg_push_execute: invalid argument");
+  for (int i = 0; i < ncopies; ++i)
+    if (!copies[i].dst || !copies[i].src) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: NULL landing copy");
   for (int i = 0; i < nwaits; ++i)
     if (waits[i].rank < 0 || waits[i].rank >= nranks || waits[i].step < 0 || waits[i].step > nsteps ||
         (i && waits[i].step < waits[i - 1].step))
       return lfail(FEDAGG_EINVAL, "fedagg_push_execute: waits out of range or unsorted");
   for (int i = 0; i < nruns; ++i)
-    if ((runs[i].op != FEDAGG_RUN_FEDAVG && runs[i].op != FEDAGG_RUN_FEDAVG_PUSH) || runs[i].step < 0 ||
-        runs[i].step >= nsteps || (i && runs[i].step < runs[i - 1].step))
-      return lfail(FEDAGG_EINVAL, "fedagg_push_execute: runs must be FedAvg row runs sorted by step");
+    if ((runs[i].op != FEDAGG_RUN_FEDAVG && runs[i].op != FEDAGG_RUN_FEDAVG_PUSH &&
+         runs[i].op != FEDAGG_RUN_SCAFFOLD_PUSH_DELTA && runs[i].op != FEDAGG_RUN_SCAFFOLD_PUSH_CV) ||
+        runs[i].step < 0 || runs[i].step >= nsteps || (i && runs[i].step < runs[i - 1].step))
+      return lfail(FEDAGG_EINVAL, "fedagg_push_execute: runs must be row push runs sorted by step");
   for (int i = 0; i < ntags; ++i)
     if (!tags[i].tag || tags[i].step < 0 || tags[i].step >= nsteps || (i && tags[i].step < tags[i - 1].step))
       return lfail(FEDAGG_EINVAL, "fedagg_push_execute: tags out of range or unsorted");
@@ -565,14 +585,17 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   if (ti != ntags || wi != nwaits) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: tags / waits beyond the last step");
   // root, once every rank's last step is in: the finished pieces others pushed, into the output;
   // the numel == 1 staging rows, summed into this rank's workspace
-  for (int i = 0; i < nranges; ++i) {
-    const uint64_t a = land_ranges[2 * i], n = land_ranges[2 * i + 1];
-    if ((rc = push_copy((char*)out + a * 4, (const char*)land + a * 4, n * 4, s))) return rc;
-  }
+  for (int i = 0; i < ncopies; ++i)
+    if ((rc = push_copy(copies[i].dst, copies[i].src, copies[i].bytes, s))) return rc;
   if (ws_stage && ws_bytes) {
-    const uint64_t n = ws_bytes / 4, g = (n + 255) / 256;
-    hipLaunchKernelGGL(push_stage_sum_kernel, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s,
-                       (float*)ws_src, (const float*)ws_stage, nranks, n);
+    const uint64_t n = ws_bytes / (ws_kind == FEDAGG_F64 ? 8 : 4), g = (n + 255) / 256;
+    const dim3 grid((unsigned)(g < 1024 ? g : 1024));
+    if (ws_kind == FEDAGG_F64)
+      hipLaunchKernelGGL(push_stage_sum_kernel<double>, grid, dim3(256), 0, s, (double*)ws_src,
+                         (const double*)ws_stage, nranks, n);
+    else
+      hipLaunchKernelGGL(push_stage_sum_kernel<float>, grid, dim3(256), 0, s, (float*)ws_src, (const float*)ws_stage,
+                         nranks, n);
     if ((rc = hip_check(hipGetLastError(), "push_stage_sum_kernel"))) return rc;
   }
   return FEDAGG_OK;

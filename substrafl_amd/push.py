@@ -33,8 +33,11 @@ number.  Every wait points to a strictly earlier step of another rank, so the sc
 deadlock whatever hardware queues the kernels share.  The numel == 1 products go to a staging row of the
 root per rank (one copy after step 0's waits) and are summed on the root (one owner per column: exact).
 
-Scope: FedAvg over row-layout client blocks of fp32 (the bench's C3 schedule) or bf16 buckets
-(C5; fp32 accumulators); Scaffold and the fp64 / fp16 kinds keep the RCCL executor.  Every rank must be on this node (the counters live in ``/dev/shm``).
+Scope: row-layout client blocks of FedAvg over fp32 (the bench's C3 schedule) or bf16 buckets
+(C5; fp32 accumulators), and of Scaffold over fp32 or fp64 buckets (fp64 accumulators: each run is
+two launches, the delta bucket and the control-variate bucket, ``fedagg_scaffold_chain_push_*``,
+scaffold.py:262-263, 293); FedAvg's fp64 / fp16 kinds keep the RCCL executor.  Every rank must be
+on this node (the counters live in ``/dev/shm``).
 """
 
 from __future__ import annotations
@@ -61,7 +64,12 @@ class _Tag(ctypes.Structure):
     _fields_ = [("step", ctypes.c_int32), ("reserved", ctypes.c_int32), ("tag", ctypes.c_void_p)]
 
 
-assert ctypes.sizeof(_Wait) == 24 and ctypes.sizeof(_Tag) == 16  # include/fedagg.h fedagg_push_wait / _tag
+class _Copy(ctypes.Structure):
+    _fields_ = [("dst", ctypes.c_void_p), ("src", ctypes.c_void_p), ("bytes", ctypes.c_uint64)]
+
+
+# include/fedagg.h fedagg_push_wait / _tag / _copy
+assert ctypes.sizeof(_Wait) == 24 and ctypes.sizeof(_Tag) == 16 and ctypes.sizeof(_Copy) == 24
 
 GPU_MAX_HW_QUEUES = 4  # HIP's hardware queues per process on the boxes (GPU_MAX_HW_QUEUES, HIP's default)
 RCCL_STREAMS = 3  # a live fedagg_comm: its own stream + RCCL's internal device and host streams
@@ -204,7 +212,7 @@ class PushTransport:
             ws_src, ws_dst = ws.data_ptr(), prog.ws_dst(ws_bytes)
         root = self.rank == prog.plan.root and self.world > 1
         stage = prog.stage_u.ptr if root and ws_bytes else None
-        ranges = prog.land_ranges if root else None
+        ncopies = prog.ncopies if root else 0
         # a native RCCL communicator live in this process holds three streams of the hardware queues
         from .rccl import RcclTransport
 
@@ -213,9 +221,9 @@ class PushTransport:
                                             ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
                                             ctypes.byref(prog.tags) if prog.ntags else None, prog.ntags,
                                             prog.nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
-                                            ws_src, ws_dst, ws_bytes, stage,
-                                            prog.land_u.ptr if root else None, prog.out_ptr if root else None,
-                                            ranges, prog.land_ranges_n // 2 if ranges is not None else 0,
+                                            ws_src, ws_dst, ws_bytes,
+                                            _native.FEDAGG_F64 if ws_kind == "f64" else _native.FEDAGG_F32, stage,
+                                            ctypes.byref(prog.copies) if ncopies else None, ncopies,
                                             self._aux_ptrs if naux else None, naux, int(stream)), "fedagg_push_execute")
         self.base += prog.nsteps + 1
 
@@ -268,30 +276,39 @@ class _Uncached:
 class PushProgram:
     """One rank's schedule compiled for the push executor: its runs split by consumer with
     every output address resolved (a mapped peer slot, the root's output, or its own output),
-    and the waits of every step.  Built collectively (every rank at once)."""
+    and the waits of every step.  Built collectively (every rank at once).  FedAvg: one fp32
+    accumulator per element; Scaffold: two fp64 accumulators (``which`` 0: the delta sum into
+    ``outs[0]``, 1: the control-variate sum into ``outs[1]``), each run two launches."""
 
     def __init__(self, tr: PushTransport, plan: lockstep.RankPlan, blocks, accs, outs, kind: str, scaffold: bool,
                  c=None, lr: float = 1.0):
         import torch
 
-        if scaffold or kind not in ("f32", "bf16"):
-            raise ValueError("push executor: FedAvg over fp32 / bf16 buckets (fp32 accumulators); the other "
-                             "kinds take the RCCL executor")
+        if (kind not in ("f32", "f64")) if scaffold else (kind not in ("f32", "bf16")):
+            raise ValueError("push executor: FedAvg over fp32 / bf16 buckets (fp32 accumulators) or Scaffold over "
+                             "fp32 / fp64 buckets; the other kinds take the RCCL executor")
         for sh in blocks.values():
-            if not isinstance(getattr(sh, "rows", None), torch.Tensor):
+            rows = (sh.delta, sh.cv) if scaffold else (getattr(sh, "rows", None),)
+            if not all(isinstance(r, torch.Tensor) for r in rows):
                 raise ValueError("push executor: row-layout client blocks only")
         self.plan, self.blocks, self.accs, self.outs, self.kind = plan, blocks, accs, outs, kind
+        self.scaffold, self.c, self.lr = scaffold, c, float(lr)
         self._keep: list = []
         G, me, root = plan.world, plan.rank, plan.root
-        out = outs[0]
-        esz = out.element_size()
+        nacc = 2 if scaffold else 1
+        outs = list(outs[:nacc])
+        out_n = int(outs[0].numel())
+        esz = outs[0].element_size()
+        if any(o.numel() != out_n or o.element_size() != esz for o in outs):
+            raise ValueError("push executor: the Scaffold outputs must have the same size and dtype")
         # What peers write lands in memory no L2 caches (a consumer's L2 could still hold the lines
         # a slot had four steps earlier): the slots, and a landing copy of the output's index space
-        # (the last block's input on every rank, the finished pieces on the root).  The caller's
-        # slots are not used; the root copies the landed finished pieces into its output.
+        # (the last block's input on every rank, the finished pieces on the root), one per
+        # accumulator.  The caller's slots are not used; the root copies the landed finished pieces
+        # into its outputs.
         se = max(1, plan.slot_elems)
-        self.slots_u = _Uncached(tr.lib, lockstep.SLOTS * se * esz)
-        self.land_u = _Uncached(tr.lib, out.numel() * esz)
+        self.slots_u = _Uncached(tr.lib, nacc * lockstep.SLOTS * se * esz)
+        self.land_u = _Uncached(tr.lib, nacc * out_n * esz)
         # landing tags: word q * n_steps + t = the generation of the call whose step-t pushes of
         # rank q into this rank landed (written by q after its data, over the same link)
         self.tags_u = _Uncached(tr.lib, max(1, G * plan.n_steps) * 8)
@@ -299,39 +316,43 @@ class PushProgram:
         mine = {"slots": tr.ipc_info(self.slots_u.ptr) if G > 1 else None,
                 "land": tr.ipc_info(self.land_u.ptr) if G > 1 else None,
                 "tags": tr.ipc_info(self.tags_u.ptr) if G > 1 else None,
+                "out_n": out_n,
                 "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
                          if o.kind == "recv"]}
         infos = tr.all_gather(mine) if G > 1 else [mine]
 
-        def local(loc) -> int:
+        def offset(rank: int, loc, which: int) -> int:
+            """Byte offset of ``loc`` in ``rank``'s landing buffer ("out") or slots."""
             where, slot, off = loc
             if where == "out":
-                return self.land_u.ptr + off * esz
-            return self.slots_u.ptr + (slot * se + off) * esz
+                return (which * infos[rank]["out_n"] + off) * esz
+            return ((which * lockstep.SLOTS + slot) * se + off) * esz
 
-        def at(rank: int, loc) -> int:
-            where, slot, off = loc
+        def local(loc, which: int) -> int:
+            return (self.land_u.ptr if loc[0] == "out" else self.slots_u.ptr) + offset(me, loc, which)
+
+        def at(rank: int, loc, which: int) -> int:
             if rank == me:
-                # the root's own finished pieces: straight into the caller's output
-                return out.data_ptr() + off * esz if where == "out" and rank == root else local(loc)
-            if where == "out":
-                return tr.remote(infos[rank]["land"]) + off * esz
-            return tr.remote(infos[rank]["slots"]) + (slot * se + off) * esz
+                # the root's own finished pieces: straight into the caller's outputs
+                return outs[which].data_ptr() + loc[2] * esz if loc[0] == "out" and rank == root else local(loc, which)
+            return tr.remote(infos[rank]["land" if loc[0] == "out" else "slots"]) + offset(rank, loc, which)
 
         specs, wait_list = push_schedule(plan, [info["recv"] for info in infos])
-        # the output ranges other ranks finish (landed on the root, copied into its output)
+        # the output ranges other ranks finish (landed on the root, copied into its outputs)
         own = sorted((p.dst[2], p.dst[2] + p.n) for p in specs if p.dst_rank == me and p.dst[0] == "out")
-        self._land_ranges, a = [], 0
-        for lo, hi in own + [(out.numel(), out.numel())]:
+        ranges, a = [], 0
+        for lo, hi in own + [(out_n, out_n)]:
             if lo > a:
-                self._land_ranges.append((a, lo))
+                ranges.append((a, lo))
             a = max(a, hi)
-        flat = [v for a, b in self._land_ranges for v in (a, b - a)]
-        self.land_ranges = (ctypes.c_uint64 * max(1, len(flat)))(*flat)
-        self.land_ranges_n = len(flat)
-        self.out_ptr = out.data_ptr()
-        runs = [self._run(p.step, blocks[p.block], p.col, p.n, at(p.dst_rank, p.dst),
-                          local(p.src) if p.src is not None else 0) for p in specs]
+        copies = [_Copy(outs[w].data_ptr() + lo * esz, self.land_u.ptr + (w * out_n + lo) * esz, (hi - lo) * esz)
+                  for lo, hi in ranges for w in range(nacc)]
+        self.land_ranges = ranges
+        self.ncopies = len(copies)
+        self.copies = (_Copy * max(1, len(copies)))(*copies)
+        runs = [rec for p in specs for rec in self._runs(p, [at(p.dst_rank, p.dst, w) for w in range(nacc)],
+                                                          [local(p.src, w) if p.src is not None else 0
+                                                           for w in range(nacc)])]
         n_steps = plan.n_steps
         outgoing = push_outgoing(plan, specs)
         everyone = tr.all_gather(outgoing) if G > 1 else [outgoing]
@@ -365,28 +386,42 @@ class PushProgram:
             return self.stage_u.ptr + self.plan.rank * ws_bytes
         return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
 
-    def _run(self, t: int, sh, col: int, n: int, dst: int, src: int, remote: bool = False) -> _Run:
-        """One launch: the block's clients (``sh.rows`` at column ``col``, n elements) continuing
-        the fp32 accumulator at ``src`` (0: from +0.0) into ``dst``.  Every launch is a push run
-        (``FEDAGG_RUN_FEDAVG_PUSH``: input accumulator separate from the output, system-scope
-        write-through stores) -- also the root's own final runs into its output, which keeps one
-        arithmetic path for every piece."""
+    def _runs(self, p: "PushRun", dst: List[int], src: List[int]) -> List[_Run]:
+        """The launches of one push run: the block's clients (rows at column ``p.col``, ``p.n``
+        elements) continuing the accumulator at ``src`` (0: from +0.0) into ``dst`` -- FedAvg one
+        launch (``FEDAGG_RUN_FEDAVG_PUSH``), Scaffold two (``FEDAGG_RUN_SCAFFOLD_PUSH_DELTA`` then
+        ``_CV``; a finished piece applies lr / adds c).  Every launch is a push run (input
+        accumulator separate from the output, system-scope write-through stores) -- also the
+        root's own final runs into its outputs, which keeps one arithmetic path for every piece."""
+        sh = self.blocks[p.block]
+        if not self.scaffold:
+            kind = _native.FEDAGG_BF16 if self.kind == "bf16" else _native.FEDAGG_F32
+            return [self._run(p, _native.FEDAGG_RUN_FEDAVG_PUSH, kind, sh.rows, np.asarray(sh.w, np.float32),
+                              ctypes.c_float, dst[0], src[0])]
+        kind = _native.FEDAGG_F32 if self.kind == "f32" else _native.FEDAGG_F64
+        w = np.asarray(sh.w, np.float64)
+        recs = [self._run(p, _native.FEDAGG_RUN_SCAFFOLD_PUSH_DELTA, kind, sh.delta, w, ctypes.c_double, dst[0], src[0]),
+                self._run(p, _native.FEDAGG_RUN_SCAFFOLD_PUSH_CV, kind, sh.cv, w, ctypes.c_double, dst[1], src[1])]
+        for rec in recs:
+            rec.finish, rec.lr = int(p.final), self.lr
+            if p.final:  # c of the piece's global elements (scaffold.py:262-263)
+                rec.c = self.c.data_ptr() + p.dst[2] * self.c.element_size()
+        return recs
+
+    def _run(self, p: "PushRun", op: int, kind: int, rows, w: np.ndarray, wtype, dst: int, src: int) -> _Run:
         rec = _Run()
-        kind = _native.FEDAGG_BF16 if self.kind == "bf16" else _native.FEDAGG_F32
-        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = t, _native.FEDAGG_RUN_FEDAVG_PUSH, kind, 0 if src else 1, 0, n
-        rows = sh.rows
+        rec.step, rec.op, rec.kind, rec.seed, rec.finish, rec.n = p.step, op, kind, 0 if src else 1, 0, p.n
         base, step, esz = rows.data_ptr(), rows.stride(0) * rows.element_size(), rows.element_size()
-        ptrs = [base + k * step + col * esz for k in range(rows.shape[0])]
-        w = [float(v) for v in np.asarray(sh.w, np.float32)]
-        rec.K = len(ptrs)
-        arr = _native.ptr_array(ptrs)
-        warr = (ctypes.c_float * len(w))(*w)
+        arr = _native.ptr_array([base + k * step + p.col * esz for k in range(rows.shape[0])])
+        warr = (wtype * len(w))(*[float(v) for v in w])
         self._keep += [arr, warr]
+        rec.K = rows.shape[0]
         rec.x, rec.w, rec.acc, rec.acc2 = ctypes.addressof(arr), ctypes.addressof(warr), dst, src or None
         return rec
 
     def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:
-        return (plan is self.plan and blocks is self.blocks and kind == self.kind and not scaffold
+        return (plan is self.plan and blocks is self.blocks and kind == self.kind and scaffold == self.scaffold
+                and c is self.c and float(lr) == self.lr
                 and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
 
 

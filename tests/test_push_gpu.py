@@ -31,6 +31,12 @@ CASES = [
     (4, 9, (0.75, 0.25), True, "default", "bf16"),
 ]
 CASES = [c if len(c) == 6 else c + ("f32",) for c in CASES]
+CASES = [c + ("fedavg",) for c in CASES] + [
+    # Scaffold: two fp64 accumulators per element, each run two launches (delta, control variate)
+    (3, 7, (0.5, 0.3, 0.2), False, "default", "f32", "scaffold"),
+    (4, 9, (0.75, 0.25), True, "default", "f32", "scaffold"),
+    (2, 5, (1.0,), False, "wide", "f64", "scaffold"),
+]
 
 
 def _port() -> int:
@@ -41,7 +47,7 @@ def _port() -> int:
     return p
 
 
-def _worker(rank, G, K, rounds, relay, shapes_name, kind, port, q):
+def _worker(rank, G, K, rounds, relay, shapes_name, kind, strategy, port, q):
     import faulthandler
 
     faulthandler.dump_traceback_later(100, exit=True)
@@ -53,53 +59,84 @@ def _worker(rank, G, K, rounds, relay, shapes_name, kind, port, q):
     import torch
     import torch.distributed as dist
 
-    from oracle import fedavg_reference_structure
-    from substrafl_amd.engine import fedavg_weights
+    from oracle import fedavg_reference_structure, scaffold_reference_structure
+    from substrafl_amd.engine import fedavg_weights, scaffold_weights
     from substrafl_amd.layout import BucketLayout
     from substrafl_amd.push import PushTransport
-    from substrafl_amd.sharding import (SLOTS, FedAvgShard, GpuShardOps, client_blocks, lockstep_fedavg,
-                                        relay_plan, striped_plan)
+    from substrafl_amd.sharding import (SLOTS, FedAvgShard, GpuShardOps, ScaffoldShard, client_blocks,
+                                        lockstep_fedavg, lockstep_scaffold, relay_plan, striped_plan)
     from test_client_shard_gpu import SHAPES, _data, _rows
 
     try:
         dist.init_process_group("gloo", rank=rank, world_size=G, timeout=timedelta(seconds=90))
         torch.cuda.set_device(0)
         shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else [(1,), (130001,), (1, 1), (77777,)]
+        scaffold = strategy == "scaffold"
+        npdt = np.float64 if kind == "f64" else np.float32
         pus, ns = _data(K, seed=17 + G, shapes=shapes)
-        pus = [[a.astype(np.float32) for a in c] for c in pus]
+        pus = [[a.astype(npdt) for a in c] for c in pus]
         if kind == "bf16":  # bf16-representable values: the reference runs on the exact upcast
             pus = [[(a.view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32) for a in c] for c in pus]
-        layout = BucketLayout(range(len(shapes)), shapes, np.float32)
+        rng = np.random.default_rng(5 + G)
+        cvs = [[rng.standard_normal(a.shape).astype(npdt) for a in pu] for pu in pus]
+        c = [rng.standard_normal(a.shape).astype(npdt) for a in pus[0]]
+        lr = 0.7
+        layout = BucketLayout(range(len(shapes)), shapes, npdt)
         plan = relay_plan(layout.M, G, rank, 4096) if relay else striped_plan(layout.M, G, rank, None, rounds)
-        blocks = {}
-        for b, segs in plan.blocks.items():
+        tdt = torch.bfloat16 if kind == "bf16" else (torch.float64 if kind == "f64" else torch.float32)
+
+        def packed(lists, b, segs):
             k0, k1 = client_blocks(K, G)[b]
-            tdt = torch.bfloat16 if kind == "bf16" else torch.float32
-            full = _rows(torch, pus[k0:k1], layout, dtype=np.float32, tdtype=tdt)
+            full = _rows(torch, lists[k0:k1], layout, dtype=npdt, tdtype=tdt)
             t = torch.zeros((k1 - k0, plan.block_len[b]), dtype=tdt, device="cuda")
             for lo, hi, col in segs:
                 t[:, col: col + hi - lo] = full[:, lo:hi]
-            blocks[b] = FedAvgShard(kind, t, fedavg_weights(ns, kind)[k0:k1], k0, K, plan.block_len[b],
-                                    np.zeros(0, np.uint64))
+            return t
+
+        blocks = {}
+        for b, segs in plan.blocks.items():
+            k0, k1 = client_blocks(K, G)[b]
+            if scaffold:
+                blocks[b] = ScaffoldShard(kind, packed(pus, b, segs), packed(cvs, b, segs), None,
+                                          scaffold_weights(ns)[k0:k1], k0, K, plan.block_len[b], lr,
+                                          np.zeros(0, np.uint64))
+            else:
+                blocks[b] = FedAvgShard(kind, packed(pus, b, segs), fedavg_weights(ns, kind)[k0:k1], k0, K,
+                                        plan.block_len[b], np.zeros(0, np.uint64))
         tr = PushTransport(timeout_s=30)
         bad, calls = [], 0
-        ref = fedavg_reference_structure(pus, ns) if rank == plan.root else None
-        out = torch.empty((layout.ld,), dtype=torch.float32, device="cuda")
-        slots = torch.empty(SLOTS * max(1, plan.slot_elems), dtype=torch.float32, device="cuda")
+        ref = None
+        if rank == plan.root:
+            if scaffold:
+                rc, ra = scaffold_reference_structure(pus, cvs, c, ns, lr)
+                ref = ra + rc  # the averaged update, then the new server control variate
+            else:
+                ref = fedavg_reference_structure(pus, ns)
+        odt = torch.float64 if scaffold else torch.float32
+        outs = [torch.empty((layout.ld,), dtype=odt, device="cuda") for _ in range(2 if scaffold else 1)]
+        slots = torch.empty((2 if scaffold else 1) * SLOTS * max(1, plan.slot_elems), dtype=odt, device="cuda")
+        full_c = _rows(torch, [c], layout, dtype=npdt)[0] if scaffold else None
+        lay_out = BucketLayout(range(len(shapes)), shapes, np.float64 if scaffold else np.float32)
+        ubits = np.uint64 if scaffold else np.uint32
         for _ in range(3):  # the cached program, and counters that keep climbing across calls
-            out.fill_(float("nan"))
-            is_root = lockstep_fedavg(plan, blocks, out, tr, GpuShardOps(), layout.pairwise_idx, slots=slots)
+            for o in outs:
+                o.fill_(float("nan"))
+            if scaffold:
+                is_root = lockstep_scaffold(plan, blocks, outs[0], outs[1], tr, GpuShardOps(), layout.pairwise_idx,
+                                            full_c, lr, slots=slots)
+            else:
+                is_root = lockstep_fedavg(plan, blocks, outs[0], tr, GpuShardOps(), layout.pairwise_idx, slots=slots)
             torch.cuda.synchronize()
             calls += 1
             if is_root:
-                got = [a for _, a in layout.unpack(out[: layout.M].cpu().numpy())]
-                nb = sum(int(np.count_nonzero(g.view(np.uint32) != r.view(np.uint32))) for g, r in zip(got, ref))
+                got = [a for o in outs for _, a in lay_out.unpack(o[: layout.M].cpu().numpy())]
+                nb = sum(int(np.count_nonzero(g.view(ubits) != r.view(ubits))) for g, r in zip(got, ref))
                 if nb and os.environ.get("PUSH_DEBUG"):
                     print(f"[push debug] call {calls}: " + "; ".join(
-                        f"layer {i} {g.shape}: idx {np.nonzero(g.reshape(-1).view(np.uint32) != r.reshape(-1).view(np.uint32))[0][:4]} "
-                        f"got {g.reshape(-1)[np.nonzero(g.reshape(-1).view(np.uint32) != r.reshape(-1).view(np.uint32))[0][:2]]} "
-                        f"ref {r.reshape(-1)[np.nonzero(g.reshape(-1).view(np.uint32) != r.reshape(-1).view(np.uint32))[0][:2]]}"
-                        for i, (g, r) in enumerate(zip(got, ref)) if np.any(g.view(np.uint32) != r.view(np.uint32))),
+                        f"layer {i} {g.shape}: idx {np.nonzero(g.reshape(-1).view(ubits) != r.reshape(-1).view(ubits))[0][:4]} "
+                        f"got {g.reshape(-1)[np.nonzero(g.reshape(-1).view(ubits) != r.reshape(-1).view(ubits))[0][:2]]} "
+                        f"ref {r.reshape(-1)[np.nonzero(g.reshape(-1).view(ubits) != r.reshape(-1).view(ubits))[0][:2]]}"
+                        for i, (g, r) in enumerate(zip(got, ref)) if np.any(g.view(ubits) != r.view(ubits))),
                         file=sys.stderr, flush=True)
                 bad.append(nb)
         errs = tr.errors()
@@ -117,14 +154,15 @@ def _worker(rank, G, K, rounds, relay, shapes_name, kind, port, q):
         q.put((rank, None, None, 0, 0, traceback.format_exc()[-2000:]))
 
 
-@pytest.mark.parametrize("G,K,rounds,relay,shapes,kind", CASES)
-def test_push_executor_processes_bit_exact(G, K, rounds, relay, shapes, kind):
+@pytest.mark.parametrize("G,K,rounds,relay,shapes,kind,strategy", CASES)
+def test_push_executor_processes_bit_exact(G, K, rounds, relay, shapes, kind, strategy):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, G, K, rounds, relay, shapes, kind, port, q)) for r in range(G)]
+    procs = [ctx.Process(target=_worker, args=(r, G, K, rounds, relay, shapes, kind, strategy, port, q))
+             for r in range(G)]
     for p in procs:
         p.start()
     res = {}
@@ -177,3 +215,47 @@ def test_push_run_continues_its_input_accumulator(kind, K, M):
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
     assert torch.equal(out0.view(torch.int32), ref0.view(torch.int32))
+
+
+@pytest.mark.parametrize("kind", ["f32", "f64"])
+@pytest.mark.parametrize("K,M,finish", [(9, 4096 * 3 + 5, True), (70, 1_000_003, False), (5, 77_777, True)])
+def test_scaffold_push_run_continues_its_input_accumulator(kind, K, M, finish):
+    """fedagg_scaffold_chain_push_{f32,f64} (one process): per bucket, d_in continued by the block's
+    rows into a separate d_out (x lr / + c at the finish), bit-identical to fedagg_scaffold_chain_*
+    continuing the same two accumulators in place; d_in NULL is the chain from +0.0.  Also across
+    client chunks (K > 64) and element remainders."""
+    import ctypes
+
+    import torch
+
+    from substrafl_amd import _native
+    from substrafl_amd.engine import scaffold_weights
+
+    lib = _native.load()
+    torch.manual_seed(K + M)
+    tdt = torch.float64 if kind == "f64" else torch.float32
+    delta = torch.randn((K, M), dtype=tdt, device="cuda")
+    cv = torch.randn((K, M), dtype=tdt, device="cuda")
+    c = torch.randn(M, dtype=tdt, device="cuda")
+    lr = 0.3
+    w = (ctypes.c_double * K)(*[float(v) for v in scaffold_weights(list(range(3, K + 3)))])
+    dp = _native.ptr_array([delta[k].data_ptr() for k in range(K)])
+    cp = _native.ptr_array([cv[k].data_ptr() for k in range(K)])
+    chain = getattr(lib, f"fedagg_scaffold_chain_{kind}")
+    push = getattr(lib, f"fedagg_scaffold_chain_push_{kind}")
+    s = torch.cuda.current_stream().cuda_stream
+    for seed in (False, True):
+        d_in = torch.randn(M, dtype=torch.float64, device="cuda")
+        c_in = torch.randn(M, dtype=torch.float64, device="cuda")
+        ref_d, ref_c = d_in.clone(), c_in.clone()
+        _native.check(chain(dp, cp, c.data_ptr(), w, K, M, int(seed), int(finish), lr, ref_d.data_ptr(),
+                            ref_c.data_ptr(), s), "chain")
+        got = []
+        for ph, (rows, acc_in) in enumerate(((dp, d_in), (cp, c_in))):
+            out = torch.full((M,), float("nan"), dtype=torch.float64, device="cuda")
+            _native.check(push(rows, w, K, M, ph, c.data_ptr(), lr, int(finish), None if seed else acc_in.data_ptr(),
+                               out.data_ptr(), s), "chain_push")
+            got.append(out)
+        torch.cuda.synchronize()
+        assert torch.equal(got[0].view(torch.int64), ref_d.view(torch.int64)), (seed, "delta")
+        assert torch.equal(got[1].view(torch.int64), ref_c.view(torch.int64)), (seed, "control variate")

@@ -52,9 +52,8 @@ def test_execute_caps_aux_streams_while_a_communicator_lives(monkeypatch):
         nruns = nwaits = ntags = 0
         runs = waits = tags = None
         nsteps = 3
-        land_ranges = None
-        land_ranges_n = 0
-        out_ptr = 0
+        ncopies = 0
+        copies = None
         stage_u = None
 
         class plan:

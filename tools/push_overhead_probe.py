@@ -71,7 +71,7 @@ def main():
                                             len(waits) if with_order else 0,
                                             ctypes.byref(T) if with_order and tags else None,
                                             len(tags) if with_order else 0, S, dev.value, 0, G, base[0],
-                                            1 << 40, None, None, 0, None, None, None, None, 0, None, 0,
+                                            1 << 40, None, None, 0, _native.FEDAGG_F32, None, None, 0, None, 0,
                                             stream.cuda_stream), "fedagg_push_execute")
         base[0] += S + 1
 

@@ -105,7 +105,7 @@ def _worker(rank, G, K, mode, calls, port, q):
                                                ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
                                                ctypes.byref(prog.tags) if prog.ntags else None, prog.ntags,
                                                prog.nsteps, tr._dev, tr.rank, tr.world, tr.base, tr._timeout,
-                                               ws_src, ws_dst, ws_bytes, None, None, None, None, 0,
+                                               ws_src, ws_dst, ws_bytes, _native.FEDAGG_F32, None, None, 0,
                                                tr._aux_ptrs, len(tr._aux), int(stream)), "fedagg_push_execute")
                 tr.base += prog.nsteps + 1
                 if not root:
@@ -120,9 +120,8 @@ def _worker(rank, G, K, mode, calls, port, q):
                                "fedagg_flat_gather_f32")
 
                 out_t = prog.outs[0]
-                for i in range(prog.land_ranges_n // 2):  # the landed pieces into the output (round 3: land_to_out)
-                    a, n = int(prog.land_ranges[2 * i]), int(prog.land_ranges[2 * i + 1])
-                    copy(out_t.data_ptr() + a * 4, prog.land_u.ptr + a * 4, n * 4)
+                for lo, hi in prog.land_ranges:  # the landed pieces into the output (round 3: land_to_out)
+                    copy(out_t.data_ptr() + lo * 4, prog.land_u.ptr + lo * 4, (hi - lo) * 4)
                 if not ws_bytes:
                     return
                 if not hasattr(prog, "stage_t"):
