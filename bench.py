@@ -90,7 +90,7 @@ def parse():
     ap.add_argument("--executor", default="native", choices=["native", "torch", "push", "gather"],
                     help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip), the "
                          "Python schedule over torch.distributed's RCCL process group, or the push executor "
-                         "(substrafl_amd/push.py: chain kernels storing into IPC-mapped peer slots, fp32 rows); "
+                         "(substrafl_amd/push.py: chain kernels storing into IPC-mapped peer slots, FedAvg fp32 / bf16 and Scaffold fp32 / fp64 rows); "
                          "gather (N > 1 line's param_range_strong_gather leg: the workload's M split over the ranks, "
                          "the result slices gathered to rank 0 over RCCL inside the timed step)")
     ap.add_argument("--client-shard-child", action="store_true", help=argparse.SUPPRESS)
@@ -946,9 +946,9 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     parity = _client_shard_spot_check(ctx, K, M, layout, n_samples, kind, scaffold, held, outs, c, tvs) \
         if variants else None
     full_compare = None
-    if variants and getattr(tr, "push", False) and world > 1 and lockstep_mode and not scaffold:
+    if variants and getattr(tr, "push", False) and world > 1 and lockstep_mode:
         # every element (numel == 1 ones included) against a second, independent transport
-        full_compare = _push_vs_native(ctx, plan, blocks, outs["out"], ops, pw, ws, slots, M)
+        full_compare = _push_vs_native(ctx, plan, blocks, outs, ops, pw, ws, slots, M, c if scaffold else None)
     # the whole output, summarised: every weak leg holds the same (client, element) values (rows),
     # so their checksums must be equal (client_shard_legs compares them across the legs)
     comparable = not scaffold and lockstep_mode and tvs == {0}
@@ -1029,32 +1029,40 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     return res
 
 
-def _push_vs_native(ctx, plan, blocks, out, ops, pw, ws, slots, M):
+def _push_vs_native(ctx, plan, blocks, outs, ops, pw, ws, slots, M, c=None):
     """The push leg's whole output against the native RCCL executor's on the same plan and client
     blocks: two independent transports (stores into IPC-mapped peer memory against RCCL's P2P),
-    one expected bit pattern -- both follow the reference's client order (fed_avg.py:221-222).
-    Collective; returns the comparison on the root (every element, numel == 1 ones included)."""
+    one expected bit pattern -- both follow the reference's client order (fed_avg.py:221-222;
+    Scaffold, ``c`` given: both sums, scaffold.py:262-263, 293).  Collective; returns the
+    comparison on the root (every element, numel == 1 ones included)."""
     torch = ctx.torch
     from substrafl_amd.rccl import RcclTransport
-    from substrafl_amd.sharding import lockstep_fedavg
+    from substrafl_amd.sharding import lockstep_fedavg, lockstep_scaffold
 
     if torch.cuda.device_count() < ctx.world:
         return {"skipped": f"{ctx.world} ranks share {torch.cuda.device_count()} GPU(s): RCCL refuses duplicate GPUs"}
-    push_out = out.clone()
+    names = ["dout", "cout"] if c is not None else ["out"]
+    push_out = {k: outs[k].clone() for k in names}
     nat = RcclTransport()  # created after the push leg's timing: never live beside a push step
     try:
         count = nat.comm_count()
-        out.fill_(float("nan"))
-        lockstep_fedavg(plan, blocks, out, nat, ops, pw, ws=ws, slots=slots)
+        for k in names:
+            outs[k].fill_(float("nan"))
+        if c is not None:
+            lockstep_scaffold(plan, blocks, outs["dout"], outs["cout"], nat, ops, pw, c, 1.0, ws=ws, slots=slots)
+        else:
+            lockstep_fedavg(plan, blocks, outs["out"], nat, ops, pw, ws=ws, slots=slots)
         torch.cuda.synchronize(ctx.device)
         res = None
         if plan.rank == plan.root:
-            a, b = push_out[:M].view(torch.int32), out[:M].view(torch.int32)
+            bits = torch.int64 if c is not None else torch.int32
+            mism = sum(int((push_out[k][:M].view(bits) != outs[k][:M].view(bits)).sum().item()) for k in names)
             res = {"against": "native RCCL executor (csrc/lockstep.hip), same plan and client blocks",
-                   "elements": M, "mismatches": int((a != b).sum().item()), "rccl_comm_count": count}
+                   "elements": M * len(names), "mismatches": mism, "rccl_comm_count": count}
     finally:
         nat.close()
-        out.copy_(push_out)
+        for k in names:
+            outs[k].copy_(push_out[k])
     return res
 
 

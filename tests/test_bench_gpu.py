@@ -82,6 +82,17 @@ def test_shared_gpu_ranks_push_leg_forced():
     assert "skipped" in push["full_compare"]
 
 
+def test_shared_gpu_ranks_scaffold_push_leg_forced():
+    """The same for Scaffold (c4): the push leg runs its two fp64 accumulators per element
+    (delta and control-variate launches per run), spot-checked bit-exact, no wait error."""
+    line = _bench("--workload", "c4", "--gpus", "2", "--client-shard", "force", "--multi-device-leg", "off",
+                  "--steps", "3", "--warmup", "1", "--client-shard-steps", "3", "--no-cpu-baseline", timeout=400)
+    push = line["client_shard_push"]
+    assert "error" not in push, push
+    assert push["parity"]["mismatches"] == 0 and push["wait_errors"] == {}
+    assert "skipped" in push["full_compare"]
+
+
 def test_strong_scaling_two_ranks_shared_gpu():
     line = _bench("--workload", "c2", "--scaling", "strong", "--gpus", "2", "--steps", "3", "--warmup", "1",
                   "--no-cpu-baseline")
