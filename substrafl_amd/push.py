@@ -316,7 +316,7 @@ class PushProgram:
         mine = {"slots": tr.ipc_info(self.slots_u.ptr) if G > 1 else None,
                 "land": tr.ipc_info(self.land_u.ptr) if G > 1 else None,
                 "tags": tr.ipc_info(self.tags_u.ptr) if G > 1 else None,
-                "out_n": out_n,
+                "out_n": out_n, "se": se,
                 "recv": [(g, o.peer, o.key, o.buf, o.n) for g, ops in enumerate(plan.groups) for o in ops
                          if o.kind == "recv"]}
         infos = tr.all_gather(mine) if G > 1 else [mine]
@@ -326,7 +326,7 @@ class PushProgram:
             where, slot, off = loc
             if where == "out":
                 return (which * infos[rank]["out_n"] + off) * esz
-            return ((which * lockstep.SLOTS + slot) * se + off) * esz
+            return ((which * lockstep.SLOTS + slot) * infos[rank]["se"] + off) * esz
 
         def local(loc, which: int) -> int:
             return (self.land_u.ptr if loc[0] == "out" else self.slots_u.ptr) + offset(me, loc, which)

@@ -36,7 +36,12 @@ CASES = [c + ("fedavg",) for c in CASES] + [
     (3, 7, (0.5, 0.3, 0.2), False, "default", "f32", "scaffold"),
     (4, 9, (0.75, 0.25), True, "default", "f32", "scaffold"),
     (2, 5, (1.0,), False, "wide", "f64", "scaffold"),
+    # ragged: the ranks' slot sizes differ (root 512, the others 1024 elements per slot), so a
+    # producer must address a consumer's slots with the CONSUMER's slot size
+    (4, 9, (0.5, 0.3, 0.2), False, "ragged", "f32", "fedavg"),
+    (4, 6, (0.5, 0.3, 0.2), False, "ragged", "f32", "scaffold"),
 ]
+SHAPE_SETS = {"wide": [(1,), (130001,), (1, 1), (77777,)], "ragged": [(4097,), (1,), (1, 1)]}
 
 
 def _port() -> int:
@@ -70,7 +75,7 @@ def _worker(rank, G, K, rounds, relay, shapes_name, kind, strategy, port, q):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=G, timeout=timedelta(seconds=90))
         torch.cuda.set_device(0)
-        shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else [(1,), (130001,), (1, 1), (77777,)]
+        shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else SHAPE_SETS[shapes_name]
         scaffold = strategy == "scaffold"
         npdt = np.float64 if kind == "f64" else np.float32
         pus, ns = _data(K, seed=17 + G, shapes=shapes)
