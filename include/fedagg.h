@@ -513,6 +513,12 @@ int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, 
 int fedagg_session_activate(fedagg_session* s);
 /* number of visible GPUs (0 when none or on error) */
 int fedagg_device_count(void);
+/* the calling thread's current HIP device, and setting it: the session calls bind their device
+ * to the calling thread, so the engine's entry points restore the caller's device on return
+ * (engine.serialized) -- a multi-device aggregation must not leave the caller's later work (its
+ * training, in simulate_experiment) on the last GPU it drove */
+int fedagg_device_get(int* device_out);
+int fedagg_device_set(int device);
 /* hipMemGetInfo of `device`: free and total HBM bytes (sizing of out-of-core shards). */
 int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes);
 /* Copy `bytes` from HBM into (pageable) host memory; returns when the data is in h_dst. */

@@ -135,6 +135,8 @@ SIGNATURES = {
     "fedagg_session_event_elapsed": (c_int, [c_void, c_int, c_int, P(ctypes.c_float)]),
     "fedagg_session_activate": (c_int, [c_void]),
     "fedagg_device_count": (c_int, []),
+    "fedagg_device_get": (c_int, [P(c_int)]),
+    "fedagg_device_set": (c_int, [c_int]),
     "fedagg_device_memory": (c_int, [c_int, P(c_u64), P(c_u64)]),
     "fedagg_session_fetch": (c_int, [c_void, c_void, c_void, c_u64]),
     "fedagg_session_memset": (c_int, [c_void, c_void, c_int, c_u64]),

@@ -491,6 +491,17 @@ int fedagg_device_count(void) {
   return n;
 }
 
+int fedagg_device_get(int* device_out) {
+  if (!device_out) return FEDAGG_EINVAL;
+  HIP_TRY(hipGetDevice(device_out));
+  return FEDAGG_OK;
+}
+
+int fedagg_device_set(int device) {
+  HIP_TRY(hipSetDevice(device));
+  return FEDAGG_OK;
+}
+
 int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes) {
   if (!free_bytes || !total_bytes) return FEDAGG_EINVAL;
   HIP_TRY(hipSetDevice(device));

@@ -340,16 +340,25 @@ def direct_rows(rows: List[List[np.ndarray]], dt: np.dtype, M: int) -> Optional[
 
 def serialized(method):
     """Run an engine call under the locks of the engine's devices (``runtime.device_lock``), taken
-    in device order, so concurrent callers never share a session's buffers mid-call."""
+    in device order, so concurrent callers never share a session's buffers mid-call; the calling
+    thread's current HIP device is restored on return (the session calls bind their own device to
+    the thread, and the caller's later work -- its training, in simulate_experiment -- must stay
+    on the GPU it chose)."""
 
     @functools.wraps(method)
     def wrapper(self, *args, **kwargs):
         locks = [runtime.device_lock(d) for d in sorted(set(self.lock_devices()))]
         for lk in locks:
             lk.acquire()
+        lib = _native.load()
+        dev = ctypes.c_int(-1)
+        if lib.fedagg_device_get(ctypes.byref(dev)) != 0:
+            dev.value = -1
         try:
             return method(self, *args, **kwargs)
         finally:
+            if dev.value >= 0:
+                lib.fedagg_device_set(dev.value)
             for lk in reversed(locks):
                 lk.release()
 

@@ -155,7 +155,7 @@ def test_cpu_threaded_variant_is_labelled():
     pus = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(5)]
     from oracle import fedavg_reference_structure
 
-    res = bench._cpu_threaded(fedavg_reference_structure, pus, [3, 1, 4, 1, 5], 1000, 3)
+    res = bench._cpu_threaded(fedavg_reference_structure, pus, [3, 1, 4, 1, 5], 10**9, 3)  # nominal bytes: value > 0 at any speed
     assert "not the reference" in res["kind"] and 1 <= res["cores"] <= 3 and res["value"] > 0
 
 
