@@ -219,3 +219,24 @@ def test_push_program_addresses(G, K, M, relay, rounds, rings, scaffold, kind):
     rows = sorted(progs[r][0].ws_row for r in range(G))
     assert all(b - a >= 3 * K * 8 for a, b in zip(rows, rows[1:]))
 
+
+
+def _random_cases(n, seed=20241018):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        G = int(rng.integers(2, 9))
+        relay = bool(rng.random() < 0.3)
+        rounds = [(1.0,), (0.75, 0.25), (0.5, 0.3, 0.2), (0.4, 0.3, 0.2, 0.1)][int(rng.integers(0, 4))]
+        rings = None if rng.random() < 0.7 else int(rng.integers(1, 5))
+        scaffold = bool(rng.random() < 0.5)
+        kind = ("f32", "f64")[int(rng.integers(0, 2))] if scaffold else ("f32", "bf16")[int(rng.integers(0, 2))]
+        out.append((G, G + int(rng.integers(0, 9)), int(rng.integers(1_000, 120_000)), relay, rounds, rings,
+                    scaffold, kind))
+    return out
+
+
+@pytest.mark.parametrize("G,K,M,relay,rounds,rings,scaffold,kind", _random_cases(24))
+def test_push_program_addresses_random_plans(G, K, M, relay, rounds, rings, scaffold, kind):
+    """The same checks over seeded random plans: ranks, clients, sizes, rounds, ring counts."""
+    test_push_program_addresses(G, K, M, relay, rounds, rings, scaffold, kind)
