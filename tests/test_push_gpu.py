@@ -44,6 +44,32 @@ CASES = [c + ("fedavg",) for c in CASES] + [
 SHAPE_SETS = {"wide": [(1,), (130001,), (1, 1), (77777,)], "ragged": [(4097,), (1,), (1, 1)]}
 
 
+def _random_cases(n, seed=31):
+    """Seeded random schedules (2-4 rank processes share the one GPU): plan, sizes, strategy, kind."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        G = int(rng.integers(2, 5))
+        scaffold = i % 2 == 1
+        kind = ("f32", "f64")[int(rng.integers(0, 2))] if scaffold else ("f32", "bf16")[int(rng.integers(0, 2))]
+        rounds = [(1.0,), (0.75, 0.25), (0.5, 0.3, 0.2)][int(rng.integers(0, 3))]
+        out.append((G, G + int(rng.integers(0, 6)), rounds, bool(rng.random() < 0.3), f"rand{int(rng.integers(1 << 20))}",
+                    kind, "scaffold" if scaffold else "fedavg"))
+    return out
+
+
+def _shapes(name):
+    if name in SHAPE_SETS:
+        return SHAPE_SETS[name]
+    rng = np.random.default_rng(int(name[4:]))  # "rand<seed>": ragged layers around numel == 1 ones
+    shapes = [(int(rng.integers(1, 40_000)),) for _ in range(int(rng.integers(1, 4)))] + [(1,), (1, 1)]
+    rng.shuffle(shapes)
+    return shapes
+
+
+CASES += _random_cases(6)
+
+
 def _port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -75,7 +101,7 @@ def _worker(rank, G, K, rounds, relay, shapes_name, kind, strategy, port, q):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=G, timeout=timedelta(seconds=90))
         torch.cuda.set_device(0)
-        shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else SHAPE_SETS[shapes_name]
+        shapes = SHAPES + [(5000,), (1,)] if shapes_name == "default" else _shapes(shapes_name)
         scaffold = strategy == "scaffold"
         npdt = np.float64 if kind == "f64" else np.float32
         pus, ns = _data(K, seed=17 + G, shapes=shapes)
