@@ -41,7 +41,8 @@ CASES = [c + ("fedavg",) for c in CASES] + [
     (4, 9, (0.5, 0.3, 0.2), False, "ragged", "f32", "fedavg"),
     (4, 6, (0.5, 0.3, 0.2), False, "ragged", "f32", "scaffold"),
 ]
-SHAPE_SETS = {"wide": [(1,), (130001,), (1, 1), (77777,)], "ragged": [(4097,), (1,), (1, 1)]}
+SHAPE_SETS = {"wide": [(1,), (130001,), (1, 1), (77777,)], "ragged": [(4097,), (1,), (1, 1)],
+              "c4": [(24_999_998,), (1,), (1, 1)]}  # BASELINE's C4 bucket: 25M parameters
 
 
 def _random_cases(n, seed=31):
@@ -68,6 +69,7 @@ def _shapes(name):
 
 
 CASES += _random_cases(6)
+CASES.append((2, 16, (1.0,), False, "c4", "f32", "scaffold"))  # C4 (16 x 25M) over two rank processes
 
 
 def _port() -> int:
