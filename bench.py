@@ -87,6 +87,9 @@ def parse():
                     help="client-shard striped: also time these round splits (';'-separated, e.g. "
                          "'1.0;0.75,0.25') over the same communicator")
     ap.add_argument("--chunk", type=int, default=2 << 20, help="relay: elements per pipelined chunk")
+    ap.add_argument("--gather-chunks", type=int, default=4,
+                    help="gather leg: the pipelined variant cuts each rank's slice into this many chunks, "
+                         "each gathered to rank 0 while the next is reduced (0: no pipelined variant)")
     ap.add_argument("--executor", default="native", choices=["native", "torch", "push", "gather"],
                     help="client-shard relay / striped: the native RCCL executor (csrc/lockstep.hip), the "
                          "Python schedule over torch.distributed's RCCL process group, or the push executor "
@@ -1142,10 +1145,16 @@ def measure_param_range_gather(args, ctx, t1_ms=None):
     if world > 1:
         dist.all_gather_object(sums, (mine, mism))
     elapsed, kern_ms, gather_ms = ctx.max_over_ranks([elapsed, kern_ms, gather_ms])
+    got = [int(full[r * chunk: r * chunk + (b - a)].view(torch.int32).to(torch.int64).sum().item()) if b > a else 0
+           for r, (a, b) in enumerate(bounds)] if rank == 0 else None
+    pipe = None
+    if args.gather_chunks > 0:  # collective: every rank runs it (an error is reported, never raised)
+        try:
+            pipe = _gather_pipelined(args, ctx, x, n_samples, pw_local, n, chunk, send, full, bounds, steps, warm)
+        except Exception as e:  # noqa: BLE001 -- the variant never costs the leg
+            pipe = {"error": f"{type(e).__name__}: {e}"[:400]}
     if rank != 0:
         return {}
-    got = [int(full[r * chunk: r * chunk + (b - a)].view(torch.int32).to(torch.int64).sum().item()) if b > a else 0
-           for r, (a, b) in enumerate(bounds)]
     ms = elapsed / steps * 1e3
     bytes_job = K * M * 4 + M * 4
     res = {
@@ -1170,7 +1179,82 @@ def measure_param_range_gather(args, ctx, t1_ms=None):
         res["single_gpu_ms"] = round(t1_ms, 5)
         res["speedup"] = round(t1_ms / ms, 4) if ms > 0 else None
         res["strong_efficiency"] = round(t1_ms / (world * ms), 4) if ms > 0 else None
+    if pipe is not None:
+        res["pipelined"] = pipe
+        if t1_ms and pipe.get("ms_per_step"):
+            pipe["speedup"] = round(t1_ms / pipe["ms_per_step"], 4)
+            pipe["strong_efficiency"] = round(t1_ms / (world * pipe["ms_per_step"]), 4)
     return res
+
+
+def _gather_cuts(chunk: int, n_chunks: int):
+    """The pipelined gather's chunks of a rank's (padded) slice: ``n_chunks`` pieces of equal,
+    SHARD_ALIGN-aligned length (the last one shorter), the same on every rank."""
+    from substrafl_amd.lockstep import SHARD_ALIGN
+
+    sub = max(SHARD_ALIGN, -(-(-(-chunk // max(1, int(n_chunks)))) // SHARD_ALIGN) * SHARD_ALIGN)
+    return [(a, min(chunk, a + sub)) for a in range(0, chunk, sub)], sub
+
+
+def _gather_pipelined(args, ctx, x, n_samples, pw_local, n, chunk, send, full, bounds, steps, warm):
+    """The gather leg's pipelined variant: this rank's slice cut into ``--gather-chunks`` chunks;
+    chunk c is reduced on the compute stream and gathered to rank 0 (RCCL, issued from a second
+    stream after the chunk's event) while chunk c + 1 is reduced -- the kernel's HBM reads and the
+    gather's xGMI traffic overlap instead of adding up.  The same elements and kernel arithmetic
+    (parameter-range chunks of the single-GPU kernel, bit-exact); rank 0's gathered slices are
+    checked against every rank's own by checksum.  Collective."""
+    torch, world, rank, device, dist = ctx.torch, ctx.world, ctx.rank, ctx.device, ctx.dist
+    from substrafl_amd.engine import FedAvgPlan, fedavg_weights
+
+    cuts, sub = _gather_cuts(chunk, args.gather_chunks)
+    w = fedavg_weights(n_samples, "f32")
+    plans = []
+    for a, b in cuts:
+        m = max(0, min(b, n) - a)
+        if m:
+            pw = pw_local.astype(np.int64)
+            pwc = (pw[(pw >= a) & (pw < a + m)] - a).astype(np.uint64)
+            ptrs = [x[k].data_ptr() + a * 4 for k in range(x.shape[0])]
+            plans.append(FedAvgPlan("f32", ptrs, w, m, send[a:b], pwc))
+        else:
+            plans.append(None)
+    glists = [[full[r * chunk + a: r * chunk + b] for r in range(world)] if rank == 0 else None for a, b in cuts]
+    stream, comm = ctx.stream, torch.cuda.Stream(device=device)
+    evs = [torch.cuda.Event() for _ in cuts]
+
+    def step():
+        works = []
+        for c, (a, b) in enumerate(cuts):
+            if plans[c] is not None:
+                plans[c].launch(stream)
+            if world > 1:
+                evs[c].record(stream)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(evs[c])
+                    works.append(dist.gather(send[a:b], gather_list=glists[c], dst=0, async_op=True))
+        for wk in works:
+            if wk is not None:
+                wk.wait()
+
+    elapsed, _ev = _timed(ctx, step, steps, warm)
+    send.zero_()
+    if full is not None:
+        full.fill_(float("nan"))
+    step()
+    torch.cuda.synchronize(device)
+    mine = int(send[:n].view(torch.int32).to(torch.int64).sum().item()) if n else 0
+    sums = [mine] * world
+    if world > 1:
+        dist.all_gather_object(sums, mine)
+    (elapsed,) = ctx.max_over_ranks([elapsed])
+    if rank != 0:
+        return {}
+    got = [int(full[r * chunk: r * chunk + (b - a)].view(torch.int32).to(torch.int64).sum().item()) if b > a else 0
+           for r, (a, b) in enumerate(bounds)]
+    return {"chunks": len(cuts), "elements_per_chunk": sub, "ms_per_step": round(elapsed / steps * 1e3, 5),
+            "gathered_slice_checksum_mismatches": int(sum(1 for r in range(world) if got[r] != sums[r])),
+            "issue": "chunk kernel on the compute stream; its gather (async, NCCL backend) from a second stream "
+                     "after the chunk's event"}
 
 
 def p2p_probe(torch, dist, rank, world, device, barrier, max_over_ranks, ring_mib=256, peers_mib=64, iters=5):
@@ -1676,6 +1760,12 @@ def _rehearse_gather(world, rank):
     mine = int(send[: hi - lo].view(torch.int32).to(torch.int64).sum().item())
     sums = [None] * world
     dist.all_gather_object(sums, mine)
+    # the pipelined variant's chunked gathers into views of the same buffer
+    full2 = torch.full((world * chunk,), float("nan"), dtype=torch.float32) if rank == 0 else None
+    cuts, _sub = _gather_cuts(chunk, 4)
+    for a, b in cuts:
+        dist.gather(send[a:b], gather_list=[full2[r * chunk + a: r * chunk + b] for r in range(world)]
+                    if rank == 0 else None, dst=0)
     if rank != 0:
         return None
     ref = np.zeros(M, np.float32)
@@ -1692,6 +1782,8 @@ def _rehearse_gather(world, rank):
                gather_bytes_into_rank0=(world - 1) * chunk * 4,
                parity={"mismatches": int(np.sum(full[:M].numpy().view(np.uint32) != ref.view(np.uint32))),
                        "gathered_slice_checksum_mismatches": int(sum(1 for r in range(world) if got[r] != sums[r]))})
+    res["pipelined"] = {"chunks": len(cuts), "rehearsal": True,
+                        "mismatches_vs_whole_gather": int(torch.sum(full2.view(torch.int32) != full.view(torch.int32)))}
     return res
 
 

@@ -161,3 +161,6 @@ def test_n_gt_1_legs_rehearsed_on_one_gpu():
     assert "error" not in g, g
     assert g["parity"] == {"sampled_per_rank": 1024, "mismatches": 0, "gathered_slice_checksum_mismatches": 0}
     assert g["kernel_ms"] > 0 and g["speedup"] > 0 and g["params_per_gpu"] >= 25_000_000
+    pipe = g["pipelined"]  # chunked kernels (no gather at one rank), same result
+    assert "error" not in pipe and pipe["chunks"] == 4 and pipe["gathered_slice_checksum_mismatches"] == 0
+    assert pipe["ms_per_step"] > 0 and pipe["speedup"] > 0

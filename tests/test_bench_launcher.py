@@ -64,6 +64,8 @@ def test_plain_gpus_2_launches_two_ranks():
     assert g["parity"] == {"mismatches": 0, "gathered_slice_checksum_mismatches": 0}
     for k in ("ms_per_step", "GBps", "kernel_ms", "gather_ms", "speedup", "strong_efficiency"):
         assert k in g
+    # its pipelined variant gathers chunk by chunk into views of the same buffer: the same result
+    assert g["pipelined"]["chunks"] > 1 and g["pipelined"]["mismatches_vs_whole_gather"] == 0
 
 
 def test_single_gpu_line_keeps_its_workload_name():
