@@ -91,6 +91,11 @@ def report(lines) -> list:
                     flags.append(f"N={n} {key}: ncclCommCount {leg['rccl_comm_count']} != {n}")
             if key == "param_range_strong_gather":
                 parts.append(f"gather {leg.get('gather_ms')} ms")
+                pipe = leg.get("pipelined") or {}
+                parts.append(f"pipelined {pipe.get('ms_per_step')} ms/step speedup {pipe.get('speedup')}"
+                             if "error" not in pipe else f"pipelined ERROR {str(pipe['error'])[:120]}")
+                if pipe.get("gathered_slice_checksum_mismatches"):
+                    flags.append(f"N={n} {key}: pipelined gather slices differ")
             if isinstance(leg.get("xgmi_p2p"), dict):
                 parts.append(f"xgmi {json.dumps(leg['xgmi_p2p'])[:200]}")
             print(f"  {key}: " + ", ".join(parts))
