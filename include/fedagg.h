@@ -27,6 +27,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* 1 when building the tuning library (__graft_entry__.build(tuning=True)); the product is 0 */
+#ifndef FEDAGG_TUNING
+#define FEDAGG_TUNING 0
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -346,9 +351,12 @@ int fedagg_host_unmap(void* host);
  * buffers, written by peers, read by this GPU's kernels without stale cache lines */
 int fedagg_device_alloc_uncached(uint64_t bytes, void** out);
 int fedagg_device_free(void* p);
-/* device-to-device runtime copy on `stream` (the same HIP runtime as the caller's streams); tools
- * only (tools/push_tail_probe.py): no product path uses it, and none reads peer-written memory with it */
+#if FEDAGG_TUNING
+/* FEDAGG_TUNING build only (the product library does not export it): device-to-device runtime
+ * copy on `stream` (the same HIP runtime as the caller's streams), for tools/push_tail_probe.py.
+ * No product path uses it, and none reads peer-written memory with it. */
 int fedagg_copy_async(void* dst, const void* src, uint64_t bytes, void* stream);
+#endif
 /* wall-clock ticks per second of the device timer the wait kernels use */
 int fedagg_wall_clock_hz(uint64_t* hz_out);
 typedef struct fedagg_push_wait {

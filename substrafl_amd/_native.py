@@ -116,7 +116,6 @@ SIGNATURES = {
     "fedagg_wall_clock_hz": (c_int, [P(c_u64)]),
     "fedagg_device_alloc_uncached": (c_int, [c_u64, P(c_void)]),
     "fedagg_device_free": (c_int, [c_void]),
-    "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
     "fedagg_push_execute": (c_int, [c_void, c_int, c_void, c_int, c_void, c_int, c_int, c_void, c_int, c_int, c_u64,
                                     c_u64, c_void, c_void, c_u64, c_int, c_void, c_void, c_int, c_void, c_int, c_void]),
     "fedagg_session_create": (c_void, [c_int]),
@@ -142,6 +141,12 @@ SIGNATURES = {
     "fedagg_session_memset": (c_int, [c_void, c_void, c_int, c_u64]),
     "fedagg_session_sync": (c_int, [c_void]),
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
+}
+
+# entry points only a FEDAGG_TUNING build exports (include/fedagg.h "#if FEDAGG_TUNING"): bound
+# when the loaded library is one, absent from the product library
+TUNING_SIGNATURES = {
+    "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
 }
 
 ABI_VERSION = 14
@@ -184,7 +189,10 @@ def load() -> ctypes.CDLL:
         lib = ctypes.CDLL(str(LIB_PATH))
     except OSError as e:  # pragma: no cover - depends on the box
         raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
-    for name, (res, args) in SIGNATURES.items():
+    sigs = dict(SIGNATURES)
+    if lib.fedagg_tuning_build():
+        sigs.update(TUNING_SIGNATURES)
+    for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -274,11 +274,12 @@ def zeros_like_parameters(model: torch.nn.Module, with_batch_norm_parameters: bo
         return [torch.zeros_like(p).to(device) for p in params]
 
 
-def export_numpy(tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
+def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True) -> List[np.ndarray]:
     """``[p.cpu().detach().numpy() for p in ...]`` (torch_fed_avg_algo.py:227-230) with ONE D2H copy
-    when the tensors are views of one flat bucket; the arrays returned are then
+    when the tensors are views of one flat bucket.  With ``wire`` the arrays returned are
     :class:`wire.BucketArray` layers of one host buffer -- they pickle as that one buffer, and the
-    aggregator stages the client as a single segment."""
+    aggregator stages the client as a single segment; without it they are plain ``np.ndarray``
+    views of that buffer, which any process unpickles (no ``substrafl_amd`` import needed)."""
     flat = flat_bucket(list(tensors))
     if flat is None or not flat.is_cuda:
         return [t.cpu().detach().numpy() for t in tensors]
@@ -289,5 +290,28 @@ def export_numpy(tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
                                        "export")  # bf16 raises, as .numpy()
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
     runtime.session(flat.device.index).fetch(flat.data_ptr(), host)
-    return bucket_views(host, [tuple(t.shape) for t in tensors])
+    shapes = [tuple(t.shape) for t in tensors]
+    if wire:
+        return bucket_views(host, shapes)
+    out, off = [], 0
+    for shp in shapes:
+        n = int(np.prod(shp, dtype=np.int64)) if len(shp) else 1
+        out.append(host[off : off + n].reshape(shp))
+        off += n
+    return out
+
+
+def to_device(arrays: Sequence[np.ndarray], device) -> List[torch.Tensor]:
+    """``[torch.from_numpy(x).to(device) for x in arrays]`` (torch_scaffold_algo.py:397,404-406):
+    on a ROCm device, when the arrays share one fp32 or fp64 dtype, ONE host->device copy into a
+    flat bucket, returned as per-layer views (so the flat kernels take the bucket as is)."""
+    arrays = list(arrays)
+    d = torch.device(device)
+    if d.type == "cuda" and arrays and all(isinstance(a, np.ndarray) for a in arrays):
+        flat = _device_flat(arrays, d)
+        if flat is not None:
+            shapes = [a.shape for a in arrays]
+            return [v.view(s) for v, s in zip(torch.split(flat, [int(np.prod(s, dtype=np.int64)) for s in shapes]),
+                                               shapes)]
+    return [torch.from_numpy(x).to(d) for x in arrays]
 

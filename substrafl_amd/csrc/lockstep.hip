@@ -487,11 +487,13 @@ int fedagg_device_alloc_uncached(uint64_t bytes, void** out) {
 
 int fedagg_device_free(void* p) { return p ? hip_check(hipFree(p), "hipFree") : 0; }
 
+#if FEDAGG_TUNING
 int fedagg_copy_async(void* dst, const void* src, uint64_t bytes, void* stream) {
   if (!bytes) return FEDAGG_OK;
   if (!dst || !src) return lfail(FEDAGG_EINVAL, "fedagg_copy_async: NULL argument");
   return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream), "hipMemcpyAsync");
 }
+#endif
 
 int fedagg_wall_clock_hz(uint64_t* hz_out) {
   if (!hz_out) return lfail(FEDAGG_EINVAL, "fedagg_wall_clock_hz: NULL output");

@@ -36,6 +36,7 @@ from typing import Optional
 
 import numpy as np
 
+from .algorithms.accelerate import accelerate_algo  # noqa: F401  (the client half)
 from .engine import Devices, engine_for
 from .strategies.fed_avg import check_same_shapes, weighted_average
 from .strategies.scaffold import Scaffold as _MirrorScaffold
@@ -44,8 +45,10 @@ from .strategies.strategy import Strategy as _MirrorStrategy
 
 def _reference_modules(strategy_cls):
     """The reference package the class comes from (``substrafl``): its strategies, schemas,
-    ``remote`` decorator and exceptions."""
-    pkg = strategy_cls.__module__.split(".")[0]
+    ``remote`` decorator and exceptions.  Found from the first class in the MRO that lives in a
+    ``<pkg>.strategies`` module, so a user subclass defined anywhere (``__main__``) works."""
+    mods = [b.__module__ for b in getattr(strategy_cls, "__mro__", ())]
+    pkg = next((m.split(".")[0] for m in mods if ".strategies" in m), strategy_cls.__module__.split(".")[0])
     return (importlib.import_module(f"{pkg}.strategies"), importlib.import_module(f"{pkg}.strategies.schemas"),
             importlib.import_module(f"{pkg}.remote").remote, importlib.import_module(f"{pkg}.exceptions"))
 

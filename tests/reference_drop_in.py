@@ -161,6 +161,25 @@ def main():
     out["linear_scaffold"] = {"final": perf, "reference_final": meta["linear_scaffold"]["final_performance"],
                               "engine_calls": engine.calls["scaffold"]}
 
+    # the client half: accelerate_algo over the reference's own algorithm classes (the user
+    # subclasses the accelerated class), both halves accelerated in one simulate_experiment
+    AccFedAvgAlgo, AccScaffoldAlgo = integ.accelerate_algo(TorchFedAvgAlgo), integ.accelerate_algo(TorchScaffoldAlgo)
+    assert issubclass(AccFedAvgAlgo, TorchFedAvgAlgo) and issubclass(AccScaffoldAlgo, TorchScaffoldAlgo)
+    calls0 = dict(engine.calls)
+    perf, strat_algo = run(AccFedAvg, AccFedAvgAlgo)
+    out["linear_fedavg_accelerate_algo"] = {
+        "final": perf, "reference_final": meta["linear_fedavg"]["final_performance"],
+        "engine_calls": engine.calls["fedavg"] - calls0["fedavg"],
+        "train_is_accelerated": type(strat_algo.algo).train.__qualname__.startswith("_fedavg_train")}
+    perf, strat_algo = run(AccScaffold, AccScaffoldAlgo)
+    out["linear_scaffold_accelerate_algo"] = {
+        "final": perf, "reference_final": meta["linear_scaffold"]["final_performance"],
+        "engine_calls": engine.calls["scaffold"] - calls0["scaffold"],
+        "train_is_accelerated": type(strat_algo.algo).train.__qualname__.startswith("_scaffold_train")}
+    # the algo's RemoteDataStruct carries the generated class (and its train) by value too
+    blob = cloudpickle.dumps(type(strat_algo.algo))
+    out["algo_class_by_value"] = b"_scaffold_train.<locals>.train" in blob
+
     # @remote: without _skip the call is a RemoteOperation naming the generated class, which
     # cloudpickle carries by value (the task process re-creates it from the RemoteStruct)
     states = [FedAvgSharedState(n_samples=n, parameters_update=[np.full((3,), float(n), np.float32)])

@@ -3,3 +3,11 @@
 
 class EmptySharedStatesError(Exception):
     """No shared state to aggregate."""
+
+
+class TorchScaffoldAlgoParametersUpdateError(Exception):
+    """The per-step Scaffold hook was not called once per update."""
+
+
+class IndexGeneratorUpdateError(Exception):
+    """The index generator was not drawn num_updates times."""

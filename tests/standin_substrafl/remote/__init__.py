@@ -22,3 +22,24 @@ def remote(method):
         return RemoteOperation(type(self), method.__name__, dict(method_parameters), shared_states)
 
     return wrapper
+
+
+@dataclass
+class RemoteDataOperation:
+    cls: type
+    method_name: str
+    data_samples: object = None
+    shared_state: object = None
+
+
+def remote_data(method):
+    """The train-side convention (decorators.py ``remote_data``): ``_skip=True`` runs
+    ``method(data_from_opener=..., shared_state=...)``, otherwise a record for the compute plan."""
+
+    @functools.wraps(method)
+    def wrapper(self, data_samples=None, shared_state=None, *, _skip: bool = False, **method_parameters):
+        if _skip:
+            return method(self=self, shared_state=shared_state, **method_parameters)
+        return RemoteDataOperation(type(self), method.__name__, data_samples, shared_state)
+
+    return wrapper

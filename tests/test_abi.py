@@ -12,8 +12,12 @@ from substrafl_amd import _native
 HEADER = Path(__file__).resolve().parents[1] / "include" / "fedagg.h"
 
 
-def declared_functions():
+def declared_functions(tuning: bool = False):
+    """The functions include/fedagg.h declares for the product library (``tuning``: the
+    ``#if FEDAGG_TUNING`` block's instead)."""
     text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    blocks = re.findall(r"^#if FEDAGG_TUNING\n(.*?)^#endif", text, flags=re.S | re.M)
+    text = "".join(blocks) if tuning else re.sub(r"^#if FEDAGG_TUNING\n.*?^#endif", "", text, flags=re.S | re.M)
     names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fedagg_[a-z0-9_]+)\s*\(", text, flags=re.M)
     return sorted(set(names))
 
@@ -30,6 +34,17 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     # and the ctypes binding covers exactly the declared set
     assert sorted(_native.SIGNATURES) == declared_functions()
+
+
+def test_product_library_does_not_export_tuning_entry_points():
+    """Experiment-only entry points (VERDICT r04 "Next 7": the runtime copy round 3 suspected in
+    the relay failure) live in the FEDAGG_TUNING build only."""
+    tuning = declared_functions(tuning=True)
+    assert tuning == ["fedagg_copy_async"] == sorted(_native.TUNING_SIGNATURES)
+    lib = ctypes.CDLL(str(_native.LIB_PATH))
+    assert lib.fedagg_tuning_build() == 0
+    for name in tuning:
+        assert not hasattr(lib, name), name
 
 
 def test_abi_version_and_invalid_arguments():

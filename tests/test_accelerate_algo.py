@@ -1,0 +1,252 @@
+"""``accelerate_algo``: the client half of the drop-in (VERDICT r04 "Next 1"; SURVEY.md §8(a) rows
+a5-a7, §8(f) rows 1 and 3).
+
+The reference's ``TorchFedAvgAlgo.train`` / ``TorchScaffoldAlgo.train``
+(torch_fed_avg_algo.py:154-230, torch_scaffold_algo.py:256-268,338-482) are driven here through the
+builder-written stand-in classes of ``tests/standin_substrafl`` (the reference's module paths and
+``train`` sequence in plain per-layer torch ops; the reference itself never travels to the GPU
+box).  A federated run -- two clients, three rounds, BatchNorm statistics in the bucket or not --
+goes twice from the same seed:
+
+* reference pipeline: the stand-in algorithm, aggregated by the oracle (the reference's NumPy
+  arithmetic restated, pinned by the golden vectors);
+* accelerated pipeline: ``accelerate_algo(stand-in)``, aggregated by ``accelerate(stand-in
+  strategy)`` on libfedagg;
+
+and every exported update, control variate and model state must match to the last bit.  On the
+GPU the accelerated ``train`` runs its weight moves on the flat-bucket kernels; a control run of
+the reference pipeline against itself checks that the training itself is deterministic first.
+The same runs on the CPU (``disable_gpu``) take the reference's torch loops and run in
+``-m "not gpu"``; the container test ``tests/test_integration_reference.py`` runs
+``accelerate_algo`` over the real reference classes under ``simulate_experiment``.
+"""
+
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+import standin_substrafl.strategies as ss
+from standin_substrafl.algorithms.pytorch import TorchFedAvgAlgo, TorchScaffoldAlgo
+from standin_substrafl.exceptions import TorchScaffoldAlgoParametersUpdateError
+from standin_substrafl.index_generator import NpIndexGenerator
+from standin_substrafl.remote import RemoteDataOperation
+from standin_substrafl.strategies import schemas as sch
+
+from oracle import fedavg_explicit, scaffold_explicit
+
+ROUNDS = 3
+
+
+class XYDataset(torch.utils.data.Dataset):
+    def __init__(self, data_from_opener, is_inference=False):
+        self.x, self.y = data_from_opener
+        self.is_inference = is_inference
+
+    def __getitem__(self, i):
+        return (torch.from_numpy(self.x[i]), torch.from_numpy(self.y[i]))
+
+    def __len__(self):
+        return len(self.x)
+
+
+def _model(seed):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(6, 24), torch.nn.BatchNorm1d(24), torch.nn.ReLU(),
+                               torch.nn.Linear(24, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
+
+
+def _data(n, seed):
+    r = np.random.default_rng(seed)
+    x = r.standard_normal((n, 6)).astype(np.float32)
+    y = (x @ r.standard_normal((6, 1)) + 0.1 * r.standard_normal((n, 1))).astype(np.float32)
+    return x, y
+
+
+DATA = [_data(300, 1), _data(170, 2)]
+
+
+def _algo(base, *, bn, disable_gpu, client, lr=0.05):
+    model = _model(7)  # every client starts from the same initial weights
+
+    class MyAlgo(base):
+        def __init__(self):
+            super().__init__(model=model, criterion=torch.nn.MSELoss(),
+                             optimizer=torch.optim.SGD(model.parameters(), lr=lr if client == 0 else lr * 0.8),
+                             index_generator=NpIndexGenerator(batch_size=32, num_updates=9, seed=11 + client),
+                             dataset=XYDataset, with_batch_norm_parameters=bn, disable_gpu=disable_gpu)
+
+    return MyAlgo
+
+
+def _bits(a):
+    a = np.asarray(a)
+    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize])
+
+
+def _same(xs, ys):
+    assert len(xs) == len(ys)
+    for x, y in zip(xs, ys):
+        x, y = np.asarray(x), np.asarray(y)
+        assert x.dtype == y.dtype and x.shape == y.shape, (x.dtype, y.dtype, x.shape, y.shape)
+        assert np.array_equal(_bits(x), _bits(y))
+
+
+def _state(algo):
+    return [t.detach().cpu().numpy().copy() for t in algo.model.state_dict().values()]
+
+
+def run_fedavg(accelerated, *, bn, disable_gpu, wire=False):
+    """Two clients, ROUNDS rounds.  Returns every exported update and every client's model state
+    after every train (a trace to compare bit for bit)."""
+    from substrafl_amd.integration import accelerate, accelerate_algo
+
+    algos = []
+    for k in range(2):
+        cls = _algo(TorchFedAvgAlgo, bn=bn, disable_gpu=disable_gpu, client=k)
+        algos.append((accelerate_algo(cls, wire=wire) if accelerated else cls)())
+    # on the GPU the accelerated pipeline aggregates on the engine too; the CPU has no engine
+    strategy = accelerate(ss.FedAvg)(algo=algos[0]) if accelerated and not disable_gpu else None
+    trace, avg = [], None
+    for _ in range(ROUNDS):
+        states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, DATA)]
+        for a, s in zip(algos, states):
+            trace += [("update", list(s.parameters_update)), ("model", _state(a)), ("n", [np.int64(s.n_samples)])]
+        if strategy is not None:
+            avg = strategy.avg_shared_states(shared_states=states, _skip=True)
+        else:
+            avg = sch.FedAvgAveragedState(avg_parameters_update=fedavg_explicit(
+                [list(s.parameters_update) for s in states], [s.n_samples for s in states]))
+        trace.append(("avg", list(avg.avg_parameters_update)))
+    return trace, algos, states
+
+
+def run_scaffold(accelerated, *, bn, disable_gpu, aggregation_lr=0.7):
+    from substrafl_amd.integration import accelerate, accelerate_algo
+
+    algos = []
+    for k in range(2):
+        cls = _algo(TorchScaffoldAlgo, bn=bn, disable_gpu=disable_gpu, client=k)
+        algos.append((accelerate_algo(cls) if accelerated else cls)())
+    strategy = (accelerate(ss.Scaffold)(algo=algos[0], aggregation_lr=aggregation_lr)
+                if accelerated and not disable_gpu else None)
+    trace, avg = [], None
+    for _ in range(ROUNDS):
+        states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, DATA)]
+        for a, s in zip(algos, states):
+            trace += [("update", list(s.parameters_update)), ("cv_update", list(s.control_variate_update)),
+                      ("server_cv", list(s.server_control_variate)), ("model", _state(a)),
+                      ("client_cv", [t.detach().cpu().numpy().copy() for t in a._client_control_variate])]
+        if strategy is not None:
+            avg = strategy.avg_shared_states(shared_states=states, _skip=True)
+        else:
+            new_c, upd = scaffold_explicit([list(s.parameters_update) for s in states],
+                                           [list(s.control_variate_update) for s in states],
+                                           list(states[0].server_control_variate), [s.n_samples for s in states],
+                                           aggregation_lr)
+            avg = sch.ScaffoldAveragedStates(server_control_variate=new_c, avg_parameters_update=upd)
+        trace += [("avg", list(avg.avg_parameters_update)), ("new_c", list(avg.server_control_variate))]
+    return trace, algos, states
+
+
+def _compare(ref, acc):
+    assert len(ref) == len(acc)
+    for (tr, r), (ta, a) in zip(ref, acc):
+        assert tr == ta
+        _same(a, r)
+
+
+# ---------------------------------------------------------------------------- CPU
+def test_accelerate_algo_class_shape():
+    from substrafl_amd.integration import accelerate_algo
+
+    cls = _algo(TorchFedAvgAlgo, bn=False, disable_gpu=True, client=0)
+    acc = accelerate_algo(cls)
+    assert issubclass(acc, cls) and acc.__name__ == cls.__name__
+    assert acc.__qualname__.startswith("accelerate_algo.<locals>.")  # carried by value by cloudpickle
+    a = acc()
+    assert a.strategies == [sch.StrategyName.FEDERATED_AVERAGING]
+    op = a.train(data_samples=["d0"], shared_state=None)  # graph mode: the package's remote_data record
+    assert isinstance(op, RemoteDataOperation) and op.method_name == "train" and op.cls is acc
+    sc = accelerate_algo(TorchScaffoldAlgo)
+    assert sc._scaffold_parameters_update is not TorchScaffoldAlgo._scaffold_parameters_update
+    # the user's one-line form: inherit from the accelerated reference class
+    assert issubclass(_algo(accelerate_algo(TorchFedAvgAlgo), bn=False, disable_gpu=True, client=0), TorchFedAvgAlgo)
+    for bad in (ss.FedAvg, object, 3):
+        with pytest.raises(TypeError):
+            accelerate_algo(bad)
+
+
+@pytest.mark.parametrize("bn", [False, True])
+def test_fedavg_cpu_run_matches_reference_pipeline(bn):
+    """On the CPU the accelerated train takes the reference's torch loops: same trace."""
+    _compare(run_fedavg(False, bn=bn, disable_gpu=True)[0], run_fedavg(True, bn=bn, disable_gpu=True)[0])
+
+
+def test_scaffold_cpu_run_matches_reference_pipeline():
+    _compare(run_scaffold(False, bn=True, disable_gpu=True)[0], run_scaffold(True, bn=True, disable_gpu=True)[0])
+
+
+def test_scaffold_hook_count_error_is_the_packages():
+    """A ``_local_train`` that skips the per-step hook raises the reference's error type."""
+    from substrafl_amd.integration import accelerate_algo
+
+    base = _algo(TorchScaffoldAlgo, bn=False, disable_gpu=True, client=0)
+
+    class NoHook(base):
+        def _step_hook(self):
+            pass
+
+    with pytest.raises(TorchScaffoldAlgoParametersUpdateError):
+        accelerate_algo(NoHook)().train(data_from_opener=DATA[0], shared_state=None, _skip=True)
+
+
+# ---------------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from substrafl_amd import _native
+
+    _native.load()  # no fallback: the accelerated weight moves run on libfedagg
+    torch.backends.cudnn.enabled = False  # the native BatchNorm kernels: deterministic training
+    yield
+    torch.backends.cudnn.enabled = True
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
+def test_fedavg_gpu_run_bit_identical(gpu, bn):
+    ref, _, _ = run_fedavg(False, bn=bn, disable_gpu=False)
+    _compare(ref, run_fedavg(False, bn=bn, disable_gpu=False)[0])  # control: the training is deterministic
+    acc, algos, states = run_fedavg(True, bn=bn, disable_gpu=False)
+    _compare(ref, acc)
+    from substrafl_amd.algorithms.weight_manager import flat_bucket, model_parameters
+
+    # the flat path ran: the model's weights are views of the one snapshot bucket set back after train
+    assert flat_bucket([p.data for p in model_parameters(algos[0].model, bn)()]) is not None
+    # plain arrays (no substrafl_amd needed to unpickle), views of one host buffer
+    assert all(type(a) is np.ndarray for a in states[0].parameters_update)
+    assert all(type(a) is np.ndarray for a in pickle.loads(pickle.dumps(states[0].parameters_update)))
+
+
+@pytest.mark.gpu
+def test_fedavg_gpu_wire_opt_in(gpu):
+    from substrafl_amd import wire
+
+    ref, _, _ = run_fedavg(False, bn=True, disable_gpu=False)
+    acc, _, states = run_fedavg(True, bn=True, disable_gpu=False, wire=True)
+    _compare(ref, acc)
+    assert wire.flat_of(list(states[1].parameters_update)) is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
+def test_scaffold_gpu_run_bit_identical(gpu, bn):
+    """fp32 model, fp64 server control variate from round 2 on (the mixed fp32/fp64 flat ops)."""
+    ref, _, _ = run_scaffold(False, bn=bn, disable_gpu=False)
+    _compare(ref, run_scaffold(False, bn=bn, disable_gpu=False)[0])
+    acc, algos, states = run_scaffold(True, bn=bn, disable_gpu=False)
+    _compare(ref, acc)
+    assert states[0].server_control_variate[0].dtype == np.float64
+    assert algos[0]._client_control_variate[0].dtype == torch.float64

@@ -26,9 +26,13 @@ def test_accelerated_strategies_in_simulate_experiment(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    for name in ("linear_fedavg", "linear_scaffold"):
+    for name in ("linear_fedavg", "linear_scaffold", "linear_fedavg_accelerate_algo",
+                 "linear_scaffold_accelerate_algo"):
         assert res[name]["final"] == res[name]["reference_final"], res[name]  # bit for bit
         assert res[name]["engine_calls"] == 3  # one aggregation per round went through the engine
+    for name in ("linear_fedavg_accelerate_algo", "linear_scaffold_accelerate_algo"):
+        assert res[name]["train_is_accelerated"], res[name]
+    assert res["algo_class_by_value"]
     assert res["remote_struct_roundtrip"]["class_by_value"]
     assert res["remote_struct_roundtrip"]["result"] == [2.5, 2.5, 2.5]  # (1*1 + 3*3) / 4
     assert res["fedpca_bit_identical"] == {"avg_shared_states": True, "avg_shared_states_with_qr": True}

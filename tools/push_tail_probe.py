@@ -38,6 +38,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
+# fedagg_copy_async (the "legacy" / "tcopyk" modes) is exported by the FEDAGG_TUNING build only
+os.environ.setdefault("FEDAGG_LIB", os.path.join(ROOT, "substrafl_amd", "libfedagg_tuning.so"))
 
 
 def _port() -> int:
