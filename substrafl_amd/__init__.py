@@ -6,7 +6,7 @@ Python host side that mirrors the reference's strategy plugin surface.  Importin
 touches the GPU (HIP initialises on the first aggregation).
 """
 
-__version__ = "0.1.0"
+__version__ = "0.5.0"
 
 from .schemas import (  # noqa: F401
     FedAvgAveragedState,

@@ -36,7 +36,6 @@ from typing import Optional
 
 import numpy as np
 
-from .algorithms.accelerate import accelerate_algo  # noqa: F401  (the client half)
 from .engine import Devices, engine_for
 from .strategies.fed_avg import check_same_shapes, weighted_average
 from .strategies.scaffold import Scaffold as _MirrorScaffold
@@ -111,6 +110,14 @@ def accelerate(strategy_cls, device: Devices = None):
     # not importable by name: cloudpickle carries the class by value into the task process
     cls.__qualname__ = f"accelerate.<locals>.{strategy_cls.__name__}"
     return cls
+
+
+def accelerate_algo(algo_cls, wire: bool = False):
+    """The client half: :func:`substrafl_amd.algorithms.accelerate.accelerate_algo`.
+    Imported on call, so the aggregation side of this module never imports torch."""
+    from .algorithms.accelerate import accelerate_algo as _accelerate_algo
+
+    return _accelerate_algo(algo_cls, wire=wire)
 
 
 def scaffold_average(strategy, shared_states, aggregation_lr, device: Optional[Devices] = None, wire: bool = False):

@@ -57,8 +57,10 @@ def rocm_base_image(python_major_minor: str, binary_dependencies: Optional[Seque
                           f" && apt-get install -y --no-install-recommends {py} {py}-venv python3-pip {extra}")
     return (
         f"\nFROM rocm/dev-ubuntu-{ubuntu}:{rocm_version}\n\n"
-        "# HIP runtime for libfedagg.so (gfx950); Python for the task entrypoint\n"
-        "ENV DEBIAN_FRONTEND=noninteractive HSA_ENABLE_IPC_MODE_LEGACY=0\n"
+        "# HIP runtime for libfedagg.so (gfx950); Python for the task entrypoint.  The substrafl_amd\n"
+        "# wheel carries the compiled library; hipcc stays on PATH so a source install builds it too\n"
+        "ENV DEBIAN_FRONTEND=noninteractive HSA_ENABLE_IPC_MODE_LEGACY=0 HIPCC=/opt/rocm/bin/hipcc \\\n"
+        "    PATH=/opt/rocm/bin:$PATH LD_LIBRARY_PATH=/opt/rocm/lib\n"
         f"RUN apt-get update -y && {install_python.strip()}"
         " && apt-get clean && rm -rf /var/lib/apt/lists/*\n\n"
     )

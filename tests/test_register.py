@@ -10,6 +10,8 @@ def test_rocm_gpu_image():
     assert "FROM rocm/dev-ubuntu-24.04:7.2" in img
     assert "python3.12 python3.12-venv" in img and "libgl1" in img
     assert "deadsnakes" not in img and "nvidia" not in img
+    # what the substrafl_amd build hook needs in the image (setup.py -> __graft_entry__._hipcc)
+    assert "HIPCC=/opt/rocm/bin/hipcc" in img and "PATH=/opt/rocm/bin:$PATH" in img
     img10 = register.get_base_docker_image("3.10", use_gpu=True)
     assert "deadsnakes" in img10 and "python3.10-venv" in img10
 
