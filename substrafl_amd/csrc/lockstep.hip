@@ -167,7 +167,8 @@ int run_one(const fedagg_lockstep_run& r, hipStream_t s) {
 // ---- push executor (fedagg_push_execute): progress counters in a node-shared host page ----
 constexpr int PUSH_MAX_WAITS = 32;  // counters / tags one wait kernel polls (one lane each)
 constexpr int PUSH_MAX_TAGS = 16;   // landing tags one signal kernel writes (one lane each)
-constexpr uint64_t PUSH_TAG_ERR = 1ull << 32;  // err word: a landing tag (not a counter) timed out
+constexpr uint64_t PUSH_TAG_ERR = 1ull << 32;   // err word: a landing tag (not a counter) timed out
+constexpr uint64_t PUSH_PEER_ERR = 1ull << 33;  // err word: gave up because rank (low bits - 1) failed
 struct PushWaitArgs {
   uint32_t n;
   uint32_t idx[PUSH_MAX_WAITS];
@@ -183,37 +184,57 @@ __device__ __forceinline__ uint64_t ld_acquire_sys(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The first rank whose err word is set (its wait gave up: the call's result is void everywhere),
+// or -1.  errs: the nranks err words of the node-shared page.
+__device__ __forceinline__ int push_failed_rank(const uint64_t* errs, uint32_t nranks) {
+  for (uint32_t j = 0; j < nranks; ++j)
+    if (ld_acquire_sys(errs + j)) return (int)j;
+  return -1;
+}
+
 // Lane i polls progress[idx[i]] until it reaches val[i] (system-scope acquire: what the producer
 // released before its signal is visible to the kernels after this one); then, for a landing tag,
 // its tag word until it holds this call's generation `gen` -- a tag still missing when the counter
 // was already there is the ordering gap between the PCIe counter and the xGMI data: counted in
 // *late and waited out.  A wait that exceeds `timeout` ticks gives up and records idx + 1 (+
-// PUSH_TAG_ERR for a tag) in *err.  Every lane reaches the end (the late count is a wave ballot).
+// PUSH_TAG_ERR for a tag) in *err.  Fail fast: a wait also gives up as soon as ANY rank's err word
+// is set (a peer's or an earlier wait of this rank: the call's result is void), recording
+// PUSH_PEER_ERR + that rank + 1 when the cause is another rank's, so a dead or slow peer costs
+// the group one timeout, not one per wait.  Every lane reaches the end (the late count is a wave
+// ballot).
 __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress, PushWaitArgs a, uint64_t gen,
-                                                       uint64_t timeout, uint64_t* err, uint64_t* late) {
+                                                       uint64_t timeout, uint64_t* err, uint64_t* late,
+                                                       const uint64_t* errs, uint32_t nranks, uint32_t rank) {
   const uint32_t i = threadIdx.x;
   bool was_late = false;
   if (i < a.n) {
     const uint64_t t0 = wall_clock64();
-    bool ok = true;
-    while (ld_acquire_sys(progress + a.idx[i]) < a.val[i]) {
-      if (wall_clock64() - t0 > timeout) {
-        __hip_atomic_store(err, (uint64_t)a.idx[i] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ok = false;
+    int peer = push_failed_rank(errs, nranks);
+    uint64_t code = 0;  // this lane's own failure
+    const uint64_t* tag = a.tag[i];
+    bool counter_done = false;
+    while (peer < 0 && !code) {
+      if (!counter_done) {
+        if (ld_acquire_sys(progress + a.idx[i]) >= a.val[i]) {
+          counter_done = true;
+          if (!tag) break;
+          if (ld_acquire_sys(tag) >= gen) break;
+          was_late = true;
+          continue;
+        }
+      } else if (ld_acquire_sys(tag) >= gen) {
         break;
       }
-      __builtin_amdgcn_s_sleep(16);
-    }
-    if (ok && a.tag[i] && ld_acquire_sys(a.tag[i]) < gen) {
-      was_late = true;
-      while (ld_acquire_sys(a.tag[i]) < gen) {
-        if (wall_clock64() - t0 > timeout) {
-          __hip_atomic_store(err, (uint64_t)a.idx[i] + 1 + PUSH_TAG_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
+      if (wall_clock64() - t0 > timeout) code = (uint64_t)a.idx[i] + 1 + (counter_done ? PUSH_TAG_ERR : 0);
+      else {
         __builtin_amdgcn_s_sleep(16);
+        peer = push_failed_rank(errs, nranks);
       }
     }
+    if (code) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (peer >= 0 && (uint32_t)peer != rank &&
+             !__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+      __hip_atomic_store(err, PUSH_PEER_ERR + (uint64_t)peer + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const uint64_t m = __ballot(was_late);
   if (i == 0 && m) {  // only this rank's wait kernels (one stream, in order) write its late word
@@ -222,10 +243,10 @@ __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress,
   }
 }
 
-// After everything before it on the stream (the step's chain kernels, each wave of which ended
-// with a system-scope release of its peer stores): the landing tags of the consumers this step
-// pushed to (peer HBM, the data's own path), then a system-scope release, then
-// progress[idx] = value (the node-shared host page).
+// After everything before it on the stream (the step's push runs, whose peer stores are
+// system-scope write-through stores each wave waited to be acknowledged before retiring -- no
+// release fence there): the landing tags of the consumers this step pushed to (peer HBM, the
+// data's own path), then a release, then progress[idx] = value (the node-shared host page).
 __global__ void __launch_bounds__(64) push_signal_kernel(uint64_t* progress, uint32_t idx, uint64_t value,
                                                          PushSignalArgs t, uint64_t gen) {
   const uint32_t i = threadIdx.x;
@@ -279,7 +300,7 @@ int push_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s) {
 }
 
 int push_waits(const fedagg_push_wait* waits, int& wi, int nwaits, int step, uint64_t* progress, uint64_t base,
-               uint64_t timeout, uint64_t* err, uint64_t* late, hipStream_t s) {
+               uint64_t timeout, uint64_t* err, uint64_t* late, int nranks, int rank, hipStream_t s) {
   while (wi < nwaits && waits[wi].step == step) {
     PushWaitArgs a;
     memset(&a, 0, sizeof(a));
@@ -293,7 +314,7 @@ int push_waits(const fedagg_push_wait* waits, int& wi, int nwaits, int step, uin
     }
     if (!a.n) continue;
     hipLaunchKernelGGL(push_wait_kernel, dim3(1), dim3(64), 0, s, (const uint64_t*)progress, a, base + 1, timeout, err,
-                       late);
+                       late, (const uint64_t*)progress + nranks, (uint32_t)nranks, (uint32_t)rank);
     int rc = hip_check(hipGetLastError(), "push_wait_kernel");
     if (rc) return rc;
   }
@@ -559,7 +580,7 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
   hipEvent_t* ev = ev_pool[dev];
   int ri = 0, wi = 0;
   for (int t = 0; t < nsteps; ++t) {
-    if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, late, s))) return rc;
+    if ((rc = push_waits(waits, wi, nwaits, t, progress, base, timeout_ticks, err, late, nranks, rank, s))) return rc;
     if (t == 0 && ws_bytes &&  // after step 0's waits, which include the root's entry
         (rc = push_copy(ws_dst, ws_src, ws_bytes, s)))
       return rc;
@@ -583,7 +604,8 @@ int fedagg_push_execute(const fedagg_lockstep_run* runs, int nruns, const fedagg
     // step t done: its consumers' landing tags, then base + t + 2
     if ((rc = push_signal(progress, rank, base + t + 2, tags, ti, ntags, t, gen, s))) return rc;
   }
-  if ((rc = push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, late, s))) return rc;
+  if ((rc = push_waits(waits, wi, nwaits, nsteps, progress, base, timeout_ticks, err, late, nranks, rank, s)))
+    return rc;
   if (ti != ntags || wi != nwaits) return lfail(FEDAGG_EINVAL, "fedagg_push_execute: tags / waits beyond the last step");
   // root, once every rank's last step is in: the finished pieces others pushed, into the output;
   // the numel == 1 staging rows, summed into this rank's workspace

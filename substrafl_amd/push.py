@@ -22,14 +22,20 @@ after the last step the root waits for every rank's last step.
 
 A counter reaches host memory over PCIe while the data of the same step travels over xGMI into
 the consumer's HBM, so the counter alone does not prove the data landed.  Landing tags close that
-gap: a run storing into a peer ends every wave with a system-scope release
-(``FEDAGG_RUN_FEDAVG_PUSH``), and the step's signal kernel then writes the call's generation into
-one tag word per consumer it pushed to -- in the consumer's own HBM, over the same link as the
-data -- before it publishes the counter.  A consumer waits for the producer's counter AND the tag
+gap: a run storing into a peer (``FEDAGG_RUN_FEDAVG_PUSH``, the Scaffold push runs) writes with
+system-scope write-through stores (``sc0 sc1``) and every wave waits for their acknowledgement
+(``s_waitcnt vmcnt(0)``) before it retires -- no L2 writeback, no release fence: the stores are
+acknowledged by the memory they target (only ``push_copy_kernel``, the root's landing copies and
+staging row, ends with a release fence) -- and the step's signal kernel, behind those runs on the
+stream, then writes the call's generation into one tag word per consumer it pushed to -- in the
+consumer's own HBM, over the same link as the data -- before it publishes the counter.  A consumer waits for the producer's counter AND the tag
 before it reads the pushes (at step t + 2, or after its last step for finished pieces and the
 staging row); a tag found missing once the counter was there is counted (``late_tags``: the gap,
 measured on the node) and waited out, and one that never comes is a timeout error, not a wrong
-number.  Every wait points to a strictly earlier step of another rank, so the schedule cannot
+number: the wait records what it waited for in its rank's error word, every other wait of the
+group gives up as soon as it sees a set error word (one timeout per failure, not one per wait), and
+``client_sharded_fedavg`` / ``client_sharded_scaffold`` raise on every rank that waited, after
+synchronising (never returning the root's output).  A failed transport stays failed.  Every wait points to a strictly earlier step of another rank, so the schedule cannot
 deadlock whatever hardware queues the kernels share.  The numel == 1 products go to a staging row of the
 root per rank (one copy after step 0's waits) and are summed on the root (one owner per column: exact).
 
@@ -98,7 +104,13 @@ class PushTransport:
     push = True
 
     def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0,
-                 aux_streams: Optional[int] = None):
+                 aux_streams: Optional[int] = None, fault: Optional[Tuple[str, int, int]] = None):
+        """``timeout_s``: how long a wait kernel polls before it gives up (the call then raises on
+        every rank that waited, naming what it waited for; the transport stays failed).
+        ``fault``: TEST ONLY (tests/test_push_gpu.py), a failure injected on one rank:
+        ``("signal", rank, t)`` -- that rank stops before its step t, so it never signals step t
+        (a peer that died mid-call); ``("tag", rank, i)`` -- that rank never writes the i-th landing
+        tag of its program (its data lands, the proof of it never does)."""
         import torch
         import torch.distributed as dist
         from multiprocessing import shared_memory
@@ -126,6 +138,9 @@ class PushTransport:
         _check(self.lib.fedagg_wall_clock_hz(ctypes.byref(hz)), "fedagg_wall_clock_hz")
         self._timeout = int(timeout_s * hz.value)
         self.base = 0
+        if fault is not None and (fault[0] not in ("signal", "tag") or len(fault) != 3):
+            raise ValueError(f"push fault injection: ('signal' | 'tag', rank, step | index), not {fault!r}")
+        self.fault = fault
         self._maps: Dict[bytes, int] = {}
         self._programs: List["PushProgram"] = []
         self._py = None
@@ -175,10 +190,9 @@ class PushTransport:
 
     def errors(self) -> Dict[int, str]:
         """Ranks whose wait kernel gave up: rank -> what it waited for (a rank's progress counter,
-        or the landing tag of a rank's push)."""
+        or the landing tag of a rank's push), or which rank's failure it stopped waiting after."""
         e = self._page[self.world: 2 * self.world]
-        return {r: (f"landing tag of rank {(int(v) & 0xFFFFFFFF) - 1}" if int(v) >> 32 else
-                    f"counter of rank {int(v) - 1}") for r, v in enumerate(e) if v}
+        return {r: _describe_wait_error(int(v)) for r, v in enumerate(e) if v}
 
     def late_tags(self) -> List[int]:
         """Per rank: landing-tag waits that found the producer's counter published but its data's
@@ -217,10 +231,23 @@ class PushTransport:
         from .rccl import RcclTransport
 
         naux = min(len(self._aux), aux_stream_budget(_hw_queues(), RcclTransport.live() > 0))
-        _check(self.lib.fedagg_push_execute(ctypes.byref(prog.runs) if prog.nruns else None, prog.nruns,
-                                            ctypes.byref(prog.waits) if prog.nwaits else None, prog.nwaits,
-                                            ctypes.byref(prog.tags) if prog.ntags else None, prog.ntags,
-                                            prog.nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
+        runs, nruns, waits, nwaits, tags, ntags, nsteps = (prog.runs, prog.nruns, prog.waits, prog.nwaits, prog.tags,
+                                                           prog.ntags, prog.nsteps)
+        if self.fault is not None and self.fault[1] == self.rank:  # TEST ONLY: the injected failure
+            what, _r, at = self.fault
+            if what == "signal":  # stop before step `at`: its signal (and every later one) never comes
+                keep = lambda arr, n: [x for x in arr[:n] if x.step < at]  # noqa: E731
+                r_, w_, t_ = keep(runs, nruns), keep(waits, nwaits), keep(tags, ntags)
+                nsteps, ws_src, ws_dst, ws_bytes, stage, ncopies = min(at, nsteps), None, None, 0, None, 0
+            else:  # the at-th landing tag is never written
+                r_, w_, t_ = list(runs[:nruns]), list(waits[:nwaits]), [x for i, x in enumerate(tags[:ntags]) if i != at]
+            runs, waits, tags = ((type(a[0]) * max(1, len(lst)))(*lst) for a, lst in ((runs, r_), (waits, w_),
+                                                                                         (tags, t_)))
+            nruns, nwaits, ntags = len(r_), len(w_), len(t_)
+        _check(self.lib.fedagg_push_execute(ctypes.byref(runs) if nruns else None, nruns,
+                                            ctypes.byref(waits) if nwaits else None, nwaits,
+                                            ctypes.byref(tags) if ntags else None, ntags,
+                                            nsteps, self._dev, self.rank, self.world, self.base, self._timeout,
                                             ws_src, ws_dst, ws_bytes,
                                             _native.FEDAGG_F64 if ws_kind == "f64" else _native.FEDAGG_F32, stage,
                                             ctypes.byref(prog.copies) if ncopies else None, ncopies,
@@ -244,6 +271,19 @@ class PushTransport:
         self._shm.close()
         if self.rank == 0:
             self._shm.unlink()
+
+
+PUSH_TAG_ERR, PUSH_PEER_ERR = 1 << 32, 1 << 33  # csrc/lockstep.hip: the err word's cause bits
+
+
+def _describe_wait_error(v: int) -> str:
+    """A rank's err word (csrc/lockstep.hip ``push_wait_kernel``) in words."""
+    who = (v & 0xFFFFFFFF) - 1
+    if v & PUSH_PEER_ERR:
+        return f"stopped after rank {who}'s wait failed"
+    if v & PUSH_TAG_ERR:
+        return f"landing tag of rank {who}"
+    return f"counter of rank {who}"
 
 
 def _native_ipc_bytes() -> int:

@@ -998,10 +998,20 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
         sh = FedAvgShard(kind, rows, w_all[k0:k1], k0, K, layout.M, layout.pairwise_idx)
         root = client_shard_fedavg(sh, out, tr, GpuShardOps(), combine, chunk_elems=chunk_elems)
     if not root:
-        return None
+        return _finish_peer(torch, tr)
     flat = out[: layout.M].cpu().numpy()
     _raise_transport_errors(tr)  # after the copy's synchronisation: a push wait that gave up is an error
     return [a for _, a in layout.unpack(np.array(flat, copy=True))]
+
+
+def _finish_peer(torch, transport) -> None:
+    """A non-root rank's end of a sharded call: with a transport that records failed exchanges
+    (push), wait for this rank's stream and raise if any rank's wait gave up -- the call failed for
+    the whole group, not only on the root.  Returns None (the result lives on the root)."""
+    if getattr(transport, "raise_errors", None) is not None:
+        torch.cuda.current_stream().synchronize()
+        _raise_transport_errors(transport)
+    return None
 
 
 def _raise_transport_errors(transport) -> None:
@@ -1078,7 +1088,7 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
         sh = ScaffoldShard(kind, delta, cv, c, w_all[k0:k1], k0, K, layout.M, lr, layout.pairwise_idx)
         root = client_shard_scaffold(sh, dout, cout, tr, GpuShardOps(), combine)
     if not root:
-        return None
+        return _finish_peer(torch, tr)
     d = dout[: layout.M].cpu().numpy().copy()
     cc = cout[: layout.M].cpu().numpy().copy()
     _raise_transport_errors(tr)

@@ -292,3 +292,97 @@ def test_scaffold_push_run_continues_its_input_accumulator(kind, K, M, finish):
         torch.cuda.synchronize()
         assert torch.equal(got[0].view(torch.int64), ref_d.view(torch.int64)), (seed, "delta")
         assert torch.equal(got[1].view(torch.int64), ref_c.view(torch.int64)), (seed, "control variate")
+
+
+# ---------------------------------------------------------------------------- the failure path
+FAULT_TIMEOUT_S = 3.0
+FAULT_SHAPES = [(37, 29), (1,), (3_000_000,), (1, 1)]  # 2-3 relay chunks: several steps
+
+
+def _fault_worker(rank, G, K, fault, strategy, port, q):
+    """One rank of a client-sharded call through a PushTransport with ``fault`` injected (on rank
+    ``fault[1]``); reports (rank, error text or None, returned a result, seconds, errors(), tb)."""
+    import faulthandler
+    import time
+
+    faulthandler.dump_traceback_later(100, exit=True)
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    from substrafl_amd._native import NativeLibraryError
+    from substrafl_amd.push import PushTransport
+    from substrafl_amd.sharding import client_sharded_fedavg, client_sharded_scaffold
+    from test_client_shard_gpu import _data
+
+    tr = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=G, timeout=timedelta(seconds=90))
+        torch.cuda.set_device(0)
+        pus, ns = _data(K, seed=3, shapes=FAULT_SHAPES)
+        tr = PushTransport(timeout_s=FAULT_TIMEOUT_S, fault=fault)
+        t0 = time.perf_counter()
+        err, res = None, None
+        try:
+            if strategy == "scaffold":
+                rng = np.random.default_rng(9)
+                cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+                c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+                res = client_sharded_scaffold(pus, cvs, [c] * K, ns, 0.7, transport=tr)
+            else:
+                res = client_sharded_fedavg(pus, ns, transport=tr, chunk_elems=1 << 20)
+        except NativeLibraryError as e:
+            err = str(e)
+        torch.cuda.synchronize()
+        q.put((rank, err, res is not None, time.perf_counter() - t0, tr.errors(), None))
+    except Exception:  # noqa: BLE001 -- reported to the parent
+        import traceback
+
+        q.put((rank, None, False, 0.0, None, traceback.format_exc()[-2000:]))
+    finally:
+        if tr is not None:
+            tr.close()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("strategy", ["fedavg", "scaffold"])
+@pytest.mark.parametrize("fault,expect", [(("signal", 1, 1), "counter of rank 1"),
+                                          (("tag", 1, 0), "landing tag of rank 1")])
+def test_push_executor_fails_cleanly(fault, expect, strategy):
+    """VERDICT r04 "Next 3": a rank that withholds its step signal (a peer dead mid-call) or one
+    landing tag makes the ROOT's client_sharded_* raise, naming the counter or the tag, within
+    about one timeout (every other wait gives up on the first failure instead of timing out in
+    turn); the root's output is never returned; every process exits."""
+    import torch.multiprocessing as mp
+
+    G, K = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, G, K, fault, strategy, port, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(G):
+            rank, err, returned, secs, errs, tb = q.get(timeout=110)
+            res[rank] = (err, returned, secs, errs, tb)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()  # our own child, by handle
+    assert all(not p.is_alive() for p in procs)
+    for rank, (err, returned, secs, errs, tb) in sorted(res.items()):
+        assert tb is None, f"rank {rank}:\n{tb}"
+    err, returned, secs, errs, _ = res[0]
+    assert err is not None and "a wait timed out" in err and expect in err, res[0]
+    assert not returned  # the root's output never comes back as a result
+    assert errs and expect in errs[0], errs
+    assert secs < FAULT_TIMEOUT_S + 15, secs  # one timeout, not one per wait
+    print(f"[push fault] {fault} {strategy}: root raised after {secs:.2f} s: {err}", file=sys.stderr)
