@@ -97,6 +97,10 @@ def parse():
                          "gather (N > 1 line's param_range_strong_gather leg: the workload's M split over the ranks, "
                          "the result slices gathered to rank 0 over RCCL inside the timed step)")
     ap.add_argument("--client-shard-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--leg-key", default="", help=argparse.SUPPRESS)  # the leg a child runs (rehearsal)
+    ap.add_argument("--rehearse-legs", action="store_true",
+                    help="with --rehearse-cpu and N > 1: run the client-shard legs as child processes "
+                         "(the N > 1 line's leg mechanism, its deadlines and failure handling) over gloo")
     ap.add_argument("--t1-ms", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--engine", default="rank", choices=["rank", "multi-device"])
     ap.add_argument("--tile", type=int, default=0, help="tiles layout: 16-B vectors per client tile "
@@ -225,12 +229,17 @@ def read_traffic(args, sha):
 # process group (N > 1)
 # ======================================================================================
 PG_TIMEOUT_S = 300  # a stuck collective or exchange ends the rank instead of holding the lease
-CLIENT_SHARD_DEADLINE_S = 180  # one client-shard leg of an N > 1 line, set-up to spot check (normally 30-60 s)
+CLIENT_SHARD_DEADLINE_S = float(os.environ.get("BENCH_LEG_DEADLINE_S", "180"))  # one client-shard leg of an
+# N > 1 line, set-up to spot check (normally 30-60 s)
 # The whole N > 1 line (parameter-range value + its legs) finishes within this many seconds of the
 # rank's start, under the driver's 600 s limit: each leg gets what is left of it (minus what the
 # legs after it and the final line need), and a leg with too little left is skipped, not started.
 LINE_BUDGET_S = float(os.environ.get("BENCH_LINE_BUDGET_S", "480"))
-LEG_MIN_S = 45  # below this a leg cannot finish; it is reported as skipped
+LEG_MIN_S = float(os.environ.get("BENCH_LEG_MIN_S", "45"))  # below this a leg cannot finish: skipped
+# a leg's set-up (process group, RCCL communicator, IPC maps) through its warm-up steps (RCCL's lazy
+# connect): its own deadline, apart from the timed part, so a leg stuck connecting costs this much
+LEG_CONNECT_S = float(os.environ.get("BENCH_LEG_CONNECT_S", "90"))
+LEG_READY = "BENCH_LEG_READY"  # a leg child's stdout line once its warm-up steps are done
 _T_START = time.monotonic()
 
 
@@ -292,6 +301,7 @@ def _timed(ctx, step, steps, warmup):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(ctx.device)
+    _leg_ready(ctx)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ctx.barrier()
     torch.cuda.synchronize(ctx.device)
@@ -304,6 +314,50 @@ def _timed(ctx, step, steps, warmup):
     elapsed = time.perf_counter() - t0
     ctx.barrier()
     return elapsed, ev0.elapsed_time(ev1)
+
+
+def _leg_ready(ctx) -> None:
+    """In a leg child (client_shard_legs): tell the parent the set-up and the warm-up steps are
+    done (RCCL connected), once; the timed part has its own deadline from here."""
+    if getattr(ctx, "leg_child", False) and not getattr(ctx, "_ready_sent", False):
+        print(LEG_READY, flush=True)
+        ctx._ready_sent = True
+
+
+def run_leg_child(cmd, env, connect_s: float, deadline: float):
+    """Run one leg child: it must print LEG_READY within ``connect_s`` (set-up + warm-up) and exit
+    within ``deadline`` of its start; a child that misses either is killed (by PID) and the reason
+    returned.  Returns (stdout, stderr, returncode, error or None)."""
+    import threading
+
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    out, err, ready = [], [], threading.Event()
+
+    def pump(stream, sink, watch):
+        for ln in stream:
+            sink.append(ln)
+            if watch and ln.strip() == LEG_READY:
+                ready.set()
+
+    th = [threading.Thread(target=pump, args=(p.stdout, out, True), daemon=True),
+          threading.Thread(target=pump, args=(p.stderr, err, False), daemon=True)]
+    for t in th:
+        t.start()
+    t0 = time.monotonic()
+    why = None
+    while p.poll() is None:
+        if not ready.is_set() and time.monotonic() - t0 > min(connect_s, deadline):
+            why = f"did not connect (set-up, RCCL connect, warm-up) within {min(connect_s, deadline):.0f} s"
+        elif time.monotonic() - t0 > deadline:
+            why = f"did not finish within {deadline:.0f} s"
+        if why:
+            p.kill()  # this rank's own child, by PID
+            break
+        time.sleep(0.05)
+    p.wait()
+    for t in th:
+        t.join(timeout=5)
+    return "".join(out), "".join(err), p.returncode, why
 
 
 # ======================================================================================
@@ -358,7 +412,8 @@ def main():
     if args.tune:
         _native.tune(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     ctx = _Ctx(torch=torch, dist=dist, world=world, rank=rank, device=device, lib=lib, native=_native,
-               wl=WORKLOADS[args.workload], stream=torch.cuda.current_stream(device), backend=backend)
+               wl=WORKLOADS[args.workload], stream=torch.cuda.current_stream(device), backend=backend,
+               leg_child=args.client_shard_child, physical_gpus=min(world, ndev))
 
     if args.client_shard_child:  # one leg of an N > 1 line (see client_shard_legs)
         try:
@@ -562,7 +617,22 @@ def measure_param_range(args, ctx):
         line["process_group"] = {"backend": ctx.backend, "timeout_s": PG_TIMEOUT_S}
         # the job's fraction of N x 8 TB/s (the driver computes T(1)/T(N) itself)
         line["frac_of_n_x_hbm_peak"] = round(value / (world * HBM_PEAK_GBPS), 4)
+    _label_shared_gpu(ctx, line, ("value", "frac_of_n_x_hbm_peak"))
     return line, {"kern_ms": kern_ms_max, "K": K, "M": M, "tiled": tiled}
+
+
+def _label_shared_gpu(ctx, rec: dict, keys) -> None:
+    """Ranks sharing one GPU (a rehearsal on a box with fewer GPUs than ranks) measure the
+    protocol, not scaling: record the physical GPU count and null the aggregate-rate fields, so
+    such a line can never read as an N-GPU scaling record."""
+    phys = getattr(ctx, "physical_gpus", ctx.world)
+    if phys >= ctx.world:
+        return
+    rec["physical_gpus"] = phys
+    rec["shared_gpu"] = f"{ctx.world} ranks on {phys} GPU(s): a rehearsal of the N > 1 path, no scaling information"
+    for k in keys:
+        if k in rec:
+            rec[k] = None
 
 
 MULTI_DEVICE_DEADLINE_S = 180
@@ -630,10 +700,11 @@ def client_shard_legs(args, ctx, info, only_push=False):
     with the Python schedule over torch's RCCL process group.  A leg that fails, crashes or exceeds
     its deadline becomes an ``error`` field -- it can never cost the line.  Deadlines: rank 0's
     ``leg_deadline`` (CLIENT_SHARD_DEADLINE_S within the line budget, keeping room for the legs
-    after it), broadcast so every rank agrees.  A leg that timed out does not cancel the next one
-    (the two executors share RCCL's bootstrap but not its exchange code); the budget bounds both."""
-    import subprocess
-
+    after it), broadcast so every rank agrees; within it, the set-up through the warm-up steps has
+    its own LEG_CONNECT_S (run_leg_child), so a leg stuck in RCCL's connect costs that, not the
+    leg's budget.  A leg that timed out does not cancel the next one (the two executors share
+    RCCL's bootstrap but not its exchange code); the budget bounds both.  A failure of the host
+    group itself ends the loop, keeping every leg gathered before it."""
     torch, dist = ctx.torch, ctx.dist
     torch.cuda.empty_cache()
     # weak (every rank holds the workload's K clients: north_star's scaling target) with both
@@ -688,50 +759,63 @@ def client_shard_legs(args, ctx, info, only_push=False):
             cmd += ["--rounds", args.rounds]
         elif scaling == "strong":  # exchange-bound: one round is the fastest (tools/lockstep_model.py)
             cmd += ["--rounds", "1.0"]
+        if getattr(args, "rehearse_cpu", False):
+            cmd += ["--rehearse-cpu", "--leg-key", key]
         t0 = time.perf_counter()
-        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         try:
-            so, se = p.communicate(timeout=deadline)
+            so, se, rc, why = run_leg_child(cmd, env, LEG_CONNECT_S, deadline)
             res = None
-            if ctx.rank == 0:
+            if why:
+                res = {"error": why}
+            elif ctx.rank == 0:
                 lines = [ln for ln in so.splitlines() if ln.startswith("{")]
                 res = json.loads(lines[-1]) if lines else None
-            if p.returncode != 0:
-                res = {"error": f"leg exited with {p.returncode}: {se[-600:]}"}
-            elif ctx.rank == 0 and res is None:
+            if not why and rc != 0:
+                res = {"error": f"leg exited with {rc}: {se[-600:]}"}
+            elif not why and ctx.rank == 0 and res is None:
                 res = {"error": f"no result line: {se[-600:]}"}
-        except subprocess.TimeoutExpired:
-            p.kill()  # this rank's own child, by PID
-            p.communicate()
-            res = {"error": f"did not finish within {deadline:.0f} s"}
-        if res is not None:
-            res["wall_s"] = round(time.perf_counter() - t0, 1)
-            res["executor"] = executor
-            if leg_env:
-                res["env"] = dict(leg_env)
-        # every rank's leg is over before the next one starts (errors are per rank: gather them)
-        errs = [(res or {}).get("error")] * ctx.world
-        if ctx.world > 1:
-            dist.all_gather_object(errs, (res or {}).get("error"))
-        if ctx.rank == 0:
-            bad = {r: e for r, e in enumerate(errs) if e}
-            if bad and "error" not in res:
-                res["errors_on_other_ranks"] = bad
-            out[key] = res
+            if res is not None:
+                res["wall_s"] = round(time.perf_counter() - t0, 1)
+                res["executor"] = executor
+                if leg_env:
+                    res["env"] = dict(leg_env)
+            # every rank's leg is over before the next one starts (errors are per rank: gather them)
+            errs = [(res or {}).get("error")] * ctx.world
+            if ctx.world > 1:
+                dist.all_gather_object(errs, (res or {}).get("error"))
+            if ctx.rank == 0:
+                bad = {r: e for r, e in enumerate(errs) if e}
+                if bad and "error" not in res:
+                    res["errors_on_other_ranks"] = bad
+                out[key] = res
+        except Exception as e:  # noqa: BLE001 -- a leg never costs the legs gathered before it
+            if ctx.rank == 0:
+                out[key] = {"error": f"{type(e).__name__}: {e}"[:600], "executor": executor}
+            break  # the host group itself failed: no later leg could meet its peers
     if ctx.rank == 0:  # every weak leg reduced the same K x M values: one expected output
         sums = {k: v.get("output_checksum") for k, v in out.items()
                 if isinstance(v, dict) and v.get("scaling") == "weak" and v.get("checksum_comparable")
                 and v.get("output_checksum") is not None}
-        out["client_shard_output_checksums"] = {"legs": sorted(sums), "agree": len({tuple(c) for c in sums.values()}) <= 1
-                                                if sums else None}
+        # agreement needs two legs at least: one leg agrees with nothing (null, not true)
+        out["client_shard_output_checksums"] = {"legs": sorted(sums), "agree": len({tuple(c) for c in sums.values()}) == 1
+                                                if len(sums) >= 2 else None}
     return out
+
+
+def _elem_hash(torch, kk, e):
+    """fp32 values in [-1, 1) hashed from (client index ``kk`` [Kb, 1], global element ``e`` [1, n])."""
+    h = (e * 2654435761 + kk * 40503 + 12345) & 0xFFFFFFFF
+    h = ((h ^ (h >> 15)) * 2246822519) & 0xFFFFFFFF
+    h = ((h ^ (h >> 13)) * 3266489917) & 0xFFFFFFFF
+    h = h ^ (h >> 16)
+    return ((h & 0xFFFFFF).to(torch.float32) - 8388608.0) * (1.0 / 8388608.0)
 
 
 def _synth_block_elems(torch, kind, k0, Kb, width, segs, device):
     """A client block's row buffer whose value at (client k, global element e) is a hash of (k, e)
     in [-1, 1): the same wherever a plan puts (k, e) -- so every weak client-shard leg (push,
-    native, torch, copy-engine, any round split) reduces the very same K x M problem and their
-    full outputs must agree bit for bit (``output_checksum``)."""
+    native, torch, copy-engine, any round split, rows or tiles) reduces the very same K x M
+    problem and their full outputs must agree bit for bit (``output_checksum``)."""
     dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}[kind]
     t = torch.zeros((max(1, Kb), max(1, width)), dtype=dt, device=device)
     if Kb == 0:
@@ -742,13 +826,35 @@ def _synth_block_elems(torch, kind, k0, Kb, width, segs, device):
         for a in range(lo, hi, step):
             b = min(hi, a + step)
             e = torch.arange(a, b, device=device, dtype=torch.int64)[None, :]
-            h = (e * 2654435761 + kk * 40503 + 12345) & 0xFFFFFFFF
-            h = ((h ^ (h >> 15)) * 2246822519) & 0xFFFFFFFF
-            h = ((h ^ (h >> 13)) * 3266489917) & 0xFFFFFFFF
-            h = h ^ (h >> 16)
-            v = ((h & 0xFFFFFF).to(torch.float32) - 8388608.0) * (1.0 / 8388608.0)
-            t[:Kb, col + a - lo: col + b - lo] = v.to(dt)
+            t[:Kb, col + a - lo: col + b - lo] = _elem_hash(torch, kk, e).to(dt)
     return t[:Kb, :width]
+
+
+def _synth_tiled_elems(torch, kind, k0, Kb, width, segs, tv, ext, device):
+    """The tile-interleaved form of :func:`_synth_block_elems` (sharding.TiledBlock, one bucket per
+    run), filled run by run in tile chunks: the same (client, element) values, so a tiled leg's
+    output is comparable with the row legs' by checksum."""
+    from substrafl_amd.engine import _ELEMS_PER_VEC
+    from substrafl_amd.sharding import TiledBlock
+
+    blk = TiledBlock.empty(torch, kind, Kb, width, tv, ext, device)
+    TL = int(tv) * _ELEMS_PER_VEC[kind]
+    kk = torch.arange(k0, k0 + Kb, device=device, dtype=torch.int64)[:, None]
+    chunk = max(1, (1 << 20) // TL)  # tiles per fill
+    for c0, (t, n) in blk.buckets.items():
+        tiles = -(-n // TL)
+        tv3 = t.view(tiles, Kb, TL)
+        for j0 in range(0, tiles, chunk):
+            j1 = min(tiles, j0 + chunk)
+            colpos = torch.arange(c0 + j0 * TL, c0 + j1 * TL, device=device, dtype=torch.int64)
+            glob = torch.full_like(colpos, -1)
+            for lo, hi, col in segs:
+                m = (colpos >= col) & (colpos < col + hi - lo) & (colpos < c0 + n)
+                glob[m] = lo + colpos[m] - col
+            v = _elem_hash(torch, kk, glob[None, :].clamp(min=0))
+            v[:, glob < 0] = 0.0  # the last tile's padding
+            tv3[j0:j1].copy_(v.to(t.dtype).view(Kb, j1 - j0, TL).permute(1, 0, 2))
+    return blk
 
 
 def _output_checksum(torch, out, M):
@@ -846,15 +952,8 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
                 continue
             ext = TiledBlock.run_extents(plan, b)
             tv = _block_layout(torch, kind, k1 - k0, ext, mode)
-            if tv:
-                rows = TiledBlock.empty(torch, kind, k1 - k0, width, tv, ext, device)
-                g = torch.Generator(device=device)
-                g.manual_seed(seed)
-                for t, _n in rows.buckets.values():
-                    if kind == "bf16":
-                        t.copy_(torch.randn(t.numel(), generator=g, device=device, dtype=torch.float32))
-                    else:
-                        t.normal_(generator=g)
+            if tv:  # tiles: the same (client, element) values as the row legs, re-tiled per run
+                rows = _synth_tiled_elems(torch, kind, k0, k1 - k0, width, segs, tv, ext, device)
                 tvs.add(tv)
             else:  # rows: values addressed by (client, element), the same in every leg and round split
                 rows = _synth_block_elems(torch, kind, k0, k1 - k0, width, segs, device)
@@ -954,7 +1053,7 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
         full_compare = _push_vs_native(ctx, plan, blocks, outs, ops, pw, ws, slots, M, c if scaffold else None)
     # the whole output, summarised: every weak leg holds the same (client, element) values (rows),
     # so their checksums must be equal (client_shard_legs compares them across the legs)
-    comparable = not scaffold and lockstep_mode and tvs == {0}
+    comparable = not scaffold and lockstep_mode  # rows and tiles hold the same (client, element) values
     checksum = _output_checksum(torch, outs["out"], M) if (not scaffold and rank == 0) else None
     if t1_ms is None:  # one GPU reducing the workload's own K x M: the weak-scaling reference
         t1_ms, t1_source = _single_gpu_ms(ctx, K_per, M, kind, scaffold, layout, n_samples), \
@@ -1008,6 +1107,7 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     else:  # the same K x M over the ranks: speedup over one GPU, and that over the rank count
         res["speedup"] = round(t1_ms / ms, 4) if ms > 0 else None
         res["strong_efficiency"] = round(t1_ms / (world * ms), 4) if ms > 0 else None
+    _label_shared_gpu(ctx, res, ("GBps", "frac_of_n_x_hbm_peak", "weak_efficiency", "speedup", "strong_efficiency"))
     if variants and combine == "striped" and getattr(args, "variant_rounds", ""):
         # the other round splits over the same communicator, this leg's buffers freed first
         del step, compute_only, blocks, held, slots, ws, outs
@@ -1184,6 +1284,8 @@ def measure_param_range_gather(args, ctx, t1_ms=None):
         if t1_ms and pipe.get("ms_per_step"):
             pipe["speedup"] = round(t1_ms / pipe["ms_per_step"], 4)
             pipe["strong_efficiency"] = round(t1_ms / (world * pipe["ms_per_step"]), 4)
+        _label_shared_gpu(ctx, pipe, ("GBps", "speedup", "strong_efficiency"))
+    _label_shared_gpu(ctx, res, ("GBps", "frac_of_n_x_hbm_peak", "speedup", "strong_efficiency"))
     return res
 
 
@@ -1624,6 +1726,8 @@ def rehearse(args, world, rank):
 
     if world > 1:
         dist.init_process_group("gloo", **pg_kwargs())
+    if args.client_shard_child:  # one leg child of a --rehearse-legs line
+        return _rehearse_leg_child(args, world, rank)
     x = np.ones(1 << 16, np.float32)
     for _ in range(args.warmup):
         x = x * np.float32(1.0)
@@ -1639,7 +1743,12 @@ def rehearse(args, world, rank):
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
-        if args.client_shard != "off":
+        if args.rehearse_legs:  # the leg mechanism itself: child processes, deadlines, failures
+            import types
+
+            ctx = _Ctx(torch=torch, dist=dist, world=world, rank=rank, device=types.SimpleNamespace(index=rank))
+            legs = client_shard_legs(args, ctx, {"kern_ms": 1.0})
+        elif args.client_shard != "off":
             cs = _rehearse_client_shard(args, world, rank)
             probe = p2p_probe(torch, dist, rank, world, torch.device("cpu"), dist.barrier,
                               lambda v: [float(x) for x in _all_max(torch, dist, v)], ring_mib=1, peers_mib=1, iters=2)
@@ -1654,15 +1763,40 @@ def rehearse(args, world, rank):
         wl = WORKLOADS[args.workload]
         line["config"] = {"workload": wl["name"] + ("_per_gpu" if world > 1 and args.scaling == "weak" else ""),
                           "parallelism": f"param-range x{world}" if world > 1 else "single-gpu"}
-        if world > 1:
+        if world > 1 and args.rehearse_legs:
+            line["process_group"] = {"backend": dist.get_backend(), "timeout_s": PG_TIMEOUT_S}
+            line.update(legs)
+            line["line_wall_s"] = round(time.monotonic() - _T_START, 1)
+        elif world > 1:
             line["process_group"] = {"backend": dist.get_backend(), "timeout_s": PG_TIMEOUT_S}
             line["client_shard"] = cs
             line["legs_order"] = [leg[2] for leg in LEGS]
-            line["client_shard_output_checksums"] = {"legs": ["client_shard"], "agree": True} if cs else None
+            # one leg agrees with nothing: null (client_shard_legs' rule)
+            line["client_shard_output_checksums"] = {"legs": ["client_shard"], "agree": None} if cs else None
             line["param_range_strong_gather"] = gather_leg
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _rehearse_leg_child(args, world, rank):
+    """A leg child under --rehearse-legs: the gloo group is up; the warm-up is one barrier, then
+    LEG_READY, then the leg's rehearsal (the gather leg's or the client-shard schedule's).
+    ``BENCH_REHEARSE_HANG=<leg key>:connect|timed`` (tests) makes that leg hang before or after
+    it reports ready -- a leg stuck in RCCL's connect, or in its timed steps."""
+    import torch.distributed as dist
+
+    hang = os.environ.get("BENCH_REHEARSE_HANG", "")
+    if hang == f"{args.leg_key}:connect":
+        time.sleep(3600)
+    dist.barrier()
+    print(LEG_READY, flush=True)
+    if hang == f"{args.leg_key}:timed":
+        time.sleep(3600)
+    res = _rehearse_gather(world, rank) if args.executor == "gather" else _rehearse_client_shard(args, world, rank)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dist.destroy_process_group()
 
 
 def _all_max(torch, dist, vals):

@@ -57,7 +57,7 @@ def test_plain_gpus_2_launches_two_ranks():
     assert fc["elements"] == cs["params"] and fc["mismatches"] == 0 and "native RCCL" in fc["against"]
     assert "late_landing_tags" in cs and cs["rccl_comm_count"] == 2
     assert cs["checksum_comparable"] and len(cs["output_checksum"]) == 2
-    assert line["client_shard_output_checksums"]["agree"] is True
+    assert line["client_shard_output_checksums"] == {"legs": ["client_shard"], "agree": None}  # one leg: no claim
     # ... and C3 as written (M split over the ranks, result gathered to rank 0) is its own leg
     g = line["param_range_strong_gather"]
     assert g["scaling"] == "strong" and g["params_per_gpu"] * 2 >= g["params"]
@@ -188,3 +188,85 @@ def test_client_shard_block_data_is_element_addressed():
     assert np.array_equal(seen[0].view(np.uint32), seen[1].view(np.uint32))
     out = torch.from_numpy(seen[0][0].copy())
     assert bench._output_checksum(torch, out, M) == bench._output_checksum(torch, out.clone(), M)
+
+
+def test_tiled_client_shard_blocks_hold_the_row_values():
+    """VERDICT r04 "Next 3": a tiled leg's blocks hold the same (client, element) values as the row
+    legs (bench._synth_tiled_elems == TiledBlock.from_rows of bench._synth_block_elems), so the
+    tiled legs' output checksums compare with the row legs'."""
+    import torch
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from substrafl_amd.sharding import TiledBlock, client_blocks, striped_plan
+
+    M, G, K = 50_003, 3, 7
+    for kind, tv in (("f32", 64), ("bf16", 32)):
+        for r in range(G):
+            plan = striped_plan(M, G, r, None, (0.5, 0.5))
+            for b, segs in plan.blocks.items():
+                k0, k1 = client_blocks(K, G)[b]
+                ext = TiledBlock.run_extents(plan, b)
+                rows = bench._synth_block_elems(torch, kind, k0, k1 - k0, plan.block_len[b], segs, torch.device("cpu"))
+                ref = TiledBlock.from_rows(torch, kind, rows, tv, ext)
+                got = bench._synth_tiled_elems(torch, kind, k0, k1 - k0, plan.block_len[b], segs, tv, ext,
+                                               torch.device("cpu"))
+                assert sorted(ref.buckets) == sorted(got.buckets)
+                for c0 in ref.buckets:
+                    assert torch.equal(ref.buckets[c0][0], got.buckets[c0][0]), (kind, r, b, c0)
+
+
+LEG_FIELDS = ("combine", "scaling", "clients", "params", "ms_per_step", "parity", "full_compare", "output_checksum")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("phase,expect", [("connect", "did not connect"), ("timed", "did not finish within")])
+def test_a_hanging_leg_keeps_the_legs_before_it(phase, expect):
+    """VERDICT r04 "Next 6": the N > 1 line's legs run as child processes; a third leg that hangs
+    (in its set-up / RCCL connect, or in its timed steps) is killed at its own deadline, the line
+    still carries the first two legs' fields, the legs after it still run, and the line exits 0
+    within its budget.  (--rehearse-legs: the real leg mechanism over gloo, 2 ranks.)"""
+    import time
+
+    budget = 150
+    env = {"BENCH_LINE_BUDGET_S": str(budget), "BENCH_LEG_MIN_S": "10", "BENCH_LEG_DEADLINE_S": "40",
+           "BENCH_LEG_CONNECT_S": "10", "BENCH_REHEARSE_HANG": f"param_range_strong_gather:{phase}"}
+    t0 = time.monotonic()
+    r = _run(["--gpus", "2", "--rehearse-cpu", "--rehearse-legs", "--multi-device-leg", "off", "--steps", "2",
+              "--warmup", "1"], env)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _line(r.stdout)
+    order = line["legs_order"]
+    assert order[:3] == ["client_shard_push", "client_shard", "param_range_strong_gather"]
+    for key in order[:2]:  # the legs gathered before the hang keep their results
+        assert "error" not in line[key], line[key]
+        assert all(k in line[key] for k in LEG_FIELDS), (key, line[key])
+        assert line[key]["parity"]["mismatches"] == 0
+    hung = line["param_range_strong_gather"]
+    assert expect in hung["error"], hung
+    assert hung["wall_s"] < (12 if phase == "connect" else 42), hung  # its own deadline, not the line's
+    for key in order[3:]:  # the legs after it still ran (or were skipped by the budget, never lost)
+        assert key in line and ("ms_per_step" in line[key] or "skipped" in line[key]), (key, line.get(key))
+    agree = line["client_shard_output_checksums"]
+    assert len(agree["legs"]) >= 2 and agree["agree"] is True
+    assert wall < budget
+
+
+def test_shared_gpu_lines_carry_no_scaling_claim():
+    """ranks sharing one GPU report physical_gpus and null aggregate-rate fields."""
+    import types
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    rec = {"value": 6695.9, "frac_of_n_x_hbm_peak": 0.4, "weak_efficiency": 0.877, "ms_per_step": 11.0}
+    bench._label_shared_gpu(types.SimpleNamespace(world=2, physical_gpus=1), rec,
+                            ("value", "frac_of_n_x_hbm_peak", "weak_efficiency"))
+    assert rec["physical_gpus"] == 1 and "no scaling information" in rec["shared_gpu"]
+    assert rec["value"] is None and rec["weak_efficiency"] is None and rec["ms_per_step"] == 11.0
+    own = {"value": 1.0}
+    bench._label_shared_gpu(types.SimpleNamespace(world=2, physical_gpus=2), own, ("value",))
+    assert own == {"value": 1.0}
