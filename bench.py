@@ -1111,8 +1111,10 @@ def measure_client_shard(args, ctx, combine, scaling, t1_ms=None, t1_source=None
     if variants and combine == "striped" and getattr(args, "variant_rounds", ""):
         # the other round splits over the same communicator, this leg's buffers freed first
         del step, compute_only, blocks, held, slots, ws, outs
-        if hasattr(tr, "_programs"):
-            tr._programs.clear()  # compiled programs hold their buffers
+        if hasattr(tr, "release_programs"):
+            tr.release_programs()  # compiled programs hold their buffers (and, push, peer mappings)
+        elif hasattr(tr, "_programs"):
+            tr._programs.clear()
         torch.cuda.empty_cache()
         res["rounds_variants"] = []
         for spec in args.variant_rounds.split(";"):

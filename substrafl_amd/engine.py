@@ -348,18 +348,22 @@ def serialized(method):
     @functools.wraps(method)
     def wrapper(self, *args, **kwargs):
         locks = [runtime.device_lock(d) for d in sorted(set(self.lock_devices()))]
-        for lk in locks:
-            lk.acquire()
-        lib = _native.load()
-        dev = ctypes.c_int(-1)
-        if lib.fedagg_device_get(ctypes.byref(dev)) != 0:
-            dev.value = -1
+        held = []
+        lib, dev = None, ctypes.c_int(-1)
         try:
+            for lk in locks:
+                lk.acquire()
+                held.append(lk)
+            # inside the try: a missing library or an ABI mismatch raises to this caller and the
+            # locks are released, never left held for the other threads of the process
+            lib = _native.load()
+            if lib.fedagg_device_get(ctypes.byref(dev)) != 0:
+                dev.value = -1
             return method(self, *args, **kwargs)
         finally:
-            if dev.value >= 0:
+            if lib is not None and dev.value >= 0:
                 lib.fedagg_device_set(dev.value)
-            for lk in reversed(locks):
+            for lk in reversed(held):
                 lk.release()
 
     return wrapper

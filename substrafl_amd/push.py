@@ -157,15 +157,38 @@ class PushTransport:
         _check(self.lib.fedagg_ipc_get(int(ptr), h, ctypes.byref(off)), "fedagg_ipc_get")
         return bytes(h.raw), int(off.value)
 
-    def remote(self, info: Tuple[bytes, int]) -> int:
-        """Address, in this process, of another rank's (handle, offset)."""
+    def remote(self, info: Tuple[bytes, int], owner: Optional["PushProgram"] = None) -> int:
+        """Address, in this process, of another rank's (handle, offset); ``owner``: the program the
+        mapping belongs to (closed with it, :meth:`release_programs`)."""
         h, off = info
         if h not in self._maps:
             base = ctypes.c_void_p()
             buf = (ctypes.c_char * len(h)).from_buffer_copy(h)
             _check(self.lib.fedagg_ipc_open(buf, ctypes.byref(base)), "fedagg_ipc_open")
             self._maps[h] = int(base.value)
+        if owner is not None:
+            owner._handles.add(h)
         return self._maps[h] + off
+
+    def release_programs(self) -> None:
+        """Free every compiled program: its uncached slots / landing / tag / staging buffers and the
+        IPC mappings of the peers' ones.  Collective (every rank at once): this rank's stream is
+        synchronised and the group meets first, so no rank's kernels still read or write what goes
+        away.  Without it each call with new client blocks (the host entry points) would keep a
+        program -- and every peer's mappings of its buffers -- alive."""
+        if not self._programs:
+            return
+        import torch
+
+        torch.cuda.synchronize(self.device)
+        if self.world > 1:
+            self.dist.barrier(group=self.group)
+        for p in self._programs:
+            for h in p._handles:
+                base = self._maps.pop(h, None)
+                if base is not None:
+                    self.lib.fedagg_ipc_close(base)
+        self._programs = []
 
     def all_gather(self, obj) -> list:
         out = [None] * self.world
@@ -201,11 +224,16 @@ class PushTransport:
 
     # -- the schedule ----------------------------------------------------------------------
     def program(self, **kw) -> "PushProgram":
+        """The compiled program of this schedule and these buffers: the cached one when the call
+        repeats (same plan, client blocks and outputs: the device-resident loop), else a new one --
+        the cached program is released first (collective, like the compile), so one program's
+        buffers and mappings are alive at a time."""
         for p in self._programs:
             if p.matches(**kw):
                 return p
+        self.release_programs()
         p = PushProgram(self, **kw)
-        self._programs = ([p] + self._programs)[:4]
+        self._programs = [p]
         return p
 
     def raise_errors(self) -> None:
@@ -334,6 +362,7 @@ class PushProgram:
         self.plan, self.blocks, self.accs, self.outs, self.kind = plan, blocks, accs, outs, kind
         self.scaffold, self.c, self.lr = scaffold, c, float(lr)
         self._keep: list = []
+        self._handles: set = set()  # the peers' IPC handles this program mapped (closed with it)
         G, me, root = plan.world, plan.rank, plan.root
         nacc = 2 if scaffold else 1
         outs = list(outs[:nacc])
@@ -375,7 +404,7 @@ class PushProgram:
             if rank == me:
                 # the root's own finished pieces: straight into the caller's outputs
                 return outs[which].data_ptr() + loc[2] * esz if loc[0] == "out" and rank == root else local(loc, which)
-            return tr.remote(infos[rank]["land" if loc[0] == "out" else "slots"]) + offset(rank, loc, which)
+            return tr.remote(infos[rank]["land" if loc[0] == "out" else "slots"], self) + offset(rank, loc, which)
 
         specs, wait_list = push_schedule(plan, [info["recv"] for info in infos])
         # the output ranges other ranks finish (landed on the root, copied into its outputs)
@@ -402,7 +431,7 @@ class PushProgram:
                        [(t, 1, q, v, self.tags_u.ptr + idx * 8) for t, q, v, idx in tag_waits],
                        key=lambda x: (x[0], x[1]))
         waits = [_Wait(t, q, v, tag) for t, _k, q, v, tag in waits]
-        tags = [_Tag(t, 0, tr.remote(infos[c]["tags"]) + (me * n_steps + t) * 8) for t, c, _e in outgoing]
+        tags = [_Tag(t, 0, tr.remote(infos[c]["tags"], self) + (me * n_steps + t) * 8) for t, c, _e in outgoing]
         self.outgoing, self.tag_waits = outgoing, tag_waits
         self.nruns, self.nwaits, self.ntags, self.nsteps = len(runs), len(waits), len(tags), n_steps
         self.runs = (_Run * max(1, len(runs)))(*runs)
@@ -424,7 +453,7 @@ class PushProgram:
             self._stage_info = (infos[self.plan.root], ws_bytes)
         if self.plan.rank == self.plan.root:
             return self.stage_u.ptr + self.plan.rank * ws_bytes
-        return tr.remote(self._stage_info[0]) + self.plan.rank * ws_bytes
+        return tr.remote(self._stage_info[0], self) + self.plan.rank * ws_bytes
 
     def _runs(self, p: "PushRun", dst: List[int], src: List[int]) -> List[_Run]:
         """The launches of one push run: the block's clients (rows at column ``p.col``, ``p.n``

@@ -1000,7 +1000,10 @@ def client_sharded_fedavg(parameters_updates: List[List[np.ndarray]], n_samples:
     if not root:
         return _finish_peer(torch, tr)
     flat = out[: layout.M].cpu().numpy()
-    _raise_transport_errors(tr)  # after the copy's synchronisation: a push wait that gave up is an error
+    try:
+        _raise_transport_errors(tr)  # after the copy's synchronisation: a push wait that gave up is an error
+    finally:
+        _release_programs(tr)  # collective: the peers release in _finish_peer, error or not
     return [a for _, a in layout.unpack(np.array(flat, copy=True))]
 
 
@@ -1008,10 +1011,22 @@ def _finish_peer(torch, transport) -> None:
     """A non-root rank's end of a sharded call: with a transport that records failed exchanges
     (push), wait for this rank's stream and raise if any rank's wait gave up -- the call failed for
     the whole group, not only on the root.  Returns None (the result lives on the root)."""
-    if getattr(transport, "raise_errors", None) is not None:
-        torch.cuda.current_stream().synchronize()
-        _raise_transport_errors(transport)
+    try:
+        if getattr(transport, "raise_errors", None) is not None:
+            torch.cuda.current_stream().synchronize()
+            _raise_transport_errors(transport)
+    finally:
+        _release_programs(transport)
     return None
+
+
+def _release_programs(transport) -> None:
+    """The host entry points stage new client blocks every call, so a compiled program never
+    repeats: free it (and the peers' mappings of its buffers) before returning, so nothing of one
+    aggregation stays on the GPUs into the next FL round.  Collective: root and peers both call it."""
+    fn = getattr(transport, "release_programs", None)
+    if fn is not None:
+        fn()
 
 
 def _raise_transport_errors(transport) -> None:
@@ -1091,7 +1106,10 @@ def client_sharded_scaffold(parameters_updates, control_variate_updates, server_
         return _finish_peer(torch, tr)
     d = dout[: layout.M].cpu().numpy().copy()
     cc = cout[: layout.M].cpu().numpy().copy()
-    _raise_transport_errors(tr)
+    try:
+        _raise_transport_errors(tr)
+    finally:
+        _release_programs(tr)
     return mism, [a for _, a in layout.unpack(cc)], [a for _, a in layout.unpack(d)]
 
 

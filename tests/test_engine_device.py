@@ -62,3 +62,29 @@ def test_abi_exports_the_device_calls():
     lib = _native.load()
     assert callable(lib.fedagg_device_get) and callable(lib.fedagg_device_set)
     assert _native.SIGNATURES["fedagg_device_get"][1] == [ctypes.POINTER(ctypes.c_int)]
+
+
+def test_locks_released_when_the_library_fails_to_load(monkeypatch):
+    """a load failure (missing library, ABI mismatch) inside serialized raises to the
+    caller and releases the device locks -- another thread's call then gets the same error
+    instead of blocking forever."""
+    import threading
+
+    from substrafl_amd import runtime
+
+    def boom():
+        raise _native.NativeLibraryError("no library")
+
+    monkeypatch.setattr(_native, "load", boom)
+    e = _Engine(None, [0, 3])
+    with pytest.raises(_native.NativeLibraryError):
+        e.call()
+    for d in (0, 3):
+        lk = runtime.device_lock(d)
+        assert lk.acquire(timeout=1)  # free
+        lk.release()
+    errs = []
+    th = threading.Thread(target=lambda: errs.append(pytest.raises(_native.NativeLibraryError, e.call)))
+    th.start()
+    th.join(timeout=5)
+    assert not th.is_alive() and errs

@@ -386,3 +386,86 @@ def test_push_executor_fails_cleanly(fault, expect, strategy):
     assert errs and expect in errs[0], errs
     assert secs < FAULT_TIMEOUT_S + 15, secs  # one timeout, not one per wait
     print(f"[push fault] {fault} {strategy}: root raised after {secs:.2f} s: {err}", file=sys.stderr)
+
+
+def _memory_worker(rank, G, K, strategy, calls, port, q):
+    """Repeated host-entry calls through one PushTransport (new client blocks every call, as in an
+    FL run): reports per call the programs / peer mappings held after it and the device's free
+    memory."""
+    import faulthandler
+
+    faulthandler.dump_traceback_later(100, exit=True)
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    from substrafl_amd import runtime
+    from substrafl_amd.push import PushTransport
+    from substrafl_amd.sharding import client_sharded_fedavg, client_sharded_scaffold
+    from test_client_shard_gpu import _data
+
+    tr = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=G, timeout=timedelta(seconds=90))
+        torch.cuda.set_device(0)
+        tr = PushTransport(timeout_s=30)
+        rec = []
+        for i in range(calls):
+            pus, ns = _data(K, seed=40 + i, shapes=FAULT_SHAPES)
+            if strategy == "scaffold":
+                rng = np.random.default_rng(i)
+                cvs = [[rng.standard_normal(a.shape).astype(np.float32) for a in pu] for pu in pus]
+                c = [rng.standard_normal(a.shape).astype(np.float32) for a in pus[0]]
+                client_sharded_scaffold(pus, cvs, [c] * K, ns, 0.7, transport=tr)
+            else:
+                client_sharded_fedavg(pus, ns, transport=tr, chunk_elems=1 << 20)
+            torch.cuda.synchronize()
+            dist.barrier()
+            rec.append((len(tr._programs), len(tr._maps), runtime.device_memory(0)[0]))
+        q.put((rank, rec, None))
+    except Exception:  # noqa: BLE001 -- reported to the parent
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()[-2000:]))
+    finally:
+        if tr is not None:
+            tr.close()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("strategy", ["scaffold", "fedavg"])
+def test_repeated_host_calls_keep_memory_flat(strategy):
+    """ADVICE r04: client_sharded_* stage new blocks every call, so the push program never repeats;
+    each call releases its program (uncached buffers, the peers' IPC mappings of them) before it
+    returns, and the device's free memory stays flat over repeated calls."""
+    import torch.multiprocessing as mp
+
+    G, K, calls = 2, 6, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_memory_worker, args=(r, G, K, strategy, calls, port, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(G):
+            rank, rec, tb = q.get(timeout=110)
+            res[rank] = (rec, tb)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()  # our own child, by handle
+    for rank, (rec, tb) in sorted(res.items()):
+        assert tb is None, f"rank {rank}:\n{tb}"
+        assert all(n_prog == 0 and n_maps == 0 for n_prog, n_maps, _f in rec), rec
+        free = [f for _p, _m, f in rec]
+        # from the second call on (torch's caching allocator holds the staged blocks' memory for reuse)
+        assert min(free[1:]) >= free[1] - (64 << 20), [f >> 20 for f in free]
+    print(f"[push memory] {strategy}: free MiB per call {[f >> 20 for _p, _m, f in res[0][0]]}", file=sys.stderr)
