@@ -97,7 +97,9 @@ def parse():
                          "gather (N > 1 line's param_range_strong_gather leg: the workload's M split over the ranks, "
                          "the result slices gathered to rank 0 over RCCL inside the timed step)")
     ap.add_argument("--client-shard-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--leg-key", default="", help=argparse.SUPPRESS)  # the leg a child runs (rehearsal)
+    ap.add_argument("--leg-key", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--md-pack-threads", type=int, default=0,
+                    help="--engine multi-device: pack workers per GPU (0: CPUs allowed // GPUs, 2..32)")  # the leg a child runs (rehearsal)
     ap.add_argument("--rehearse-legs", action="store_true",
                     help="with --rehearse-cpu and N > 1: run the client-shard legs as child processes "
                          "(the N > 1 line's leg mechanism, its deadlines and failure handling) over gloo")
@@ -1659,7 +1661,7 @@ def multi_device_bench(args):
     base = [rng.standard_normal(int(np.prod(s)), dtype=np.float32).reshape(s) for s in shapes]
     pus = [[(a * np.float32(1 + 0.01 * k)).astype(np.float32) for a in base] for k in range(K)]
     n_samples = [int(v) for v in np.random.default_rng(7).integers(100, 10000, K)]
-    eng = MultiDeviceEngine(devices)
+    eng = MultiDeviceEngine(devices, pack_threads=args.md_pack_threads or None)
     eng.kernel_events = True
     for _ in range(max(1, args.warmup)):
         eng.fedavg(pus, n_samples)
@@ -1691,6 +1693,10 @@ def multi_device_bench(args):
         "config": {"workload": wl["name"], "clients": K, "params": M, "layers": len(shapes),
                    "engine": "MultiDeviceEngine (one process, one thread + native session per GPU)"},
         "shards": per_shard,
+        # host ingress per shard: pack threads (CPUs allowed // GPUs), their NUMA node (the GPU's,
+        # from sysfs), the CPUs they are bound to and the node the pinned ring landed on
+        "placement": eng.placement_report(),
+        "cpus_allowed": len(os.sched_getaffinity(0)),
         "note": "end-to-end (pinned-ring pack + H2D + kernel + D2H); not the device-resident metric",
     }), flush=True)
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 14
+#define FEDAGG_ABI_VERSION 15
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -475,6 +475,17 @@ void* fedagg_session_stream(fedagg_session* s);
  * "copy_streams" (1 or 2 H2D queues for staging; default 2), "fail_copy_after" (tests: the n-th
  * copy enqueued from now on fails with FEDAGG_EHIP; 0 = never) */
 int fedagg_session_set(fedagg_session* s, const char* key, long long value);
+/* Host placement (multi_device.host_placement): the session's pack workers bind to `cpus`
+ * (ncpus == 0: no binding), and its pinned staging ring is allocated by a thread bound to them
+ * under the user's NUMA policy (hipHostMallocNumaUser), so the ring lands on their node --
+ * the GPU's own NUMA node.  Takes effect at the next stage / fetch (the ring is re-allocated). */
+int fedagg_session_affinity(fedagg_session* s, const int* cpus, int ncpus);
+/* NUMA node of the page holding the session's pinned ring (get_mempolicy), -1 if unknown or the
+ * ring is not allocated yet */
+int fedagg_session_ring_node(fedagg_session* s);
+/* hipDeviceGetPCIBusId: "dddd:bb:dd.f" of `device` into buf (len >= 13), for the NUMA node
+ * lookup in /sys/bus/pci/devices/<id>/numa_node */
+int fedagg_device_pci_bus_id(int device, char* buf, int len);
 /* grow-only device buffer number `slot` (0..FEDAGG_SESSION_BUFFERS-1) of at least `bytes` */
 int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr);
 /* Prepare everything the first aggregation would otherwise pay for, so a one-shot task process

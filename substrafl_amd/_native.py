@@ -122,6 +122,9 @@ SIGNATURES = {
     "fedagg_session_destroy": (None, [c_void]),
     "fedagg_session_stream": (c_void, [c_void]),
     "fedagg_session_set": (c_int, [c_void, ctypes.c_char_p, ctypes.c_longlong]),
+    "fedagg_session_affinity": (c_int, [c_void, P(c_int), c_int]),
+    "fedagg_session_ring_node": (c_int, [c_void]),
+    "fedagg_device_pci_bus_id": (c_int, [c_int, ctypes.c_char_p, c_int]),
     "fedagg_session_buffer": (c_int, [c_void, c_int, c_u64, P(c_void)]),
     "fedagg_session_warm": (c_int, [c_void, P(c_u64), c_int]),
     "fedagg_session_stage": (c_int, [c_void, c_void, c_u64, c_int, c_int, P(c_void), P(c_u64)]),
@@ -149,7 +152,7 @@ TUNING_SIGNATURES = {
     "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

@@ -15,11 +15,26 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
 namespace fedagg_host {
+
+// Bind the calling thread to `cpus` (none: leave it as it is); false if the kernel refused.
+inline bool bind_thread(const std::vector<int>& cpus) {
+  if (cpus.empty()) return true;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus)
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+  return pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0;
+}
 
 class Pool {
  public:
-  explicit Pool(int n) {
+  // n workers; with `cpus`, each binds itself to those CPUs before taking work (a GPU's pack
+  // workers on that GPU's NUMA node, next to its pinned ring: multi_device.host_placement)
+  explicit Pool(int n, std::vector<int> cpus = {}) : cpus_(std::move(cpus)) {
     for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
   }
   ~Pool() {
@@ -38,9 +53,11 @@ class Pool {
     cv_.notify_one();
   }
   int size() const { return (int)th_.size(); }
+  const std::vector<int>& cpus() const { return cpus_; }
 
  private:
   void run() {
+    bind_thread(cpus_);  // best effort: a refused mask leaves the worker where the OS put it
     for (;;) {
       std::function<void()> f;
       {
@@ -53,6 +70,7 @@ class Pool {
       f();
     }
   }
+  const std::vector<int> cpus_;  // before th_: the workers read it as they start
   std::vector<std::thread> th_;
   std::deque<std::function<void()>> q_;
   std::mutex m_;

@@ -28,6 +28,9 @@
 #include <thread>
 #include <vector>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "fedagg.h"
 #include "host_pool.h"
 
@@ -80,6 +83,7 @@ struct fedagg_session {
   double last_stage_s = 0, last_fetch_s = 0;
   uint64_t fail_copy_after = 0;  // test knob: the n-th copy of the session fails (0 = never)
   uint64_t copies = 0;
+  std::vector<int> cpus;  // fedagg_session_affinity: the pack workers' and the ring's CPUs (empty: any)
 
   int ensure_ring() {
     if (ring.size() == slots && ring.chunk_bytes == chunk_bytes) return FEDAGG_OK;
@@ -88,7 +92,21 @@ struct fedagg_session {
     ring_ev.assign(slots, nullptr);
     ring.used.assign(slots, false);
     ring.chunk_bytes = chunk_bytes;
-    hipError_t e = hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocDefault);
+    hipError_t e;
+    if (cpus.empty()) {
+      e = hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocDefault);
+    } else {
+      // allocated under the user's NUMA policy (hipHostMallocNumaUser) by a thread bound to the
+      // session's CPUs: the default local policy puts the pinned pages on their node
+      e = hipErrorUnknown;
+      std::thread t([&] {
+        if (fedagg_host::bind_thread(cpus))
+          e = hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocNumaUser);
+        else
+          e = hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocDefault);
+      });
+      t.join();
+    }
     if (e != hipSuccess) {
       ring_base = nullptr;
       release_ring();
@@ -121,9 +139,9 @@ struct fedagg_session {
   std::mutex pool_m;  // workers() may be reached from a compare-only check beside a stage call
   Pool& workers() {
     std::lock_guard<std::mutex> g(pool_m);
-    if (!pool || pool->size() != threads) {
+    if (!pool || pool->size() != threads || pool->cpus() != cpus) {
       delete pool;
-      pool = new Pool(threads);
+      pool = new Pool(threads, cpus);
     }
     return *pool;
   }
@@ -239,6 +257,42 @@ int fedagg_session_set(fedagg_session* s, const char* key, long long value) {
     return FEDAGG_EINVAL;
   }
   return FEDAGG_OK;
+}
+
+int fedagg_session_affinity(fedagg_session* s, const int* cpus, int ncpus) {
+  if (!s || ncpus < 0 || (ncpus && !cpus)) {
+    fedagg_internal::set_error("fedagg_session_affinity: invalid argument");
+    return FEDAGG_EINVAL;
+  }
+  std::vector<int> v(cpus, cpus + ncpus);
+  for (int c : v)
+    if (c < 0 || c >= CPU_SETSIZE) {
+      fedagg_internal::set_error("fedagg_session_affinity: CPU index out of range");
+      return FEDAGG_EINVAL;
+    }
+  if (v != s->cpus) {
+    (void)hipSetDevice(s->device);
+    s->release_ring();  // re-allocated on the new CPUs' node at the next stage / fetch
+    s->cpus = std::move(v);
+  }
+  return FEDAGG_OK;
+}
+
+int fedagg_session_ring_node(fedagg_session* s) {
+  if (!s || !s->ring_base) return -1;
+  int node = -1;
+  // get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR): the node of the page holding the address
+  if (syscall(SYS_get_mempolicy, &node, nullptr, 0UL, s->ring_base, 3UL) != 0) return -1;
+  return node;
+}
+
+int fedagg_device_pci_bus_id(int device, char* buf, int len) {
+  if (!buf || len < 13) {
+    fedagg_internal::set_error("fedagg_device_pci_bus_id: buffer too small");
+    return FEDAGG_EINVAL;
+  }
+  hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+  return e == hipSuccess ? FEDAGG_OK : hip_fail("hipDeviceGetPCIBusId", e);
 }
 
 int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_ptr) {

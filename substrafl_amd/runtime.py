@@ -82,6 +82,18 @@ class Session:
     def set(self, key: str, value: int) -> None:
         _native.check(self.lib.fedagg_session_set(self._h, key.encode(), int(value)), f"session_set({key})")
 
+    def affinity(self, cpus: Optional[Sequence[int]]) -> None:
+        """Bind this session's pack workers, and allocate its pinned ring, on ``cpus`` (None or
+        empty: no binding) -- ``fedagg_session_affinity``; the ring is re-allocated at the next
+        stage / fetch."""
+        cpus = [int(c) for c in (cpus or [])]
+        arr = (ctypes.c_int * max(1, len(cpus)))(*cpus)
+        _native.check(self.lib.fedagg_session_affinity(self._h, arr, len(cpus)), "session_affinity")
+
+    def ring_node(self) -> int:
+        """NUMA node of the pinned staging ring's pages (-1: unknown, or not allocated yet)."""
+        return int(self.lib.fedagg_session_ring_node(self._h))
+
     def warm(self, slot_bytes: Dict[int, int]) -> None:
         """Pinned ring, worker pool, HBM buffers ``{slot: bytes}`` and the kernels' code object,
         ahead of the first aggregation (``fedagg_session_warm``)."""
@@ -286,6 +298,14 @@ def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
     buf = np.empty(n, dtype=key[1])
     _host_cache[key] = buf
     return buf
+
+
+def device_pci_bus_id(device: int) -> str:
+    """``dddd:bb:dd.f`` of ``device`` (hipDeviceGetPCIBusId), lower case as sysfs names it."""
+    lib = _native.load()
+    buf = ctypes.create_string_buffer(64)
+    _native.check(lib.fedagg_device_pci_bus_id(int(device), buf, len(buf)), "device_pci_bus_id")
+    return buf.value.decode().lower()
 
 
 def device_memory(device: int) -> tuple:
