@@ -191,13 +191,30 @@ def _device_flat(updates, device) -> Optional[torch.Tensor]:
         return flat if flat is not None else _gather_flat(updates)
     if all(isinstance(u, np.ndarray) for u in updates) and updates[0].dtype in (np.float32, np.float64) and all(
             u.dtype == updates[0].dtype for u in updates):
-        host = flat_of(updates)
-        if host is None:
-            host = _host_flat(updates)
-        if host is None:
-            host = np.concatenate([np.ascontiguousarray(u).reshape(-1) for u in updates])
-        return torch.from_numpy(host).to(device)  # ONE H2D copy instead of one per layer
+        return _stage_host_layers(updates, torch.device(device))
     return None
+
+
+def _stage_host_layers(arrays: Sequence[np.ndarray], device) -> torch.Tensor:
+    """Host layers (one dtype) -> ONE flat device bucket through the native session's pinned ring:
+    the layers are packed chunk by chunk into pinned memory by its workers while earlier chunks
+    are on the PCIe link (``fedagg_session_stage``, one row of L segments) -- no host-side
+    concatenation, no pageable copy.  Wherever the layers live: one unpickled array each (the
+    subprocess / docker task inputs), or views of one aggregator output (simulation)."""
+    from .. import runtime
+
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    layers = [np.ascontiguousarray(a) for a in arrays]
+    n = sum(int(a.size) for a in layers)
+    flat = torch.empty(n, dtype=torch.from_numpy(layers[0][:0].reshape(-1)).dtype, device=torch.device("cuda", idx))
+    if n:
+        # the bucket may reuse memory torch's stream still reads: the copy starts after that stream
+        torch.cuda.current_stream(flat.device).synchronize()
+        with runtime.device_lock(idx):  # the session's ring is shared with the aggregation engine
+            s = runtime.session(idx)
+            s.stage(flat.data_ptr(), n * flat.element_size(), [layers])
+            s.sync()
+    return flat
 
 
 def _host_flat(arrays: Sequence[np.ndarray]) -> Optional[np.ndarray]:
@@ -289,7 +306,8 @@ def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True) -> List[np.
     host = runtime.reusable_host_array(flat.numel(), torch.empty(0, dtype=flat.dtype).numpy().dtype,
                                        "export")  # bf16 raises, as .numpy()
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
-    runtime.session(flat.device.index).fetch(flat.data_ptr(), host)
+    with runtime.device_lock(flat.device.index):  # the session's ring is shared with the engine
+        runtime.session(flat.device.index).fetch(flat.data_ptr(), host)
     shapes = [tuple(t.shape) for t in tensors]
     if wire:
         return bucket_views(host, shapes)
