@@ -196,3 +196,17 @@ def test_accelerated_calls_load_the_native_library(acc, gpu):
     assert [float(v) for v in res.avg_parameters_update[0]] == [2.5, 2.5, 2.5]  # (1*1 + 3*3) / 4
     maps = Path("/proc/self/maps").read_text()
     assert "libfedagg.so" in maps
+
+
+def test_accelerate_takes_a_user_subclass_defined_anywhere():
+    """A user's own FedAvg subclass (defined in the user's module, not the package's) finds the
+    package's modules through its MRO."""
+    from substrafl_amd.integration import accelerate
+
+    class MyFedAvg(ss.FedAvg):
+        pass
+
+    acc = accelerate(MyFedAvg)
+    assert issubclass(acc, MyFedAvg) and acc._aggregation_methods == {"avg_shared_states": "fedavg"}
+    with pytest.raises(sx.EmptySharedStatesError):
+        acc(algo=_Algo()).avg_shared_states(shared_states=[], _skip=True)
