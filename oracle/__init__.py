@@ -22,4 +22,6 @@ from .aggregation import (  # noqa: F401
     numpy_pairwise_sum,
     fedavg_weights_f32,
     scaffold_weights_f64,
+    newton_raphson_sums,
+    newton_raphson_reference_structure,
 )

@@ -20,6 +20,8 @@ Reference anchors:
   Scaffold._weight_arrays       substrafl/strategies/scaffold.py:204-231
   Scaffold._update_server_control_variate  scaffold.py:233-265 (c appended last, 262-263)
   Scaffold._avg_weight_update   substrafl/strategies/scaffold.py:267-295 (lr * sum, 293)
+  NewtonRaphson.compute_averaged_states  substrafl/strategies/newton_raphson.py:151-216
+                                (explicit in-place += chain from client 0's product, 195-211)
   NumPy pairwise summation      numpy/_core/src/umath/loops_utils.h.src (pairwise_sum,
                                 PW_BLOCKSIZE 128), numpy 2.x -- third-party, restated below.
 """
@@ -185,3 +187,38 @@ def scaffold_explicit(
         terms = [np.multiply(w[k], parameters_updates[k][li].astype(np.float64)) for k in range(K)]
         avg.append(np.multiply(lr, reduce(terms)))
     return new_c, avg
+
+
+# --------------------------------------------------------------------------------------
+# Newton-Raphson
+# --------------------------------------------------------------------------------------
+def newton_raphson_sums(gradients: List[List[np.ndarray]], hessians: List[np.ndarray], n_samples: Sequence[int]):
+    """The weighted sums of newton_raphson.py:195-211, same calls: ``total = x_0 * c_0`` then
+    ``total += x_k * c_k`` (``c_k = n_k / n``, a Python float), the gradients concatenated per
+    client first.  Returns ``(total_hessians, total_gradient_one_d)``."""
+    n_all = sum(n_samples)
+    total_h = total_g = None
+    for idx, (g, h, n) in enumerate(zip(gradients, hessians, n_samples)):
+        c = n / n_all
+        gc = np.concatenate([x.reshape(-1) for x in g])
+        if idx == 0:
+            total_h = h * c
+            total_g = gc * c
+        else:
+            total_h += h * c
+            total_g += gc * c
+    return total_h, total_g
+
+
+def newton_raphson_reference_structure(gradients: List[List[np.ndarray]], hessians: List[np.ndarray],
+                                       n_samples: Sequence[int], damping_factor):
+    """newton_raphson.py:195-216: the sums, ``-damping * solve(H, G)``, unflattened like the last
+    client's gradients (``_unflatten_array``, :218-244)."""
+    total_h, total_g = newton_raphson_sums(gradients, hessians, n_samples)
+    upd = -damping_factor * np.linalg.solve(total_h, total_g)
+    out, i = [], 0
+    for a in gradients[-1]:
+        n = len(a.ravel())
+        out.append(np.array(upd[i: i + n].reshape(a.shape)))
+        i += n
+    return out

@@ -206,7 +206,8 @@ def _stage_host_layers(arrays: Sequence[np.ndarray], device) -> torch.Tensor:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     layers = [np.ascontiguousarray(a) for a in arrays]
     n = sum(int(a.size) for a in layers)
-    flat = torch.empty(n, dtype=torch.from_numpy(layers[0][:0].reshape(-1)).dtype, device=torch.device("cuda", idx))
+    dt = torch.float64 if layers[0].dtype == np.float64 else torch.float32  # the caller checked: one of the two
+    flat = torch.empty(n, dtype=dt, device=torch.device("cuda", idx))
     if n:
         # the bucket may reuse memory torch's stream still reads: the copy starts after that stream
         torch.cuda.current_stream(flat.device).synchronize()

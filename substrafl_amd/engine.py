@@ -729,6 +729,55 @@ class AggregationEngine:
 
     # ----------------------------------------------------------------------------------
     @serialized
+    def sequential_sum(self, rows: List[List[np.ndarray]], n_samples: Sequence[int],
+                       wire: bool = False) -> List[np.ndarray]:
+        """NewtonRaphson's averaging (substrafl/strategies/newton_raphson.py:195-211) per element:
+        ``total = x_0 * c_0``, then ``total += x_k * c_k`` in client order, ``c_k = n_k / n``
+        (a Python float: rounded to the array's float type, NEP 50).  Two differences from
+        FedAvg's ``np.sum`` (:meth:`fedavg`): no ``+0.0`` seed -- a column of ``-0.0`` products
+        stays ``-0.0`` -- and no pairwise order for ``numel == 1`` layers (the loop is an explicit
+        ``+=``).  On the device: client 0's product written by ``fedagg_scale_cast`` (its own
+        float type, exactly ``x_0 * c_0``), then ``fedagg_fedavg_chain_*`` continuing that
+        accumulator over clients 1..K-1 (seed 0), one stage of the K rows, one fetch.  Layers of
+        ONE float product dtype across clients (fp32 / fp64; integer layers multiply as fp64 and
+        are cast on the device); other mixes raise NotImplementedError (the reference's in-place
+        ``+=`` would cast into client 0's type)."""
+        rows = native_byte_order(rows)
+        K, L = len(rows), len(rows[0])
+        if L == 0:
+            return []
+        pds = {np.result_type(a.dtype, 1.0) for row in rows for a in row}
+        R = np.dtype(next(iter(pds)))
+        if len(pds) != 1 or R not in (np.float32, np.float64):
+            raise NotImplementedError(f"sequential_sum: one float32 / float64 product dtype across clients and "
+                                      f"layers (got {sorted(str(d) for d in pds)})")
+        kind = kind_of(R)
+        layout = BucketLayout(list(range(L)), [a.shape for a in rows[0]], R)
+        isz = R.itemsize
+        s = self.session()
+        self._prestaged = {}
+        self.last_timing = tm = {}
+        t0 = time.perf_counter()
+        d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * isz)
+        self._stage_rows(s, rows, layout, d_bucket)
+        tm["stage_s"] = time.perf_counter() - t0
+        d_out = s.buffer(self._B_OUT, layout.ld * isz)
+        n_all = sum(int(n) for n in n_samples)
+        s.scale_cast(d_bucket, R, int(n_samples[0]) / n_all, d_out, R, layout.M)
+        if K > 1:
+            lib = _native.load()
+            w = fedavg_weights(n_samples, kind)[1:]
+            warr = ((ctypes.c_float if kind == "f32" else ctypes.c_double) * len(w))(*[float(v) for v in w])
+            ptrs = _native.ptr_array([d_bucket + k * layout.ld * isz for k in range(1, K)])
+            _native.check(getattr(lib, f"fedagg_fedavg_chain_{kind}")(ptrs, warr, K - 1, layout.M, 0, d_out,
+                                                                        s.stream), "fedavg_chain")
+        out = runtime.reusable_host_array(layout.M, R, "seqsum")
+        s.fetch(d_out, out)
+        tm["total_s"] = time.perf_counter() - t0
+        return [arr for _, arr in layout.unpack(out, wire)]
+
+    # ----------------------------------------------------------------------------------
+    @serialized
     def scaffold(
         self,
         parameters_updates: List[List[np.ndarray]],

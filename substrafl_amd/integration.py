@@ -12,7 +12,10 @@ everything of it -- constructor, ``name``, graph building (``build_compute_plan`
   and ``aggregation_lr`` after the sum, with the ``c`` equality check of scaffold.py:193-196
   counted while ``c`` is staged;
 * ``FedPCA.avg_shared_states`` / ``avg_shared_states_with_qr`` (fed_pca.py:210-299): FedAvg's
-  reduction (+ the reference's ``np.linalg.qr`` of each averaged matrix).
+  reduction (+ the reference's ``np.linalg.qr`` of each averaged matrix);
+* ``NewtonRaphson.compute_averaged_states`` (newton_raphson.py:151-216): the weighted sums of the
+  clients' Hessians and gradients (the explicit ``+=`` chain, ``engine.sequential_sum``), then the
+  reference's own ``np.linalg.solve`` and unflatten on the host.
 
 So the class goes straight into ``simulate_experiment`` / ``execute_experiment``::
 
@@ -103,13 +106,46 @@ def accelerate(strategy_cls, device: Devices = None):
 
         ns["avg_shared_states"] = remote(avg_shared_states)
         ns["_aggregation_methods"] = {"avg_shared_states": "fedavg"}
+    elif getattr(strategies, "NewtonRaphson", None) is not None and issubclass(strategy_cls, strategies.NewtonRaphson):
+        averaged_cls = schemas.NewtonRaphsonAveragedStates
+
+        def compute_averaged_states(self, shared_states):
+            """newton_raphson.py:151-216: the reference's checks, the two weighted sums on the
+            engine, then the reference's own dense solve and unflatten on the host."""
+            self._check_shared_states(shared_states)
+            hessian, gradient = newton_raphson_sums(shared_states, self._fedagg_device)
+            update = -self._damping_factor * np.linalg.solve(hessian, gradient)
+            return averaged_cls(parameters_update=self._unflatten_array(update, shared_states[-1].gradients))
+
+        ns["compute_averaged_states"] = remote(compute_averaged_states)
+        ns["_aggregation_methods"] = {"compute_averaged_states": "sequential"}
     else:
-        raise TypeError(f"accelerate takes SubstraFL's FedAvg, Scaffold or FedPCA (or a subclass), "
+        raise TypeError(f"accelerate takes SubstraFL's FedAvg, Scaffold, FedPCA or NewtonRaphson (or a subclass), "
                         f"not {strategy_cls!r}")
     cls = type(strategy_cls.__name__, (strategy_cls,), ns)
     # not importable by name: cloudpickle carries the class by value into the task process
     cls.__qualname__ = f"accelerate.<locals>.{strategy_cls.__name__}"
     return cls
+
+
+def newton_raphson_sums(shared_states, device: Optional[Devices] = None):
+    """The weighted Hessian and gradient sums of NewtonRaphson.compute_averaged_states
+    (newton_raphson.py:195-211) on the engine (:meth:`engine.AggregationEngine.sequential_sum`:
+    the explicit ``+=`` chain from client 0's product, bit for bit).  Returns ``(total_hessians,
+    total_gradient_one_d)``; the gradients are concatenated per client first, as there.
+    ``ZeroDivisionError`` for ``sum(n_samples) == 0`` and ``ValueError`` for sizes that differ
+    between clients, before any device work."""
+    n_samples = [s.n_samples for s in shared_states]
+    if sum(int(n) for n in n_samples) == 0:
+        raise ZeroDivisionError("division by zero")  # n_samples / n_all_samples (:201)
+    hessians = [[np.asarray(s.hessian)] for s in shared_states]
+    gradients = [[np.concatenate([np.asarray(g).reshape(-1) for g in s.gradients])] for s in shared_states]
+    check_same_shapes(hessians)  # total_hessians += ... (:208)
+    check_same_shapes(gradients)
+    eng = engine_for(device)
+    (total_h,) = eng.sequential_sum(hessians, n_samples)
+    (total_g,) = eng.sequential_sum(gradients, n_samples)
+    return total_h, total_g
 
 
 def accelerate_algo(algo_cls, wire: bool = False):

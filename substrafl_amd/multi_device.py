@@ -215,6 +215,11 @@ class MultiDeviceEngine:
             self._fallback = engine_for(self.devices[0])
         return self._fallback
 
+    def sequential_sum(self, rows, n_samples, wire: bool = False):
+        """NewtonRaphson's averaging (:meth:`engine.AggregationEngine.sequential_sum`) on the first
+        device: its inputs (a P x P Hessian per client) are not sharded by this engine."""
+        return self._single().sequential_sum(rows, n_samples, wire)
+
     _FEDAVG_SLOTS = (0, 1, 2)
     _SCAFFOLD_SLOTS = (0, 1, 2, 4, 5, 6, 7)
 

@@ -46,6 +46,23 @@ class OracleEngine:
         self.calls["fedavg"] += 1
         return fedavg_explicit(parameters_updates, n_samples)
 
+    def sequential_sum(self, rows, n_samples, wire=False):
+        """NewtonRaphson's chain (newton_raphson.py:195-211), per layer, by the oracle's restatement."""
+        assert not wire
+        self.calls["sequential"] = self.calls.get("sequential", 0) + 1
+        n_all = sum(n_samples)
+        out = []
+        for li in range(len(rows[0])):
+            total = None
+            for k, row in enumerate(rows):
+                p = row[li] * (n_samples[k] / n_all)
+                if total is None:
+                    total = p
+                else:
+                    total += p
+            out.append(total)
+        return out
+
     def scaffold(self, parameters_updates, control_variate_updates, server_control_variates, n_samples,
                  aggregation_lr, wire=False):
         assert not wire
@@ -227,6 +244,62 @@ def main():
         same[meth] = len(r) == len(a) and all(x.dtype == y.dtype and np.array_equal(x.view(np.uint64), y.view(np.uint64))
                                                for x, y in zip(r, a))
     out["fedpca_bit_identical"] = same
+
+    # NewtonRaphson: accelerate(NewtonRaphson) against the unmodified class on the same states
+    # (the reference's own unit-test inputs and the golden file's), bit for bit
+    from substrafl.strategies import NewtonRaphson
+    from substrafl.strategies.schemas import NewtonRaphsonSharedState
+
+    nr_arrays = np.load(HERE / "golden" / "golden_newton_raphson.npz", allow_pickle=False)
+    nr_meta = json.loads((HERE / "golden" / "golden_newton_raphson_meta.json").read_text())
+    nr_same = []
+    AccNR = integ.accelerate(NewtonRaphson)
+    for c in nr_meta["cases"]:
+        key, K, L = c["key"], c["K"], c["layers"]
+        states = [NewtonRaphsonSharedState(gradients=[nr_arrays[f"{key}/k{k}/g{li}"] for li in range(L)],
+                                           hessian=nr_arrays[f"{key}/k{k}/h"], n_samples=int(nr_arrays[f"{key}/n_samples"][k]))
+                  for k in range(K)]
+        r = NewtonRaphson(algo=PcaAlgo(), damping_factor=c["damping_factor"]).compute_averaged_states(
+            shared_states=states, _skip=True).parameters_update
+        a = AccNR(algo=PcaAlgo(), damping_factor=c["damping_factor"]).compute_averaged_states(
+            shared_states=states, _skip=True).parameters_update
+        nr_same.append(len(r) == len(a) and all(x.dtype == y.dtype and np.array_equal(x.view(np.uint64), y.view(np.uint64))
+                                                for x, y in zip(r, a)))
+    out["newton_raphson_bit_identical"] = {"cases": len(nr_same), "all": all(nr_same),
+                                           "engine_calls": engine.calls.get("sequential", 0)}
+
+    # ... and in the reference's simulate_experiment with its TorchNewtonRaphsonAlgo (2-org linear
+    # data): the accelerated run's final performance equals the unmodified one's
+    from substrafl.algorithms.pytorch import TorchNewtonRaphsonAlgo
+
+    def run_nr(strategy_cls, rounds=2):
+        data.clear()
+        for i, d in enumerate(train):
+            data[f"train{i}"] = d
+        data["test0"] = test
+        torch.manual_seed(42)
+        model = Perceptron()
+
+        class NRAlgo(TorchNewtonRaphsonAlgo):
+            def __init__(self):
+                super().__init__(model=model, criterion=torch.nn.MSELoss(), batch_size=64, dataset=TorchDataset,
+                                 l2_coeff=0)
+
+        strategy = strategy_cls(algo=NRAlgo(), metric_functions=mae_score, damping_factor=0.8)
+        perf, _, _ = simulate_experiment(
+            client=Client(), strategy=strategy,
+            train_data_nodes=[TrainDataNode(f"org{i}", "ds", [f"train{i}"]) for i in range(2)],
+            evaluation_strategy=EvaluationStrategy(test_data_nodes=[TestDataNode("org0", "ds", ["test0"])],
+                                                   eval_rounds=[rounds]),
+            aggregation_node=AggregationNode("org0"), num_rounds=rounds, clean_models=True,
+            experiment_folder=tempfile.mkdtemp())
+        return float(perf.performance[-1])
+
+    calls0 = engine.calls.get("sequential", 0)
+    ref_perf = run_nr(NewtonRaphson)
+    acc_perf = run_nr(AccNR)
+    out["newton_raphson_simulate"] = {"reference": ref_perf, "accelerated": acc_perf,
+                                      "engine_calls": engine.calls.get("sequential", 0) - calls0}
 
     # the reference's error types
     errs = {}

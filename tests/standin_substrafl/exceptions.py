@@ -11,3 +11,7 @@ class TorchScaffoldAlgoParametersUpdateError(Exception):
 
 class IndexGeneratorUpdateError(Exception):
     """The index generator was not drawn num_updates times."""
+
+
+class SharedStatesError(Exception):
+    """A shared state of the wrong type or with inconsistent sizes."""

@@ -12,6 +12,7 @@ class StrategyName(str, Enum):
     FEDERATED_AVERAGING = "Federated Averaging"
     FEDERATED_PCA = "Federated PCA"
     SCAFFOLD = "Scaffold"
+    NEWTON_RAPHSON = "Newton Raphson"
 
 
 class _State(pydantic.BaseModel):
@@ -46,3 +47,13 @@ class ScaffoldSharedState(_State):
 class ScaffoldAveragedStates(_State):
     server_control_variate: List[np.ndarray]
     avg_parameters_update: List[np.ndarray]
+
+
+class NewtonRaphsonSharedState(_State):
+    n_samples: int
+    gradients: List[np.ndarray]
+    hessian: np.ndarray
+
+
+class NewtonRaphsonAveragedStates(_State):
+    parameters_update: List[np.ndarray]

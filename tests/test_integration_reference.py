@@ -36,5 +36,9 @@ def test_accelerated_strategies_in_simulate_experiment(tmp_path):
     assert res["remote_struct_roundtrip"]["class_by_value"]
     assert res["remote_struct_roundtrip"]["result"] == [2.5, 2.5, 2.5]  # (1*1 + 3*3) / 4
     assert res["fedpca_bit_identical"] == {"avg_shared_states": True, "avg_shared_states_with_qr": True}
+    nr = res["newton_raphson_bit_identical"]
+    assert nr["cases"] >= 9 and nr["all"] and nr["engine_calls"] == 2 * nr["cases"]
+    sim = res["newton_raphson_simulate"]
+    assert sim["accelerated"] == sim["reference"] and sim["engine_calls"] == 2 * 2  # 2 rounds x (H, G)
     assert res["errors"] == {"empty": "EmptySharedStatesError", "zero_samples": "ZeroDivisionError",
                              "layer_count": "AssertionError"}

@@ -139,3 +139,29 @@ def test_golden_fedpca_is_fedavg_arithmetic(golden):
         pus = [[arrays[f"{key}/x{li}"][k] for li in range(L)] for k in range(K)]
         for g, r in zip(fedavg_reference_structure(pus, ns), [arrays[f"{key}/avg{li}"] for li in range(L)]):
             assert np.array_equal(_bits(g), _bits(r))
+
+
+def test_golden_newton_raphson_bit_exact():
+    """The oracle's restatement of NewtonRaphson.compute_averaged_states (newton_raphson.py:
+    195-216) reproduces the reference's outputs (golden_newton_raphson.npz, gen_golden_nr.py) bit
+    for bit, including the -0.0 case."""
+    import json
+    from pathlib import Path
+
+    from oracle import newton_raphson_reference_structure
+
+    d = Path(__file__).resolve().parent / "golden"
+    arrays = np.load(d / "golden_newton_raphson.npz", allow_pickle=False)
+    meta = json.loads((d / "golden_newton_raphson_meta.json").read_text())
+    assert len(meta["cases"]) >= 9
+    for c in meta["cases"]:
+        key, K, L = c["key"], c["K"], c["layers"]
+        grads = [[arrays[f"{key}/k{k}/g{li}"] for li in range(L)] for k in range(K)]
+        hess = [arrays[f"{key}/k{k}/h"] for k in range(K)]
+        ns = [int(v) for v in arrays[f"{key}/n_samples"]]
+        got = newton_raphson_reference_structure(grads, hess, ns, c["damping_factor"])
+        ref = [arrays[f"{key}/out{li}"] for li in range(c["outputs"])]
+        assert len(got) == len(ref)
+        for g, r in zip(got, ref):
+            assert g.dtype == r.dtype and g.shape == r.shape
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), key
