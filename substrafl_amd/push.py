@@ -102,6 +102,7 @@ class PushTransport:
 
     native = True
     push = True
+    fault: Optional[Tuple[str, int, int]] = None  # TEST ONLY: see __init__
 
     def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0,
                  aux_streams: Optional[int] = None, fault: Optional[Tuple[str, int, int]] = None):

@@ -64,8 +64,10 @@ class _FakeTransport:
     def ipc_info(self, ptr: int):
         return (self.rank, int(ptr)), 0
 
-    def remote(self, info) -> int:
+    def remote(self, info, owner=None) -> int:
         (_owner, base), off = info
+        if owner is not None:
+            owner._handles.add((_owner, base))
         return base + off
 
     def all_gather(self, obj) -> list:
