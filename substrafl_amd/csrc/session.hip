@@ -100,6 +100,7 @@ struct fedagg_session {
       // session's CPUs: the default local policy puts the pinned pages on their node
       e = hipErrorUnknown;
       std::thread t([&] {
+        (void)hipSetDevice(device);  // the new thread's current device: this session's GPU
         if (fedagg_host::bind_thread(cpus))
           e = hipHostMalloc(&ring_base, (size_t)slots * chunk_bytes, hipHostMallocNumaUser);
         else
