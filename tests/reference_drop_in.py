@@ -28,53 +28,13 @@ HERE = Path(__file__).resolve().parent
 ROOT = HERE.parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(HERE / "golden"))
+sys.path.insert(0, str(HERE / "refplugin"))
 from gen_golden import REF, _install_stubs  # noqa: E402
 from gen_plumbing import linear_data  # noqa: E402
 
-from oracle import fedavg_explicit, scaffold_explicit  # noqa: E402
 
 
-class OracleEngine:
-    """Test double of :class:`substrafl_amd.engine.AggregationEngine` for a GPU-less container:
-    the same two entry points, computed by the oracle; counts its calls."""
-
-    def __init__(self):
-        self.calls = {"fedavg": 0, "scaffold": 0}
-
-    def fedavg(self, parameters_updates, n_samples, wire=False):
-        assert not wire, "reference schemas take plain NumPy arrays"
-        self.calls["fedavg"] += 1
-        return fedavg_explicit(parameters_updates, n_samples)
-
-    def sequential_sum(self, rows, n_samples, wire=False):
-        """NewtonRaphson's chain (newton_raphson.py:195-211), per layer, by the oracle's restatement."""
-        assert not wire
-        self.calls["sequential"] = self.calls.get("sequential", 0) + 1
-        n_all = sum(n_samples)
-        out = []
-        for li in range(len(rows[0])):
-            total = None
-            for k, row in enumerate(rows):
-                p = row[li] * (n_samples[k] / n_all)
-                if total is None:
-                    total = p
-                else:
-                    total += p
-            out.append(total)
-        return out
-
-    def scaffold(self, parameters_updates, control_variate_updates, server_control_variates, n_samples,
-                 aggregation_lr, wire=False):
-        assert not wire
-        self.calls["scaffold"] += 1
-        c0 = server_control_variates[0]
-        mism = 0
-        for ci in server_control_variates[1:]:
-            for a, b in zip(c0, ci):
-                a, b = np.asarray(a), np.asarray(b)
-                mism += int(np.sum(~((a == b) | (np.isnan(a) & np.isnan(b)))))
-        new_c, avg = scaffold_explicit(parameters_updates, control_variate_updates, c0, n_samples, aggregation_lr)
-        return mism, new_c, avg
+from oracle_engine import OracleEngine  # noqa: E402  (tests/refplugin/oracle_engine.py)
 
 
 def main():

@@ -42,3 +42,20 @@ def test_accelerated_strategies_in_simulate_experiment(tmp_path):
     assert sim["accelerated"] == sim["reference"] and sim["engine_calls"] == 2 * 2  # 2 rounds x (H, G)
     assert res["errors"] == {"empty": "EmptySharedStatesError", "zero_samples": "ZeroDivisionError",
                              "layer_count": "AssertionError"}
+
+
+def test_reference_own_unit_tests_pass_with_accelerated_classes(tmp_path):
+    """The reference's own strategy and torch-algorithm unit tests (tests/strategies/*,
+    tests/algorithms/pytorch/{test_fed_avg,test_scaffold,test_weight_manager}.py), run in place
+    with FedAvg / Scaffold / FedPCA / NewtonRaphson swapped for accelerate()'d classes and
+    TorchFedAvgAlgo / TorchScaffoldAlgo for accelerate_algo()'d ones: every test the unmodified
+    reference passes here passes (tests/reference_own_tests.py)."""
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, str(HERE / "reference_own_tests.py")], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["passed_by_reference_but_not_accelerated"] == [], res
+    assert res["passed_reference"] >= 70 and res["passed_accelerated"] >= res["passed_reference"]
+    calls = res["engine_calls"]
+    assert calls["fedavg"] > 0 and calls["scaffold"] > 0 and calls["sequential"] > 0  # the bodies ran
