@@ -752,6 +752,9 @@ class AggregationEngine:
             raise NotImplementedError(f"sequential_sum: one float32 / float64 product dtype across clients and "
                                       f"layers (got {sorted(str(d) for d in pds)})")
         kind = kind_of(R)
+        n_all = sum(int(n) for n in n_samples)
+        if n_all == 0:
+            raise ZeroDivisionError("division by zero")  # n_samples / n_all_samples (newton_raphson.py:201)
         layout = BucketLayout(list(range(L)), [a.shape for a in rows[0]], R)
         isz = R.itemsize
         s = self.session()
@@ -762,7 +765,6 @@ class AggregationEngine:
         self._stage_rows(s, rows, layout, d_bucket)
         tm["stage_s"] = time.perf_counter() - t0
         d_out = s.buffer(self._B_OUT, layout.ld * isz)
-        n_all = sum(int(n) for n in n_samples)
         s.scale_cast(d_bucket, R, int(n_samples[0]) / n_all, d_out, R, layout.M)
         if K > 1:
             lib = _native.load()
