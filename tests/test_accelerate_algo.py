@@ -22,6 +22,7 @@ The same runs on the CPU (``disable_gpu``) take the reference's torch loops and 
 """
 
 import pickle
+import sys
 
 import numpy as np
 import pytest
@@ -228,6 +229,24 @@ def test_fedavg_gpu_run_bit_identical(gpu, bn):
     # plain arrays (no substrafl_amd needed to unpickle), views of one host buffer
     assert all(type(a) is np.ndarray for a in states[0].parameters_update)
     assert all(type(a) is np.ndarray for a in pickle.loads(pickle.dumps(states[0].parameters_update)))
+
+
+@pytest.mark.gpu
+def test_fedavg_gpu_float64_model_bit_identical(gpu, monkeypatch):
+    """A float64 model (the flat increment takes fp32 weights only): the accelerated train keeps
+    the reference's torch loops where the kernels do not apply, and every result stays
+    bit-identical."""
+    base = _model
+
+    def model64(seed):
+        return base(seed).double()
+
+    monkeypatch.setattr(sys.modules[__name__], "_model", model64)
+    monkeypatch.setattr(sys.modules[__name__], "DATA", [(x.astype(np.float64), y.astype(np.float64)) for x, y in DATA])
+    ref, _, _ = run_fedavg(False, bn=True, disable_gpu=False)
+    acc, _, states = run_fedavg(True, bn=True, disable_gpu=False)
+    _compare(ref, acc)
+    assert states[0].parameters_update[0].dtype == np.float64
 
 
 @pytest.mark.gpu
