@@ -2,4 +2,4 @@
 # and roofline checks for every workload (tools/profile_round.sh).
 set -o pipefail
 export PYTHONUNBUFFERED=1
-bash tools/profile_round.sh r05e c3 c2 c4 c5 > gpurun_out/r05e_profile.log 2>&1
+bash tools/profile_round.sh ${1:-r05e} c3 c2 c4 c5 > gpurun_out/${1:-r05e}_profile.log 2>&1

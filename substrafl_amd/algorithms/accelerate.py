@@ -60,8 +60,8 @@ def _reference_base(algo_cls):
                     f"not {algo_cls!r}")
 
 
-def _export(self, tensors):
-    return wm.export_numpy(tensors, wire=self._fedagg_wire)
+def _export(self, tensors, tag="export"):
+    return wm.export_numpy(tensors, wire=self._fedagg_wire, tag=tag)
 
 
 def _fedavg_train(shared_state_cls):
@@ -143,9 +143,10 @@ def _scaffold_train(shared_state_cls, fast_rule, update_error):
                                                [-1.0, -1.0 / (self._current_lr * gen.num_updates)])
         self._client_control_variate = wm.add_parameters(self._client_control_variate, cv_update)
         wm.set_parameters(self._model, before, with_batch_norm_parameters=bn)
+        # one recycled host buffer per list: the three are alive together until the next round
         return shared_state_cls(parameters_update=_export(self, delta),
-                                control_variate_update=_export(self, cv_update),
-                                server_control_variate=_export(self, self._server_control_variate),
+                                control_variate_update=_export(self, cv_update, "export_cv"),
+                                server_control_variate=_export(self, self._server_control_variate, "export_c"),
                                 n_samples=len(train_dataset))
 
     return train

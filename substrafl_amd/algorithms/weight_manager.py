@@ -292,12 +292,15 @@ def zeros_like_parameters(model: torch.nn.Module, with_batch_norm_parameters: bo
         return [torch.zeros_like(p).to(device) for p in params]
 
 
-def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True) -> List[np.ndarray]:
+def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True, tag: str = "export") -> List[np.ndarray]:
     """``[p.cpu().detach().numpy() for p in ...]`` (torch_fed_avg_algo.py:227-230) with ONE D2H copy
     when the tensors are views of one flat bucket.  With ``wire`` the arrays returned are
     :class:`wire.BucketArray` layers of one host buffer -- they pickle as that one buffer, and the
     aggregator stages the client as a single segment; without it they are plain ``np.ndarray``
-    views of that buffer, which any process unpickles (no ``substrafl_amd`` import needed)."""
+    views of that buffer, which any process unpickles (no ``substrafl_amd`` import needed).
+    ``tag`` names the host buffer recycled across calls (``runtime.reusable_host_array``): exports
+    that are alive together (Scaffold's three lists) need one tag each, or every round after the
+    first re-faults a fresh buffer for all but one of them."""
     flat = flat_bucket(list(tensors))
     if flat is None or not flat.is_cuda:
         return [t.cpu().detach().numpy() for t in tensors]
@@ -305,7 +308,7 @@ def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True) -> List[np.
 
     # one D2H through the native session's pinned ring (chunked, copied out by its worker pool)
     host = runtime.reusable_host_array(flat.numel(), torch.empty(0, dtype=flat.dtype).numpy().dtype,
-                                       "export")  # bf16 raises, as .numpy()
+                                       tag)  # bf16 raises, as .numpy()
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
     with runtime.device_lock(flat.device.index):  # the session's ring is shared with the engine
         runtime.session(flat.device.index).fetch(flat.data_ptr(), host)

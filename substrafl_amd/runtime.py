@@ -279,25 +279,36 @@ def device_lock(device: int) -> threading.RLock:
         return lk
 
 
-_host_cache: Dict[tuple, np.ndarray] = {}
+_host_cache: Dict[tuple, list] = {}
+_host_lock = threading.Lock()
+HOST_POOL_DEPTH = 4  # recycled buffers kept per call site and dtype
 
 
 def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
     """A host array of ``n`` elements for a D2H result (``tag`` names the call site).  A fresh
     100 MB allocation costs ~8 ms of first-touch page faults (glibc maps every block above 32 MiB
-    anew), three times the D2H itself, so the previous call's buffer is recycled -- but only when
-    nothing references it any more (every array handed out from it was a view holding it), so no
-    caller ever sees its data change."""
+    anew), three times the D2H itself, so earlier calls' buffers are recycled -- but only one that
+    nothing references any more (every array handed out from it was a view holding it), so no
+    caller ever sees its data change.  Up to ``HOST_POOL_DEPTH`` buffers per site: in simulation
+    mode the previous round's results are still held while the next round's are made (the
+    strategy keeps its last train states, and its last average, until the new ones are returned),
+    so with one buffer per site every call after the first would fault a fresh one."""
     import sys
 
     key = (tag, np.dtype(dtype))
-    buf = _host_cache.get(key)
-    # references: the cache dict, the local name and getrefcount's argument; a live view adds one
-    if buf is not None and buf.size >= n and sys.getrefcount(buf) <= 3:
-        return buf[:n]
-    buf = np.empty(n, dtype=key[1])
-    _host_cache[key] = buf
-    return buf
+    with _host_lock:
+        pool = _host_cache.setdefault(key, [])
+        for i in range(len(pool)):  # (not enumerate: its cached result tuple would hold one more reference)
+            buf = pool[i]
+            # references: the pool list, the local name and getrefcount's argument; a live view adds one
+            if buf.size >= n and sys.getrefcount(buf) <= 3:
+                pool.append(pool.pop(i))  # most recently used last
+                return buf[:n]
+        buf = np.empty(n, dtype=key[1])
+        pool.append(buf)
+        if len(pool) > HOST_POOL_DEPTH:
+            pool.pop(0)  # the least recently used; still alive through its holders' views, if any
+        return buf
 
 
 def device_pci_bus_id(device: int) -> str:

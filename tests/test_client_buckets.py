@@ -208,3 +208,23 @@ def test_host_result_buffer_reused_only_when_released():
     del c
     d = reusable_host_array(64, np.float32, "t")
     assert not any(np.shares_memory(d, v) for v in views)
+
+
+def test_host_result_buffers_pooled_across_held_rounds():
+    """Simulation mode holds round r's results while round r+1's are made (the strategy keeps its
+    last train states and last average until the new ones return): two buffers per call site then
+    alternate instead of one fresh allocation per call; the pool is bounded."""
+    from substrafl_amd import runtime
+
+    ptrs = []
+    held = runtime.reusable_host_array(1000, np.float32, "pool_t")
+    ptrs.append(held.__array_interface__["data"][0])
+    for _ in range(6):
+        nxt = runtime.reusable_host_array(1000, np.float32, "pool_t")  # made while the last is held
+        assert not np.shares_memory(nxt, held)
+        ptrs.append(nxt.__array_interface__["data"][0])
+        held = nxt  # the previous round's result is released here
+    assert len(set(ptrs)) == 2, ptrs
+    keep = [runtime.reusable_host_array(10, np.float64, "pool_cap") for _ in range(runtime.HOST_POOL_DEPTH + 3)]
+    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64))]) == runtime.HOST_POOL_DEPTH
+    assert len({a.__array_interface__["data"][0] for a in keep}) == len(keep)  # every live one distinct
