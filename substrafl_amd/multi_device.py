@@ -164,7 +164,21 @@ class MultiDeviceEngine:
 
     # ----------------------------------------------------------------------------------
     def sessions(self):
-        """One native session per shard (created on first use)."""
+        """One native session per shard (created on first use).  A shard's session is the GPU's
+        process-wide one, which other engines stage on: its threads and CPUs are changed under the
+        device locks (``runtime.device_lock``, reentrant: an engine call already holds them)."""
+        if self._sessions is not None:
+            return self._sessions
+        locks = [runtime.device_lock(d) for d in sorted(set(self.devices))]
+        for lk in locks:
+            lk.acquire()
+        try:
+            return self._make_sessions()
+        finally:
+            for lk in reversed(locks):
+                lk.release()
+
+    def _make_sessions(self):
         if self._sessions is None:
             place = host_placement([runtime.device_pci_bus_id(d) for d in self.devices], self._pack_threads)
             seen = set()

@@ -231,6 +231,7 @@ class PushTransport:
         buffers and mappings are alive at a time."""
         for p in self._programs:
             if p.matches(**kw):
+                p.rebase_outs(kw["outs"])
                 return p
         self.release_programs()
         p = PushProgram(self, **kw)
@@ -440,6 +441,7 @@ class PushProgram:
         self.tags = (_Tag * max(1, len(tags)))(*tags)
         self._tr = tr
         self._stage_info = None
+        self._out_ptrs, self._out_bytes = [o.data_ptr() for o in outs], out_n * esz
 
     def ws_dst(self, ws_bytes: int) -> int:
         """This rank's staging row on the root for the numel == 1 products (collective at first use)."""
@@ -490,9 +492,43 @@ class PushProgram:
         return rec
 
     def matches(self, plan, blocks, accs, outs, kind, scaffold, c=None, lr=1.0) -> bool:
+        """Whether a call can run this program.  Only what is the same on every rank by construction
+        (the caller's plan / blocks / c objects, kind, lr, the outputs' size) decides: the compile
+        of a miss is collective, so a decision that could differ between ranks -- the outputs'
+        addresses, fresh tensors that one rank's allocator happens to place where the last ones
+        were -- would leave one rank compiling while the others execute.  New output addresses are
+        patched in instead (:meth:`rebase_outs`)."""
+        nacc = 2 if self.scaffold else 1
         return (plan is self.plan and blocks is self.blocks and kind == self.kind and scaffold == self.scaffold
-                and c is self.c and float(lr) == self.lr
-                and [o.data_ptr() for o in outs] == [o.data_ptr() for o in self.outs])
+                and c is self.c and float(lr) == self.lr and len(outs) >= nacc
+                and all(int(o.numel()) * o.element_size() == self._out_bytes
+                        and o.element_size() == self.outs[0].element_size() for o in outs[:nacc]))
+
+    def rebase_outs(self, outs) -> None:
+        """Point the launches and landing copies that write the caller's outputs (the root's
+        finished pieces) at ``outs``; a no-op when the addresses did not move."""
+        nacc = 2 if self.scaffold else 1
+        new = [o.data_ptr() for o in outs[:nacc]]
+        if new == self._out_ptrs:
+            return
+        span = self._out_bytes
+
+        def moved(addr):
+            if addr:
+                for old, nw in zip(self._out_ptrs, new):
+                    if old <= addr < old + span:
+                        return addr - old + nw
+            return None
+
+        for r in self.runs[: self.nruns]:
+            a = moved(r.acc)
+            if a is not None:
+                r.acc = a
+        for cp in self.copies[: self.ncopies]:
+            a = moved(cp.dst)
+            if a is not None:
+                cp.dst = a
+        self._out_ptrs, self.outs = new, list(outs)
 
 
 @dataclass(frozen=True)

@@ -242,3 +242,37 @@ def _random_cases(n, seed=20241018):
 def test_push_program_addresses_random_plans(G, K, M, relay, rounds, rings, scaffold, kind):
     """The same checks over seeded random plans: ranks, clients, sizes, rounds, ring counts."""
     test_push_program_addresses(G, K, M, relay, rounds, rings, scaffold, kind)
+
+
+@pytest.mark.parametrize("G,K,M,relay,rounds,rings,scaffold,kind", [CASES[1], CASES[3], CASES[7], CASES[9]])
+def test_push_program_rebased_to_new_outputs(G, K, M, relay, rounds, rings, scaffold, kind):
+    """A call with the same plan and blocks but outputs at new addresses reuses the program on
+    EVERY rank (the decision cannot differ between ranks: a miss compiles collectively), and the
+    root's launches and landing copies that wrote the old outputs write the new ones at the same
+    offsets; nothing else moves."""
+    plans, progs, allocs, layout = _build(G, K, M, relay, rounds, rings, scaffold, kind)
+    for r in range(G):
+        prog, outs, c = progs[r]
+        fresh = [torch.zeros_like(o) for o in outs]
+        kw = dict(plan=prog.plan, blocks=prog.blocks, accs=[], outs=fresh, kind=kind, scaffold=scaffold, c=c, lr=0.5)
+        assert prog.matches(**kw), r
+        assert not prog.matches(**dict(kw, outs=[torch.zeros(o.numel() + 1, dtype=o.dtype) for o in outs]))
+        span = layout.ld * outs[0].element_size()
+        old = [o.data_ptr() for o in outs]
+
+        def expect(addr):
+            for o, f in zip(old, fresh):
+                if addr and o <= addr < o + span:
+                    return addr - o + f.data_ptr()
+            return addr
+
+        want_runs = [(expect(prog.runs[i].acc), prog.runs[i].acc2) for i in range(prog.nruns)]
+        want_copies = [(expect(prog.copies[i].dst), prog.copies[i].src) for i in range(prog.ncopies)]
+        moved = sum(1 for i in range(prog.nruns) if want_runs[i][0] != prog.runs[i].acc)
+        moved += sum(1 for i in range(prog.ncopies) if want_copies[i][0] != prog.copies[i].dst)
+        assert moved > 0 or r != plans[r].root, (r, moved)  # the root writes its outputs
+        prog.rebase_outs(fresh)
+        assert [(prog.runs[i].acc, prog.runs[i].acc2) for i in range(prog.nruns)] == want_runs
+        assert [(prog.copies[i].dst, prog.copies[i].src) for i in range(prog.ncopies)] == want_copies
+        prog.rebase_outs(fresh)  # same addresses: a no-op
+        assert [(prog.runs[i].acc, prog.runs[i].acc2) for i in range(prog.nruns)] == want_runs

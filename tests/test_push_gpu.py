@@ -151,7 +151,11 @@ def _worker(rank, G, K, rounds, relay, shapes_name, kind, strategy, port, q):
         full_c = _rows(torch, [c], layout, dtype=npdt)[0] if scaffold else None
         lay_out = BucketLayout(range(len(shapes)), shapes, np.float64 if scaffold else np.float32)
         ubits = np.uint64 if scaffold else np.uint32
-        for _ in range(3):  # the cached program, and counters that keep climbing across calls
+        held = []
+        for call in range(3):  # the cached program, and counters that keep climbing across calls
+            if call == 2:  # fresh outputs at new addresses (the old ones held): the program is reused, rebased
+                held.append(outs)
+                outs = [torch.empty_like(o) for o in outs]
             for o in outs:
                 o.fill_(float("nan"))
             if scaffold:
