@@ -102,6 +102,7 @@ def main():
                               "optimizer_steps_per_round": 1, "rounds_timed": len(times),
                               "train_ms_median": round(1e3 * float(np.median(times)), 2),
                               "train_ms_min": round(1e3 * float(np.min(times)), 2),
+                              "train_ms_rounds": [round(1e3 * t, 2) for t in times],
                               "exports_bit_identical": same}), flush=True)
 
 
