@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--layers", type=int, default=24)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--strategies", default="fedavg,scaffold")
+    ap.add_argument("--breakdown", action="store_true",
+                    help="also time each weight_manager call of the accelerated train (synchronised "
+                         "before and after: the total then includes those syncs)")
     args = ap.parse_args()
 
     import torch
@@ -67,6 +70,28 @@ def main():
 
         return (accelerate_algo(Algo) if accelerated else Algo)()
 
+    phases: dict = {}
+    if args.breakdown:
+        import functools
+
+        from substrafl_amd.algorithms import weight_manager as wm
+
+        def timed(name, fn):
+            @functools.wraps(fn)
+            def inner(*a, **k):
+                sync()
+                t = time.perf_counter()
+                try:
+                    return fn(*a, **k)
+                finally:
+                    sync()
+                    phases.setdefault(name, []).append(time.perf_counter() - t)
+            return inner
+
+        for name in ("increment_parameters", "to_device", "get_parameters", "subtract_parameters",
+                     "weighted_sum_parameters", "add_parameters", "set_parameters", "export_numpy"):
+            setattr(wm, name, timed(name, getattr(wm, name)))
+
     params = sum(p.numel() for p in make(TorchFedAvgAlgo, False).model.parameters())
     for strat in args.strategies.split(","):
         base = TorchScaffoldAlgo if strat == "scaffold" else TorchFedAvgAlgo
@@ -75,6 +100,8 @@ def main():
             algo = make(base, path == "accelerate_algo")
             times, shared, outs = [], None, []
             for r in range(args.rounds + 1):
+                if r == 1:
+                    phases.clear()
                 sync()
                 t0 = time.perf_counter()
                 st = algo.train(data_from_opener=data, shared_state=shared, _skip=True)
@@ -95,6 +122,11 @@ def main():
                     shared = FedAvgAveragedState(avg_parameters_update=outs[-1])
             results[path] = times
             exports[path] = outs
+            if phases and path == "accelerate_algo":
+                print(json.dumps({"strategy": strat, "path": path, "breakdown_ms_per_round": {
+                    k: round(1e3 * sum(v) / len(times), 2) for k, v in phases.items()},
+                    "calls_per_round": {k: len(v) / len(times) for k, v in phases.items()}}), flush=True)
+            phases.clear()
         same = all(np.array_equal(a.view(np.uint32), b.view(np.uint32))
                    for ra, rb in zip(exports["reference_torch_loops"], exports["accelerate_algo"]) for a, b in zip(ra, rb))
         for path, times in results.items():
