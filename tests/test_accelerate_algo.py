@@ -98,9 +98,11 @@ def _state(algo):
     return [t.detach().cpu().numpy().copy() for t in algo.model.state_dict().values()]
 
 
-def run_fedavg(accelerated, *, bn, disable_gpu, wire=False):
+def run_fedavg(accelerated, *, bn, disable_gpu, wire=False, copy_exports=False):
     """Two clients, ROUNDS rounds.  Returns every exported update and every client's model state
-    after every train (a trace to compare bit for bit)."""
+    after every train (a trace to compare bit for bit).  ``copy_exports``: the trace keeps copies,
+    so a round's exports are released once the next round's are made (the strategy's pattern),
+    and their host buffers are recycled."""
     from substrafl_amd.integration import accelerate, accelerate_algo
 
     algos = []
@@ -113,7 +115,10 @@ def run_fedavg(accelerated, *, bn, disable_gpu, wire=False):
     for _ in range(ROUNDS):
         states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, DATA)]
         for a, s in zip(algos, states):
-            trace += [("update", list(s.parameters_update)), ("model", _state(a)), ("n", [np.int64(s.n_samples)])]
+            upd = [np.array(u, copy=True) for u in s.parameters_update] if copy_exports else list(s.parameters_update)
+            trace += [("update", upd), ("model", _state(a)), ("n", [np.int64(s.n_samples)])]
+            if copy_exports:
+                trace.append(("ptr", [np.int64(s.parameters_update[0].__array_interface__["data"][0])]))
         if strategy is not None:
             avg = strategy.avg_shared_states(shared_states=states, _skip=True)
         else:
@@ -269,3 +274,34 @@ def test_scaffold_gpu_run_bit_identical(gpu, bn):
     _compare(ref, acc)
     assert states[0].server_control_variate[0].dtype == np.float64
     assert algos[0]._client_control_variate[0].dtype == torch.float64
+
+
+@pytest.mark.gpu
+def test_fedavg_gpu_recycled_export_buffers(gpu):
+    """Exports released round by round (only copies kept) land in recycled host buffers from the
+    third round on -- two clients' exports of round r are still held while round r + 1's are made
+    -- and every value stays the reference's."""
+    ref, _, _ = run_fedavg(False, bn=True, disable_gpu=False, copy_exports=True)
+    acc, _, _ = run_fedavg(True, bn=True, disable_gpu=False, copy_exports=True)
+    ptrs = [int(v[0]) for t, v in acc if t == "ptr"]
+    _compare([x for x in ref if x[0] != "ptr"], [x for x in acc if x[0] != "ptr"])
+    assert len(ptrs) == 2 * ROUNDS and ROUNDS >= 3
+    assert set(ptrs[4:6]) == set(ptrs[0:2]), ptrs  # round 3 reuses round 1's buffers
+    assert not set(ptrs[2:4]) & set(ptrs[0:2]), ptrs  # round 2's could not (round 1's still held)
+
+
+@pytest.mark.gpu
+def test_scaffold_gpu_float64_model_bit_identical(gpu, monkeypatch):
+    """A float64 model under Scaffold: the client's weights, both control variates and the
+    per-step hook all in fp64; bit-identical to the reference's torch loops."""
+    base = _model
+
+    def model64(seed):
+        return base(seed).double()
+
+    monkeypatch.setattr(sys.modules[__name__], "_model", model64)
+    monkeypatch.setattr(sys.modules[__name__], "DATA", [(x.astype(np.float64), y.astype(np.float64)) for x, y in DATA])
+    ref, _, _ = run_scaffold(False, bn=True, disable_gpu=False)
+    acc, _, states = run_scaffold(True, bn=True, disable_gpu=False)
+    _compare(ref, acc)
+    assert states[0].parameters_update[0].dtype == np.float64
