@@ -1514,3 +1514,93 @@ def test_non_native_byte_order_layers(torch_gpu, dummy_algo_class, device):
     rc, ra = scaffold_reference_structure(dpus, cvs, c, ns, 0.7)
     _assert_same(res.server_control_variate, rc)
     _assert_same(res.avg_parameters_update, ra)
+
+
+BIG = 2 ** 32 + 4099  # a client row past 2^32 elements: every 32-bit element or vector index would wrap
+
+
+@pytest.mark.parametrize("kind, K, layout", [("f32", 2, "rows"), ("f32", 2, "tiles"), ("bf16", 3, "rows")])
+def test_rows_beyond_2_32_elements(torch_gpu, kind, K, layout):
+    """Maximum sizes: client rows of 2^32 + 4099 elements (17 GB fp32 each), a ragged tail for
+    the scalar remainder and a numel == 1 layer at index 2^32 + 4098 for the fused pairwise
+    patch; bit-exact on every element against torch eager ops in list order, built in place so
+    the check's own temporaries stay within one GPU's 288 GB."""
+    torch = torch_gpu
+    from substrafl_amd.engine import (FedAvgPlan, TiledFedAvgPlan, fedavg_weights, tiled_client_view, tiled_elems,
+                                      tiled_tile)
+    from substrafl_amd.layout import BucketLayout
+
+    M = BIG
+    lay = BucketLayout(range(2), [(M - 1,), (1,)], np.float32)
+    assert lay.pairwise_idx.tolist() == [M - 1]
+    dt = torch.bfloat16 if kind == "bf16" else torch.float32
+    g = torch.Generator(device="cuda").manual_seed(23)
+    ns = [int(v) for v in np.random.default_rng(23).integers(100, 10000, K)]
+    w = fedavg_weights(ns, kind)
+    out = torch.empty(lay.ld, device="cuda")
+    if layout == "tiles":
+        tv = tiled_tile(kind, K, M)
+        x = torch.zeros(tiled_elems(kind, K, M, tv), device="cuda", dtype=dt)
+        for k in range(K):
+            view = tiled_client_view(x, kind, K, k, tv)  # strided: filled through a contiguous row
+            row = torch.zeros(view.numel(), device="cuda", dtype=dt)
+            row[:M].normal_(generator=g)
+            view.copy_(row.view(view.shape))
+            del row
+
+        def row_of(k):
+            return tiled_client_view(x, kind, K, k, tv).reshape(-1)  # a contiguous copy
+        TiledFedAvgPlan(kind, x, K, w, M, out, lay.pairwise_idx, tv=tv).launch()
+    else:
+        x = torch.empty((K, lay.ld), device="cuda", dtype=dt)
+        for k in range(K):
+            x[k].normal_(generator=g)
+
+        def row_of(k):
+            return x[k]
+        FedAvgPlan(kind, x, w, M, out, lay.pairwise_idx).launch()
+    acc = torch.zeros(M - 1, device="cuda")
+    prods = np.zeros(K, np.float32)
+    for k in range(K):
+        r = row_of(k)
+        acc.add_(r[: M - 1].float() * torch.tensor(w[k], device="cuda"))
+        prods[k] = (r[M - 1: M].float().cpu().numpy() * w[k]).astype(np.float32)[0]
+        del r
+    torch.cuda.synchronize()
+    same = torch.equal(out[: M - 1].view(torch.int32), acc.view(torch.int32))
+    same = same and _bits(np.float32(0.0) + numpy_pairwise_sum(prods)) == _bits(out[M - 1].cpu().numpy())
+    del x, acc, out
+    torch.cuda.empty_cache()
+    assert same
+
+
+def test_scaffold_rows_beyond_2_31_elements(torch_gpu):
+    """Scaffold with rows of 2^31 + 4097 elements (fp64 outputs of 17 GB each): every element
+    bit-exact against torch fp64 eager ops (w*x, +, c last, lr*) on the device."""
+    torch = torch_gpu
+    from substrafl_amd.engine import ScaffoldPlan, scaffold_weights
+
+    K, M = 2, 2 ** 31 + 4097
+    ld = (M + 63) // 64 * 64
+    g = torch.Generator(device="cuda").manual_seed(29)
+    d = torch.randn((K, ld), device="cuda", generator=g)
+    cv = torch.randn((K, ld), device="cuda", generator=g)
+    c = torch.randn(ld, device="cuda", generator=g)
+    w = scaffold_weights([int(v) for v in np.random.default_rng(29).integers(100, 10000, K)])
+    do = torch.empty(ld, dtype=torch.float64, device="cuda")
+    co = torch.empty(ld, dtype=torch.float64, device="cuda")
+    ScaffoldPlan("f32", d, cv, c, w, M, 0.7, do, co).launch()
+    acc = torch.zeros(M, dtype=torch.float64, device="cuda")
+    for k in range(K):
+        acc.add_(torch.tensor(w[k], dtype=torch.float64, device="cuda") * d[k, :M].double())
+    acc.mul_(torch.tensor(0.7, dtype=torch.float64, device="cuda"))  # lr * sum (lr first operand: same product)
+    same = torch.equal(do[:M].view(torch.int64), acc.view(torch.int64))
+    acc.zero_()
+    for k in range(K):
+        acc.add_(torch.tensor(w[k], dtype=torch.float64, device="cuda") * cv[k, :M].double())
+    acc.add_(c[:M].double())
+    torch.cuda.synchronize()
+    same = same and torch.equal(co[:M].view(torch.int64), acc.view(torch.int64))
+    del d, cv, c, do, co, acc
+    torch.cuda.empty_cache()
+    assert same
