@@ -1604,3 +1604,33 @@ def test_scaffold_rows_beyond_2_31_elements(torch_gpu):
     del d, cv, c, do, co, acc
     torch.cuda.empty_cache()
     assert same
+
+
+def test_host_path_rows_beyond_2_32_elements(torch_gpu):
+    """The drop-in host path (pinned-ring staging, kernel, fetch) with two clients whose one layer
+    holds 2^32 + 4099 fp32 elements (17 GB each): every element bit-exact against the reference's
+    arithmetic (fed_avg.py:217-222: fl32(x * fl32(n_k / n)), summed in list order), checked in
+    chunks.  The values repeat with a period of 1_000_003 elements, which does not divide 2^32:
+    a wrapped 32-bit index would read the wrong value."""
+    from substrafl_amd.engine import AggregationEngine, fedavg_weights
+
+    M, P = BIG, 1_000_003
+    rng = np.random.default_rng(31)
+    rows = []
+    for _ in range(2):
+        base = rng.standard_normal(P).astype(np.float32)
+        a = np.empty(M, np.float32)
+        for lo in range(0, M, P * 64):  # block copies: no full-size temporaries
+            hi = min(M, lo + P * 64)
+            a[lo:hi] = np.resize(base, hi - lo) if hi - lo < P * 64 else np.tile(base, 64)
+        rows.append([a])
+    ns = [3, 5]
+    (out,) = AggregationEngine(0).fedavg(rows, ns)
+    w = fedavg_weights(ns, "f32")
+    assert out.shape == (M,) and out.dtype == np.float32
+    step = 1 << 28
+    for lo in range(0, M, step):
+        hi = min(M, lo + step)
+        ref = np.float32(0.0) + rows[0][0][lo:hi] * w[0]
+        ref += rows[1][0][lo:hi] * w[1]
+        assert np.array_equal(ref.view(np.uint32), out[lo:hi].view(np.uint32)), lo
