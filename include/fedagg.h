@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 15
+#define FEDAGG_ABI_VERSION 16
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -543,6 +543,12 @@ int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes
 /* Copy `bytes` from HBM into (pageable) host memory; returns when the data is in h_dst. */
 int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes);
 int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes);
+/* Copy `bytes` between two allocations of the session's GPU, ordered on its stream (the device
+ * hand-off of simulation mode, substrafl_amd/handoff.py: a client's exported bucket into the
+ * aggregator's [K, ld] rows, the aggregator's output into a client's update bucket, instead of a
+ * D2H + H2D round trip; replaces the H2D of `torch.from_numpy(x).to(device)`,
+ * torch_fed_avg_algo.py:189-194, and the staging of fed_avg.py:217-222's inputs). */
+int fedagg_session_copy_d2d(fedagg_session* s, void* d_dst, const void* d_src, uint64_t bytes);
 int fedagg_session_sync(fedagg_session* s);
 /* timing events on the session stream (0 <= ev < FEDAGG_SESSION_EVENTS): record, and the time
  * between two recorded events in ms (waits for ev1) -- per-shard kernel time of the one-process

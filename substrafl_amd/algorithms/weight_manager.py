@@ -203,6 +203,8 @@ def _stage_host_layers(arrays: Sequence[np.ndarray], device) -> torch.Tensor:
     subprocess / docker task inputs), or views of one aggregator output (simulation)."""
     from .. import runtime
 
+    from .. import handoff
+
     idx = device.index if device.index is not None else torch.cuda.current_device()
     layers = [np.ascontiguousarray(a) for a in arrays]
     n = sum(int(a.size) for a in layers)
@@ -213,7 +215,13 @@ def _stage_host_layers(arrays: Sequence[np.ndarray], device) -> torch.Tensor:
         torch.cuda.current_stream(flat.device).synchronize()
         with runtime.device_lock(idx):  # the session's ring is shared with the aggregation engine
             s = runtime.session(idx)
-            s.stage(flat.data_ptr(), n * flat.element_size(), [layers])
+            # simulation mode: an aggregator output (or another client's export) still on this GPU
+            # is copied device to device (handoff.py); otherwise staged through the pinned ring
+            hit = handoff.lookup(list(arrays), idx)
+            if hit is not None and hit[1] == n * flat.element_size():
+                s.copy_d2d(flat.data_ptr(), hit[0], hit[1])
+            else:
+                s.stage(flat.data_ptr(), n * flat.element_size(), [layers])
             s.sync()
     return flat
 
@@ -312,6 +320,9 @@ def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True, tag: str = 
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
     with runtime.device_lock(flat.device.index):  # the session's ring is shared with the engine
         runtime.session(flat.device.index).fetch(flat.data_ptr(), host)
+    from .. import handoff
+
+    handoff.record_tensor(host, flat)  # simulation mode (opt-in): freezes host, keeps flat for the aggregator
     shapes = [tuple(t.shape) for t in tensors]
     if wire:
         return bucket_views(host, shapes)

@@ -574,6 +574,14 @@ int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes)
   return FEDAGG_OK;
 }
 
+int fedagg_session_copy_d2d(fedagg_session* s, void* d_dst, const void* d_src, uint64_t bytes) {
+  if (!s || (bytes && (!d_dst || !d_src))) return FEDAGG_EINVAL;
+  if (!bytes) return FEDAGG_OK;
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, s->stream));
+  return FEDAGG_OK;
+}
+
 int fedagg_session_sync(fedagg_session* s) {
   if (!s) return FEDAGG_EINVAL;
   HIP_TRY(hipSetDevice(s->device));

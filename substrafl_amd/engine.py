@@ -34,7 +34,7 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
-from . import _native, runtime
+from . import _native, handoff, runtime
 from .layout import BucketLayout
 from .wire import flat_of
 
@@ -359,6 +359,7 @@ def serialized(method):
             lib = _native.load()
             if lib.fedagg_device_get(ctypes.byref(dev)) != 0:
                 dev.value = -1
+            handoff.invalidate_slots(self.lock_devices())  # this call may rewrite its output slots
             return method(self, *args, **kwargs)
         finally:
             if lib is not None and dev.value >= 0:
@@ -632,6 +633,27 @@ class AggregationEngine:
                     s.cast(tmp, a.dtype, dst, layout.dtype, a.size)
                 s.sync()  # tmp is reused by the next segment's stage
 
+    _last_handoff: List[bool] = []
+
+    def _handoff_rows(self, s, rows: List[List[np.ndarray]], layout: BucketLayout, R: np.dtype, K: int) -> Optional[int]:
+        """Simulation mode (``handoff``): client rows whose bytes are still on this GPU (an
+        ``accelerate_algo`` export recorded with its device bucket) are copied device to device
+        into the ``[K, ld]`` rows; the others are staged from the host as usual.  None when no
+        row can be handed off (the caller stages everything, tiled where recommended)."""
+        hits = [handoff.lookup(row, s.device) for row in rows]
+        self._last_handoff = [h is not None and h[1] == layout.M * R.itemsize for h in hits]
+        if not any(self._last_handoff):
+            return None
+        ld_bytes = layout.ld * R.itemsize
+        d_bucket = s.buffer(self._B_BUCKET, K * ld_bytes)
+        for k, (row, h, ok) in enumerate(zip(rows, hits, self._last_handoff)):
+            if ok:
+                s.copy_d2d(d_bucket + k * ld_bytes, h[0], h[1])
+            else:
+                self._stage_rows(s, [row], layout, d_bucket + k * ld_bytes)
+        s.sync()  # the copies' sources are kept alive by `hits` only until here
+        return d_bucket
+
     # ----------------------------------------------------------------------------------
     @serialized
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
@@ -696,8 +718,14 @@ class AggregationEngine:
                         staged, d_bucket, tv = True, d_t, -rec[1]
                 else:
                     staged = self._take_prestaged(self._B_BUCKET, d_bucket, layout.ld * R.itemsize, rows)
+            if not staged and prescale is None and len(groups) == 1:
+                hand = self._handoff_rows(s, rows, layout, R, K)
+                if hand is not None:
+                    self._prestaged.pop(self._B_BUCKET, None)
+                    staged, d_bucket = True, hand
+                    tm["handoff_rows"] = sum(1 for r in self._last_handoff if r)
             if staged:
-                tm["prestaged"] = True
+                tm["prestaged"] = not tm.get("handoff_rows")
             else:
                 self._prestaged.pop(self._B_BUCKET, None)
                 tiled = self._tiled_rows(rows, R, kind, K, layout.M) if prescale is None else None
@@ -720,6 +748,8 @@ class AggregationEngine:
                 FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
             out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}")
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
+            if len(groups) == 1:
+                handoff.record_slot(out, s, self._B_OUT, d_out)  # simulation mode: clients copy it on the device
             tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
             for li, arr in layout.unpack(out, wire):
                 results[li] = arr

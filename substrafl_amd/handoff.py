@@ -1,0 +1,193 @@
+"""Device hand-off of simulation-mode buckets (opt-in: ``FEDAGG_HANDOFF=1`` or :func:`enable`).
+
+In ``simulate_experiment`` every organisation's ``train`` and the aggregation run in ONE process
+on the same GPU (``SimuTrainDataNode.update_states`` /
+``SimuAggregationNode.update_states``, nodes/train_data_node.py:336-382,
+nodes/aggregation_node.py:197-227): a client's update is fetched to the host
+(``.cpu().numpy()``, torch_fed_avg_algo.py:227-230) only for the aggregator to stage the same
+bytes back to the GPU (fed_avg.py:217-222), and the average makes the same round trip into every
+client (torch_fed_avg_algo.py:189-194).  The host arrays are still produced -- they are what the
+reference's schemas, pickles and ``model_loading`` see -- but each one that left a device bucket
+is recorded here with that bucket, and a consumer on the same GPU copies device to device
+(``fedagg_session_copy_d2d``) instead of over PCIe.
+
+What makes a record usable (all checked at every lookup, anything else falls back to the host
+copy, so results never depend on the hand-off):
+
+* the arrays handed in are, in order, views covering exactly the recorded byte range of the
+  recorded host buffer, and the consumer is on the recorded GPU;
+* that buffer and the views are read-only: a hand-off FREEZES the exported arrays (and the buffer
+  they view), so what the host holds is what the device holds.  This is the one visible change
+  of the opt-in: the reference's exports are writable arrays; nothing in the reference writes into
+  a shared state (the strategies, ``model_loading`` and the pickles only read them);
+* a recorded torch tensor has not been modified in place since (``tensor._version``);
+* a recorded engine output slot has not been written since: every engine call invalidates the
+  slot records of its GPUs (``engine.serialized``), and the slot's write generation is unchanged.
+
+A process that never enables the hand-off records nothing, and every lookup is a dictionary miss.
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+import weakref
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_enabled = os.environ.get("FEDAGG_HANDOFF", "0") == "1"
+_lock = threading.Lock()
+_records: Dict[int, "_Record"] = {}  # start address of the recorded host byte range -> record
+stats = {"recorded": 0, "taken": 0, "refused": 0}  # counters (tests, benches)
+
+
+def enable(flag: bool = True) -> None:
+    """Turn the device hand-off on (or off) for this process; off drops every record."""
+    global _enabled
+    _enabled = bool(flag)
+    if not _enabled:
+        with _lock:
+            _records.clear()
+            for fin in _finalizers.values():
+                fin.detach()
+            _finalizers.clear()
+
+
+def enabled() -> bool:
+    return _enabled
+
+
+class _Record:
+    __slots__ = ("base", "start", "nbytes", "dtype", "device", "tensor", "version", "session", "slot", "gen",
+                 "dptr", "valid")
+
+    def __init__(self, base, start, nbytes, dtype, device):
+        self.base = weakref.ref(base)
+        self.start, self.nbytes, self.dtype, self.device = start, nbytes, dtype, device
+        self.tensor = self.version = self.session = self.slot = self.gen = None
+        self.dptr = 0
+        self.valid = True
+
+
+def _owner(a: np.ndarray) -> np.ndarray:
+    while isinstance(a.base, np.ndarray):
+        a = a.base
+    return a
+
+
+def span(arrays: Sequence[np.ndarray]) -> Optional[Tuple[np.ndarray, int, int, np.dtype]]:
+    """(owning buffer, start address, bytes, dtype) when ``arrays`` are C-contiguous views of one
+    buffer, back to back in order, all of one dtype; else None."""
+    arrays = list(arrays)
+    if not arrays or not all(isinstance(a, np.ndarray) for a in arrays):
+        return None
+    dt = arrays[0].dtype
+    base = _owner(arrays[0])
+    start = arrays[0].__array_interface__["data"][0]
+    off = start
+    for a in arrays:
+        if a.dtype != dt or not a.flags.c_contiguous or _owner(a) is not base:
+            return None
+        if a.__array_interface__["data"][0] != off:
+            return None
+        off += a.nbytes
+    return base, start, off - start, dt
+
+
+def _freeze(host: np.ndarray) -> np.ndarray:
+    host.flags.writeable = False
+    base = _owner(host)
+    base.flags.writeable = False
+    return base
+
+
+_finalizers: Dict[int, weakref.finalize] = {}  # start address -> the finalizer of the buffer recorded there
+
+
+def _put(host: np.ndarray, device: int) -> _Record:
+    base = _freeze(host)
+    start = host.__array_interface__["data"][0]
+    rec = _Record(base, start, host.nbytes, host.dtype, int(device))
+    with _lock:
+        _records[start] = rec  # replaces (and releases) an earlier record of a recycled buffer
+        stats["recorded"] += 1
+        fin = _finalizers.get(start)
+        if fin is None or not fin.alive or fin.peek()[0] is not base:
+            # one finalizer per buffer, holding nothing but the address: the record (and the
+            # device bucket it keeps alive) goes when the host buffer does
+            _finalizers[start] = weakref.finalize(base, _drop, start)
+    return rec
+
+
+def _drop(start: int) -> None:
+    with _lock:
+        rec = _records.get(start)
+        if rec is not None and rec.base() is None:
+            del _records[start]
+        fin = _finalizers.get(start)
+        if fin is not None and not fin.alive:
+            del _finalizers[start]
+
+
+def record_tensor(host: np.ndarray, flat) -> None:
+    """``host`` (1-D, the exported bytes, C-contiguous) was fetched from the torch tensor ``flat``
+    (same bytes, on a GPU): freeze ``host`` and remember ``flat`` for device consumers."""
+    if not _enabled or not getattr(flat, "is_cuda", False) or host.nbytes != flat.numel() * flat.element_size():
+        return
+    rec = _put(host, flat.device.index)
+    rec.tensor, rec.version, rec.dptr = flat, flat._version, int(flat.data_ptr())
+
+
+def record_slot(host: np.ndarray, session, slot: int, dptr: int) -> None:
+    """``host`` was fetched from session buffer ``slot`` at ``dptr`` (an engine output): freeze it
+    and remember the slot, valid until the slot is written again."""
+    if not _enabled:
+        return
+    rec = _put(host, session.device)
+    rec.session, rec.slot, rec.gen, rec.dptr = session, int(slot), session.generation(slot), int(dptr)
+
+
+def invalidate_slots(devices: Iterable[int]) -> None:
+    """An engine call on ``devices`` is about to write its session buffers: their slot records
+    stop being usable (called by ``engine.serialized`` under the device locks)."""
+    if not _records:
+        return
+    devs = {int(d) for d in devices}
+    with _lock:
+        for rec in _records.values():
+            if rec.slot is not None and rec.device in devs:
+                rec.valid = False
+
+
+def lookup(arrays: Sequence[np.ndarray], device: int) -> Optional[Tuple[int, int, object]]:
+    """``(device pointer, bytes, keep-alive)`` of a usable record whose bytes ``arrays`` are
+    (module docstring), else None."""
+    if not _records:
+        return None
+    sp = span(arrays)
+    if sp is None:
+        return None
+    base, start, nbytes, dt = sp
+    with _lock:
+        rec = _records.get(start)
+    if rec is None:
+        return None
+    ok = (rec.valid and rec.base() is base and rec.nbytes == nbytes and rec.dtype == dt and rec.device == int(device)
+          and not base.flags.writeable and not any(a.flags.writeable for a in arrays))
+    if ok and rec.tensor is not None:
+        ok = rec.tensor._version == rec.version and int(rec.tensor.data_ptr()) == rec.dptr
+    if ok and rec.slot is not None:
+        ok = rec.session.generation(rec.slot) == rec.gen
+    with _lock:
+        stats["taken" if ok else "refused"] += 1
+    if not ok:
+        return None
+    return rec.dptr, nbytes, (rec.tensor if rec.tensor is not None else rec.session)
+
+
+def records() -> List[dict]:
+    """The live records (tests, diagnostics)."""
+    with _lock:
+        return [{"start": r.start, "bytes": r.nbytes, "dtype": str(r.dtype), "device": r.device,
+                 "kind": "tensor" if r.tensor is not None else "slot", "valid": r.valid} for r in _records.values()]

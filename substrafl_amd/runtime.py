@@ -223,6 +223,12 @@ class Session:
         _native.check(self.lib.fedagg_session_memset(self._h, ctypes.c_void_p(d), int(value), int(nbytes)),
                       "session_memset")
 
+    def copy_d2d(self, d_dst: int, d_src: int, nbytes: int) -> None:
+        """Device-to-device copy on the session stream (``fedagg_session_copy_d2d``)."""
+        self._bump(d_dst)
+        _native.check(self.lib.fedagg_session_copy_d2d(self._h, ctypes.c_void_p(d_dst), ctypes.c_void_p(d_src),
+                                                       int(nbytes)), "session_copy_d2d")
+
     def sync(self) -> None:
         _native.check(self.lib.fedagg_session_sync(self._h), "session_sync")
 
@@ -303,6 +309,7 @@ def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
             # references: the pool list, the local name and getrefcount's argument; a live view adds one
             if buf.size >= n and sys.getrefcount(buf) <= 3:
                 pool.append(pool.pop(i))  # most recently used last
+                buf.flags.writeable = True  # a device hand-off (handoff.py) may have frozen it
                 return buf[:n]
         buf = np.empty(n, dtype=key[1])
         pool.append(buf)

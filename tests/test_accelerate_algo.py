@@ -305,3 +305,73 @@ def test_scaffold_gpu_float64_model_bit_identical(gpu, monkeypatch):
     acc, _, states = run_scaffold(True, bn=True, disable_gpu=False)
     _compare(ref, acc)
     assert states[0].parameters_update[0].dtype == np.float64
+
+
+@pytest.fixture()
+def handoff_on():
+    from substrafl_amd import handoff
+
+    handoff.enable(True)
+    yield handoff
+    handoff.enable(False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
+def test_fedavg_gpu_handoff_bit_identical(gpu, bn):
+    """Simulation mode with the device hand-off (substrafl_amd/handoff.py): the clients' exports
+    reach the aggregator, and the average reaches the clients, device to device -- every exported
+    update, average and model state still bit-identical to the reference sequence's."""
+    from substrafl_amd import handoff
+
+    ref, _, _ = run_fedavg(False, bn=bn, disable_gpu=False)
+    handoff.enable(True)
+    try:
+        t0 = handoff.stats["taken"]
+        acc, _, states = run_fedavg(True, bn=bn, disable_gpu=False)
+        taken = handoff.stats["taken"] - t0
+    finally:
+        handoff.enable(False)
+    _compare(ref, acc)
+    # every round's 2 client rows, and the 2 clients' update applies of rounds 2 and 3
+    assert taken >= 2 * ROUNDS + 2 * (ROUNDS - 1), taken
+    assert not any(a.flags.writeable for a in states[0].parameters_update)  # the opt-in's visible change
+
+
+@pytest.mark.gpu
+def test_fedavg_gpu_handoff_refuses_a_thawed_export(gpu, handoff_on):
+    """An export whose buffer was thawed and written is staged from the host, not copied from the
+    device: the aggregate is the reference's over the MODIFIED values."""
+    from substrafl_amd.integration import accelerate, accelerate_algo
+
+    algos = [accelerate_algo(_algo(TorchFedAvgAlgo, bn=False, disable_gpu=False, client=k))() for k in range(2)]
+    strategy = accelerate(ss.FedAvg)(algo=algos[0])
+    states = [a.train(data_from_opener=d, shared_state=None, _skip=True) for a, d in zip(algos, DATA)]
+    pu = list(states[0].parameters_update)
+    base = pu[0].base
+    while isinstance(base.base, np.ndarray):
+        base = base.base
+    base.flags.writeable = True
+    for a in pu:
+        a.flags.writeable = True
+        a *= np.float32(3.0)
+    refused = handoff_on.stats["refused"]
+    avg = strategy.avg_shared_states(shared_states=states, _skip=True)
+    assert handoff_on.stats["refused"] > refused
+    _same(avg.avg_parameters_update, fedavg_explicit([list(s.parameters_update) for s in states],
+                                                     [s.n_samples for s in states]))
+
+
+@pytest.mark.gpu
+def test_scaffold_gpu_handoff_bit_identical(gpu):
+    """Scaffold clients with the hand-off on: their server control variate and update applies
+    take the device copies where recorded; bit-identical to the reference sequence."""
+    from substrafl_amd import handoff
+
+    ref, _, _ = run_scaffold(False, bn=True, disable_gpu=False)
+    handoff.enable(True)
+    try:
+        acc, _, _ = run_scaffold(True, bn=True, disable_gpu=False)
+    finally:
+        handoff.enable(False)
+    _compare(ref, acc)
