@@ -654,6 +654,32 @@ class AggregationEngine:
         s.sync()  # the copies' sources are kept alive by `hits` only until here
         return d_bucket
 
+    def _handoff_into(self, s, rows: List[List[np.ndarray]], lay: BucketLayout, d: int) -> bool:
+        """All K rows recorded by the hand-off (one source dtype): copied device to device into
+        ``[K, lay.ld]`` of ``lay.dtype`` at ``d`` -- through one exact device cast when the
+        recorded bytes are of another float type (Scaffold's fp32 deltas into its fp64 buckets),
+        as ``_stage_rows`` does for host rows.  False (nothing written) otherwise."""
+        hits = [handoff.lookup(row, s.device) for row in rows]
+        if not hits or any(h is None for h in hits):
+            return False
+        src = {row[0].dtype for row in rows}
+        if len(src) != 1:
+            return False
+        (sdt,) = src
+        if any(h[1] != lay.M * sdt.itemsize for h in hits):
+            return False
+        K = len(rows)
+        if sdt == lay.dtype:
+            for k, h in enumerate(hits):
+                s.copy_d2d(d + k * lay.ld * sdt.itemsize, h[0], h[1])
+        else:
+            tmp = s.buffer(self._B_TMP, K * lay.ld * sdt.itemsize)
+            for k, h in enumerate(hits):
+                s.copy_d2d(tmp + k * lay.ld * sdt.itemsize, h[0], h[1])
+            s.cast(tmp, sdt, d, lay.dtype, K * lay.ld)
+        s.sync()  # the copies' sources are kept alive by `hits` only until here
+        return True
+
     # ----------------------------------------------------------------------------------
     @serialized
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
@@ -879,6 +905,8 @@ class AggregationEngine:
             rows = [list(r) for r in rows]
             if self._take_prestaged(slot, d, lay.ld * isz, rows):
                 pre += 1
+            elif self._handoff_into(s, rows, lay, d):  # simulation mode: the clients' exports, on the device
+                tm["handoff_rows"] = tm.get("handoff_rows", 0) + len(rows)
             else:
                 self._stage_rows(s, rows, lay, d)
         c_rows = [list(r) for r in server_control_variates]
@@ -927,6 +955,8 @@ class AggregationEngine:
         s.fetch(cnt, mism)
         s.fetch(dout, out_d)
         s.fetch(cout, out_c)
+        handoff.record_slot(out_d, s, self._B_OUT, dout)  # simulation mode: the clients copy them on the device
+        handoff.record_slot(out_c, s, self._B_COUT, cout)
         tm["kernel_fetch_s"] = time.perf_counter() - t1
         avg = [a for _, a in lay_d.unpack(out_d, wire)]
         new_c = [a for _, a in lay_c.unpack(out_c, wire)]

@@ -364,14 +364,21 @@ def test_fedavg_gpu_handoff_refuses_a_thawed_export(gpu, handoff_on):
 
 @pytest.mark.gpu
 def test_scaffold_gpu_handoff_bit_identical(gpu):
-    """Scaffold clients with the hand-off on: their server control variate and update applies
-    take the device copies where recorded; bit-identical to the reference sequence."""
+    """Scaffold with the hand-off on: the clients' delta and control-variate exports reach the
+    aggregator's fp64 buckets device to device (the fp32 deltas through the exact device cast),
+    and the averaged update and new server control variate reach the clients the same way;
+    bit-identical to the reference sequence."""
     from substrafl_amd import handoff
 
     ref, _, _ = run_scaffold(False, bn=True, disable_gpu=False)
     handoff.enable(True)
     try:
+        t0 = handoff.stats["taken"]
         acc, _, _ = run_scaffold(True, bn=True, disable_gpu=False)
+        taken = handoff.stats["taken"] - t0
     finally:
         handoff.enable(False)
     _compare(ref, acc)
+    # every round: 2 delta + 2 cv rows into the aggregator; rounds 2-3: each client's update
+    # apply and server control variate
+    assert taken >= 4 * ROUNDS + 4 * (ROUNDS - 1), taken
