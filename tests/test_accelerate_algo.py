@@ -382,3 +382,25 @@ def test_scaffold_gpu_handoff_bit_identical(gpu):
     # every round: 2 delta + 2 cv rows into the aggregator; rounds 2-3: each client's update
     # apply and server control variate
     assert taken >= 4 * ROUNDS + 4 * (ROUNDS - 1), taken
+
+
+@pytest.mark.gpu
+def test_scaffold_gpu_handoff_device_c_check_catches_a_mismatch(gpu, handoff_on):
+    """With every client's server control variate handed off, the aggregator checks their equality
+    on the device over the recorded copies (scaffold.py:193-196): a client that trained against a
+    different c still makes the aggregation raise the reference's AssertionError."""
+    from substrafl_amd.integration import accelerate, accelerate_algo
+
+    algos = [accelerate_algo(_algo(TorchScaffoldAlgo, bn=False, disable_gpu=False, client=k))() for k in range(2)]
+    strategy = accelerate(ss.Scaffold)(algo=algos[0], aggregation_lr=0.7)
+    states = [a.train(data_from_opener=d, shared_state=None, _skip=True) for a, d in zip(algos, DATA)]
+    avg = strategy.avg_shared_states(shared_states=states, _skip=True)
+    other = sch.ScaffoldAveragedStates(  # client 1 is sent another c (host arrays, not recorded)
+        avg_parameters_update=[np.array(a) for a in avg.avg_parameters_update],
+        server_control_variate=[np.array(c) + 1.0 for c in avg.server_control_variate])
+    states = [algos[0].train(data_from_opener=DATA[0], shared_state=avg, _skip=True),
+              algos[1].train(data_from_opener=DATA[1], shared_state=other, _skip=True)]
+    taken = handoff_on.stats["taken"]
+    with pytest.raises(AssertionError):
+        strategy.avg_shared_states(shared_states=states, _skip=True)
+    assert handoff_on.stats["taken"] - taken >= 6  # deltas, control variates and both c copies
