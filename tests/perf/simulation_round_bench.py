@@ -14,7 +14,7 @@ model, data and seeds:
 
 Every round's average is compared bit for bit across the paths.  One JSON line per path.
 
-    python3 tools/simulation_round_bench.py --strategy fedavg --clients 8 --params 25000000 --rounds 5
+    python3 tests/perf/simulation_round_bench.py --strategy fedavg --clients 8 --params 25000000 --rounds 5
 """
 
 from __future__ import annotations
@@ -27,7 +27,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

@@ -50,7 +50,9 @@ def test_wheel_carries_the_library_and_installs(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     pkg, lib, abi = r.stdout.split()
     assert pkg.startswith(str(tmp_path / "site")) and lib == str(tmp_path / "site" / "substrafl_amd" / "libfedagg.so")
-    assert int(abi) == 15
+    from substrafl_amd import _native
+
+    assert int(abi) == _native.ABI_VERSION
 
 
 def test_wheel_build_without_hipcc_fails_loudly(tmp_path):
