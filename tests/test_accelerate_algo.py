@@ -404,3 +404,22 @@ def test_scaffold_gpu_handoff_device_c_check_catches_a_mismatch(gpu, handoff_on)
     with pytest.raises(AssertionError):
         strategy.avg_shared_states(shared_states=states, _skip=True)
     assert handoff_on.stats["taken"] - taken >= 6  # deltas, control variates and both c copies
+
+
+@pytest.mark.gpu
+def test_handoff_device_memory_stays_flat_over_rounds(gpu, handoff_on):
+    """The hand-off's records keep the exported device buckets alive only while their host arrays
+    live: over many rounds of 4 clients the allocated device memory reaches a steady state."""
+    from substrafl_amd.integration import accelerate, accelerate_algo
+
+    algos = [accelerate_algo(_algo(TorchFedAvgAlgo, bn=True, disable_gpu=False, client=k % 2))() for k in range(4)]
+    strategy = accelerate(ss.FedAvg)(algo=algos[0])
+    data = [DATA[k % 2] for k in range(4)]
+    avg, used = None, []
+    for _ in range(8):
+        states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, data)]
+        avg = strategy.avg_shared_states(shared_states=states, _skip=True)
+        torch.cuda.synchronize()
+        used.append(torch.cuda.memory_allocated())
+    assert used[-1] == used[3], used
+    assert len(handoff_on.records()) <= 4 * 4 + 8, handoff_on.records()
