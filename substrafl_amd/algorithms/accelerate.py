@@ -111,13 +111,16 @@ def _scaffold_train(shared_state_cls, fast_rule, update_error):
             assert self._server_control_variate is None
             self._server_control_variate = wm.zeros_like_parameters(self.model, with_batch_norm_parameters=bn,
                                                                     device=self._device)
+            self._fedagg_c_host = None
         else:
             assert self._client_control_variate is not None
             assert gen.n_samples is not None
             # avg_parameters_update already carries aggregation_lr (scaffold.py:293)
             wm.increment_parameters(self._model, list(shared_state.avg_parameters_update),
                                     with_batch_norm_parameters=bn)
-            self._server_control_variate = wm.to_device(shared_state.server_control_variate, self._device)
+            c_host = list(shared_state.server_control_variate)
+            self._server_control_variate = wm.to_device(c_host, self._device)
+            self._fedagg_c_host = _frozen_source(c_host, self._server_control_variate)
         gen.reset_counter()
         before = wm.get_parameters(self._model, with_batch_norm_parameters=bn)
         # c_i - c, added lr-scaled after every optimizer step by _scaffold_parameters_update
@@ -144,12 +147,43 @@ def _scaffold_train(shared_state_cls, fast_rule, update_error):
         self._client_control_variate = wm.add_parameters(self._client_control_variate, cv_update)
         wm.set_parameters(self._model, before, with_batch_norm_parameters=bn)
         # one recycled host buffer per list: the three are alive together until the next round
+        c_out = _unchanged_source(getattr(self, "_fedagg_c_host", None), self._server_control_variate)
         return shared_state_cls(parameters_update=_export(self, delta),
                                 control_variate_update=_export(self, cv_update, "export_cv"),
-                                server_control_variate=_export(self, self._server_control_variate, "export_c"),
+                                server_control_variate=(c_out if c_out is not None else
+                                                        _export(self, self._server_control_variate, "export_c")),
                                 n_samples=len(train_dataset))
 
     return train
+
+
+def _frozen_source(host: list, tensors):
+    """Simulation mode with the device hand-off (``handoff``): the server control variate's host
+    arrays as received, when they are frozen (an engine output) -- the client's export of c may
+    then return them instead of copying the same bytes back from the device."""
+    from .. import handoff
+
+    flat = wm.flat_bucket(list(tensors)) if tensors else None
+    if not handoff.enabled() or flat is None or not handoff.frozen(host):
+        return None
+    return host, flat, flat._version
+
+
+def _unchanged_source(rec, tensors):
+    """The recorded host arrays of c (``_frozen_source``) if they are still frozen and the device
+    bucket still holds what was copied from them (not modified in place since); else None.  The
+    export then returns those very arrays (read-only, the same bytes the reference's
+    ``.cpu().numpy()`` would produce), which also lets the aggregator see every client's c as one
+    object (its identity shortcut of scaffold.py:193-196)."""
+    from .. import handoff
+
+    if rec is None or not handoff.enabled():
+        return None
+    host, flat, version = rec
+    cur = wm.flat_bucket(list(tensors)) if tensors else None
+    if cur is None or cur.data_ptr() != flat.data_ptr() or flat._version != version or not handoff.frozen(host):
+        return None
+    return list(host)
 
 
 def _scaffold_parameters_update(self):

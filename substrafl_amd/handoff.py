@@ -95,6 +95,13 @@ def span(arrays: Sequence[np.ndarray]) -> Optional[Tuple[np.ndarray, int, int, n
     return base, start, off - start, dt
 
 
+def frozen(arrays: Sequence[np.ndarray]) -> bool:
+    """Every array, and the buffer it views, read-only (what a hand-off record leaves behind)."""
+    arrays = list(arrays)
+    return bool(arrays) and all(isinstance(a, np.ndarray) and not a.flags.writeable
+                                and not _owner(a).flags.writeable for a in arrays)
+
+
 def _freeze(host: np.ndarray) -> np.ndarray:
     host.flags.writeable = False
     base = _owner(host)
