@@ -60,7 +60,7 @@ def enabled() -> bool:
 
 class _Record:
     __slots__ = ("base", "start", "nbytes", "dtype", "device", "tensor", "version", "session", "slot", "gen",
-                 "dptr", "valid")
+                 "dptr", "valid", "stable")
 
     def __init__(self, base, start, nbytes, dtype, device):
         self.base = weakref.ref(base)
@@ -68,6 +68,7 @@ class _Record:
         self.tensor = self.version = self.session = self.slot = self.gen = None
         self.dptr = 0
         self.valid = True
+        self.stable = False
 
 
 def _owner(a: np.ndarray) -> np.ndarray:
@@ -146,13 +147,16 @@ def record_tensor(host: np.ndarray, flat) -> None:
     rec.tensor, rec.version, rec.dptr = flat, flat._version, int(flat.data_ptr())
 
 
-def record_slot(host: np.ndarray, session, slot: int, dptr: int) -> None:
+def record_slot(host: np.ndarray, session, slot: int, dptr: int, stable: bool = False) -> None:
     """``host`` was fetched from session buffer ``slot`` at ``dptr`` (an engine output): freeze it
-    and remember the slot, valid until the slot is written again."""
+    and remember the slot, valid until the slot is written again.  ``stable``: a slot that only
+    the runtime's own copies write (each bumps its generation), so engine calls on the device do
+    not invalidate the record -- the next call can still read it before replacing it."""
     if not _enabled:
         return
     rec = _put(host, session.device)
     rec.session, rec.slot, rec.gen, rec.dptr = session, int(slot), session.generation(slot), int(dptr)
+    rec.stable = bool(stable)
 
 
 def invalidate_slots(devices: Iterable[int]) -> None:
@@ -163,7 +167,7 @@ def invalidate_slots(devices: Iterable[int]) -> None:
     devs = {int(d) for d in devices}
     with _lock:
         for rec in _records.values():
-            if rec.slot is not None and rec.device in devs:
+            if rec.slot is not None and not rec.stable and rec.device in devs:
                 rec.valid = False
 
 

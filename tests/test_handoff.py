@@ -136,3 +136,17 @@ def test_record_goes_with_its_buffer(on):
     del buf
     gc.collect()
     assert not any(r["start"] == start for r in handoff.records())
+
+
+def test_stable_slot_survives_engine_calls_not_writes(on):
+    """A stable slot (written only by the runtime's own copies) outlives the invalidation of an
+    engine call on its device -- the next Scaffold call reads it back as the clients' c -- and is
+    refused once the slot is written again (its generation)."""
+    s = _Session()
+    host = _export(tag="handoff_s")
+    handoff.record_slot(host, s, 12, 0x3000, stable=True)
+    views = _views(host)
+    handoff.invalidate_slots([0])
+    assert handoff.lookup(views, 0)[0] == 0x3000
+    s.gen[12] = 1
+    assert handoff.lookup(views, 0) is None
