@@ -312,16 +312,15 @@ def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True, tag: str = 
     flat = flat_bucket(list(tensors))
     if flat is None or not flat.is_cuda:
         return [t.cpu().detach().numpy() for t in tensors]
-    from .. import runtime
+    from .. import handoff, runtime
 
-    # one D2H through the native session's pinned ring (chunked, copied out by its worker pool)
+    # one D2H: through the native session's pinned ring (chunked, copied out by its worker pool),
+    # or straight into a pinned buffer in simulation mode with the hand-off on (recycled pools)
     host = runtime.reusable_host_array(flat.numel(), torch.empty(0, dtype=flat.dtype).numpy().dtype,
-                                       tag)  # bf16 raises, as .numpy()
+                                       tag, pinned=handoff.enabled())  # bf16 raises, as .numpy()
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
     with runtime.device_lock(flat.device.index):  # the session's ring is shared with the engine
         runtime.session(flat.device.index).fetch(flat.data_ptr(), host)
-    from .. import handoff
-
     handoff.record_tensor(host, flat)  # simulation mode (opt-in): freezes host, keeps flat for the aggregator
     shapes = [tuple(t.shape) for t in tensors]
     if wire:

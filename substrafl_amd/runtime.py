@@ -290,7 +290,35 @@ _host_lock = threading.Lock()
 HOST_POOL_DEPTH = 4  # recycled buffers kept per call site and dtype
 
 
-def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
+pinned_blocks = {"allocated": 0, "freed": 0}  # fedagg_host_alloc / _free calls (tests)
+
+
+def _pinned_free(ptr: int) -> None:
+    try:
+        _native.load().fedagg_host_free(ctypes.c_void_p(ptr))
+    except Exception:  # noqa: BLE001 -- interpreter shutdown
+        pass
+    pinned_blocks["freed"] += 1
+
+
+def pinned_empty(n: int, dtype) -> np.ndarray:
+    """An ``n``-element array in a pinned host block (``fedagg_host_alloc``): a fetch into it is one
+    direct D2H DMA.  Freed when the array and every view of it are gone (views of it hold it:
+    NumPy points them at this array, which does not own its memory)."""
+    import weakref
+
+    dt = np.dtype(dtype)
+    nbytes = max(1, int(n) * dt.itemsize)
+    p = ctypes.c_void_p()
+    _native.check(_native.load().fedagg_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
+    raw = (ctypes.c_char * nbytes).from_address(int(p.value))
+    arr = np.frombuffer(raw, dtype=dt, count=int(n))
+    weakref.finalize(arr, _pinned_free, int(p.value))
+    pinned_blocks["allocated"] += 1
+    return arr
+
+
+def reusable_host_array(n: int, dtype, tag: str, pinned: bool = False) -> np.ndarray:
     """A host array of ``n`` elements for a D2H result (``tag`` names the call site).  A fresh
     100 MB allocation costs ~8 ms of first-touch page faults (glibc maps every block above 32 MiB
     anew), three times the D2H itself, so earlier calls' buffers are recycled -- but only one that
@@ -298,10 +326,12 @@ def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
     caller ever sees its data change.  Up to ``HOST_POOL_DEPTH`` buffers per site: in simulation
     mode the previous round's results are still held while the next round's are made (the
     strategy keeps its last train states, and its last average, until the new ones are returned),
-    so with one buffer per site every call after the first would fault a fresh one."""
+    so with one buffer per site every call after the first would fault a fresh one.  ``pinned``:
+    buffers of pinned host blocks (``pinned_empty``), a separate pool -- simulation mode, where
+    the pools recycle, so the pinning is paid once (handoff.py)."""
     import sys
 
-    key = (tag, np.dtype(dtype))
+    key = (tag, np.dtype(dtype), bool(pinned))
     with _host_lock:
         pool = _host_cache.setdefault(key, [])
         for i in range(len(pool)):  # (not enumerate: its cached result tuple would hold one more reference)
@@ -311,7 +341,7 @@ def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
                 pool.append(pool.pop(i))  # most recently used last
                 buf.flags.writeable = True  # a device hand-off (handoff.py) may have frozen it
                 return buf[:n]
-        buf = np.empty(n, dtype=key[1])
+        buf = pinned_empty(n, key[1]) if pinned else np.empty(n, dtype=key[1])
         pool.append(buf)
         if len(pool) > HOST_POOL_DEPTH:
             pool.pop(0)  # the least recently used; still alive through its holders' views, if any

@@ -226,5 +226,5 @@ def test_host_result_buffers_pooled_across_held_rounds():
         held = nxt  # the previous round's result is released here
     assert len(set(ptrs)) == 2, ptrs
     keep = [runtime.reusable_host_array(10, np.float64, "pool_cap") for _ in range(runtime.HOST_POOL_DEPTH + 3)]
-    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64))]) == runtime.HOST_POOL_DEPTH
+    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64), False)]) == runtime.HOST_POOL_DEPTH
     assert len({a.__array_interface__["data"][0] for a in keep}) == len(keep)  # every live one distinct
