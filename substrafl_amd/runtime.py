@@ -287,7 +287,8 @@ def device_lock(device: int) -> threading.RLock:
 
 _host_cache: Dict[tuple, list] = {}
 _host_lock = threading.Lock()
-HOST_POOL_DEPTH = 4  # recycled buffers kept per call site and dtype
+HOST_POOL_DEPTH = 64  # buffers kept per call site and dtype (and pinned or not) ...
+HOST_POOL_BYTES = 16 << 30  # ... within this many bytes
 
 
 pinned_blocks = {"allocated": 0, "freed": 0}  # fedagg_host_alloc / _free calls (tests)
@@ -323,10 +324,12 @@ def reusable_host_array(n: int, dtype, tag: str, pinned: bool = False) -> np.nda
     100 MB allocation costs ~8 ms of first-touch page faults (glibc maps every block above 32 MiB
     anew), three times the D2H itself, so earlier calls' buffers are recycled -- but only one that
     nothing references any more (every array handed out from it was a view holding it), so no
-    caller ever sees its data change.  Up to ``HOST_POOL_DEPTH`` buffers per site: in simulation
-    mode the previous round's results are still held while the next round's are made (the
-    strategy keeps its last train states, and its last average, until the new ones are returned),
-    so with one buffer per site every call after the first would fault a fresh one.  ``pinned``:
+    caller ever sees its data change.  Up to ``HOST_POOL_DEPTH`` buffers and ``HOST_POOL_BYTES``
+    per site: in simulation mode the previous round's results are still held while the next
+    round's are made (the strategy keeps its last train states, and its last average, until the
+    new ones are returned), K clients' exports of two rounds at once, so the pool grows to that
+    working set and then recycles it; past the caps the least recently used buffer is forgotten
+    (its holders keep it; it is freed with them).  ``pinned``:
     buffers of pinned host blocks (``pinned_empty``), a separate pool -- simulation mode, where
     the pools recycle, so the pinning is paid once (handoff.py)."""
     import sys
@@ -343,9 +346,17 @@ def reusable_host_array(n: int, dtype, tag: str, pinned: bool = False) -> np.nda
                 return buf[:n]
         buf = pinned_empty(n, key[1]) if pinned else np.empty(n, dtype=key[1])
         pool.append(buf)
-        if len(pool) > HOST_POOL_DEPTH:
+        while len(pool) > 1 and (len(pool) > HOST_POOL_DEPTH or sum(b.nbytes for b in pool) > HOST_POOL_BYTES):
             pool.pop(0)  # the least recently used; still alive through its holders' views, if any
         return buf
+
+
+def drop_host_pools(pinned_only: bool = False) -> None:
+    """Forget the recycled result buffers (the pinned ones only): each is freed once nothing else
+    holds it (handoff.enable(False) releases the pinned blocks this way)."""
+    with _host_lock:
+        for key in [k for k in _host_cache if (k[2] or not pinned_only)]:
+            del _host_cache[key]
 
 
 def device_pci_bus_id(device: int) -> str:
