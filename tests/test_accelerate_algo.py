@@ -282,7 +282,10 @@ def test_fedavg_gpu_recycled_export_buffers(gpu):
     """Exports released round by round (only copies kept) land in recycled host buffers from the
     third round on -- two clients' exports of round r are still held while round r + 1's are made
     -- and every value stays the reference's."""
+    from substrafl_amd import runtime
+
     ref, _, _ = run_fedavg(False, bn=True, disable_gpu=False, copy_exports=True)
+    runtime.drop_host_pools()  # the buffers earlier tests left free would be recycled first
     acc, _, _ = run_fedavg(True, bn=True, disable_gpu=False, copy_exports=True)
     ptrs = [int(v[0]) for t, v in acc if t == "ptr"]
     _compare([x for x in ref if x[0] != "ptr"], [x for x in acc if x[0] != "ptr"])
