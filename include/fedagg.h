@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 17
+#define FEDAGG_ABI_VERSION 16
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -540,17 +540,8 @@ int fedagg_device_get(int* device_out);
 int fedagg_device_set(int device);
 /* hipMemGetInfo of `device`: free and total HBM bytes (sizing of out-of-core shards). */
 int fedagg_device_memory(int device, uint64_t* free_bytes, uint64_t* total_bytes);
-/* Copy `bytes` from HBM into host memory; returns when the data is in h_dst.  Pageable memory goes
- * through the pinned ring; a range inside a block of fedagg_host_alloc takes one direct DMA. */
+/* Copy `bytes` from HBM into (pageable) host memory; returns when the data is in h_dst. */
 int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes);
-/* Pinned (page-locked, portable) host blocks for result buffers that are recycled across calls
- * (simulation mode's exports and outputs, runtime.reusable_host_array(pinned=True)): a fetch into
- * one is a single D2H DMA at the link's rate instead of the ring's chunked copy-out (the
- * `.cpu().numpy()` of torch_fed_avg_algo.py:227-230 and the result of fed_avg.py:217-222).
- * fedagg_host_pinned: 1 when [p, p + bytes) lies inside one such block. */
-int fedagg_host_alloc(uint64_t bytes, void** out);
-int fedagg_host_free(void* p);
-int fedagg_host_pinned(const void* p, uint64_t bytes);
 int fedagg_session_memset(fedagg_session* s, void* d, int value, uint64_t bytes);
 /* Copy `bytes` between two allocations of the session's GPU, ordered on its stream (the device
  * hand-off of simulation mode, substrafl_amd/handoff.py: a client's exported bucket into the

@@ -143,9 +143,6 @@ SIGNATURES = {
     "fedagg_session_fetch": (c_int, [c_void, c_void, c_void, c_u64]),
     "fedagg_session_memset": (c_int, [c_void, c_void, c_int, c_u64]),
     "fedagg_session_copy_d2d": (c_int, [c_void, c_void, c_void, c_u64]),
-    "fedagg_host_alloc": (c_int, [c_u64, P(c_void)]),
-    "fedagg_host_free": (c_int, [c_void]),
-    "fedagg_host_pinned": (c_int, [c_void, c_u64]),
     "fedagg_session_sync": (c_int, [c_void]),
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
 }
@@ -156,7 +153,7 @@ TUNING_SIGNATURES = {
     "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
 }
 
-ABI_VERSION = 17
+ABI_VERSION = 16
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16

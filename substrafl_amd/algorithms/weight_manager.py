@@ -314,10 +314,9 @@ def export_numpy(tensors: Sequence[torch.Tensor], wire: bool = True, tag: str = 
         return [t.cpu().detach().numpy() for t in tensors]
     from .. import handoff, runtime
 
-    # one D2H: through the native session's pinned ring (chunked, copied out by its worker pool),
-    # or straight into a pinned buffer in simulation mode with the hand-off on (recycled pools)
+    # one D2H through the native session's pinned ring (chunked, copied out by its worker pool)
     host = runtime.reusable_host_array(flat.numel(), torch.empty(0, dtype=flat.dtype).numpy().dtype,
-                                       tag, pinned=handoff.enabled())  # bf16 raises, as .numpy()
+                                       tag)  # bf16 raises, as .numpy()
     torch.cuda.current_stream(flat.device).synchronize()  # the bucket was written on torch's stream
     with runtime.device_lock(flat.device.index):  # the session's ring is shared with the engine
         runtime.session(flat.device.index).fetch(flat.data_ptr(), host)

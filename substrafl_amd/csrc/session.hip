@@ -24,7 +24,6 @@
 #include <cstring>
 #include <deque>
 #include <functional>
-#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -503,60 +502,10 @@ int fedagg_session_stage_check(fedagg_session* s, void* d_dst, int K, int nseg, 
   return stage_run(s, d_dst, row, K, nseg, h_seg, seg_bytes, byte_lo, row, esz, mismatches);
 }
 
-}  // extern "C"
-namespace {
-// pinned host blocks handed out by fedagg_host_alloc: base -> bytes
-std::mutex g_pinned_m;
-std::map<uintptr_t, uint64_t> g_pinned;
-
-bool pinned_range(const void* p, uint64_t n) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  std::lock_guard<std::mutex> g(g_pinned_m);
-  auto it = g_pinned.upper_bound(a);
-  if (it == g_pinned.begin()) return false;
-  --it;
-  return a >= it->first && a + n <= it->first + it->second;
-}
-}  // namespace
-extern "C" {
-
-int fedagg_host_alloc(uint64_t bytes, void** out) {
-  if (!out || !bytes) return FEDAGG_EINVAL;
-  void* p = nullptr;
-  HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocPortable));
-  {
-    std::lock_guard<std::mutex> g(g_pinned_m);
-    g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes;
-  }
-  *out = p;
-  return FEDAGG_OK;
-}
-
-int fedagg_host_free(void* p) {
-  if (!p) return FEDAGG_OK;
-  {
-    std::lock_guard<std::mutex> g(g_pinned_m);
-    if (!g_pinned.erase(reinterpret_cast<uintptr_t>(p))) {
-      fedagg_internal::set_error("fedagg_host_free: not a block of fedagg_host_alloc");
-      return FEDAGG_EINVAL;
-    }
-  }
-  HIP_TRY(hipHostFree(p));
-  return FEDAGG_OK;
-}
-
-int fedagg_host_pinned(const void* p, uint64_t bytes) { return p && pinned_range(p, bytes) ? 1 : 0; }
-
 int fedagg_session_fetch(fedagg_session* s, const void* d_src, void* h_dst, uint64_t bytes) {
   if (!s || !d_src || (!h_dst && bytes)) return FEDAGG_EINVAL;
   const double t0 = now_s();
   HIP_TRY(hipSetDevice(s->device));
-  if (bytes && pinned_range(h_dst, bytes)) {  // a pinned block of fedagg_host_alloc: one direct DMA
-    HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    s->last_fetch_s = now_s() - t0;
-    return FEDAGG_OK;
-  }
   int rc = s->ensure_ring();
   if (rc) return rc;
   // D2H in super-chunks of adjacent slots (16 MiB copies run at 55 GB/s where 4 MiB ones reach

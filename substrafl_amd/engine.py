@@ -773,8 +773,7 @@ class AggregationEngine:
             else:
                 ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
                 FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
-            out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}",
-                                              pinned=handoff.enabled())
+            out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}")
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
             if len(groups) == 1:
                 handoff.record_slot(out, s, self._B_OUT, d_out)  # simulation mode: clients copy it on the device
@@ -972,8 +971,8 @@ class AggregationEngine:
                          ws).launch(s.stream)
             ScaffoldPlan(kind, rows_c, rows_c, d_cc, w, lay_c.M, lr, scratch, cout, lay_c.pairwise_idx,
                          ws).launch(s.stream)
-        out_d = runtime.reusable_host_array(lay_d.M, np.float64, "scaffold-delta", pinned=handoff.enabled())
-        out_c = runtime.reusable_host_array(lay_c.M, np.float64, "scaffold-c", pinned=handoff.enabled())
+        out_d = runtime.reusable_host_array(lay_d.M, np.float64, "scaffold-delta")
+        out_c = runtime.reusable_host_array(lay_c.M, np.float64, "scaffold-c")
         mism = np.zeros(1, np.int64)
         s.fetch(cnt, mism)
         s.fetch(dout, out_d)

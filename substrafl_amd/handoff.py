@@ -52,9 +52,6 @@ def enable(flag: bool = True) -> None:
             for fin in _finalizers.values():
                 fin.detach()
             _finalizers.clear()
-        from . import runtime
-
-        runtime.drop_host_pools(pinned_only=True)  # the pinned result blocks of simulation mode
 
 
 def enabled() -> bool:

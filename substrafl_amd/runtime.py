@@ -287,39 +287,11 @@ def device_lock(device: int) -> threading.RLock:
 
 _host_cache: Dict[tuple, list] = {}
 _host_lock = threading.Lock()
-HOST_POOL_DEPTH = 64  # buffers kept per call site and dtype (and pinned or not) ...
+HOST_POOL_DEPTH = 64  # buffers kept per call site and dtype ...
 HOST_POOL_BYTES = 16 << 30  # ... within this many bytes
 
 
-pinned_blocks = {"allocated": 0, "freed": 0}  # fedagg_host_alloc / _free calls (tests)
-
-
-def _pinned_free(ptr: int) -> None:
-    try:
-        _native.load().fedagg_host_free(ctypes.c_void_p(ptr))
-    except Exception:  # noqa: BLE001 -- interpreter shutdown
-        pass
-    pinned_blocks["freed"] += 1
-
-
-def pinned_empty(n: int, dtype) -> np.ndarray:
-    """An ``n``-element array in a pinned host block (``fedagg_host_alloc``): a fetch into it is one
-    direct D2H DMA.  Freed when the array and every view of it are gone (views of it hold it:
-    NumPy points them at this array, which does not own its memory)."""
-    import weakref
-
-    dt = np.dtype(dtype)
-    nbytes = max(1, int(n) * dt.itemsize)
-    p = ctypes.c_void_p()
-    _native.check(_native.load().fedagg_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
-    raw = (ctypes.c_char * nbytes).from_address(int(p.value))
-    arr = np.frombuffer(raw, dtype=dt, count=int(n))
-    weakref.finalize(arr, _pinned_free, int(p.value))
-    pinned_blocks["allocated"] += 1
-    return arr
-
-
-def reusable_host_array(n: int, dtype, tag: str, pinned: bool = False) -> np.ndarray:
+def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
     """A host array of ``n`` elements for a D2H result (``tag`` names the call site).  A fresh
     100 MB allocation costs ~8 ms of first-touch page faults (glibc maps every block above 32 MiB
     anew), three times the D2H itself, so earlier calls' buffers are recycled -- but only one that
@@ -329,12 +301,10 @@ def reusable_host_array(n: int, dtype, tag: str, pinned: bool = False) -> np.nda
     round's are made (the strategy keeps its last train states, and its last average, until the
     new ones are returned), K clients' exports of two rounds at once, so the pool grows to that
     working set and then recycles it; past the caps the least recently used buffer is forgotten
-    (its holders keep it; it is freed with them).  ``pinned``:
-    buffers of pinned host blocks (``pinned_empty``), a separate pool -- simulation mode, where
-    the pools recycle, so the pinning is paid once (handoff.py)."""
+    (its holders keep it; it is freed with them)."""
     import sys
 
-    key = (tag, np.dtype(dtype), bool(pinned))
+    key = (tag, np.dtype(dtype))
     with _host_lock:
         pool = _host_cache.setdefault(key, [])
         for i in range(len(pool)):  # (not enumerate: its cached result tuple would hold one more reference)
@@ -344,19 +314,17 @@ def reusable_host_array(n: int, dtype, tag: str, pinned: bool = False) -> np.nda
                 pool.append(pool.pop(i))  # most recently used last
                 buf.flags.writeable = True  # a device hand-off (handoff.py) may have frozen it
                 return buf[:n]
-        buf = pinned_empty(n, key[1]) if pinned else np.empty(n, dtype=key[1])
+        buf = np.empty(n, dtype=key[1])
         pool.append(buf)
         while len(pool) > 1 and (len(pool) > HOST_POOL_DEPTH or sum(b.nbytes for b in pool) > HOST_POOL_BYTES):
             pool.pop(0)  # the least recently used; still alive through its holders' views, if any
         return buf
 
 
-def drop_host_pools(pinned_only: bool = False) -> None:
-    """Forget the recycled result buffers (the pinned ones only): each is freed once nothing else
-    holds it (handoff.enable(False) releases the pinned blocks this way)."""
+def drop_host_pools() -> None:
+    """Forget the recycled result buffers: each is freed once nothing else holds it."""
     with _host_lock:
-        for key in [k for k in _host_cache if (k[2] or not pinned_only)]:
-            del _host_cache[key]
+        _host_cache.clear()
 
 
 def device_pci_bus_id(device: int) -> str:

@@ -49,7 +49,7 @@ def test_product_library_does_not_export_tuning_entry_points():
 
 def test_abi_version_and_invalid_arguments():
     lib = _native.load()
-    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 17
+    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 16
     w = (ctypes.c_float * 1)(1.0)
     ptrs = _native.ptr_array([0])
     assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, 0, None, None, None) == -1  # K == 0

@@ -21,7 +21,6 @@ The same runs on the CPU (``disable_gpu``) take the reference's torch loops and 
 ``accelerate_algo`` over the real reference classes under ``simulate_experiment``.
 """
 
-import ctypes
 import pickle
 import sys
 
@@ -431,35 +430,3 @@ def test_handoff_device_memory_stays_flat_over_rounds(gpu, handoff_on):
         used.append(torch.cuda.memory_allocated())
     assert used[-1] == used[3], used
     assert len(handoff_on.records()) <= 4 * 4 + 8, handoff_on.records()
-
-
-@pytest.mark.gpu
-def test_handoff_exports_land_in_recycled_pinned_blocks(gpu, handoff_on):
-    """With the hand-off on, exports and engine outputs are fetched into pinned host blocks (one
-    direct DMA each) from recycled pools: after the first rounds no new block is pinned, and a
-    block is freed once its arrays are gone."""
-    from substrafl_amd import _native, runtime
-    from substrafl_amd.integration import accelerate, accelerate_algo
-
-    lib = _native.load()
-    algos = [accelerate_algo(_algo(TorchFedAvgAlgo, bn=False, disable_gpu=False, client=k))() for k in range(2)]
-    strategy = accelerate(ss.FedAvg)(algo=algos[0])
-    avg, allocated = None, []
-    for _ in range(6):
-        states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, DATA)]
-        avg = strategy.avg_shared_states(shared_states=states, _skip=True)
-        allocated.append(runtime.pinned_blocks["allocated"])
-        for arrs in [states[0].parameters_update, avg.avg_parameters_update]:
-            a = arrs[0]
-            assert lib.fedagg_host_pinned(ctypes.c_void_p(a.__array_interface__["data"][0]), a.nbytes) == 1
-    assert allocated[-1] == allocated[3], allocated  # steady state: the pools recycle
-    freed = runtime.pinned_blocks["freed"]
-    blk = runtime.pinned_empty(1000, np.float32)
-    view = blk[10:20]
-    del blk
-    assert runtime.pinned_blocks["freed"] == freed  # a view keeps the block
-    del view
-    import gc
-
-    gc.collect()
-    assert runtime.pinned_blocks["freed"] == freed + 1

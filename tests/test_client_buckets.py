@@ -226,7 +226,7 @@ def test_host_result_buffers_pooled_across_held_rounds():
         held = nxt  # the previous round's result is released here
     assert len(set(ptrs)) == 2, ptrs
     keep = [runtime.reusable_host_array(10, np.float64, "pool_cap") for _ in range(runtime.HOST_POOL_DEPTH + 3)]
-    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64), False)]) == runtime.HOST_POOL_DEPTH
+    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64))]) == runtime.HOST_POOL_DEPTH
     assert len({a.__array_interface__["data"][0] for a in keep}) == len(keep)  # every live one distinct
 
 
@@ -236,5 +236,5 @@ def test_host_result_pool_byte_cap(monkeypatch):
 
     monkeypatch.setattr(runtime, "HOST_POOL_BYTES", 10_000)
     keep = [runtime.reusable_host_array(1000, np.float32, "pool_bytes") for _ in range(5)]  # 4000 B each
-    pool = runtime._host_cache[("pool_bytes", np.dtype(np.float32), False)]
+    pool = runtime._host_cache[("pool_bytes", np.dtype(np.float32))]
     assert len(pool) == 2 and pool[-1] is keep[-1]  # a fresh buffer is handed out itself
