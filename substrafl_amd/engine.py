@@ -642,7 +642,8 @@ class AggregationEngine:
         into the ``[K, ld]`` rows; the others are staged from the host as usual.  None when no
         row can be handed off (the caller stages everything, tiled where recommended)."""
         hits = [handoff.lookup(row, s.device) for row in rows]
-        self._last_handoff = [h is not None and h[1] == layout.M * R.itemsize for h in hits]
+        self._last_handoff = [h is not None and h[1] == layout.M * R.itemsize and all(a.dtype == R for a in row)
+                              for h, row in zip(hits, rows)]
         if not any(self._last_handoff):
             return None
         ld_bytes = layout.ld * R.itemsize
