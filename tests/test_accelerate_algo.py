@@ -320,8 +320,8 @@ def handoff_on():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bn", [False, True])
-def test_fedavg_gpu_handoff_bit_identical(gpu, bn):
+@pytest.mark.parametrize("bn, wire", [(False, False), (True, False), (True, True)])
+def test_fedavg_gpu_handoff_bit_identical(gpu, bn, wire):
     """Simulation mode with the device hand-off (substrafl_amd/handoff.py): the clients' exports
     reach the aggregator, and the average reaches the clients, device to device -- every exported
     update, average and model state still bit-identical to the reference sequence's."""
@@ -331,7 +331,7 @@ def test_fedavg_gpu_handoff_bit_identical(gpu, bn):
     handoff.enable(True)
     try:
         t0 = handoff.stats["taken"]
-        acc, _, states = run_fedavg(True, bn=bn, disable_gpu=False)
+        acc, _, states = run_fedavg(True, bn=bn, disable_gpu=False, wire=wire)  # wire: BucketArray exports
         taken = handoff.stats["taken"] - t0
     finally:
         handoff.enable(False)
