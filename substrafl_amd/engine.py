@@ -636,16 +636,24 @@ class AggregationEngine:
 
     _last_handoff: List[bool] = []
 
-    def _handoff_rows(self, s, rows: List[List[np.ndarray]], layout: BucketLayout, R: np.dtype, K: int) -> Optional[int]:
+    _handoff_keep = None
+
+    def _handoff_rows(self, s, rows: List[List[np.ndarray]], layout: BucketLayout, R: np.dtype, K: int):
         """Simulation mode (``handoff``): client rows whose bytes are still on this GPU (an
-        ``accelerate_algo`` export recorded with its device bucket) are copied device to device
-        into the ``[K, ld]`` rows; the others are staged from the host as usual.  None when no
-        row can be handed off (the caller stages everything, tiled where recommended)."""
+        ``accelerate_algo`` export recorded with its device bucket).  All of them: the list of
+        their device pointers -- the kernel reads the clients' buckets in place, nothing is copied
+        (kept alive in ``_handoff_keep`` until the result is fetched).  Some: those are copied
+        device to device into the ``[K, ld]`` rows, the others staged from the host as usual, and
+        the bucket's address is returned.  None when no row can be handed off (the caller stages
+        everything, tiled where recommended)."""
         hits = [handoff.lookup(row, s.device) for row in rows]
         self._last_handoff = [h is not None and h[1] == layout.M * R.itemsize and all(a.dtype == R for a in row)
                               for h, row in zip(hits, rows)]
         if not any(self._last_handoff):
             return None
+        if all(self._last_handoff):
+            self._handoff_keep = hits
+            return [int(h[0]) for h in hits]
         ld_bytes = layout.ld * R.itemsize
         d_bucket = s.buffer(self._B_BUCKET, K * ld_bytes)
         for k, (row, h, ok) in enumerate(zip(rows, hits, self._last_handoff)):
@@ -746,11 +754,16 @@ class AggregationEngine:
                         staged, d_bucket, tv = True, d_t, -rec[1]
                 else:
                     staged = self._take_prestaged(self._B_BUCKET, d_bucket, layout.ld * R.itemsize, rows)
+            row_ptrs = None  # the clients' own device buckets (a full hand-off), read in place
             if not staged and prescale is None and len(groups) == 1:
                 hand = self._handoff_rows(s, rows, layout, R, K)
                 if hand is not None:
                     self._prestaged.pop(self._B_BUCKET, None)
-                    staged, d_bucket = True, hand
+                    staged = True
+                    if isinstance(hand, list):
+                        row_ptrs = hand
+                    else:
+                        d_bucket = hand
                     tm["handoff_rows"] = sum(1 for r in self._last_handoff if r)
             if staged:
                 tm["prestaged"] = not tm.get("handoff_rows")
@@ -772,10 +785,11 @@ class AggregationEngine:
             if tv is not None:
                 TiledFedAvgPlan(kind, d_bucket, K, w, layout.M, d_out, layout.pairwise_idx, ws, tv).launch(s.stream)
             else:
-                ptrs = [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
+                ptrs = row_ptrs if row_ptrs is not None else [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
                 FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
             out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}")
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
+            self._handoff_keep = None  # the kernel is done with the clients' buckets
             if len(groups) == 1:
                 handoff.record_slot(out, s, self._B_OUT, d_out)  # simulation mode: clients copy it on the device
             tm["kernel_fetch_s"] = tm.get("kernel_fetch_s", 0.0) + time.perf_counter() - t1
