@@ -428,5 +428,5 @@ def test_handoff_device_memory_stays_flat_over_rounds(gpu, handoff_on):
         avg = strategy.avg_shared_states(shared_states=states, _skip=True)
         torch.cuda.synchronize()
         used.append(torch.cuda.memory_allocated())
-    assert used[-1] == used[3], used
+    assert max(used[4:]) <= used[3], used  # no growth once the pools and records turn over
     assert len(handoff_on.records()) <= 4 * 4 + 8, handoff_on.records()
