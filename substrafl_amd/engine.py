@@ -664,11 +664,13 @@ class AggregationEngine:
         s.sync()  # the copies' sources are kept alive by `hits` only until here
         return d_bucket
 
-    def _handoff_into(self, s, rows: List[List[np.ndarray]], lay: BucketLayout, d: int) -> bool:
-        """All K rows recorded by the hand-off (one source dtype): copied device to device into
-        ``[K, lay.ld]`` of ``lay.dtype`` at ``d`` -- through one exact device cast when the
-        recorded bytes are of another float type (Scaffold's fp32 deltas into its fp64 buckets),
-        as ``_stage_rows`` does for host rows.  False (nothing written) otherwise."""
+    def _handoff_into(self, s, rows: List[List[np.ndarray]], lay: BucketLayout, d: int):
+        """All K rows recorded by the hand-off (one source dtype).  Of the bucket's dtype: the
+        list of their device pointers -- the kernel reads the clients' buckets in place (kept
+        alive in ``_handoff_keep`` until the results are fetched).  Of another float type
+        (Scaffold's fp32 deltas into its fp64 buckets): copied device to device into ``[K,
+        lay.ld]`` at ``d`` through one exact device cast, as ``_stage_rows`` does for host rows,
+        and True.  False (nothing written) otherwise."""
         hits = [handoff.lookup(row, s.device) for row in rows]
         if not hits or any(h is None for h in hits):
             return False
@@ -680,8 +682,8 @@ class AggregationEngine:
             return False
         K = len(rows)
         if sdt == lay.dtype:
-            for k, h in enumerate(hits):
-                s.copy_d2d(d + k * lay.ld * sdt.itemsize, h[0], h[1])
+            self._handoff_keep = (self._handoff_keep or []) + hits
+            return [int(h[0]) for h in hits]
         else:
             tmp = s.buffer(self._B_TMP, K * lay.ld * sdt.itemsize)
             for k, h in enumerate(hits):
@@ -916,15 +918,21 @@ class AggregationEngine:
         d_cc = s.buffer(self._B_C, Kc * lay_s.ld * isz)
         pre = 0
         host_mism = 0
+        in_place: Dict[int, List[int]] = {}  # bucket slot -> the clients' own device rows (hand-off)
+        self._handoff_keep = None
         for rows, lay, d, slot in ((parameters_updates, lay_d, d_d, self._B_BUCKET),
                                    (control_variate_updates, lay_c, d_cv, self._B_CV)):
             rows = [list(r) for r in rows]
             if self._take_prestaged(slot, d, lay.ld * isz, rows):
                 pre += 1
-            elif self._handoff_into(s, rows, lay, d):  # simulation mode: the clients' exports, on the device
-                tm["handoff_rows"] = tm.get("handoff_rows", 0) + len(rows)
-            else:
+                continue
+            hand = self._handoff_into(s, rows, lay, d)  # simulation mode: the clients' exports, on the device
+            if hand is False:
                 self._stage_rows(s, rows, lay, d)
+                continue
+            tm["handoff_rows"] = tm.get("handoff_rows", 0) + len(rows)
+            if isinstance(hand, list):
+                in_place[slot] = hand
         c_rows = [list(r) for r in server_control_variates]
         c_ingested = host_c and self._take_prestaged(self._B_C, d_cc, lay_s.ld * isz, c_rows)
         # simulation mode: every client's c is its export, still on this GPU (handoff.py) -- one
@@ -972,8 +980,8 @@ class AggregationEngine:
         cout = s.buffer(self._B_COUT, lay_c.ld * 8)
         ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(
             K, max(1, lay_d.pairwise_idx.size, lay_c.pairwise_idx.size), 8))
-        rows_d = [d_d + k * lay_d.ld * isz for k in range(K)]
-        rows_c = [d_cv + k * lay_c.ld * isz for k in range(K)]
+        rows_d = in_place.get(self._B_BUCKET) or [d_d + k * lay_d.ld * isz for k in range(K)]
+        rows_c = in_place.get(self._B_CV) or [d_cv + k * lay_c.ld * isz for k in range(K)]
         if [g.shape for g in lay_d.segments] == [g.shape for g in lay_c.segments]:
             ScaffoldPlan(kind, rows_d, rows_c, d_cc, w, lay_d.M, lr, dout, cout, lay_d.pairwise_idx, ws).launch(s.stream)
         else:
@@ -992,6 +1000,7 @@ class AggregationEngine:
         s.fetch(cnt, mism)
         s.fetch(dout, out_d)
         s.fetch(cout, out_c)
+        self._handoff_keep = None  # the kernels are done with the clients' buckets
         handoff.record_slot(out_d, s, self._B_OUT, dout)  # simulation mode: the clients copy them on the device
         if handoff.enabled():
             # c outlives this call on the device: the clients send it back as their c next round
