@@ -329,16 +329,19 @@ def _leg_ready(ctx) -> None:
 def run_leg_child(cmd, env, connect_s: float, deadline: float):
     """Run one leg child: it must print LEG_READY within ``connect_s`` (set-up + warm-up) and exit
     within ``deadline`` of its start; a child that misses either is killed (by PID) and the reason
-    returned.  Returns (stdout, stderr, returncode, error or None)."""
+    returned.  Returns (stdout, stderr, returncode, error or None, seconds to LEG_READY or None)."""
     import threading
 
+    t_start = time.monotonic()
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     out, err, ready = [], [], threading.Event()
+    ready_at = []
 
     def pump(stream, sink, watch):
         for ln in stream:
             sink.append(ln)
             if watch and ln.strip() == LEG_READY:
+                ready_at.append(time.monotonic() - t_start)
                 ready.set()
 
     th = [threading.Thread(target=pump, args=(p.stdout, out, True), daemon=True),
@@ -359,7 +362,7 @@ def run_leg_child(cmd, env, connect_s: float, deadline: float):
     p.wait()
     for t in th:
         t.join(timeout=5)
-    return "".join(out), "".join(err), p.returncode, why
+    return "".join(out), "".join(err), p.returncode, why, (round(ready_at[0], 2) if ready_at else None)
 
 
 # ======================================================================================
@@ -765,7 +768,7 @@ def client_shard_legs(args, ctx, info, only_push=False):
             cmd += ["--rehearse-cpu", "--leg-key", key]
         t0 = time.perf_counter()
         try:
-            so, se, rc, why = run_leg_child(cmd, env, LEG_CONNECT_S, deadline)
+            so, se, rc, why, ready_s = run_leg_child(cmd, env, LEG_CONNECT_S, deadline)
             res = None
             if why:
                 res = {"error": why}
@@ -781,14 +784,23 @@ def client_shard_legs(args, ctx, info, only_push=False):
                 res["executor"] = executor
                 if leg_env:
                     res["env"] = dict(leg_env)
-            # every rank's leg is over before the next one starts (errors are per rank: gather them)
-            errs = [(res or {}).get("error")] * ctx.world
+            # every rank's leg is over before the next one starts (errors and set-up times are per
+            # rank: gather them)
+            mine = ((res or {}).get("error"), ready_s)
+            got = [mine] * ctx.world
             if ctx.world > 1:
-                dist.all_gather_object(errs, (res or {}).get("error"))
+                dist.all_gather_object(got, mine)
+            errs = [g[0] for g in got]
             if ctx.rank == 0:
                 bad = {r: e for r, e in enumerate(errs) if e}
                 if bad and "error" not in res:
                     res["errors_on_other_ranks"] = bad
+                # the leg's set-up through its warm-up steps (process start, process group, RCCL
+                # connect, warm-up), slowest rank, beside the deadline it had (VERDICT r05 "Next 1")
+                ready = [g[1] for g in got if g[1] is not None]
+                res["connect_s"] = max(ready) if len(ready) == ctx.world else None
+                res["connect_deadline_s"] = round(min(LEG_CONNECT_S, deadline), 1)
+                res["deadline_s"] = round(deadline, 1)
                 out[key] = res
         except Exception as e:  # noqa: BLE001 -- a leg never costs the legs gathered before it
             if ctx.rank == 0:

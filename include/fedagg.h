@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 16
+#define FEDAGG_ABI_VERSION 17
 #define FEDAGG_KCHUNK 128          /* clients per launch for FedAvg (kernel-argument table)      */
 #define FEDAGG_KCHUNK_SCAFFOLD 64  /* clients per launch for Scaffold (two tables)               */
 #define FEDAGG_FUSED_PAIRWISE 16   /* numel==1 segments patched inside the bucket launch         */
@@ -557,6 +557,49 @@ int fedagg_session_event_record(fedagg_session* s, int ev);
 int fedagg_session_event_elapsed(fedagg_session* s, int ev0, int ev1, float* ms);
 /* wall time of the last stage / fetch call, seconds */
 int fedagg_session_timing(fedagg_session* s, double* stage_s, double* fetch_s);
+/* Start-up phases of the session, seconds, into out[0 .. min(n, FEDAGG_SESSION_PHASES)): 0 the HIP
+ * runtime's initialisation and the device (fedagg_session_create's first calls: the whole runtime
+ * start-up when it is the process's first HIP call), 1 its streams and events, then
+ * fedagg_session_warm's 2 pinned staging ring (hipHostMalloc, on the NUMA node of the session's
+ * CPUs), 3 worker pool, 4 HBM buffers, 5 code-object load (the first kernel launch, synchronised);
+ * 0.0 for a phase that has not run.  The task process's start-up attribution
+ * (remote/substratools_methods.py:94-118: the prewarm overlapped with the unpickling). */
+#define FEDAGG_SESSION_PHASES 6
+int fedagg_session_phases(fedagg_session* s, double* out, int n);
+
+/* ---------------------------------------------------------------------------
+ * One process, several GPUs (csrc/multi.hip): the parameter-range FedAvg of an aggregate task in
+ * one call -- the plan of substrafl_amd/multi_device.py (MultiDeviceEngine) for a host in any
+ * language (SURVEY.md §8(b) "fa_multi_init / fa_reduce_sharded_*", §8(e) primary partitioning).
+ * A Substra aggregate task is one OS process (remote/register/register.py:96), so a host that
+ * wants the node's GPUs drives them from one process.  Replaces fed_avg.py:217-222 over host
+ * buckets, bit-identical to fedagg_fedavg_* over the whole range (no collective):
+ *   - [0, M) is cut into one contiguous 512-element-aligned shard per device (equal chunks, the
+ *     last shards may get less or nothing);
+ *   - one thread and one private session per shard (a repeated device index gets its own, so a
+ *     one-GPU box exercises the sharded path), its `pack_threads` pack workers (0: the CPUs this
+ *     process may use / ndev, 2..32) and pinned ring bound to the GPU's NUMA node;
+ *   - each shard streams through its GPU in sub-ranges sized to 85 % of its free HBM (or the
+ *     "max_shard_bytes" knob): stage bytes [lo, hi) of every row (fedagg_session_stage_range),
+ *     the bucket kernel with the numel == 1 patch of the elements it owns, fetch into h_out.
+ * Rows: K clients x nseg host segments each (h_seg[k * nseg + i], seg_bytes[i] bytes; pageable
+ * host memory, as fedagg_session_stage), M = sum(seg_bytes) / element size; h_w the K weights
+ * fl(n_k / n); h_idx the P flat indices of numel == 1 tensors; h_out M elements of host memory.
+ * Blocking: returns when h_out holds the result; the caller's current device is unchanged.  One
+ * call at a time per object (calls on one object serialise). */
+typedef struct fedagg_multi fedagg_multi;
+fedagg_multi* fedagg_multi_create(int ndev, const int* devs, int pack_threads);
+void fedagg_multi_destroy(fedagg_multi* m);
+/* knobs: "max_shard_bytes" (HBM one sub-range may take; 0 = 85 % of free HBM), "threads" */
+int fedagg_multi_set(fedagg_multi* m, const char* key, long long value);
+int fedagg_multi_fedavg_f32(fedagg_multi* m, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
+                            const float* h_w, const uint64_t* h_idx, int P, float* h_out);
+int fedagg_multi_fedavg_f64(fedagg_multi* m, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
+                            const double* h_w, const uint64_t* h_idx, int P, double* h_out);
+/* shard g: its device, the GPU's NUMA node (-1 unknown), pack workers, CPUs they are bound to, and
+ * of the last call its element range [lo, hi) and the sub-ranges it streamed (any pointer NULL) */
+int fedagg_multi_shard_info(fedagg_multi* m, int g, int* device, int* numa_node, int* threads, int* ncpus,
+                            uint64_t* lo, uint64_t* hi, int* ranges);
 
 #ifdef __cplusplus
 }

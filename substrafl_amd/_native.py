@@ -145,6 +145,15 @@ SIGNATURES = {
     "fedagg_session_copy_d2d": (c_int, [c_void, c_void, c_void, c_u64]),
     "fedagg_session_sync": (c_int, [c_void]),
     "fedagg_session_timing": (c_int, [c_void, P(c_dbl), P(c_dbl)]),
+    "fedagg_session_phases": (c_int, [c_void, P(c_dbl), c_int]),
+    # one process, several GPUs (csrc/multi.hip)
+    "fedagg_multi_create": (c_void, [c_int, P(c_int), c_int]),
+    "fedagg_multi_destroy": (None, [c_void]),
+    "fedagg_multi_set": (c_int, [c_void, ctypes.c_char_p, ctypes.c_longlong]),
+    "fedagg_multi_fedavg_f32": (c_int, [c_void, c_int, c_int, P(c_void), P(c_u64), c_void, c_void, c_int, c_void]),
+    "fedagg_multi_fedavg_f64": (c_int, [c_void, c_int, c_int, P(c_void), P(c_u64), c_void, c_void, c_int, c_void]),
+    "fedagg_multi_shard_info": (c_int, [c_void, c_int, P(c_int), P(c_int), P(c_int), P(c_int), P(c_u64), P(c_u64),
+                                        P(c_int)]),
 }
 
 # entry points only a FEDAGG_TUNING build exports (include/fedagg.h "#if FEDAGG_TUNING"): bound
@@ -153,7 +162,7 @@ TUNING_SIGNATURES = {
     "fedagg_copy_async": (c_int, [c_void, c_void, c_u64, c_void]),
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 FEDAGG_KCHUNK = 128
 FEDAGG_KCHUNK_SCAFFOLD = 64
 FEDAGG_FUSED_PAIRWISE = 16
@@ -164,6 +173,7 @@ FEDAGG_MAX_PAIRWISE = 64
 FEDAGG_FLAT_MAX_LISTS = 4
 FEDAGG_SESSION_BUFFERS = 16
 FEDAGG_SESSION_EVENTS = 8
+FEDAGG_SESSION_PHASES = 6
 FEDAGG_F16 = 0  # kinds (include/fedagg.h enum)
 FEDAGG_F32 = 1
 FEDAGG_F64 = 2

@@ -194,6 +194,19 @@ def _scaffold_parameters_update(self):
                             updates_multiplier=self._current_lr)
 
 
+def _registering_init(base_init):
+    """The class's own constructor, then the instance registered as a hand-off consumer of the
+    engine's outputs (``handoff.register``: only then are they recorded, and frozen, for it)."""
+
+    def __init__(self, *args, **kwargs):
+        base_init(self, *args, **kwargs)
+        from .. import handoff
+
+        handoff.register("client", self)
+
+    return __init__
+
+
 def accelerate_algo(algo_cls, wire: bool = False):
     """A subclass of ``algo_cls`` (SubstraFL's ``TorchFedAvgAlgo`` / ``TorchScaffoldAlgo`` or a
     subclass of one) whose ``train`` moves weights with the flat-bucket kernels.  ``wire``:
@@ -204,6 +217,7 @@ def accelerate_algo(algo_cls, wire: bool = False):
     schemas = importlib.import_module(f"{pkg}.strategies.schemas")
     ns = {"__doc__": f"{algo_cls.__name__} with its weight moves on MI355X (substrafl_amd.accelerate_algo).",
           "_fedagg_wire": bool(wire),
+          "__init__": _registering_init(algo_cls.__init__),
           "__module__": __name__}  # type() under ABCMeta would otherwise record "abc"
     if _BASES[base.__name__] == "scaffold":
         exceptions = importlib.import_module(f"{pkg}.exceptions")

@@ -200,8 +200,12 @@ __device__ __forceinline__ int push_failed_rank(const uint64_t* errs, uint32_t n
 // PUSH_TAG_ERR for a tag) in *err.  Fail fast: a wait also gives up as soon as ANY rank's err word
 // is set (a peer's or an earlier wait of this rank: the call's result is void), recording
 // PUSH_PEER_ERR + that rank + 1 when the cause is another rank's, so a dead or slow peer costs
-// the group one timeout, not one per wait.  Every lane reaches the end (the late count is a wave
-// ballot).
+// the group one timeout, not one per wait.  The err words are scanned once on entry and then every
+// PUSH_ERR_SCAN_EVERY polls (not nranks more uncached host-page reads per poll on the
+// error-free path; a failure is still seen within tens of microseconds).  Every lane reaches the
+// end (the late count is a wave ballot).
+constexpr uint32_t PUSH_ERR_SCAN_EVERY = 16;
+
 __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress, PushWaitArgs a, uint64_t gen,
                                                        uint64_t timeout, uint64_t* err, uint64_t* late,
                                                        const uint64_t* errs, uint32_t nranks, uint32_t rank) {
@@ -213,6 +217,7 @@ __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress,
     uint64_t code = 0;  // this lane's own failure
     const uint64_t* tag = a.tag[i];
     bool counter_done = false;
+    uint32_t polls = 0;
     while (peer < 0 && !code) {
       if (!counter_done) {
         if (ld_acquire_sys(progress + a.idx[i]) >= a.val[i]) {
@@ -228,7 +233,7 @@ __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress,
       if (wall_clock64() - t0 > timeout) code = (uint64_t)a.idx[i] + 1 + (counter_done ? PUSH_TAG_ERR : 0);
       else {
         __builtin_amdgcn_s_sleep(16);
-        peer = push_failed_rank(errs, nranks);
+        if (++polls % PUSH_ERR_SCAN_EVERY == 0) peer = push_failed_rank(errs, nranks);
       }
     }
     if (code) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -84,6 +84,9 @@ struct fedagg_session {
   uint64_t fail_copy_after = 0;  // test knob: the n-th copy of the session fails (0 = never)
   uint64_t copies = 0;
   std::vector<int> cpus;  // fedagg_session_affinity: the pack workers' and the ring's CPUs (empty: any)
+  // start-up phases, seconds (fedagg_session_phases): create's HIP runtime init + device, its
+  // streams / events; warm's pinned ring, worker pool, HBM buffers, code-object load
+  double phase[FEDAGG_SESSION_PHASES] = {};
 
   int ensure_ring() {
     if (ring.size() == slots && ring.chunk_bytes == chunk_bytes) return FEDAGG_OK;
@@ -187,8 +190,9 @@ struct HipEngine {
 extern "C" {
 
 fedagg_session* fedagg_session_create(int device) {
+  const double t0 = now_s();
   int n = 0;
-  hipError_t e = hipGetDeviceCount(&n);
+  hipError_t e = hipGetDeviceCount(&n);  // the process's first HIP call initialises the runtime
   if (e != hipSuccess || n <= 0) {
     hip_fail("fedagg_session_create: no HIP device", e == hipSuccess ? hipErrorNoDevice : e);
     return nullptr;
@@ -203,6 +207,8 @@ fedagg_session* fedagg_session_create(int device) {
   }
   auto* s = new fedagg_session();
   s->device = device;
+  const double t1 = now_s();
+  s->phase[0] = t1 - t0;
   if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&s->join_ev, hipEventDisableTiming)) != hipSuccess) {
@@ -212,6 +218,7 @@ fedagg_session* fedagg_session_create(int device) {
     delete s;
     return nullptr;
   }
+  s->phase[1] = now_s() - t1;
   return s;
 }
 
@@ -271,10 +278,16 @@ int fedagg_session_affinity(fedagg_session* s, const int* cpus, int ncpus) {
       fedagg_internal::set_error("fedagg_session_affinity: CPU index out of range");
       return FEDAGG_EINVAL;
     }
+  // workers() compares s->cpus under pool_m (a compare-only check may run beside this call): swap
+  // them under the same lock; the ring is released on the session's device, the caller's restored
+  std::lock_guard<std::mutex> g(s->pool_m);
   if (v != s->cpus) {
+    int caller = -1;
+    (void)hipGetDevice(&caller);
     (void)hipSetDevice(s->device);
     s->release_ring();  // re-allocated on the new CPUs' node at the next stage / fetch
     s->cpus = std::move(v);
+    if (caller >= 0) (void)hipSetDevice(caller);
   }
   return FEDAGG_OK;
 }
@@ -316,9 +329,14 @@ int fedagg_session_buffer(fedagg_session* s, int slot, uint64_t bytes, void** d_
 int fedagg_session_warm(fedagg_session* s, const uint64_t* slot_bytes, int nslots) {
   if (!s || nslots < 0 || nslots > FEDAGG_SESSION_BUFFERS || (nslots > 0 && !slot_bytes)) return FEDAGG_EINVAL;
   HIP_TRY(hipSetDevice(s->device));
+  double t = now_s();
   int rc = s->ensure_ring();
   if (rc) return rc;
+  s->phase[2] = now_s() - t;
+  t = now_s();
   (void)s->workers();
+  s->phase[3] = now_s() - t;
+  t = now_s();
   void* probe = nullptr;
   for (int i = 0; i < nslots; ++i) {
     if (!slot_bytes[i]) continue;
@@ -331,12 +349,15 @@ int fedagg_session_warm(fedagg_session* s, const uint64_t* slot_bytes, int nslot
     rc = fedagg_session_buffer(s, FEDAGG_SESSION_BUFFERS - 1, 4096, &probe);
     if (rc) return rc;
   }
+  s->phase[4] = now_s() - t;
+  t = now_s();
   // one tiny launch loads the kernels' code object now rather than at the first aggregation
   HIP_TRY(hipMemsetAsync(probe, 0, 4096, s->stream));
   rc = fedagg_read_probe_f32(static_cast<const float*>(probe), 512, static_cast<float*>(probe) + 512, 1,
                              (void*)s->stream);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s->stream));
+  s->phase[5] = now_s() - t;
   return FEDAGG_OK;
 }
 
@@ -586,6 +607,12 @@ int fedagg_session_sync(fedagg_session* s) {
   if (!s) return FEDAGG_EINVAL;
   HIP_TRY(hipSetDevice(s->device));
   HIP_TRY(hipStreamSynchronize(s->stream));
+  return FEDAGG_OK;
+}
+
+int fedagg_session_phases(fedagg_session* s, double* out, int n) {
+  if (!s || n < 0 || (n && !out)) return FEDAGG_EINVAL;
+  for (int i = 0; i < n && i < FEDAGG_SESSION_PHASES; ++i) out[i] = s->phase[i];
   return FEDAGG_OK;
 }
 

@@ -30,6 +30,7 @@ import ctypes
 import functools
 import os
 import time
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -370,6 +371,19 @@ def serialized(method):
     return wrapper
 
 
+@dataclass
+class StagedRows:
+    """Where one FedAvg call's client rows are in HBM (:meth:`AggregationEngine._resolve_rows`):
+    ``reason`` names the path; ``ptrs`` the K row addresses (row layouts) or ``base`` / ``tv`` the
+    tile-interleaved bucket; ``handoff_rows`` how many rows came from the hand-off."""
+
+    reason: str
+    ptrs: Optional[List[int]]
+    base: Optional[int]
+    tv: Optional[int]
+    handoff_rows: int
+
+
 class AggregationEngine:
     """Drop-in host path bound to one GPU (``device``, else ``LOCAL_RANK``, else 0).
 
@@ -692,6 +706,53 @@ class AggregationEngine:
         s.sync()  # the copies' sources are kept alive by `hits` only until here
         return True
 
+    def _resolve_rows(self, s, rows: List[List[np.ndarray]], layout: BucketLayout, R: np.dtype, kind: str, K: int,
+                      prescale: Optional[Dict[int, float]], single: bool) -> "StagedRows":
+        """Where the K client rows of one FedAvg dtype group come from, and where they are in HBM
+        (VERDICT r05 "Next 3": one resolver, one reason).  In order of preference:
+
+        * ``prestaged-tiles`` / ``prestaged-rows``: :meth:`ingest` staged these very arrays while
+          the task loaded them (tile-interleaved or ``[K, ld]`` rows) and nothing wrote the slot since;
+        * ``handoff-in-place``: simulation mode, every row is a client export still on this GPU
+          (``handoff``): the kernel reads the clients' own buckets, nothing is copied;
+        * ``handoff-partial``: some rows are: copied device to device into ``[K, ld]``, the others
+          staged from the host;
+        * ``host-tiles`` / ``host-rows``: staged over PCIe through the pinned ring (tiled where the
+          library recommends it; rows with exact device casts for other dtypes).
+
+        The prestaged and hand-off paths take only one dtype group with no per-client prescale
+        (what :meth:`ingest` and the exports produce).  The out-of-core path (``out-of-core``) is
+        decided before this, for the whole call."""
+        isz = R.itemsize
+        ld_bytes = layout.ld * isz
+        d_rows = s.buffer(self._B_BUCKET, K * ld_bytes)
+        rows_at = lambda d: [d + k * ld_bytes for k in range(K)]  # noqa: E731
+        if prescale is None and single:
+            rec = self._prestaged.get(self._B_BUCKET)
+            if rec is not None and rec[1] < 0 and kind in TILED_KINDS:  # ingest staged them tiled
+                d_t = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, -rec[1]) * isz)
+                if self._take_prestaged(self._B_BUCKET, d_t, rec[1], rows):
+                    return StagedRows("prestaged-tiles", None, d_t, -rec[1], 0)
+            elif self._take_prestaged(self._B_BUCKET, d_rows, ld_bytes, rows):
+                return StagedRows("prestaged-rows", rows_at(d_rows), None, None, 0)
+            hand = self._handoff_rows(s, rows, layout, R, K)
+            if hand is not None:
+                self._prestaged.pop(self._B_BUCKET, None)
+                n = sum(1 for r in self._last_handoff if r)
+                if isinstance(hand, list):
+                    return StagedRows("handoff-in-place", hand, None, None, n)
+                return StagedRows("handoff-partial", rows_at(hand), None, None, n)
+        self._prestaged.pop(self._B_BUCKET, None)
+        tiled = self._tiled_rows(rows, R, kind, K, layout.M) if prescale is None else None
+        if tiled is not None:  # tile-interleaved buckets, one gather per pinned chunk
+            tv = tiled_tile(kind, K, layout.M)
+            d_t = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, tv) * isz)
+            s.stage_tiled(d_t, tv * 16, tiled)
+            return StagedRows("host-tiles", None, d_t, tv, 0)
+        d_rows = s.buffer(self._B_BUCKET, K * ld_bytes)  # current after a regrow
+        self._stage_rows(s, rows, layout, d_rows, prescale)
+        return StagedRows("host-rows", rows_at(d_rows), None, None, 0)
+
     # ----------------------------------------------------------------------------------
     @serialized
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int],
@@ -727,7 +788,7 @@ class AggregationEngine:
             ooc = self._out_of_core(need, (self._B_BUCKET, self._B_OUT, self._B_WS)) if direct else None
             if ooc is not None:
                 out = ooc.fedavg(parameters_updates, n_samples, wire)
-                self.last_timing = {"out_of_core": ooc.last_timing}
+                self.last_timing = {"out_of_core": ooc.last_timing, "staging": "out-of-core"}
                 return out
         results: List[Optional[np.ndarray]] = [None] * L
         if len(groups) != 1:
@@ -744,51 +805,22 @@ class AggregationEngine:
                 prescale = {k: w64[k] for k, d in enumerate(mixed) if np.dtype(d) != R}
                 for k in prescale:
                     w[k] = 1  # x * 1 is exact: the client's product was formed in its own dtype
-            d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * R.itemsize)
             t0 = time.perf_counter()
-            tv = None  # tile-interleaved buckets (TiledFedAvgPlan) when set
-            staged = False
-            if prescale is None and len(groups) == 1:
-                rec = self._prestaged.get(self._B_BUCKET)
-                if rec is not None and rec[1] < 0 and kind in TILED_KINDS:  # ingest staged them tiled
-                    d_t = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, -rec[1]) * R.itemsize)
-                    if self._take_prestaged(self._B_BUCKET, d_t, rec[1], rows):
-                        staged, d_bucket, tv = True, d_t, -rec[1]
-                else:
-                    staged = self._take_prestaged(self._B_BUCKET, d_bucket, layout.ld * R.itemsize, rows)
-            row_ptrs = None  # the clients' own device buckets (a full hand-off), read in place
-            if not staged and prescale is None and len(groups) == 1:
-                hand = self._handoff_rows(s, rows, layout, R, K)
-                if hand is not None:
-                    self._prestaged.pop(self._B_BUCKET, None)
-                    staged = True
-                    if isinstance(hand, list):
-                        row_ptrs = hand
-                    else:
-                        d_bucket = hand
-                    tm["handoff_rows"] = sum(1 for r in self._last_handoff if r)
-            if staged:
-                tm["prestaged"] = not tm.get("handoff_rows")
-            else:
-                self._prestaged.pop(self._B_BUCKET, None)
-                tiled = self._tiled_rows(rows, R, kind, K, layout.M) if prescale is None else None
-                if tiled is not None:  # tile-interleaved buckets, one gather per pinned chunk
-                    tv = tiled_tile(kind, K, layout.M)
-                    d_bucket = s.buffer(self._B_BUCKET, tiled_elems(kind, K, layout.M, tv) * R.itemsize)
-                    s.stage_tiled(d_bucket, tv * 16, tiled)
-                else:
-                    d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * R.itemsize)  # current after a regrow
-                    self._stage_rows(s, rows, layout, d_bucket, prescale)
+            st = self._resolve_rows(s, rows, layout, R, kind, K, prescale, len(groups) == 1)
+            tm["staging"] = st.reason if len(groups) == 1 else "per-dtype-groups"
+            if st.handoff_rows:
+                tm["handoff_rows"] = st.handoff_rows
+            tm["prestaged"] = st.reason.startswith("prestaged")
+            tv = st.tv
             tm["stage_s"] = tm.get("stage_s", 0.0) + time.perf_counter() - t0
             tm["layout"] = "tiles" if tv is not None else "rows"
             d_out = s.buffer(self._B_OUT, layout.ld * R.itemsize)
             ws = s.buffer(self._B_WS, _native.load().fedagg_pairwise_ws_bytes(K, layout.pairwise_idx.size, 8))
             t1 = time.perf_counter()
             if tv is not None:
-                TiledFedAvgPlan(kind, d_bucket, K, w, layout.M, d_out, layout.pairwise_idx, ws, tv).launch(s.stream)
+                TiledFedAvgPlan(kind, st.base, K, w, layout.M, d_out, layout.pairwise_idx, ws, tv).launch(s.stream)
             else:
-                ptrs = row_ptrs if row_ptrs is not None else [d_bucket + k * layout.ld * R.itemsize for k in range(K)]
-                FedAvgPlan(kind, ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
+                FedAvgPlan(kind, st.ptrs, w, layout.M, d_out, layout.pairwise_idx, ws).launch(s.stream)
             out = runtime.reusable_host_array(layout.M, R, f"fedavg{'-mixed' if mixed else ''}")
             s.fetch(d_out, out)  # stream-ordered after the kernel; returns when the data is home
             self._handoff_keep = None  # the kernel is done with the clients' buckets
@@ -812,45 +844,91 @@ class AggregationEngine:
         stays ``-0.0`` -- and no pairwise order for ``numel == 1`` layers (the loop is an explicit
         ``+=``).  On the device: client 0's product written by ``fedagg_scale_cast`` (its own
         float type, exactly ``x_0 * c_0``), then ``fedagg_fedavg_chain_*`` continuing that
-        accumulator over clients 1..K-1 (seed 0), one stage of the K rows, one fetch.  Layers of
-        ONE float product dtype across clients (fp32 / fp64; integer layers multiply as fp64 and
-        are cast on the device); other mixes raise NotImplementedError (the reference's in-place
-        ``+=`` would cast into client 0's type)."""
+        accumulator over clients 1..K-1 (seed 0), one fetch.
+
+        dtypes: each client's product type is ``result_type(x_k, float)`` (fp16 / fp32 / fp64;
+        integers multiply as fp64, cast on the device); the accumulator keeps CLIENT 0's type, as
+        the in-place ``+=`` does.  A client of another type is added the way NumPy's
+        ``+=`` adds it: its product in its own type, the sum in the promoted type P of the two
+        (accumulator widened exactly, ``fedagg_fedavg_chain`` with weight 1.0: ``acc + p``), then
+        rounded back into client 0's type (``fedagg_cast``).  Every client's layers must share one
+        product type (a concatenated gradient is one array)."""
         rows = native_byte_order(rows)
         K, L = len(rows), len(rows[0])
         if L == 0:
             return []
-        pds = {np.result_type(a.dtype, 1.0) for row in rows for a in row}
-        R = np.dtype(next(iter(pds)))
-        if len(pds) != 1 or R not in (np.float32, np.float64):
-            raise NotImplementedError(f"sequential_sum: one float32 / float64 product dtype across clients and "
-                                      f"layers (got {sorted(str(d) for d in pds)})")
-        kind = kind_of(R)
+        pdt = []
+        for row in rows:
+            ds = {np.result_type(a.dtype, 1.0) for a in row}
+            if len(ds) != 1 or next(iter(ds)) not in (np.float16, np.float32, np.float64):
+                raise NotImplementedError(f"sequential_sum: one float16 / float32 / float64 product dtype per client "
+                                          f"(got {sorted(str(d) for d in ds)})")
+            pdt.append(np.dtype(next(iter(ds))))
+        T0 = pdt[0]  # total = x_0 * c_0 keeps this type through every +=
         n_all = sum(int(n) for n in n_samples)
         if n_all == 0:
             raise ZeroDivisionError("division by zero")  # n_samples / n_all_samples (newton_raphson.py:201)
-        layout = BucketLayout(list(range(L)), [a.shape for a in rows[0]], R)
-        isz = R.itemsize
+        coeff = [int(n) / n_all for n in n_samples]
+        shapes = [a.shape for a in rows[0]]
+        layout = BucketLayout(list(range(L)), shapes, T0)
+        M = layout.M
         s = self.session()
         self._prestaged = {}
         self.last_timing = tm = {}
         t0 = time.perf_counter()
-        d_bucket = s.buffer(self._B_BUCKET, K * layout.ld * isz)
-        self._stage_rows(s, rows, layout, d_bucket)
+        uniform = all(d == T0 for d in pdt)
+        # row stride: room for a row of any float type (the fp16 layout's ld is a multiple of the others')
+        stride = layout.ld * T0.itemsize if uniform else BucketLayout(list(range(L)), shapes, np.float16).ld * 8
+        d_bucket = s.buffer(self._B_BUCKET, K * stride)
+        if uniform:
+            self._stage_rows(s, rows, layout, d_bucket)
+        else:
+            for k in range(K):
+                self._stage_rows(s, [rows[k]], BucketLayout(list(range(L)), shapes, pdt[k]), d_bucket + k * stride)
         tm["stage_s"] = time.perf_counter() - t0
-        d_out = s.buffer(self._B_OUT, layout.ld * isz)
-        s.scale_cast(d_bucket, R, int(n_samples[0]) / n_all, d_out, R, layout.M)
-        if K > 1:
-            lib = _native.load()
-            w = fedavg_weights(n_samples, kind)[1:]
-            warr = ((ctypes.c_float if kind == "f32" else ctypes.c_double) * len(w))(*[float(v) for v in w])
-            ptrs = _native.ptr_array([d_bucket + k * layout.ld * isz for k in range(1, K)])
-            _native.check(getattr(lib, f"fedagg_fedavg_chain_{kind}")(ptrs, warr, K - 1, layout.M, 0, d_out,
-                                                                        s.stream), "fedavg_chain")
-        out = runtime.reusable_host_array(layout.M, R, "seqsum")
+        d_out = s.buffer(self._B_OUT, stride)
+        s.scale_cast(d_bucket, T0, coeff[0], d_out, T0, M)
+        k = 1
+        while k < K:
+            if pdt[k] == T0:  # a run of clients of client 0's type: one chain launch continues the total
+                j = k
+                while j < K and pdt[j] == T0:
+                    j += 1
+                self._chain(s, kind_of(T0), [d_bucket + i * stride for i in range(k, j)],
+                            [coeff[i] for i in range(k, j)], M, d_out)
+                k = j
+                continue
+            P = np.dtype(np.result_type(T0, pdt[k]))  # the type NumPy's += adds in
+            d_p = s.buffer(self._B_CV, stride)
+            s.scale_cast(d_bucket + k * stride, pdt[k], coeff[k], d_p, P, M)  # x_k * c_k in its own type
+            if P == T0:
+                self._chain(s, kind_of(P), [d_p], [1.0], M, d_out)
+            else:
+                d_acc = s.buffer(self._B_C, stride)
+                s.cast(d_out, T0, d_acc, P, M)  # exact widening
+                self._chain(s, kind_of(P), [d_p], [1.0], M, d_acc)
+                s.cast(d_acc, P, d_out, T0, M)  # rounded back into client 0's type
+            k += 1
+        out = runtime.reusable_host_array(M, T0, "seqsum")
         s.fetch(d_out, out)
         tm["total_s"] = time.perf_counter() - t0
+        tm["mixed_dtypes"] = not uniform
         return [arr for _, arr in layout.unpack(out, wire)]
+
+    @staticmethod
+    def _chain(s, kind: str, ptrs: List[int], coeffs: List[float], M: int, d_acc: int) -> None:
+        """acc = fl(acc + fl(x_i * fl_kind(c_i))) over the rows ``ptrs`` in order, on the session
+        stream (``fedagg_fedavg_chain_{kind}``, seed 0: the accumulator continues)."""
+        lib = _native.load()
+        w = np.asarray(coeffs, dtype=np.float64)
+        if kind == "f32":
+            warr = (ctypes.c_float * len(w))(*[float(v) for v in w.astype(np.float32)])
+        elif kind == "f64":
+            warr = (ctypes.c_double * len(w))(*[float(v) for v in w])
+        else:
+            warr = (ctypes.c_uint16 * len(w))(*[int(v) for v in w.astype(np.float16).view(np.uint16)])
+        _native.check(getattr(lib, f"fedagg_fedavg_chain_{kind}")(_native.ptr_array(ptrs), warr, len(ptrs), M, 0,
+                                                                    d_acc, s.stream), "fedavg_chain")
 
     # ----------------------------------------------------------------------------------
     @serialized

@@ -24,6 +24,20 @@ copy, so results never depend on the hand-off):
 * a recorded engine output slot has not been written since: every engine call invalidates the
   slot records of its GPUs (``engine.serialized``), and the slot's write generation is unchanged.
 
+Who records (VERDICT r05 "Next 3"): a side of the hand-off freezes its host arrays only when the
+other side is an accelerated consumer that can take them on the device -- the engine's outputs
+while an ``accelerate_algo`` client lives (:func:`register` "client"), a client's exports while an
+``accelerate``-d strategy lives ("aggregator").  The reference's own algorithms next to an
+accelerated strategy therefore receive writable outputs, exactly the reference's
+(``torch.from_numpy`` at torch_fed_avg_algo.py:189 / torch_scaffold_algo.py:397,405 warns on a
+read-only array), and nothing is recorded for them.
+
+Lifetime: a client export's record (it keeps the client's device bucket alive) is
+used once -- the aggregation that takes it drops it; an engine output's record holds no device
+memory of its own.  When the last registered consumer of the process is gone (the experiment's
+strategy and algorithms were released) every record is dropped and the recycled host buffers are
+forgotten (``runtime.drop_host_pools``).
+
 A process that never enables the hand-off records nothing, and every lookup is a dictionary miss.
 """
 
@@ -40,6 +54,9 @@ _enabled = os.environ.get("FEDAGG_HANDOFF", "0") == "1"
 _lock = threading.Lock()
 _records: Dict[int, "_Record"] = {}  # start address of the recorded host byte range -> record
 stats = {"recorded": 0, "taken": 0, "refused": 0}  # counters (tests, benches)
+# live accelerated consumers: "client" (accelerate_algo instances: take the engine's outputs on the
+# device), "aggregator" (accelerate-d strategies: take the clients' exports on the device)
+_consumers: Dict[str, int] = {"client": 0, "aggregator": 0}
 
 
 def enable(flag: bool = True) -> None:
@@ -47,15 +64,48 @@ def enable(flag: bool = True) -> None:
     global _enabled
     _enabled = bool(flag)
     if not _enabled:
-        with _lock:
-            _records.clear()
-            for fin in _finalizers.values():
-                fin.detach()
-            _finalizers.clear()
+        _clear()
+
+
+def _clear() -> None:
+    with _lock:
+        _records.clear()
+        for fin in _finalizers.values():
+            fin.detach()
+        _finalizers.clear()
 
 
 def enabled() -> bool:
     return _enabled
+
+
+def register(kind: str, obj) -> None:
+    """``obj`` takes part in the hand-off while it lives: an ``accelerate_algo`` client (``kind``
+    "client": the engine's outputs are then recorded for it) or an ``accelerate``-d strategy
+    ("aggregator": the clients' exports are then recorded for it).  Called by their constructors
+    whether or not the hand-off is enabled (a dictionary increment)."""
+    if kind not in _consumers:
+        raise ValueError(f"hand-off consumer kind {kind!r}: 'client' or 'aggregator'")
+    with _lock:
+        _consumers[kind] += 1
+    fin = weakref.finalize(obj, _unregister, kind)
+    fin.atexit = False
+
+
+def consumers() -> Dict[str, int]:
+    with _lock:
+        return dict(_consumers)
+
+
+def _unregister(kind: str) -> None:
+    with _lock:
+        _consumers[kind] -= 1
+        last = not any(_consumers.values())
+    if last:  # the experiment's strategy and algorithms are gone: nothing will consume a record
+        _clear()
+        from . import runtime
+
+        runtime.drop_host_pools()
 
 
 class _Record:
@@ -141,7 +191,8 @@ def _drop(start: int) -> None:
 def record_tensor(host: np.ndarray, flat) -> None:
     """``host`` (1-D, the exported bytes, C-contiguous) was fetched from the torch tensor ``flat``
     (same bytes, on a GPU): freeze ``host`` and remember ``flat`` for device consumers."""
-    if not _enabled or not getattr(flat, "is_cuda", False) or host.nbytes != flat.numel() * flat.element_size():
+    if not _enabled or not _consumers["aggregator"] or not getattr(flat, "is_cuda", False) or \
+            host.nbytes != flat.numel() * flat.element_size():
         return
     rec = _put(host, flat.device.index)
     rec.tensor, rec.version, rec.dptr = flat, flat._version, int(flat.data_ptr())
@@ -152,7 +203,7 @@ def record_slot(host: np.ndarray, session, slot: int, dptr: int, stable: bool = 
     and remember the slot, valid until the slot is written again.  ``stable``: a slot that only
     the runtime's own copies write (each bumps its generation), so engine calls on the device do
     not invalidate the record -- the next call can still read it before replacing it."""
-    if not _enabled:
+    if not _enabled or not _consumers["client"]:
         return
     rec = _put(host, session.device)
     rec.session, rec.slot, rec.gen, rec.dptr = session, int(slot), session.generation(slot), int(dptr)
@@ -192,6 +243,8 @@ def lookup(arrays: Sequence[np.ndarray], device: int) -> Optional[Tuple[int, int
         ok = rec.session.generation(rec.slot) == rec.gen
     with _lock:
         stats["taken" if ok else "refused"] += 1
+        if ok and rec.tensor is not None and _records.get(start) is rec:
+            del _records[start]  # a client export is consumed once: its device bucket goes with the caller's keep-alive
     if not ok:
         return None
     return rec.dptr, nbytes, (rec.tensor if rec.tensor is not None else rec.session)

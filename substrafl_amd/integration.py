@@ -39,6 +39,7 @@ from typing import Optional
 
 import numpy as np
 
+from . import handoff
 from .engine import Devices, engine_for
 from .strategies.fed_avg import check_same_shapes, weighted_average
 from .strategies.scaffold import Scaffold as _MirrorScaffold
@@ -61,7 +62,14 @@ def accelerate(strategy_cls, device: Devices = None):
     ``device`` (:func:`engine.engine_for`: None = the current GPU, an index, a list, or "all")."""
     strategies, schemas, remote, exceptions = _reference_modules(strategy_cls)
     empty = exceptions.EmptySharedStatesError
+    base_init = strategy_cls.__init__
+
+    def __init__(self, *args, **kwargs):
+        base_init(self, *args, **kwargs)
+        handoff.register("aggregator", self)  # the clients' exports are recorded for it (handoff.py)
+
     ns = {"__doc__": f"{strategy_cls.__name__} with its aggregation on MI355X (substrafl_amd.integration).",
+          "__init__": __init__,
           "_fedagg_device": device,
           # the task-process hooks of INTEGRATION.md §3 (prewarm, overlapped ingest), as the mirrors have them
           "prewarm_aggregation": _MirrorStrategy.prewarm_aggregation,

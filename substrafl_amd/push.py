@@ -110,8 +110,10 @@ class PushTransport:
         every rank that waited, naming what it waited for; the transport stays failed).
         ``fault``: TEST ONLY (tests/test_push_gpu.py), a failure injected on one rank:
         ``("signal", rank, t)`` -- that rank stops before its step t, so it never signals step t
-        (a peer that died mid-call); ``("tag", rank, i)`` -- that rank never writes the i-th landing
-        tag of its program (its data lands, the proof of it never does)."""
+        (a peer stuck mid-call); ``("exit", rank, t)`` -- the same, then that rank's process exits
+        without releasing anything (a peer that died mid-call: it never meets another collective);
+        ``("tag", rank, i)`` -- that rank never writes the i-th landing tag of its program (its data
+        lands, the proof of it never does)."""
         import torch
         import torch.distributed as dist
         from multiprocessing import shared_memory
@@ -139,8 +141,8 @@ class PushTransport:
         _check(self.lib.fedagg_wall_clock_hz(ctypes.byref(hz)), "fedagg_wall_clock_hz")
         self._timeout = int(timeout_s * hz.value)
         self.base = 0
-        if fault is not None and (fault[0] not in ("signal", "tag") or len(fault) != 3):
-            raise ValueError(f"push fault injection: ('signal' | 'tag', rank, step | index), not {fault!r}")
+        if fault is not None and (fault[0] not in ("signal", "exit", "tag") or len(fault) != 3):
+            raise ValueError(f"push fault injection: ('signal' | 'exit' | 'tag', rank, step | index), not {fault!r}")
         self.fault = fault
         self._maps: Dict[bytes, int] = {}
         self._programs: List["PushProgram"] = []
@@ -182,6 +184,12 @@ class PushTransport:
         import torch
 
         torch.cuda.synchronize(self.device)
+        if self.failed():
+            # a rank whose peer died would wait in this barrier for the backend's timeout, and a
+            # gloo barrier that raises would replace the error that names the failed wait: after a
+            # failure nothing collective runs, the buffers stay allocated
+            self._abandon_programs()
+            return
         if self.world > 1:
             self.dist.barrier(group=self.group)
         for p in self._programs:
@@ -229,6 +237,7 @@ class PushTransport:
         repeats (same plan, client blocks and outputs: the device-resident loop), else a new one --
         the cached program is released first (collective, like the compile), so one program's
         buffers and mappings are alive at a time."""
+        self.raise_errors()  # a failed group cannot compile a program (its set-up is collective)
         for p in self._programs:
             if p.matches(**kw):
                 p.rebase_outs(kw["outs"])
@@ -265,7 +274,7 @@ class PushTransport:
                                                            prog.ntags, prog.nsteps)
         if self.fault is not None and self.fault[1] == self.rank:  # TEST ONLY: the injected failure
             what, _r, at = self.fault
-            if what == "signal":  # stop before step `at`: its signal (and every later one) never comes
+            if what in ("signal", "exit"):  # stop before step `at`: its signal (and every later one) never comes
                 keep = lambda arr, n: [x for x in arr[:n] if x.step < at]  # noqa: E731
                 r_, w_, t_ = keep(runs, nruns), keep(waits, nwaits), keep(tags, ntags)
                 nsteps, ws_src, ws_dst, ws_bytes, stage, ncopies = min(at, nsteps), None, None, 0, None, 0
@@ -283,6 +292,23 @@ class PushTransport:
                                             ctypes.byref(prog.copies) if ncopies else None, ncopies,
                                             self._aux_ptrs if naux else None, naux, int(stream)), "fedagg_push_execute")
         self.base += prog.nsteps + 1
+        if self.fault is not None and self.fault[1] == self.rank and self.fault[0] == "exit":  # TEST ONLY
+            import torch
+
+            torch.cuda.synchronize(self.device)  # its steps before `at` are done; then it dies
+            os._exit(FAULT_EXIT_CODE)
+
+    def failed(self) -> bool:
+        """Whether a wait of some rank gave up (:meth:`errors`): the group cannot meet again -- a
+        peer may have died, and a surviving one may still be finishing its steps into this rank's
+        buffers.  A failed transport runs no collective and frees no program buffer any more."""
+        return self._page is not None and bool(self.errors())
+
+    def _abandon_programs(self) -> None:
+        """Keep the programs' buffers alive for the life of the process (a surviving peer may still
+        push into them after its waits gave up) and drop this transport's references to them."""
+        _ABANDONED.extend(self._programs)
+        self._programs = []
 
     def close(self) -> None:
         if getattr(self, "_dev", None) is None:
@@ -290,7 +316,10 @@ class PushTransport:
         import torch
 
         torch.cuda.synchronize(self.device)
-        self.dist.barrier(group=self.group)  # nobody writes into a mapping that is going away
+        if self.failed():  # no barrier a dead peer would never meet
+            self._abandon_programs()
+        else:
+            self.dist.barrier(group=self.group)  # nobody writes into a mapping that is going away
         self._programs.clear()
         for base in self._maps.values():
             self.lib.fedagg_ipc_close(base)
@@ -302,6 +331,9 @@ class PushTransport:
         if self.rank == 0:
             self._shm.unlink()
 
+
+FAULT_EXIT_CODE = 17  # TEST ONLY: the exit status of a rank the ("exit", rank, t) fault kills
+_ABANDONED: List["PushProgram"] = []  # programs of failed transports: never freed while the process lives
 
 PUSH_TAG_ERR, PUSH_PEER_ERR = 1 << 32, 1 << 33  # csrc/lockstep.hip: the err word's cause bits
 

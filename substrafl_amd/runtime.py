@@ -237,6 +237,17 @@ class Session:
         self.lib.fedagg_session_timing(self._h, ctypes.byref(a), ctypes.byref(b))
         return {"stage_s": a.value, "fetch_s": b.value}
 
+    PHASES = ("hip_init_s", "streams_s", "ring_s", "pool_s", "buffers_s", "code_object_s")
+
+    def phases(self) -> Dict[str, float]:
+        """Start-up phases of this session (``fedagg_session_phases``): the HIP runtime's start and
+        the device, the streams, then the warm's pinned ring, worker pool, HBM buffers and
+        code-object load; seconds, 0.0 for a phase that has not run."""
+        n = _native.FEDAGG_SESSION_PHASES
+        out = (ctypes.c_double * n)()
+        _native.check(self.lib.fedagg_session_phases(self._h, out, n), "session_phases")
+        return {k: round(float(v), 6) for k, v in zip(self.PHASES, out)}
+
     # ----------------------------------------------------------------------------------
     def cast(self, d_in: int, in_dtype, d_out: int, out_dtype, n: int) -> None:
         self._bump(d_out)
@@ -285,10 +296,11 @@ def device_lock(device: int) -> threading.RLock:
         return lk
 
 
-_host_cache: Dict[tuple, list] = {}
+_host_cache: Dict[tuple, dict] = {}
 _host_lock = threading.Lock()
 HOST_POOL_DEPTH = 64  # buffers kept per call site and dtype ...
 HOST_POOL_BYTES = 16 << 30  # ... within this many bytes
+HOST_POOL_IDLE = 2  # a free buffer not handed out again within this many turns of its pool is released
 
 
 def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
@@ -296,29 +308,50 @@ def reusable_host_array(n: int, dtype, tag: str) -> np.ndarray:
     100 MB allocation costs ~8 ms of first-touch page faults (glibc maps every block above 32 MiB
     anew), three times the D2H itself, so earlier calls' buffers are recycled -- but only one that
     nothing references any more (every array handed out from it was a view holding it), so no
-    caller ever sees its data change.  Up to ``HOST_POOL_DEPTH`` buffers and ``HOST_POOL_BYTES``
-    per site: in simulation mode the previous round's results are still held while the next
-    round's are made (the strategy keeps its last train states, and its last average, until the
-    new ones are returned), K clients' exports of two rounds at once, so the pool grows to that
-    working set and then recycles it; past the caps the least recently used buffer is forgotten
-    (its holders keep it; it is freed with them)."""
+    caller ever sees its data change.  The pool follows the site's working set: in simulation mode
+    the previous round's results are still held while the next round's are made (the strategy
+    keeps its last train states, and its last average, until the new ones are returned), K
+    clients' exports of two rounds at once, so it grows to that and then recycles it; a free buffer
+    not handed out again within ``HOST_POOL_IDLE`` turns of the pool (one turn = as many requests
+    as the pool holds buffers) is released, so a working set that shrinks gives its buffers back
+    (ADVICE r05); ``HOST_POOL_DEPTH`` / ``HOST_POOL_BYTES`` bound it, the least recently used going
+    first (its holders keep it; it is freed with them)."""
     import sys
 
     key = (tag, np.dtype(dtype))
     with _host_lock:
-        pool = _host_cache.setdefault(key, [])
-        for i in range(len(pool)):  # (not enumerate: its cached result tuple would hold one more reference)
-            buf = pool[i]
-            # references: the pool list, the local name and getrefcount's argument; a live view adds one
+        site = _host_cache.setdefault(key, {"tick": 0, "pool": []})
+        site["tick"] += 1
+        tick, pool = site["tick"], site["pool"]  # entries [buffer, tick of its last hand-out]
+        out = None
+        # the most recently used free buffer first (warm pages; the others can age out)
+        for i in range(len(pool) - 1, -1, -1):  # (not enumerate: its cached tuple would hold one more reference)
+            buf = pool[i][0]
+            # references: the entry, the local name and getrefcount's argument; a live view adds one
             if buf.size >= n and sys.getrefcount(buf) <= 3:
-                pool.append(pool.pop(i))  # most recently used last
+                ent = pool.pop(i)
+                ent[1] = tick
+                pool.append(ent)  # most recently used last
                 buf.flags.writeable = True  # a device hand-off (handoff.py) may have frozen it
-                return buf[:n]
-        buf = np.empty(n, dtype=key[1])
-        pool.append(buf)
-        while len(pool) > 1 and (len(pool) > HOST_POOL_DEPTH or sum(b.nbytes for b in pool) > HOST_POOL_BYTES):
+                out = buf[:n]
+                break
+        buf = None
+        if out is None:
+            out = np.empty(n, dtype=key[1])
+            pool.append([out, tick])
+        idle = HOST_POOL_IDLE * max(2, len(pool))
+        keep = []
+        for ent in pool:  # free buffers idle past the working set go (a held one stays listed)
+            b = ent[0]
+            if tick - ent[1] > idle and b is not out and b is not getattr(out, "base", None) \
+                    and sys.getrefcount(b) <= 3:
+                continue
+            keep.append(ent)
+        b = None
+        pool[:] = keep
+        while len(pool) > 1 and (len(pool) > HOST_POOL_DEPTH or sum(e[0].nbytes for e in pool) > HOST_POOL_BYTES):
             pool.pop(0)  # the least recently used; still alive through its holders' views, if any
-        return buf
+        return out
 
 
 def drop_host_pools() -> None:
@@ -348,6 +381,12 @@ _lock = threading.Lock()
 _warming: Dict[int, threading.Thread] = {}
 _warm_errors: Dict[int, BaseException] = {}
 warm_times: Dict[int, tuple] = {}  # device -> (perf_counter at start, at end) of the last prewarm
+# device -> the prewarm's phases, seconds (VERDICT r05 "Next 4"): library_load_s (dlopen of
+# libfedagg.so and its code object's registration), session_s (the session object: the native
+# create below plus the Python side), then Session.phases() -- hip_init_s, streams_s, ring_s,
+# pool_s, buffers_s, code_object_s -- and total_s; "created_by_prewarm" False when another caller
+# had opened the session first (its create phases were then paid there)
+warm_phases: Dict[int, dict] = {}
 
 
 def session(device: int = 0) -> Session:
@@ -377,11 +416,24 @@ def prewarm(device: int = 0, slot_bytes: Optional[Dict[int, int]] = None) -> thr
             import time
 
             t0 = time.perf_counter()
+            ph: Dict[str, object] = {}
             try:
-                session(device).warm(slot_bytes or {})
+                _native.load()
+                t1 = time.perf_counter()
+                ph["library_load_s"] = round(t1 - t0, 6)
+                with _lock:
+                    created = device not in _sessions
+                s = session(device)
+                ph["session_s"] = round(time.perf_counter() - t1, 6)
+                ph["created_by_prewarm"] = created
+                s.warm(slot_bytes or {})
+                ph.update(s.phases())
             except BaseException as e:  # noqa: BLE001 - surfaced by the aggregation call
                 _warm_errors[device] = e
-            warm_times[device] = (t0, time.perf_counter())
+            t_end = time.perf_counter()
+            ph["total_s"] = round(t_end - t0, 6)
+            warm_phases[device] = ph
+            warm_times[device] = (t0, t_end)
 
         t = threading.Thread(target=run, name=f"fedagg-prewarm-{device}", daemon=True)
         _warming[device] = t

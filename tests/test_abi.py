@@ -49,7 +49,7 @@ def test_product_library_does_not_export_tuning_entry_points():
 
 def test_abi_version_and_invalid_arguments():
     lib = _native.load()
-    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 16
+    assert lib.fedagg_abi_version() == _native.ABI_VERSION == 17
     w = (ctypes.c_float * 1)(1.0)
     ptrs = _native.ptr_array([0])
     assert lib.fedagg_fedavg_f32(ptrs, w, 0, 16, None, 0, None, None, None) == -1  # K == 0
@@ -97,9 +97,9 @@ def test_missing_library_is_loud(monkeypatch, tmp_path):
         _native.load()
 
 
-def _build_c_demo(tmp_path):
-    """Compile tests/c/fedavg_abi_demo.c with gcc against include/fedagg.h and libfedagg.so: the
-    header is plain C and the library links without any HIP or Python headers."""
+def _build_c_demo(tmp_path, name="fedavg_abi_demo"):
+    """Compile tests/c/<name>.c with gcc against include/fedagg.h and libfedagg.so: the header is
+    plain C and the library links without any HIP or Python headers."""
     import shutil
     import subprocess
 
@@ -107,16 +107,30 @@ def _build_c_demo(tmp_path):
     gcc = shutil.which("gcc")
     if gcc is None:
         pytest.skip("gcc not available")
-    exe = tmp_path / "fedavg_abi_demo"
+    exe = tmp_path / name
     libdir = _native.LIB_PATH.parent
     subprocess.run([gcc, "-O2", "-ffp-contract=off", "-Wall", "-Werror", f"-I{root / 'include'}",
-                    str(root / "tests" / "c" / "fedavg_abi_demo.c"), f"-L{libdir}", "-lfedagg",
+                    str(root / "tests" / "c" / f"{name}.c"), f"-L{libdir}", "-lfedagg",
                     f"-Wl,-rpath,{libdir}", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)], check=True)
     return exe
 
 
 def test_c_demo_compiles_against_the_header(tmp_path):
     assert _build_c_demo(tmp_path).exists()
+    assert _build_c_demo(tmp_path, "fedavg_multi_demo").exists()
+
+
+def test_multi_entry_rejects_bad_arguments():
+    """fedagg_multi_* (VERDICT r05 "Next 5"): argument checks return before any HIP call."""
+    lib = _native.load()
+    assert lib.fedagg_multi_create(0, None, 0) is None
+    assert b"ndev" in lib.fedagg_last_error()
+    devs = (ctypes.c_int * 1)(0)
+    assert lib.fedagg_multi_create(1, devs, -1) is None
+    assert lib.fedagg_multi_fedavg_f32(None, 1, 0, None, None, None, None, 0, None) == -1
+    assert b"invalid argument" in lib.fedagg_last_error()
+    assert lib.fedagg_multi_set(None, b"max_shard_bytes", 1) == -1
+    assert lib.fedagg_multi_shard_info(None, 0, None, None, None, None, None, None, None) == -1
 
 
 @pytest.mark.gpu
@@ -127,6 +141,18 @@ def test_c_demo_runs_bit_exact(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches=0" in r.stdout
+
+
+@pytest.mark.gpu
+def test_c_multi_demo_runs_bit_exact(tmp_path):
+    """The one-call multi-device entry from plain C, two shards on GPU 0 (each its own session,
+    several sub-ranges each): bit-identical to the single-device call and to the reference order."""
+    import subprocess
+
+    exe = _build_c_demo(tmp_path, "fedavg_multi_demo")
+    r = subprocess.run([str(exe), "0", "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches=0 again=0 vs_reference_order=0" in r.stdout and "used=2" in r.stdout, r.stdout
 
 
 def _declared_arity():

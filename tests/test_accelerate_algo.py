@@ -98,7 +98,7 @@ def _state(algo):
     return [t.detach().cpu().numpy().copy() for t in algo.model.state_dict().values()]
 
 
-def run_fedavg(accelerated, *, bn, disable_gpu, wire=False, copy_exports=False):
+def run_fedavg(accelerated, *, bn, disable_gpu, wire=False, copy_exports=False, accel_strategy=None):
     """Two clients, ROUNDS rounds.  Returns every exported update and every client's model state
     after every train (a trace to compare bit for bit).  ``copy_exports``: the trace keeps copies,
     so a round's exports are released once the next round's are made (the strategy's pattern),
@@ -110,7 +110,9 @@ def run_fedavg(accelerated, *, bn, disable_gpu, wire=False, copy_exports=False):
         cls = _algo(TorchFedAvgAlgo, bn=bn, disable_gpu=disable_gpu, client=k)
         algos.append((accelerate_algo(cls, wire=wire) if accelerated else cls)())
     # on the GPU the accelerated pipeline aggregates on the engine too; the CPU has no engine
-    strategy = accelerate(ss.FedAvg)(algo=algos[0]) if accelerated and not disable_gpu else None
+    if accel_strategy is None:
+        accel_strategy = accelerated and not disable_gpu
+    strategy = accelerate(ss.FedAvg)(algo=algos[0]) if accel_strategy else None
     trace, avg = [], None
     for _ in range(ROUNDS):
         states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, DATA)]
@@ -128,15 +130,16 @@ def run_fedavg(accelerated, *, bn, disable_gpu, wire=False, copy_exports=False):
     return trace, algos, states
 
 
-def run_scaffold(accelerated, *, bn, disable_gpu, aggregation_lr=0.7):
+def run_scaffold(accelerated, *, bn, disable_gpu, aggregation_lr=0.7, accel_strategy=None):
     from substrafl_amd.integration import accelerate, accelerate_algo
 
     algos = []
     for k in range(2):
         cls = _algo(TorchScaffoldAlgo, bn=bn, disable_gpu=disable_gpu, client=k)
         algos.append((accelerate_algo(cls) if accelerated else cls)())
-    strategy = (accelerate(ss.Scaffold)(algo=algos[0], aggregation_lr=aggregation_lr)
-                if accelerated and not disable_gpu else None)
+    if accel_strategy is None:
+        accel_strategy = accelerated and not disable_gpu
+    strategy = accelerate(ss.Scaffold)(algo=algos[0], aggregation_lr=aggregation_lr) if accel_strategy else None
     trace, avg = [], None
     for _ in range(ROUNDS):
         states = [a.train(data_from_opener=d, shared_state=avg, _skip=True) for a, d in zip(algos, DATA)]
@@ -430,3 +433,56 @@ def test_handoff_device_memory_stays_flat_over_rounds(gpu, handoff_on):
         used.append(torch.cuda.memory_allocated())
     assert max(used[4:]) <= used[3], used  # no growth once the pools and records turn over
     assert len(handoff_on.records()) <= 4 * 4 + 8, handoff_on.records()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["fedavg", "scaffold"])
+def test_handoff_with_the_reference_algorithms_changes_nothing(gpu, strategy):
+    """VERDICT r05 "Next 3": ``accelerate(FedAvg)`` / ``accelerate(Scaffold)`` next to the
+    reference-shaped, NON-accelerated client algorithms with the hand-off on.  No accelerated
+    client lives to take the engine's outputs on the device, so they are neither recorded nor
+    frozen: the reference's ``torch.from_numpy`` (torch_fed_avg_algo.py:189,
+    torch_scaffold_algo.py:397,405) gets writable arrays and warns nothing, and the run is
+    bit-identical to the reference pipeline's."""
+    import gc
+    import warnings
+
+    from substrafl_amd import handoff
+
+    gc.collect()  # accelerated objects of earlier tests gone: no consumer outlives its test
+    assert handoff.consumers()["client"] == 0, handoff.consumers()
+    run = run_fedavg if strategy == "fedavg" else run_scaffold
+    ref, _, _ = run(False, bn=True, disable_gpu=False)
+    handoff.enable(True)
+    try:
+        recorded = handoff.stats["recorded"]
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            mixed, _, _ = run(False, bn=True, disable_gpu=False, accel_strategy=True)
+        assert handoff.stats["recorded"] == recorded and not handoff.records()
+    finally:
+        handoff.enable(False)
+    _compare(ref, mixed)
+    outs = [v for t, v in mixed if t in ("avg", "new_c")]
+    assert outs and all(a.flags.writeable for arrs in outs for a in arrs)
+    assert not [w for w in caught if "not writable" in str(w.message)], [str(w.message) for w in caught]
+
+
+@pytest.mark.gpu
+def test_handoff_with_a_reference_aggregator_freezes_nothing(gpu):
+    """The other mixed pairing: accelerated clients aggregated by the reference's arithmetic (no
+    accelerated strategy alive): the clients' exports are not recorded, so they stay writable."""
+    import gc
+
+    from substrafl_amd import handoff
+
+    gc.collect()
+    assert handoff.consumers()["aggregator"] == 0, handoff.consumers()
+    ref, _, _ = run_fedavg(False, bn=True, disable_gpu=False)
+    handoff.enable(True)
+    try:
+        acc, _, states = run_fedavg(True, bn=True, disable_gpu=False, accel_strategy=False)
+        assert all(a.flags.writeable for a in states[0].parameters_update)
+    finally:
+        handoff.enable(False)
+    _compare(ref, acc)

@@ -270,3 +270,40 @@ def test_shared_gpu_lines_carry_no_scaling_claim():
     own = {"value": 1.0}
     bench._label_shared_gpu(types.SimpleNamespace(world=2, physical_gpus=2), own, ("value",))
     assert own == {"value": 1.0}
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_rehearsed_n_gpu_line_with_every_leg(n, tmp_path):
+    """VERDICT r05 "Next 1": the N = 4 and N = 8 lines as the driver's node will run them, every leg
+    on its CPU stand-in (--rehearse-legs: the legs' child processes per rank, their gloo groups,
+    connect deadlines and result gathering at 4 / 8 ranks).  The line exits 0 inside
+    LINE_BUDGET_S, reports the N, carries the decisive legs' fields with each leg's set-up time
+    beside its deadline, and reads through tools/n_gt_1_report.py without a flag."""
+    import time
+
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tools"))
+    import bench
+    import n_gt_1_report as rep
+
+    t0 = time.monotonic()
+    r = _run(["--gpus", str(n), "--rehearse-cpu", "--rehearse-legs", "--steps", "3", "--warmup", "1"])
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert wall < bench.LINE_BUDGET_S, wall
+    line = _line(r.stdout)
+    assert line["n_gpus"] == n and line["ranks_seen"] == n and line["value"] is None
+    assert line["legs_order"] == [leg[2] for leg in bench.LEGS]
+    for key in ("client_shard_push", "client_shard", "param_range_strong_gather"):
+        leg = line[key]
+        assert "error" not in leg and "skipped" not in leg, (key, leg)
+        assert leg["parity"]["mismatches"] == 0, (key, leg)
+        assert leg["connect_s"] is not None and leg["connect_s"] < leg["connect_deadline_s"], (key, leg)
+    assert line["client_shard_push"]["full_compare"]["mismatches"] == 0
+    assert line["client_shard"]["rccl_comm_count"] == n
+    assert line["client_shard_output_checksums"]["agree"] is True
+    p = tmp_path / f"line_n{n}.json"
+    p.write_text(r.stdout)
+    assert rep.main([str(p)]) == 0
+    print(f"[N={n} rehearsal] wall {wall:.1f} s, legs' set-up "
+          + ", ".join(f"{k} {line[k].get('connect_s')} s" for k in line["legs_order"]), file=sys.stderr)

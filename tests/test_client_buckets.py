@@ -226,7 +226,7 @@ def test_host_result_buffers_pooled_across_held_rounds():
         held = nxt  # the previous round's result is released here
     assert len(set(ptrs)) == 2, ptrs
     keep = [runtime.reusable_host_array(10, np.float64, "pool_cap") for _ in range(runtime.HOST_POOL_DEPTH + 3)]
-    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64))]) == runtime.HOST_POOL_DEPTH
+    assert len(runtime._host_cache[("pool_cap", np.dtype(np.float64))]["pool"]) == runtime.HOST_POOL_DEPTH
     assert len({a.__array_interface__["data"][0] for a in keep}) == len(keep)  # every live one distinct
 
 
@@ -236,5 +236,23 @@ def test_host_result_pool_byte_cap(monkeypatch):
 
     monkeypatch.setattr(runtime, "HOST_POOL_BYTES", 10_000)
     keep = [runtime.reusable_host_array(1000, np.float32, "pool_bytes") for _ in range(5)]  # 4000 B each
-    pool = runtime._host_cache[("pool_bytes", np.dtype(np.float32))]
-    assert len(pool) == 2 and pool[-1] is keep[-1]  # a fresh buffer is handed out itself
+    pool = runtime._host_cache[("pool_bytes", np.dtype(np.float32))]["pool"]
+    assert len(pool) == 2 and pool[-1][0] is keep[-1]  # a fresh buffer is handed out itself
+
+
+def test_host_result_pool_follows_a_shrinking_working_set():
+    """the pool is sized by the working set it sees -- six results held at once grow it
+    to six buffers; once only one is held at a time, the five that stay free past HOST_POOL_IDLE
+    turns of the pool are released (not kept for the life of the process)."""
+    from substrafl_amd import runtime
+
+    key = ("pool_shrink", np.dtype(np.float32))
+    held = [runtime.reusable_host_array(1000, np.float32, "pool_shrink") for _ in range(6)]
+    assert len(runtime._host_cache[key]["pool"]) == 6
+    del held
+    for _ in range(runtime.HOST_POOL_IDLE * 6 + 4):
+        a = runtime.reusable_host_array(1000, np.float32, "pool_shrink")
+        del a
+    assert len(runtime._host_cache[key]["pool"]) == 1
+    runtime.drop_host_pools()
+    assert key not in runtime._host_cache

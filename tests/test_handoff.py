@@ -40,11 +40,20 @@ class _Tensor:
         return 0xABC000
 
 
+class _Consumer:
+    """Stands for an accelerated client / strategy (handoff.register)."""
+
+
 @pytest.fixture()
 def on():
     handoff.enable(True)
-    yield
+    consumers = [_Consumer(), _Consumer()]  # an accelerate_algo client and an accelerate-d strategy
+    handoff.register("client", consumers[0])
+    handoff.register("aggregator", consumers[1])
+    yield consumers
     handoff.enable(False)
+    del consumers
+    gc.collect()
 
 
 def _export(n=100, tag="handoff_t"):
@@ -97,9 +106,13 @@ def test_tensor_record_and_in_place_change(on):
     t = _Tensor(100)
     handoff.record_tensor(host, t)
     views = _views(host)
-    assert handoff.lookup(views, 0)[0] == 0xABC000
     handoff.invalidate_slots([0])  # engine calls leave tensor records alone
-    assert handoff.lookup(views, 0) is not None
+    hit = handoff.lookup(views, 0)
+    assert hit[0] == 0xABC000 and hit[2] is t
+    # a client export is consumed once -- the record (and its hold on the device
+    # bucket) goes with the aggregation that took it
+    assert handoff.lookup(views, 0) is None and not handoff.records()
+    handoff.record_tensor(host, t)
     t._version += 1  # modified in place since the export
     assert handoff.lookup(views, 0) is None
     handoff.record_tensor(_export(50, "handoff_u"), _Tensor(100))  # size mismatch: not recorded
@@ -150,3 +163,40 @@ def test_stable_slot_survives_engine_calls_not_writes(on):
     assert handoff.lookup(views, 0)[0] == 0x3000
     s.gen[12] = 1
     assert handoff.lookup(views, 0) is None
+
+
+def test_records_only_for_a_live_consumer():
+    """VERDICT r05 "Next 3": the engine's outputs are recorded (and frozen) only while an
+    accelerated client lives to take them on the device, a client's exports only while an
+    accelerated strategy lives -- the reference's own algorithms next to an accelerated strategy
+    get writable arrays, exactly the reference's (torch.from_numpy warns on read-only ones)."""
+    handoff.enable(True)
+    try:
+        assert handoff.consumers() == {"client": 0, "aggregator": 0}
+        out = _export(tag="handoff_c1")
+        handoff.record_slot(out, _Session(), 1, 0x1000)  # no accelerated client: not recorded
+        exp = _export(tag="handoff_c2")
+        handoff.record_tensor(exp, _Tensor(100))  # no accelerated strategy: not recorded
+        assert out.flags.writeable and exp.flags.writeable and not handoff.records()
+        strategy = _Consumer()
+        handoff.register("aggregator", strategy)
+        handoff.record_slot(out, _Session(), 1, 0x1000)
+        assert out.flags.writeable  # still no client consumer for the engine's outputs
+        handoff.record_tensor(exp, _Tensor(100))
+        assert not exp.flags.writeable and len(handoff.records()) == 1
+        client = _Consumer()
+        handoff.register("client", client)
+        handoff.record_slot(out, _Session(), 1, 0x1000)
+        assert not out.flags.writeable and len(handoff.records()) == 2
+        # the experiment's strategy and clients released: every record and pooled buffer goes
+        del strategy
+        gc.collect()
+        assert len(handoff.records()) == 2
+        del client
+        gc.collect()
+        assert handoff.consumers() == {"client": 0, "aggregator": 0}
+        assert not handoff.records() and not runtime._host_cache
+        with pytest.raises(ValueError):
+            handoff.register("server", _Consumer())
+    finally:
+        handoff.enable(False)

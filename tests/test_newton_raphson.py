@@ -150,12 +150,30 @@ def test_integer_inputs_and_large_hessian(gpu):
     _same([H, G], list(newton_raphson_sums(grads, hess, ns)))
 
 
+_DT = {"f16": np.float16, "f32": np.float32, "f64": np.float64, "i64": np.int64}
+
+
 @pytest.mark.gpu
-def test_mixed_client_dtypes_are_refused(gpu):
-    """The reference casts later clients into client 0's type (in-place +=); the engine refuses
-    such mixes loudly instead of reproducing NumPy's stacking promotion."""
+@pytest.mark.parametrize("dts", [("f32", "f64"), ("f64", "f32", "f32"), ("f16", "f16", "f16"), ("f16", "f32", "f16"),
+                                 ("f32", "i64", "f64", "f32"), ("f16", "f64"), ("i64", "f32")])
+def test_mixed_and_half_client_dtypes_bit_exact(gpu, dts):
+    """the reference's ``total += x_k * c_k`` casts every later client into client 0's
+    type (NumPy adds in the promoted type, then rounds back) and takes float16 arrays; the engine
+    does the same on the device, bit for bit -- no input the reference accepts is refused."""
     from substrafl_amd.integration import newton_raphson_sums as engine_sums
 
-    st = _states([[np.ones(2, np.float32)], [np.ones(2, np.float64)]], [np.eye(2)] * 2, [1, 1])
-    with pytest.raises(NotImplementedError):
-        engine_sums(st)
+    rng = np.random.default_rng(len(dts) * 7 + sum(map(len, dts)))
+    P = 37
+
+    def arr(shape, dt):
+        x = rng.standard_normal(shape) * 3
+        x[rng.random(shape) < 0.1] = -0.0
+        return (np.round(x) if dt == "i64" else x).astype(_DT[dt])
+
+    grads = [[arr((P - 1,), dt), arr((1,), dt)] for dt in dts]
+    hess = [arr((P, P), dt) for dt in dts]
+    ns = [int(v) for v in rng.integers(1, 5000, len(dts))]
+    H, G = engine_sums(_states(grads, hess, ns))
+    Hr, Gr = newton_raphson_sums(grads, hess, ns)
+    assert H.dtype == Hr.dtype and G.dtype == Gr.dtype
+    _same([H, G], [Hr, Gr])

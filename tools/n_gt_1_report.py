@@ -76,6 +76,11 @@ def report(lines) -> list:
                      f"exchange+tail {leg.get('exchange_and_tail_ms')} ms"]
             if (leg.get("parity") or {}).get("mismatches"):
                 flags.append(f"N={n} {key}: spot check mismatches {leg['parity']}")
+            if leg.get("connect_s") is not None:
+                parts.append(f"set-up {leg['connect_s']} s of {leg.get('connect_deadline_s')} s")
+                if leg.get("connect_deadline_s") and leg["connect_s"] > 0.8 * leg["connect_deadline_s"]:
+                    flags.append(f"N={n} {key}: set-up took {leg['connect_s']} s, over 80 % of its "
+                                 f"{leg['connect_deadline_s']} s deadline")
             fc = leg.get("full_compare")
             if isinstance(fc, dict) and "mismatches" in fc:
                 parts.append(f"full_compare {fc['mismatches']}/{fc.get('elements')}")
