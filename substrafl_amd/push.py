@@ -103,6 +103,8 @@ class PushTransport:
     native = True
     push = True
     fault: Optional[Tuple[str, int, int]] = None  # TEST ONLY: see __init__
+    _settle_failed = False  # settle() ran out of time: some rank neither finished nor failed
+    _timeout_s = 60.0
 
     def __init__(self, group=None, device: Optional[int] = None, timeout_s: float = 60.0,
                  aux_streams: Optional[int] = None, fault: Optional[Tuple[str, int, int]] = None):
@@ -140,6 +142,8 @@ class PushTransport:
         hz = ctypes.c_uint64()
         _check(self.lib.fedagg_wall_clock_hz(ctypes.byref(hz)), "fedagg_wall_clock_hz")
         self._timeout = int(timeout_s * hz.value)
+        self._timeout_s = float(timeout_s)
+        self._settle_failed = False  # settle() ran out of time: some rank neither finished nor failed
         self.base = 0
         if fault is not None and (fault[0] not in ("signal", "exit", "tag") or len(fault) != 3):
             raise ValueError(f"push fault injection: ('signal' | 'exit' | 'tag', rank, step | index), not {fault!r}")
@@ -184,6 +188,7 @@ class PushTransport:
         import torch
 
         torch.cuda.synchronize(self.device)
+        self.settle()
         if self.failed():
             # a rank whose peer died would wait in this barrier for the backend's timeout, and a
             # gloo barrier that raises would replace the error that names the failed wait: after a
@@ -255,6 +260,9 @@ class PushTransport:
         bad = self.errors()
         if bad:
             raise _native.NativeLibraryError(f"push executor: a wait timed out (rank -> what it waited for: {bad})")
+        if self._settle_failed:
+            raise _native.NativeLibraryError("push executor: a rank neither finished the call nor reported a failed "
+                                             f"wait within {self._timeout_s + 5.0:.0f} s")
 
     def execute(self, prog: "PushProgram", stream: int, ws=None, ws_kind: str = "f32") -> None:
         self.raise_errors()
@@ -298,11 +306,31 @@ class PushTransport:
             torch.cuda.synchronize(self.device)  # its steps before `at` are done; then it dies
             os._exit(FAULT_EXIT_CODE)
 
+    def settle(self) -> None:
+        """Host-side end of a call (this rank's stream already synchronised): wait until every
+        rank's progress counter shows the call finished (the counters' final value is the next
+        call's base) or some rank's wait gave up -- so a rank whose own part succeeded learns
+        whether the GROUP's call did before it meets its peers again (a peer that died never
+        would).  Bounded by the wait kernels' timeout: past it plus a margin the transport is
+        marked failed."""
+        import time
+
+        if self._page is None or self.world == 1:
+            return
+        deadline = time.monotonic() + self._timeout_s + 5.0
+        while not self.errors():
+            if all(int(v) >= self.base for v in self._page[: self.world]):
+                return
+            if time.monotonic() > deadline:
+                self._settle_failed = True
+                return
+            time.sleep(0.0005)
+
     def failed(self) -> bool:
         """Whether a wait of some rank gave up (:meth:`errors`): the group cannot meet again -- a
         peer may have died, and a surviving one may still be finishing its steps into this rank's
         buffers.  A failed transport runs no collective and frees no program buffer any more."""
-        return self._page is not None and bool(self.errors())
+        return self._page is not None and (bool(self.errors()) or self._settle_failed)
 
     def _abandon_programs(self) -> None:
         """Keep the programs' buffers alive for the life of the process (a surviving peer may still

@@ -1014,6 +1014,9 @@ def _finish_peer(torch, transport) -> None:
     try:
         if getattr(transport, "raise_errors", None) is not None:
             torch.cuda.current_stream().synchronize()
+            settle = getattr(transport, "settle", None)
+            if settle is not None:  # this rank's part is done: did the group's call succeed?
+                settle()
             _raise_transport_errors(transport)
     finally:
         _release_programs(transport)

@@ -301,3 +301,57 @@ def test_raise_errors_reports_a_timed_out_wait():
     with pytest.raises(_native.NativeLibraryError, match="landing tag of rank 1"):
         tr.raise_errors()
     _raise_transport_errors(object())  # transports without a record of their own: no-op
+
+
+def test_settle_waits_for_the_group_or_its_failure():
+    """a rank whose own part of a push call is done learns from the shared page whether
+    the GROUP's call finished (every rank's progress counter at the call's end value) or failed (an
+    err word set) before it meets its peers again -- a failed call runs no collective release (a
+    dead peer would never meet it) and frees no program buffer."""
+    import threading
+    import time
+
+    from substrafl_amd import _native
+    from substrafl_amd.push import PushTransport
+
+    tr = PushTransport.__new__(PushTransport)
+    tr.world, tr.base, tr._timeout_s, tr._programs = 3, 7, 2.0, []
+    tr._page = np.zeros(3 * tr.world, dtype=np.uint64)
+    tr._page[:3] = 7
+    t0 = time.monotonic()
+    tr.settle()  # every counter at the call's end value: done at once
+    assert time.monotonic() - t0 < 0.5 and not tr.failed()
+    tr._page[1] = 5  # rank 1 stopped short; rank 2's wait gives up 0.2 s later
+
+    def give_up():
+        time.sleep(0.2)
+        tr._page[tr.world + 2] = 1 + 1  # rank 2 gave up on rank 1's counter
+
+    th = threading.Thread(target=give_up)
+    th.start()
+    t0 = time.monotonic()
+    tr.settle()
+    th.join()
+    assert 0.15 < time.monotonic() - t0 < 1.5
+    assert tr.failed()
+    with pytest.raises(_native.NativeLibraryError, match="counter of rank 1"):
+        tr.raise_errors()
+    tr._programs = ["program"]
+    tr.device = None
+    import torch
+
+    orig = torch.cuda.synchronize
+    torch.cuda.synchronize = lambda *a: None
+    try:
+        tr.release_programs()  # failed: no barrier (tr has no process group at all), nothing freed
+    finally:
+        torch.cuda.synchronize = orig
+    assert tr._programs == [] and "program" in __import__("substrafl_amd.push", fromlist=["_ABANDONED"])._ABANDONED
+    # a rank that neither finishes nor reports a failure within the timeout: failed as well
+    tr2 = PushTransport.__new__(PushTransport)
+    tr2.world, tr2.base, tr2._timeout_s = 2, 3, 0.0
+    tr2._page = np.zeros(3 * tr2.world, dtype=np.uint64)
+    tr2.settle()  # waits the 5 s margin
+    assert tr2.failed()
+    with pytest.raises(_native.NativeLibraryError, match="neither finished"):
+        tr2.raise_errors()
