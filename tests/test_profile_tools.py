@@ -61,3 +61,29 @@ def test_cli_applies_the_fetch_correction_and_records_the_build(tmp_path):
     assert res["hbm_write_bytes_per_launch"] == 500.0 * 1024
     assert res["traffic_over_alg"] == pytest.approx(4500 / 5000)
     assert len(res["lib_sha256"]) == 16
+
+
+def test_roofline_check_reports_first_launch_and_steady_state_apart(tmp_path):
+    """VERDICT r05 "Next 2": from the traced process's per-launch durations, roofline_check puts the
+    first launch (a fresh allocation's first touch, the clock ramp) and the steady state apart, and
+    finds a step in the launch sequence if there is one."""
+    import csv
+
+    sys.path.insert(0, str(ROOT / "tools"))
+    import roofline_check as rc
+
+    p = tmp_path / "trace.csv"
+    durs = [16.0] + [13.0] * 26 + [12.7] * 33  # first launch, then a 2.4 % step at launch 27
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        t = 1_000_000
+        for ms in durs:
+            w.writerow(["void (anonymous namespace)::fedavg_kernel<x>", t, t + int(ms * 1e6)])
+            w.writerow(["read_probe_kernel", t + int(ms * 1e6), t + int(ms * 1e6) + 10])
+            t += int(ms * 1e6) + 1000
+    frac = lambda ms: round(91e9 / (ms / 1e3) / 1e9 / 8000, 4)  # noqa: E731
+    res = rc.per_launch(str(p), "fedavg_kernel", 1, frac)
+    assert res["launches"] == 60 and res["first_ms"] == 16.0 and res["steady_ms"] == 12.7
+    assert res["step"]["at_launch"] == 27 and abs(res["step"]["relative"] - 0.0236) < 0.002
+    assert res["frac_steady"] == frac(12.7)

@@ -40,10 +40,13 @@ class Sampler(threading.Thread):
               "ppt_residency_acc", "socket_thm_residency_acc", "hbm_thm_residency_acc", "gfxclk_lock_status",
               "average_umc_activity", "average_gfx_activity", "firmware_timestamp")
 
-    def __init__(self, bdf, period=0.002):
+    def __init__(self, bdf, period=0.002, enabled=True):
         super().__init__(daemon=True)
         self.period, self.samples, self.error, self.stop_ev = period, [], None, threading.Event()
         self.handle = None
+        if not enabled:
+            self.error = "disabled (--no-sampler)"
+            return
         try:
             import amdsmi
 
@@ -151,6 +154,7 @@ def main():
     ap.add_argument("--second", type=int, default=60)
     ap.add_argument("--fresh", type=int, default=60)
     ap.add_argument("--old", type=int, default=40)
+    ap.add_argument("--no-sampler", action="store_true", help="no amdsmi polling (does the polling itself matter?)")
     args = ap.parse_args()
 
     import torch
@@ -164,7 +168,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
-    sampler = Sampler(device_pci_bus_id(0))
+    sampler = Sampler(device_pci_bus_id(0), enabled=not args.no_sampler)
     sampler.start()
     out = {"workload": "c5 fedavg_bf16_128x350M tiled", "bytes_alg_per_launch": BYTES,
            "sampler": {"error": sampler.error, "period_s": sampler.period,

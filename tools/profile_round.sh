@@ -45,9 +45,12 @@ print(_native.load().fedagg_scaffold_launches(16, 4, 25000000, 1))") ;;
     --traffic "$OUT/${TAG}_traffic_${WL}.json" > "$OUT/${TAG}_profiled_bench_${WL}.json"
   STATS=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_stats.csv' | head -1)
   cp "$STATS" "$OUT/${TAG}_${WL}_kernel_stats.csv"
+  TRACE=$(find "$OUT/${TAG}_prof_${WL}" -name '*kernel_trace.csv' | head -1)
+  cp "$TRACE" "$OUT/${TAG}_${WL}_kernel_trace.csv"
   KPFX=$([ "$KERN" = scaffold ] && echo scaffold || echo fedavg_kernel)
   python3 "$ROOT/tools/roofline_check.py" --bench "$OUT/${TAG}_bench_${WL}.json" \
     --profiled "$OUT/${TAG}_profiled_bench_${WL}.json" --stats "$OUT/${TAG}_${WL}_kernel_stats.csv" \
-    --kernel "$KPFX" --group $GROUP --out "$OUT/${TAG}_${WL}_roofline_check.json" > /dev/null
+    --kernel "$KPFX" --group $GROUP --trace "$OUT/${TAG}_${WL}_kernel_trace.csv" \
+    --out "$OUT/${TAG}_${WL}_roofline_check.json" > /dev/null
 done
 echo "[$TAG] done" >&2

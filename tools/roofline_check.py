@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--stats", required=True, help="rocprofv3 *_kernel_stats.csv of that run")
     ap.add_argument("--kernel", required=True, help="kernel name prefix (after 'void (anonymous namespace)::')")
     ap.add_argument("--group", type=int, default=1, help="launches per step (Scaffold one-bucket pair: 2)")
+    ap.add_argument("--trace", default="", help="rocprofv3 *_kernel_trace.csv of that run: per-launch durations")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -68,11 +69,47 @@ def main():
         "profiled_events_vs_rocprof_avg": round(prof["roofline"]["kernel_ms"] / avg_ms - 1, 4) if avg_ms else None,
         "plain_vs_profiled": round(plain["roofline"]["kernel_ms"] / prof["roofline"]["kernel_ms"] - 1, 4),
     }
+    if args.trace:
+        out["per_launch"] = per_launch(args.trace, args.kernel, args.group, frac)
     text = json.dumps(out, indent=1)
     if args.out:
         with open(args.out, "w") as f:
             f.write(text + "\n")
     print(text)
+
+
+def per_launch(path, kernel, group, frac):
+    """The kernel's launches in the traced process, in order (VERDICT r05 "Next 2"): the first
+    launch apart (the first touch of a fresh allocation and the clock ramp), the steady state
+    (median of the second half), and the split of the launches after the first into two levels that
+    leaves the least squared error (a step, if the process has one) with the mean on either side."""
+    d = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+            if name.startswith(kernel):
+                d.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    d = [ms for _, ms in sorted(d)]
+    if group > 1:  # launches of one step summed
+        d = [sum(d[i: i + group]) for i in range(0, len(d) - group + 1, group)]
+    if len(d) < 6:
+        return {"launches": len(d)}
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    steady = med(d[len(d) // 2:])
+    best = None
+    rest = d[1:]  # the first launch is reported apart: the step is looked for after it
+    for s in range(2, len(rest) - 1):
+        a, b = rest[:s], rest[s:]
+        ma, mb = sum(a) / len(a), sum(b) / len(b)
+        err = sum((x - ma) ** 2 for x in a) + sum((x - mb) ** 2 for x in b)
+        if best is None or err < best[0]:
+            best = (err, s, ma, mb)
+    _, s, ma, mb = best
+    return {"launches": len(d), "first_ms": round(d[0], 5), "frac_first": frac(d[0]),
+            "steady_ms": round(steady, 5), "frac_steady": frac(steady),
+            "mean_after_first_ms": round(sum(d[1:]) / (len(d) - 1), 5),
+            "step": {"at_launch": s + 1, "mean_before_ms": round(ma, 5), "mean_after_ms": round(mb, 5),
+                     "relative": round(ma / mb - 1, 4)}}
 
 
 if __name__ == "__main__":
