@@ -30,6 +30,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 BYTES = 128 * 350_000_000 * 2 + 350_000_000 * 4
+_T0 = time.time()  # this process's start (wall clock, comparable across processes)
 
 
 class Sampler(threading.Thread):
@@ -170,7 +171,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sampler = Sampler(device_pci_bus_id(0), enabled=not args.no_sampler)
     sampler.start()
-    out = {"workload": "c5 fedavg_bf16_128x350M tiled", "bytes_alg_per_launch": BYTES,
+    out = {"workload": "c5 fedavg_bf16_128x350M tiled", "bytes_alg_per_launch": BYTES, "process_start_wall": _T0,
            "sampler": {"error": sampler.error, "period_s": sampler.period,
                        "bdfs": getattr(sampler, "bdfs", None)}, "bursts": []}
     shapes = synthetic_state_dict_shapes(M)
@@ -186,22 +187,27 @@ def main():
     out["synth_s"] = round(time.perf_counter() - t0, 2)
     plan_a = TiledFedAvgPlan(kind, buf_a, K, w, M, out_a, pw, tv=tv)
     print(f"synth {out['synth_s']} s; sampler {sampler.error or 'ok'}", flush=True)
+    out["process_start_to_first_launch_s"] = round(time.time() - _T0, 2)
     out["bursts"].append(burst(torch, plan_a, stream, args.first, sampler, "first: right after synthesis"))
     print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
-    time.sleep(args.idle_s)
-    out["bursts"].append(burst(torch, plan_a, stream, args.second, sampler, f"idle: same buffer after {args.idle_s} s idle"))
-    print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
-    t0 = time.perf_counter()
-    buf_b = bench.synth_tiled(torch, K, M, kind, dev, 20241016, tv)  # a second, newly allocated buffer
-    out_b = torch.empty(ld, dtype=torch.float32, device=dev)
-    torch.cuda.synchronize()
-    out["synth_fresh_s"] = round(time.perf_counter() - t0, 2)
-    plan_b = TiledFedAvgPlan(kind, buf_b, K, w, M, out_b, pw, tv=tv)
-    out["bursts"].append(burst(torch, plan_b, stream, args.fresh, sampler, "fresh: a newly allocated 91 GB buffer"))
-    print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
-    out["bursts"].append(burst(torch, plan_a, stream, args.old, sampler, "old: the first buffer again"))
-    print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
-    out["outputs_equal"] = bool(torch.equal(out_a[:M].view(torch.int32), out_b[:M].view(torch.int32)))
+    if args.second:
+        time.sleep(args.idle_s)
+        out["bursts"].append(burst(torch, plan_a, stream, args.second, sampler,
+                                   f"idle: same buffer after {args.idle_s} s idle"))
+        print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
+    if args.fresh:
+        t0 = time.perf_counter()
+        buf_b = bench.synth_tiled(torch, K, M, kind, dev, 20241016, tv)  # a second, newly allocated buffer
+        out_b = torch.empty(ld, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        out["synth_fresh_s"] = round(time.perf_counter() - t0, 2)
+        plan_b = TiledFedAvgPlan(kind, buf_b, K, w, M, out_b, pw, tv=tv)
+        out["bursts"].append(burst(torch, plan_b, stream, args.fresh, sampler, "fresh: a newly allocated 91 GB buffer"))
+        print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
+        out["outputs_equal"] = bool(torch.equal(out_a[:M].view(torch.int32), out_b[:M].view(torch.int32)))
+    if args.old:
+        out["bursts"].append(burst(torch, plan_a, stream, args.old, sampler, "old: the first buffer again"))
+        print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
     sampler.stop_ev.set()
     sampler.join(timeout=2)
     out["sampler"]["samples"] = len(sampler.samples)
