@@ -200,10 +200,11 @@ __device__ __forceinline__ int push_failed_rank(const uint64_t* errs, uint32_t n
 // PUSH_TAG_ERR for a tag) in *err.  Fail fast: a wait also gives up as soon as ANY rank's err word
 // is set (a peer's or an earlier wait of this rank: the call's result is void), recording
 // PUSH_PEER_ERR + that rank + 1 when the cause is another rank's, so a dead or slow peer costs
-// the group one timeout, not one per wait.  The err words are scanned once on entry and then every
-// PUSH_ERR_SCAN_EVERY polls (not nranks more uncached host-page reads per poll on the
-// error-free path; a failure is still seen within tens of microseconds).  Every lane reaches the
-// end (the late count is a wave ballot).
+// the group one timeout, not one per wait.  The err words are scanned every PUSH_ERR_SCAN_EVERY
+// polls and not on entry (on the error-free path a wait whose counter is already there
+// reads no err word at all -- the entry scan of nranks uncached host-page words cost ~9 us per step,
+// profiles/r06f_push_overhead_probe.jsonl; a failure is still seen within tens of microseconds).
+// Every lane reaches the end (the late count is a wave ballot).
 constexpr uint32_t PUSH_ERR_SCAN_EVERY = 16;
 
 __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress, PushWaitArgs a, uint64_t gen,
@@ -213,7 +214,7 @@ __global__ void __launch_bounds__(64) push_wait_kernel(const uint64_t* progress,
   bool was_late = false;
   if (i < a.n) {
     const uint64_t t0 = wall_clock64();
-    int peer = push_failed_rank(errs, nranks);
+    int peer = -1;      // the first failed rank, once a scan has seen one
     uint64_t code = 0;  // this lane's own failure
     const uint64_t* tag = a.tag[i];
     bool counter_done = false;

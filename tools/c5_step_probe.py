@@ -103,8 +103,9 @@ def step_split(d):
     return s, float(d[:s].mean()), float(d[s:].mean())
 
 
-def burst(torch, plan, stream, n, sampler, label):
-    torch.cuda.synchronize()
+def burst(torch, plan, stream, n, sampler, label, sync=True):
+    if sync:  # (False: the launches queue behind whatever the stream still has to run)
+        torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
     ref = torch.cuda.Event(enable_timing=True)
     t_ref = time.perf_counter()
@@ -156,6 +157,9 @@ def main():
     ap.add_argument("--fresh", type=int, default=60)
     ap.add_argument("--old", type=int, default=40)
     ap.add_argument("--no-sampler", action="store_true", help="no amdsmi polling (does the polling itself matter?)")
+    ap.add_argument("--no-sync-after-synth", action="store_true",
+                    help="enqueue the first launches right behind the synthesis, as bench.py does")
+    ap.add_argument("--sleep-after-synth", type=float, default=0.0, help="idle seconds between synthesis and launches")
     args = ap.parse_args()
 
     import torch
@@ -183,12 +187,18 @@ def main():
     buf_a = bench.synth_tiled(torch, K, M, kind, dev, 20241016, tv)
     ld = BucketLayout(list(range(len(shapes))), shapes, np.float32).ld
     out_a = torch.empty(ld, dtype=torch.float32, device=dev)
-    torch.cuda.synchronize()
+    if not args.no_sync_after_synth:  # bench.py enqueues its first launches behind the synthesis
+        torch.cuda.synchronize()
     out["synth_s"] = round(time.perf_counter() - t0, 2)
+    out["sync_after_synth"] = not args.no_sync_after_synth
+    if args.sleep_after_synth:
+        time.sleep(args.sleep_after_synth)
+    out["sleep_after_synth_s"] = args.sleep_after_synth
     plan_a = TiledFedAvgPlan(kind, buf_a, K, w, M, out_a, pw, tv=tv)
     print(f"synth {out['synth_s']} s; sampler {sampler.error or 'ok'}", flush=True)
     out["process_start_to_first_launch_s"] = round(time.time() - _T0, 2)
-    out["bursts"].append(burst(torch, plan_a, stream, args.first, sampler, "first: right after synthesis"))
+    out["bursts"].append(burst(torch, plan_a, stream, args.first, sampler, "first: right after synthesis",
+                               sync=not args.no_sync_after_synth))
     print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
     if args.second:
         time.sleep(args.idle_s)
