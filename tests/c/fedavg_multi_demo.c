@@ -106,7 +106,53 @@ int main(int argc, char** argv) {
     fprintf(stderr, "multi_fedavg (2): %s\n", fedagg_last_error());
     return 2;
   }
+  /* fp64 buckets through the same object: the f64 entry against the single-device f64 kernel */
+  int bad64 = 0;
+  {
+    double* l64[K][NSEG];
+    const void* seg64[K * NSEG];
+    uint64_t bytes64[NSEG];
+    for (int i = 0; i < NSEG; ++i) bytes64[i] = numel[i] * sizeof(double);
+    for (int k = 0; k < K; ++k)
+      for (int i = 0; i < NSEG; ++i) {
+        l64[k][i] = malloc(bytes64[i]);
+        for (uint64_t e = 0; e < numel[i]; ++e) l64[k][i][e] = (double)layers[k][i][e] * 1.000000119;
+        seg64[k * NSEG + i] = l64[k][i];
+      }
+    double w64[K];
+    for (int k = 0; k < K; ++k) w64[k] = (double)n[k] / (double)n_all;
+    double* multi64 = calloc(M, sizeof(double));
+    double* single64 = calloc(M, sizeof(double));
+    if (fedagg_multi_fedavg_f64(m, K, NSEG, seg64, bytes64, w64, idx, 1, multi64)) {
+      fprintf(stderr, "multi_fedavg_f64: %s\n", fedagg_last_error());
+      return 2;
+    }
+    fedagg_session* s64 = fedagg_session_create(devs[0]);
+    const uint64_t ld64 = (M + 31) / 32 * 32;
+    void *r64 = NULL, *o64 = NULL, *w64s = NULL;
+    if (!s64 || fedagg_session_buffer(s64, 0, K * ld64 * sizeof(double), &r64) ||
+        fedagg_session_buffer(s64, 1, ld64 * sizeof(double), &o64) ||
+        fedagg_session_buffer(s64, 2, fedagg_pairwise_ws_bytes(K, 1, 8), &w64s) ||
+        fedagg_session_stage(s64, r64, ld64 * sizeof(double), K, NSEG, seg64, bytes64)) {
+      fprintf(stderr, "stage f64: %s\n", fedagg_last_error());
+      return 2;
+    }
+    const double* rows64[K];
+    for (int k = 0; k < K; ++k) rows64[k] = (const double*)((const char*)r64 + k * ld64 * sizeof(double));
+    if (fedagg_fedavg_f64(rows64, w64, K, M, idx, 1, w64s, (double*)o64, fedagg_session_stream(s64)) ||
+        fedagg_session_fetch(s64, o64, single64, sizeof(double) * M)) {
+      fprintf(stderr, "fedavg_f64: %s\n", fedagg_last_error());
+      return 2;
+    }
+    fedagg_session_destroy(s64);
+    for (uint64_t e = 0; e < M; ++e) bad64 += memcmp(&multi64[e], &single64[e], sizeof(double)) != 0;
+  }
   fedagg_multi_destroy(m);
+  /* a device that does not exist: no object, the error names it */
+  int nodev[1] = {4096};
+  fedagg_multi* none = fedagg_multi_create(1, nodev, 0);
+  const int refused = none == NULL && strstr(fedagg_last_error(), "device 4096") != NULL;
+  if (none) fedagg_multi_destroy(none);
 
   int bad = 0, bad_again = 0, bad_ref = 0;
   for (uint64_t e = 0; e < M; ++e) {
@@ -127,7 +173,8 @@ int main(int argc, char** argv) {
     base += numel[i];
   }
   printf("fedavg_multi_demo: K=%d M=%llu shards=%d used=%d sub_ranges=%d mismatches=%d again=%d vs_reference_order=%d "
-         "(abi %d)\n",
-         K, (unsigned long long)M, ndev, shards_used, ranges_total, bad, bad_again, bad_ref, fedagg_abi_version());
-  return (bad || bad_again || bad_ref || ranges_total <= ndev) ? 1 : 0;
+         "f64=%d bad_device_refused=%d (abi %d)\n",
+         K, (unsigned long long)M, ndev, shards_used, ranges_total, bad, bad_again, bad_ref, bad64, refused,
+         fedagg_abi_version());
+  return (bad || bad_again || bad_ref || bad64 || !refused || ranges_total <= ndev) ? 1 : 0;
 }

@@ -152,7 +152,8 @@ def test_c_multi_demo_runs_bit_exact(tmp_path):
     exe = _build_c_demo(tmp_path, "fedavg_multi_demo")
     r = subprocess.run([str(exe), "0", "0"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "mismatches=0 again=0 vs_reference_order=0" in r.stdout and "used=2" in r.stdout, r.stdout
+    assert "mismatches=0 again=0 vs_reference_order=0 f64=0 bad_device_refused=1" in r.stdout, r.stdout
+    assert "used=2" in r.stdout, r.stdout
 
 
 def _declared_arity():
