@@ -1680,10 +1680,32 @@ def multi_device_bench(args):
     walls, shards = [], []
     for _ in range(args.steps):
         t0 = time.perf_counter()
-        eng.fedavg(pus, n_samples)
+        res = eng.fedavg(pus, n_samples)
         walls.append(time.perf_counter() - t0)
         shards.append(eng.last_timing["shards"])
     wall = float(np.median(walls))
+    py_bits = np.concatenate([np.asarray(a).reshape(-1) for a in res]).view(np.uint32).copy()
+    del res
+    # the same plan through the one-call C entry (fedagg_multi_fedavg_f32, csrc/multi.hip): the
+    # orchestration in C++ instead of Python threads, same devices, same host buckets
+    from substrafl_amd.multi_device import NativeMultiFedAvg
+
+    nat = NativeMultiFedAvg(devices, pack_threads=args.md_pack_threads or 0)
+    for _ in range(max(1, args.warmup)):
+        nat.fedavg(pus, n_samples)
+    nwalls = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        nres = nat.fedavg(pus, n_samples)
+        nwalls.append(time.perf_counter() - t0)
+    nwall = float(np.median(nwalls))
+    native_entry = {"ms_per_call_median": round(nwall * 1e3, 3),
+                    "value": round((K * M * 4 + M * 4) / nwall / 1e9, 2), "unit": "GB/s",
+                    "mismatches_vs_python_engine": int(np.sum(np.concatenate(
+                        [np.asarray(a).reshape(-1) for a in nres]).view(np.uint32) != py_bits)),
+                    "shards": nat.shard_info(), "entry": "fedagg_multi_fedavg_f32 (one C call per aggregation)"}
+    del nres
+    nat.close()
     bytes_alg = K * M * 4 + M * 4
     per_shard = []
     for g in range(len(devices)):
@@ -1708,6 +1730,7 @@ def multi_device_bench(args):
         # host ingress per shard: pack threads (CPUs allowed // GPUs), their NUMA node (the GPU's,
         # from sysfs), the CPUs they are bound to and the node the pinned ring landed on
         "placement": eng.placement_report(),
+        "native_c_entry": native_entry,
         "cpus_allowed": len(os.sched_getaffinity(0)),
         "note": "end-to-end (pinned-ring pack + H2D + kernel + D2H); not the device-resident metric",
     }), flush=True)

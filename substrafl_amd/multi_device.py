@@ -424,3 +424,69 @@ class MultiDeviceEngine:
         avg = [a for _, a in layout.unpack(out_d, wire)]
         new_c = [a for _, a in layout.unpack(out_c, wire)]
         return int(sum(mism)), new_c, avg
+
+
+class NativeMultiFedAvg:
+    """The one-call C entry ``fedagg_multi_*`` (csrc/multi.hip) from Python: the same
+    parameter-range plan as :class:`MultiDeviceEngine` -- shards, one thread and one private session
+    per device, NUMA-bound pack workers, HBM-sized sub-ranges -- run entirely in C++, one ctypes call
+    per aggregation (what a host in another language binds).  FedAvg over
+    uniform fp32 or fp64 layer lists; bit-identical to :class:`MultiDeviceEngine` and to the
+    reference (fed_avg.py:217-222)."""
+
+    def __init__(self, devices: Sequence[int], pack_threads: int = 0, max_shard_bytes: int = 0):
+        import ctypes
+
+        self.lib = _native.load()
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        self._h = self.lib.fedagg_multi_create(len(self.devices), arr, int(pack_threads))
+        if not self._h:
+            raise _native.NativeLibraryError(
+                "fedagg_multi_create failed: " + self.lib.fedagg_last_error().decode(errors="replace"))
+        if max_shard_bytes:
+            _native.check(self.lib.fedagg_multi_set(self._h, b"max_shard_bytes", int(max_shard_bytes)), "multi_set")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.fedagg_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int]) -> List[np.ndarray]:
+        """fed_avg.py:217-222 for validated inputs whose layers all share one dtype, fp32 or fp64."""
+        import ctypes
+
+        K, L = len(parameters_updates), len(parameters_updates[0])
+        dts = {a.dtype for pu in parameters_updates for a in pu}
+        if len(dts) != 1 or next(iter(dts)) not in (np.float32, np.float64):
+            raise NotImplementedError("fedagg_multi_fedavg takes layers of one dtype, float32 or float64")
+        dt = np.dtype(next(iter(dts)))
+        kind = kind_of(dt)
+        layout = BucketLayout(list(range(L)), [a.shape for a in parameters_updates[0]], dt)
+        nseg, ptrs, sizes, keep = runtime._segments(native_byte_order(parameters_updates))
+        w = fedavg_weights(n_samples, kind)
+        idx = layout.pairwise_idx.astype(np.uint64)
+        out = runtime.reusable_host_array(layout.M, dt, "multi-native")
+        fn = self.lib.fedagg_multi_fedavg_f32 if kind == "f32" else self.lib.fedagg_multi_fedavg_f64
+        _native.check(fn(self._h, K, nseg, ptrs, sizes, w.ctypes.data, idx.ctypes.data if idx.size else None,
+                         int(idx.size), out.ctypes.data), "fedagg_multi_fedavg")
+        del keep
+        return [a for _, a in layout.unpack(out)]
+
+    def shard_info(self) -> List[Dict[str, int]]:
+        """Per shard: device, NUMA node, pack workers, bound CPUs, and of the last call its element
+        range and sub-ranges (``fedagg_multi_shard_info``)."""
+        import ctypes
+
+        out = []
+        for g in range(len(self.devices)):
+            v = [ctypes.c_int() for _ in range(4)] + [ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()]
+            _native.check(self.lib.fedagg_multi_shard_info(self._h, g, *[ctypes.byref(x) for x in v]), "shard_info")
+            out.append(dict(zip(("device", "numa_node", "threads", "cpus", "lo", "hi", "ranges"), [x.value for x in v])))
+        return out
