@@ -27,6 +27,16 @@ def _pip_wheel(dest, env=None):
                           env=env)
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _no_build_leftovers():
+    """setuptools builds a local directory in place (``build/``, ``*.egg-info``): whatever these
+    tests create there is removed afterwards, so no second copy of the package stays in the tree."""
+    made = [d for d in (ROOT / "build", ROOT / "substrafl_amd.egg-info") if not d.exists()]
+    yield
+    for d in made:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 @needs_hipcc
 def test_wheel_carries_the_library_and_installs(tmp_path):
     r = _pip_wheel(tmp_path / "w")
