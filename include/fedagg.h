@@ -596,6 +596,9 @@ int fedagg_multi_fedavg_f32(fedagg_multi* m, int K, int nseg, const void* const*
                             const float* h_w, const uint64_t* h_idx, int P, float* h_out);
 int fedagg_multi_fedavg_f64(fedagg_multi* m, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
                             const double* h_w, const uint64_t* h_idx, int P, double* h_out);
+/* fp16 buckets: h_w and h_out hold fp16 bit patterns (fedagg_fedavg_f16's semantics, NumPy's half loops) */
+int fedagg_multi_fedavg_f16(fedagg_multi* m, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
+                            const uint16_t* h_w, const uint64_t* h_idx, int P, uint16_t* h_out);
 /* shard g: its device, the GPU's NUMA node (-1 unknown), pack workers, CPUs they are bound to, and
  * of the last call its element range [lo, hi) and the sub-ranges it streamed (any pointer NULL) */
 int fedagg_multi_shard_info(fedagg_multi* m, int g, int* device, int* numa_node, int* threads, int* ncpus,

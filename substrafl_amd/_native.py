@@ -152,6 +152,7 @@ SIGNATURES = {
     "fedagg_multi_set": (c_int, [c_void, ctypes.c_char_p, ctypes.c_longlong]),
     "fedagg_multi_fedavg_f32": (c_int, [c_void, c_int, c_int, P(c_void), P(c_u64), c_void, c_void, c_int, c_void]),
     "fedagg_multi_fedavg_f64": (c_int, [c_void, c_int, c_int, P(c_void), P(c_u64), c_void, c_void, c_int, c_void]),
+    "fedagg_multi_fedavg_f16": (c_int, [c_void, c_int, c_int, P(c_void), P(c_u64), c_void, c_void, c_int, c_void]),
     "fedagg_multi_shard_info": (c_int, [c_void, c_int, P(c_int), P(c_int), P(c_int), P(c_int), P(c_u64), P(c_u64),
                                         P(c_int)]),
 }

@@ -29,6 +29,8 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -172,6 +174,15 @@ struct KernelOf<double> {
   }
 };
 
+template <>
+struct KernelOf<uint16_t> {  // fp16 buckets (bit patterns), fp16 weights and output: NumPy's half loops
+  static int run(const uint16_t* const* rows, const void* w, int K, uint64_t n, const uint64_t* idx, int P, void* ws,
+                 void* out, void* stream) {
+    return fedagg_fedavg_f16(rows, static_cast<const uint16_t*>(w), K, n, idx, P, ws, static_cast<uint16_t*>(out),
+                             stream);
+  }
+};
+
 // One shard: its sub-ranges through its GPU, in order.
 template <class T>
 int run_shard(fedagg_multi* m, Shard& sh, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
@@ -245,12 +256,22 @@ int multi_fedavg(fedagg_multi* m, int K, int nseg, const void* const* h_seg, con
   std::vector<int> rcs(G, FEDAGG_OK);
   std::vector<std::string> errs(G);
   std::vector<std::thread> th;
-  for (uint64_t gi = 0; gi < G; ++gi)
-    th.emplace_back([&, gi] {
-      rcs[gi] = run_shard<T>(m, m->shards[gi], K, nseg, h_seg, seg_bytes, h_w, idx, h_out, ws_bytes);
-      if (rcs[gi]) errs[gi] = fedagg_last_error();  // the error text is per thread: carry it back
-    });
+  int spawn_rc = FEDAGG_OK;
+  try {
+    for (uint64_t gi = 0; gi < G; ++gi)
+      th.emplace_back([&, gi] {
+        rcs[gi] = run_shard<T>(m, m->shards[gi], K, nseg, h_seg, seg_bytes, h_w, idx, h_out, ws_bytes);
+        if (rcs[gi]) errs[gi] = fedagg_last_error();  // the error text is per thread: carry it back
+      });
+  } catch (const std::exception& e) {  // no thread for a shard: the started ones finish, the call fails
+    spawn_rc = FEDAGG_EINVAL;
+    errs.assign(G, std::string("cannot start a shard thread: ") + e.what());
+  }
   for (auto& t : th) t.join();
+  if (spawn_rc) {
+    if (caller >= 0) (void)hipSetDevice(caller);
+    return fail(std::string(name) + ": " + errs[0]);
+  }
   if (caller >= 0) (void)hipSetDevice(caller);  // the caller's later work stays on its own device
   for (uint64_t gi = 0; gi < G; ++gi)
     if (rcs[gi]) {
@@ -273,7 +294,11 @@ fedagg_multi* fedagg_multi_create(int ndev, const int* devs, int pack_threads) {
   }
   int caller = -1;
   (void)hipGetDevice(&caller);
-  auto* m = new fedagg_multi();
+  auto* m = new (std::nothrow) fedagg_multi();
+  if (!m) {
+    fail("fedagg_multi_create: out of host memory");
+    return nullptr;
+  }
   const std::vector<int> allowed = allowed_cpus();
   const int per = pack_threads ? pack_threads
                                : std::max(2, std::min(kPackThreadsCap, (int)allowed.size() / ndev));
@@ -352,6 +377,11 @@ int fedagg_multi_fedavg_f32(fedagg_multi* m, int K, int nseg, const void* const*
 int fedagg_multi_fedavg_f64(fedagg_multi* m, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
                             const double* h_w, const uint64_t* h_idx, int P, double* h_out) {
   return multi_fedavg<double>(m, K, nseg, h_seg, seg_bytes, h_w, h_idx, P, h_out, "fedagg_multi_fedavg_f64");
+}
+
+int fedagg_multi_fedavg_f16(fedagg_multi* m, int K, int nseg, const void* const* h_seg, const uint64_t* seg_bytes,
+                            const uint16_t* h_w, const uint64_t* h_idx, int P, uint16_t* h_out) {
+  return multi_fedavg<uint16_t>(m, K, nseg, h_seg, seg_bytes, h_w, h_idx, P, h_out, "fedagg_multi_fedavg_f16");
 }
 
 int fedagg_multi_shard_info(fedagg_multi* m, int g, int* device, int* numa_node, int* threads, int* ncpus,

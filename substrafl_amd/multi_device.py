@@ -431,7 +431,7 @@ class NativeMultiFedAvg:
     parameter-range plan as :class:`MultiDeviceEngine` -- shards, one thread and one private session
     per device, NUMA-bound pack workers, HBM-sized sub-ranges -- run entirely in C++, one ctypes call
     per aggregation (what a host in another language binds).  FedAvg over
-    uniform fp32 or fp64 layer lists; bit-identical to :class:`MultiDeviceEngine` and to the
+    uniform fp16, fp32 or fp64 layer lists; bit-identical to :class:`MultiDeviceEngine` and to the
     reference (fed_avg.py:217-222)."""
 
     def __init__(self, devices: Sequence[int], pack_threads: int = 0, max_shard_bytes: int = 0):
@@ -459,21 +459,21 @@ class NativeMultiFedAvg:
             pass
 
     def fedavg(self, parameters_updates: List[List[np.ndarray]], n_samples: Sequence[int]) -> List[np.ndarray]:
-        """fed_avg.py:217-222 for validated inputs whose layers all share one dtype, fp32 or fp64."""
+        """fed_avg.py:217-222 for validated inputs whose layers all share one dtype, fp16, fp32 or fp64."""
         import ctypes
 
         K, L = len(parameters_updates), len(parameters_updates[0])
         dts = {a.dtype for pu in parameters_updates for a in pu}
-        if len(dts) != 1 or next(iter(dts)) not in (np.float32, np.float64):
-            raise NotImplementedError("fedagg_multi_fedavg takes layers of one dtype, float32 or float64")
+        if len(dts) != 1 or next(iter(dts)) not in (np.float16, np.float32, np.float64):
+            raise NotImplementedError("fedagg_multi_fedavg takes layers of one dtype, float16, float32 or float64")
         dt = np.dtype(next(iter(dts)))
         kind = kind_of(dt)
         layout = BucketLayout(list(range(L)), [a.shape for a in parameters_updates[0]], dt)
         nseg, ptrs, sizes, keep = runtime._segments(native_byte_order(parameters_updates))
-        w = fedavg_weights(n_samples, kind)
+        w = fedavg_weights(n_samples, kind)  # fp16: the weights' bit patterns, as the C entry takes them
         idx = layout.pairwise_idx.astype(np.uint64)
         out = runtime.reusable_host_array(layout.M, dt, "multi-native")
-        fn = self.lib.fedagg_multi_fedavg_f32 if kind == "f32" else self.lib.fedagg_multi_fedavg_f64
+        fn = getattr(self.lib, f"fedagg_multi_fedavg_{kind}")
         _native.check(fn(self._h, K, nseg, ptrs, sizes, w.ctypes.data, idx.ctypes.data if idx.size else None,
                          int(idx.size), out.ctypes.data), "fedagg_multi_fedavg")
         del keep

@@ -2,15 +2,15 @@
 driven through its ctypes binding at the shapes the plain-C demo does not reach: client counts
 past the kernels' 128-client argument chunk, many ``numel == 1`` layers (the separate pairwise
 path with its workspace, not the fused patch), ragged layers cut by shard and sub-range
-boundaries, three shards on one GPU, fp32 and fp64 -- every element bit-identical to the
-reference's order (oracle.fedavg_explicit, fed_avg.py:217-222)."""
+boundaries, three shards on one GPU, fp16, fp32 and fp64 -- every element bit-identical to the
+reference's order (oracle.fedavg_explicit; for fp16 NumPy's own calls, fed_avg.py:217-222)."""
 
 import ctypes
 
 import numpy as np
 import pytest
 
-from oracle import fedavg_explicit
+from oracle import fedavg_explicit, fedavg_reference_structure
 
 pytestmark = pytest.mark.gpu
 
@@ -29,7 +29,7 @@ def _multi_fedavg(lib, devs, rows, n_samples, dt, max_shard_bytes=0):
     keep = [np.ascontiguousarray(a) for row in rows for a in row]
     seg = _native.ptr_array([a.ctypes.data for a in keep])
     seg_bytes = (ctypes.c_uint64 * L)(*[a.nbytes for a in rows[0]])
-    kind = "f32" if dt == np.float32 else "f64"
+    kind = {np.dtype(np.float16): "f16", np.dtype(np.float32): "f32", np.dtype(np.float64): "f64"}[np.dtype(dt)]
     w = fedavg_weights(n_samples, kind)
     idx = layout.pairwise_idx.astype(np.uint64)
     out = np.empty(layout.M, dtype=dt)
@@ -39,7 +39,7 @@ def _multi_fedavg(lib, devs, rows, n_samples, dt, max_shard_bytes=0):
     try:
         if max_shard_bytes:
             _native.check(lib.fedagg_multi_set(m, b"max_shard_bytes", max_shard_bytes), "multi_set")
-        fn = lib.fedagg_multi_fedavg_f32 if kind == "f32" else lib.fedagg_multi_fedavg_f64
+        fn = getattr(lib, f"fedagg_multi_fedavg_{kind}")
         _native.check(fn(m, K, L, seg, seg_bytes, w.ctypes.data, idx.ctypes.data if idx.size else None, int(idx.size),
                          out.ctypes.data), "multi_fedavg")
         info = []
@@ -53,7 +53,7 @@ def _multi_fedavg(lib, devs, rows, n_samples, dt, max_shard_bytes=0):
     return [a for _, a in layout.unpack(out)], info
 
 
-@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("dt", [np.float16, np.float32, np.float64])
 @pytest.mark.parametrize("K,npw", [(130, 20), (9, 3)])
 def test_multi_entry_bit_exact(dt, K, npw):
     import torch
@@ -69,7 +69,8 @@ def test_multi_entry_bit_exact(dt, K, npw):
     shapes += [(50_001,), (3, 1, 1)]
     rows = _rows(rng, K, shapes, dt)
     ns = [int(v) for v in rng.integers(1, 5000, K)]
-    ref = fedavg_explicit(rows, ns)
+    # fp16: NumPy's own calls (its half loops; HALF_pairwise_sum adds in fp32) are the reference
+    ref = fedavg_reference_structure(rows, ns) if dt == np.float16 else fedavg_explicit(rows, ns)
     got, info = _multi_fedavg(lib, [0, 0, 0], rows, ns, dt, max_shard_bytes=(K + 1) * np.dtype(dt).itemsize * 8192)
     assert sum(1 for lo, hi, _ in info if hi > lo) >= 2 and sum(r for _, _, r in info) > 3, info
     for g, r in zip(got, ref):
