@@ -39,7 +39,10 @@ class Sampler(threading.Thread):
     FIELDS = ("current_gfxclks", "current_socclks", "current_uclk", "current_socket_power", "average_socket_power",
               "temperature_hotspot", "temperature_mem", "throttle_status", "indep_throttle_status",
               "ppt_residency_acc", "socket_thm_residency_acc", "hbm_thm_residency_acc", "gfxclk_lock_status",
-              "average_umc_activity", "average_gfx_activity", "firmware_timestamp")
+              "average_umc_activity", "average_gfx_activity", "firmware_timestamp", "average_gfxclk_frequency",
+              "average_socclk_frequency", "average_uclk_frequency", "prochot_residency_acc", "vr_thm_residency_acc",
+              "mem_activity_acc", "gfx_activity_acc", "accumulation_counter", "voltage_soc", "voltage_gfx",
+              "voltage_mem", "energy_accumulator", "pcie_bandwidth_inst")
 
     def __init__(self, bdf, period=0.002, enabled=True):
         super().__init__(daemon=True)
@@ -136,7 +139,10 @@ def burst(torch, plan, stream, n, sampler, label, sync=True):
            "step_at_s": round(start[s] - t_ref, 4) if s else None,
            "frac_before": round(BYTES / (before / 1e3) / 8e12, 4) if before else None,
            "frac_after": round(BYTES / (after / 1e3) / 8e12, 4) if after else None,
-           "per_launch": per_launch}
+           "per_launch": per_launch,
+           # the raw samples of the burst (time from its first launch, every field), for a step
+           "samples": [[round(t - t_ref, 5), m] for (t, m) in samples
+                       if start and start[0] - 0.05 <= t <= start[-1] + dur[-1] / 1e3 + 0.05]}
     if s:  # the sampled state on either side of the step
         for side, rng in (("before", per_launch[:s]), ("after", per_launch[s:])):
             for f in ("current_gfxclks", "current_socclks", "current_uclk", "current_socket_power",
