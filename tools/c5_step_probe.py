@@ -110,16 +110,20 @@ def burst(torch, plan, stream, n, sampler, label, sync=True):
     if sync:  # (False: the launches queue behind whatever the stream still has to run)
         torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
-    ref = torch.cuda.Event(enable_timing=True)
     t_ref = time.perf_counter()
-    ref.record(stream)
     for a, b in evs:
         a.record(stream)
         plan.launch(stream)
         b.record(stream)
     torch.cuda.synchronize()
+    t_end = time.perf_counter()
     dur = [a.elapsed_time(b) for a, b in evs]
-    start = [t_ref + ref.elapsed_time(a) / 1e3 for a, _ in evs]
+    # host-clock starts anchored at the burst's END (the synchronize returns right after the last
+    # launch): with sync=False the first launch waits behind the synthesis, so t_ref (enqueue time)
+    # is not when it ran
+    last = evs[-1][1]
+    start = [t_end - a.elapsed_time(last) / 1e3 for a, _ in evs]
+    t_ref = start[0] if sync is False else t_ref
     s, before, after = step_split(dur)
     samples = list(sampler.samples) if sampler.handle is not None else []
     per_launch = []
