@@ -89,6 +89,10 @@ class Sampler(threading.Thread):
             self.error = f"{type(e).__name__}: {e}"[:300]
 
 
+TRACE_FIELDS = ("current_socclks", "current_gfxclks", "current_uclk", "average_umc_activity", "average_gfx_activity",
+                "current_socket_power", "pcie_bandwidth_inst")
+
+
 def step_split(d):
     """The index s (2 <= s <= n-2) splitting durations d into two levels with the least
     within-level squared error; returns (s, mean before, mean after)."""
@@ -170,6 +174,8 @@ def main():
     ap.add_argument("--no-sync-after-synth", action="store_true",
                     help="enqueue the first launches right behind the synthesis, as bench.py does")
     ap.add_argument("--sleep-after-synth", type=float, default=0.0, help="idle seconds between synthesis and launches")
+    ap.add_argument("--sleep-before-synth", type=float, default=0.0,
+                    help="idle seconds between HIP start-up and the 91 GB allocation (does the step move with it?)")
     args = ap.parse_args()
 
     import torch
@@ -183,8 +189,15 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
+    marks = {}  # wall seconds since process start of each phase
+    torch.zeros(1, device=dev)
+    torch.cuda.synchronize()
+    marks["hip_ready"] = round(time.time() - _T0, 4)
     sampler = Sampler(device_pci_bus_id(0), enabled=not args.no_sampler)
     sampler.start()
+    marks["sampler_started"] = round(time.time() - _T0, 4)
+    if args.sleep_before_synth:
+        time.sleep(args.sleep_before_synth)
     out = {"workload": "c5 fedavg_bf16_128x350M tiled", "bytes_alg_per_launch": BYTES, "process_start_wall": _T0,
            "sampler": {"error": sampler.error, "period_s": sampler.period,
                        "bdfs": getattr(sampler, "bdfs", None)}, "bursts": []}
@@ -194,9 +207,11 @@ def main():
     w = fedavg_weights(n_samples, kind)
     tv = tiled_tile(kind, K, M)
     t0 = time.perf_counter()
+    marks["alloc_start"] = round(time.time() - _T0, 4)
     buf_a = bench.synth_tiled(torch, K, M, kind, dev, 20241016, tv)
     ld = BucketLayout(list(range(len(shapes))), shapes, np.float32).ld
     out_a = torch.empty(ld, dtype=torch.float32, device=dev)
+    marks["synth_enqueued"] = round(time.time() - _T0, 4)
     if not args.no_sync_after_synth:  # bench.py enqueues its first launches behind the synthesis
         torch.cuda.synchronize()
     out["synth_s"] = round(time.perf_counter() - t0, 2)
@@ -207,6 +222,9 @@ def main():
     plan_a = TiledFedAvgPlan(kind, buf_a, K, w, M, out_a, pw, tv=tv)
     print(f"synth {out['synth_s']} s; sampler {sampler.error or 'ok'}", flush=True)
     out["process_start_to_first_launch_s"] = round(time.time() - _T0, 2)
+    marks["first_launch_enqueued"] = round(time.time() - _T0, 4)
+    out["marks"] = marks
+    out["sleep_before_synth_s"] = args.sleep_before_synth
     out["bursts"].append(burst(torch, plan_a, stream, args.first, sampler, "first: right after synthesis",
                                sync=not args.no_sync_after_synth))
     print(json.dumps({k: v for k, v in out["bursts"][-1].items() if k != "per_launch"}), flush=True)
@@ -231,6 +249,11 @@ def main():
     sampler.stop_ev.set()
     sampler.join(timeout=2)
     out["sampler"]["samples"] = len(sampler.samples)
+    # the whole process's trace of the firmware-averaged clocks and activity (seconds since process
+    # start), to place the SOC clock's fall against the marks above
+    t_off = time.time() - time.perf_counter() - _T0
+    out["trace"] = [[round(t + t_off, 4)] + [m.get(f) for f in TRACE_FIELDS] for t, m in sampler.samples]
+    out["trace_fields"] = ["t_s"] + list(TRACE_FIELDS)
     out["sampler"]["error"] = sampler.error
     if sampler.samples:
         dt = np.diff([t for t, _ in sampler.samples])
