@@ -112,6 +112,8 @@ def parse():
                          "FedAvg fp32/bf16), or (default) tiles where the library recommends them -- the "
                          "layout the drop-in host path stages (AggregationEngine.tiled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wait-quiet", action="store_true",
+                    help="time at once, even while the driver still clears the previous process's freed device memory")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--grid-cap", type=int, default=0)
     ap.add_argument("--tune", default="", help="library launch knobs for experiments, key=value[,key=value] "
@@ -296,10 +298,71 @@ class _Ctx:
         return [float(v) for v in t]
 
 
+QUIET_SOCCLK_MHZ = 200.0  # firmware-averaged SOC clock at or above this: the driver is clearing freed VRAM
+QUIET_WAIT_MAX_S = 12.0  # a 288 GB clear at the measured ~38 GB/s takes ~7.5 s
+
+
+def wait_device_quiet(dev_index: int, limit_s: float = QUIET_WAIT_MAX_S) -> dict:
+    """Wait, bounded, until the kernel driver has finished clearing the device memory that the
+    PREVIOUS process on this GPU freed.  The driver zeroes freed VRAM in the background at ~38 GB/s
+    (a process that held 91 GB leaves ~2.5 s of it; 45 GB ~1 s; 8 GB ~0.1 s; none without device
+    memory), and while it runs the SOC clock domain sits at its high level and HBM-bound launches
+    are 2.0-2.5 % slower ("C5 per launch": profiles/r06s_*, r06q_*, r06r_*).  That is
+    another process's cost, so the timed region starts after it; the line reports what was seen
+    and waited (``device_quiet``).  The signal is amdsmi's gpu_metrics ``current_socclks``, the
+    firmware's average (it decays over ~0.25 s once the clear ends); without amdsmi nothing is
+    waited and the record says why."""
+    rec = {"signal": "amdsmi gpu_metrics current_socclks (firmware-averaged MHz)", "threshold_mhz": QUIET_SOCCLK_MHZ}
+    try:
+        import amdsmi
+
+        from substrafl_amd.runtime import device_pci_bus_id
+
+        amdsmi.amdsmi_init()
+    except Exception as e:  # noqa: BLE001 -- the measurement stands without it, labelled
+        rec["skipped"] = f"{type(e).__name__}: {e}"[:200]
+        return rec
+    try:
+        bdf = device_pci_bus_id(dev_index)
+        handles = amdsmi.amdsmi_get_processor_handles()
+        match = [h for h in handles if amdsmi.amdsmi_get_gpu_device_bdf(h).lower().endswith(bdf[-7:])]
+        if not match:
+            rec["skipped"] = f"no amdsmi handle for {bdf}"
+            return rec
+
+        def soc():
+            v = amdsmi.amdsmi_get_gpu_metrics_info(match[0]).get("current_socclks")
+            v = [x for x in v if isinstance(x, (int, float))] if isinstance(v, list) else [v]
+            v = [float(x) for x in v if isinstance(x, (int, float)) and x < 0xFFFF]
+            return sum(v) / len(v) if v else None
+
+        t0 = time.perf_counter()
+        first = cur = soc()
+        while cur is not None and cur >= QUIET_SOCCLK_MHZ and time.perf_counter() - t0 < limit_s:
+            time.sleep(0.02)
+            cur = soc()
+        rec.update(soc_clock_mhz_at_check=first, soc_clock_mhz_at_start=cur,
+                   waited_s=round(time.perf_counter() - t0, 3),
+                   gave_up=bool(cur is not None and cur >= QUIET_SOCCLK_MHZ))
+    except Exception as e:  # noqa: BLE001
+        rec["skipped"] = f"{type(e).__name__}: {e}"[:200]
+    finally:
+        try:
+            amdsmi.amdsmi_shut_down()
+        except Exception:  # noqa: BLE001
+            pass
+    return rec
+
+
 def _timed(ctx, step, steps, warmup):
     """W untimed steps, then EXACTLY `steps` steps bracketed by a barrier + synchronize on both
-    sides; returns this rank's wall time of the region and its HIP-event time."""
+    sides; returns this rank's wall time of the region and its HIP-event time.  Once per process,
+    before the warm-up, waits for the driver's clear of the previous process's freed memory
+    (wait_device_quiet; ``--no-wait-quiet`` skips it)."""
     torch = ctx.torch
+    if getattr(ctx, "quiet", None) is None:
+        ctx.quiet = wait_device_quiet(ctx.device.index) if getattr(ctx, "wait_quiet", True) else \
+            {"skipped": "--no-wait-quiet"}
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(ctx.device)
@@ -418,7 +481,7 @@ def main():
         _native.tune(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     ctx = _Ctx(torch=torch, dist=dist, world=world, rank=rank, device=device, lib=lib, native=_native,
                wl=WORKLOADS[args.workload], stream=torch.cuda.current_stream(device), backend=backend,
-               leg_child=args.client_shard_child, physical_gpus=min(world, ndev))
+               leg_child=args.client_shard_child, physical_gpus=min(world, ndev), wait_quiet=not args.no_wait_quiet)
 
     if args.client_shard_child:  # one leg of an N > 1 line (see client_shard_legs)
         try:
@@ -429,6 +492,8 @@ def main():
                                            t1_source="the parameter-range line's kernel (one GPU, the workload's K x M)")
         except Exception as e:  # noqa: BLE001 -- reported in the parent's line
             res = {"error": f"{type(e).__name__}: {e}"[:800]}
+        if getattr(ctx, "quiet", None) is not None:
+            res["device_quiet"] = ctx.quiet
         if args.executor == "torch" and world > 1 and "error" not in res:
             try:  # the xGMI rates the schedule model needs, measured on this node (tools/lockstep_model.py)
                 res["xgmi_p2p"] = p2p_probe(torch, dist, rank, world, device, ctx.barrier, ctx.max_over_ranks)
@@ -617,6 +682,7 @@ def measure_param_range(args, ctx):
         "cpu_baseline": cpu,
         "parity": parity,
         "build": {"lib_sha256": sha},
+        "device_quiet": getattr(ctx, "quiet", None),
     }
     if world > 1:
         line["process_group"] = {"backend": ctx.backend, "timeout_s": PG_TIMEOUT_S}
