@@ -16,7 +16,10 @@
 // buffers.  One JSON line per buffer on stdout.
 //   hipcc --offload-arch=gfx950 -O3 -Iinclude tools/alloc_probe.hip -Lsubstrafl_amd -lfedagg \
 //         -Wl,-rpath,'$ORIGIN/../substrafl_amd' -o tools/_alloc_probe
-//   tools/_alloc_probe [launches=30]
+//   tools/_alloc_probe [launches=30] [settle_s=8]
+// settle_s: idle after each hipFree before the next allocation, so the driver's background clear
+// of the freed VRAM (~38 GB/s) is over before the next buffer is timed (0: as round 6's
+// first run, whose C and D buffers were timed inside the clear of A and B).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <vector>
 
 #include "fedagg.h"
@@ -91,6 +95,10 @@ static Res run(const uint16_t* base, float* out, float* h_out, const float* w, i
 
 int main(int argc, char** argv) {
   const int launches = argc > 1 ? atoi(argv[1]) : 30;
+  const double settle_s = argc > 2 ? atof(argv[2]) : 8.0;
+  auto settle = [&] {
+    if (settle_s > 0) usleep((useconds_t)(settle_s * 1e6));
+  };
   const uint64_t nvec = (M + L - 1) / L;
   const uint64_t elems = (nvec + TV - 1) / TV * K * TV * L;
   const uint64_t bytes = elems * sizeof(uint16_t);
@@ -122,6 +130,7 @@ int main(int argc, char** argv) {
     return ts.tv_sec + ts.tv_nsec * 1e-9;
   };
   uint16_t *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+  settle();  // and any clear a previous process left
   double t0 = now();
   CHECK(hipMalloc(&a, bytes));
   measure("A hipMalloc (first)", a, now() - t0);
@@ -131,11 +140,13 @@ int main(int argc, char** argv) {
   measure("A again", a, 0.0);
   CHECK(hipFree(a));
   CHECK(hipFree(b));
+  settle();
   t0 = now();
   hipError_t e = hipExtMallocWithFlags((void**)&c, bytes, hipDeviceMallocContiguous);
   if (e == hipSuccess) {
     measure("C hipExtMallocWithFlags(contiguous)", c, now() - t0);
     CHECK(hipFree(c));
+    settle();
   } else {
     printf("{\"buffer\": \"C hipExtMallocWithFlags(contiguous)\", \"refused\": \"%s\"}\n", hipGetErrorString(e));
     (void)hipGetLastError();
