@@ -38,3 +38,20 @@ def test_bad_legs_are_flagged():
     for needle in ("full comparison differs", "wait errors", "spot check mismatches", "ncclCommCount 7 != 8",
                    "client_shard_torch_pg: error", "outputs differ"):
         assert needle in flags, (needle, flags)
+
+
+def test_timing_inside_the_drivers_clear_is_flagged(capsys):
+    """bench.wait_device_quiet gave up (the driver still clearing freed VRAM when the timed region
+    started): the line and the leg are flagged; a wait that ended is only printed."""
+    ok = _line(2, client_shard={"ms_per_step": 4.4, "parity": {"mismatches": 0}, "rccl_comm_count": 2,
+                                "device_quiet": {"waited_s": 0.8, "gave_up": False}})
+    ok["device_quiet"] = {"waited_s": 1.3, "gave_up": False, "soc_clock_mhz_at_check": 328.5,
+                          "soc_clock_mhz_at_start": 180.0}
+    assert rep.report([ok]) == []
+    assert "waited 1.3 s for the driver's clear" in capsys.readouterr().out
+    bad = _line(8, client_shard={"ms_per_step": 4.4, "parity": {"mismatches": 0}, "rccl_comm_count": 8,
+                                 "device_quiet": {"waited_s": 12.0, "gave_up": True}})
+    bad["device_quiet"] = {"waited_s": 12.0, "gave_up": True}
+    flags = "\n".join(rep.report([bad]))
+    assert "N=8: timed while the driver was still clearing" in flags
+    assert "N=8 client_shard: timed while the driver was still clearing" in flags

@@ -64,6 +64,13 @@ def report(lines) -> list:
               f"T(1)/T(N) {eff}  parity {ln.get('parity')}")
         if (ln.get("parity") or {}).get("mismatches"):
             flags.append(f"N={n}: parameter-range spot check mismatches")
+        quiet = ln.get("device_quiet") or {}
+        if quiet.get("waited_s") is not None:  # bench.wait_device_quiet: the driver's clear of freed VRAM
+            print(f"  waited {quiet['waited_s']} s for the driver's clear (SOC clock {quiet.get('soc_clock_mhz_at_check')}"
+                  f" -> {quiet.get('soc_clock_mhz_at_start')} MHz)")
+        if quiet.get("gave_up"):
+            flags.append(f"N={n}: timed while the driver was still clearing freed memory (gave up after "
+                         f"{quiet.get('waited_s')} s)")
         for key in ln.get("legs_order", []):
             leg = ln.get(key) or {}
             if "error" in leg or "skipped" in leg:
@@ -76,6 +83,8 @@ def report(lines) -> list:
                      f"exchange+tail {leg.get('exchange_and_tail_ms')} ms"]
             if (leg.get("parity") or {}).get("mismatches"):
                 flags.append(f"N={n} {key}: spot check mismatches {leg['parity']}")
+            if (leg.get("device_quiet") or {}).get("gave_up"):
+                flags.append(f"N={n} {key}: timed while the driver was still clearing freed memory")
             if leg.get("connect_s") is not None:
                 parts.append(f"set-up {leg['connect_s']} s of {leg.get('connect_deadline_s')} s")
                 if leg.get("connect_deadline_s") and leg["connect_s"] > 0.8 * leg["connect_deadline_s"]:
